@@ -1,0 +1,249 @@
+/*
+ * nrgpu.h — C ABI of the MI355X-native node-replication (NR) log-replay path.
+ *
+ * One `nrg_ctx` is one NR *replica* living on one GPU: it owns the replicated data
+ * structure in HBM (NrHashMap / Stack / AbstractDataStructure), its copy of the shared
+ * operation log (an HBM ring of fixed-width records tagged by logical log index), the
+ * per-replica replay epoch (`ltail`), scratch for the replay kernels, and a HIP stream.
+ *
+ * Each entry point replaces one piece of the reference's Rust API (paths relative to the
+ * reference checkout `junghan0611/node-replication`):
+ *
+ *   nrg_open / nrg_close          Replica::new + Log::new            nr/src/replica.rs:184-232, nr/src/log.rs:179-242
+ *   nrg_log_append*               Log::append                        nr/src/log.rs:343-427
+ *   nrg_log_exec*                 Log::exec -> Dispatch::dispatch_mut nr/src/log.rs:473-524, nr/src/replica.rs:572-581
+ *   nrg_log_state                 head/tail/ctail/ltails            nr/src/log.rs:88-131, :671-679
+ *   nrg_log_reset                 Log::reset                         nr/src/log.rs:593-611
+ *   nrg_hashmap_get*              Replica::execute -> dispatch       nr/src/replica.rs:404-410,483-497; benches/hashmap.rs:107-111
+ *   nrg_hashmap_round_async       Replica::combine (append+exec) + read batch   nr/src/replica.rs:544-595
+ *   nrg_hashmap_prefill*          NrHashMap::default                 benches/hashmap.rs:91-100
+ *   nrg_hashmap_dump / digest     Replica::verify(closure)           nr/src/replica.rs:443-467
+ *   nrg_stack_*                   Stack Dispatch                     benches/stack.rs:36-84, nr/tests/stack.rs:31-96
+ *   nrg_synth_*                   AbstractDataStructure Dispatch     benches/synthetic.rs:60-195
+ *
+ * Conventions
+ *   - Every function returns NRG_OK (0) or a negative NRG_E_* code. Nothing throws or aborts.
+ *   - A context is NOT thread-safe; callers serialise calls on one context, exactly as the
+ *     combiner lock serialises Log::exec on one replica (nr/src/replica.rs:508-540).
+ *     Distinct contexts (one per GPU) may be driven from distinct threads.
+ *   - `*_async` functions take DEVICE pointers and are ordered on the context's stream
+ *     (see nrg_set_stream); buffers are borrowed until the stream reaches that point.
+ *     Device-side failures (table full, probe overrun) are latched and reported by the
+ *     next nrg_sync / synchronous call.
+ *   - Functions without `_async` take HOST pointers and return after the work completed.
+ *   - Records in the log are fixed-width structs (below); the log index of a record is its
+ *     position in the global total order of writes, exactly as in the reference.
+ *   - Responses are produced only for a caller-chosen window [resp_lo, resp_hi) of log
+ *     indices: in NR only the replica that appended an op receives its response
+ *     (nr/src/replica.rs:576-578), and a replica's own ops form contiguous windows.
+ */
+#ifndef NRGPU_H
+#define NRGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- error codes ---------------------------------------------------------------- */
+#define NRG_OK 0
+#define NRG_E_INVAL (-1)        /* bad argument / wrong data-structure kind              */
+#define NRG_E_HIP (-2)          /* a HIP runtime call failed                             */
+#define NRG_E_TABLE_FULL (-3)   /* hash table probe exhausted (reference would grow)     */
+#define NRG_E_RING_FULL (-4)    /* log ring cannot hold the append even after GC         */
+#define NRG_E_NOMEM (-5)        /* device allocation failed                              */
+#define NRG_E_NOT_SYNCED (-6)   /* read requested while ltail < tail (sync first)        */
+#define NRG_E_CAPACITY (-7)     /* batch exceeds configured max / stack capacity         */
+#define NRG_E_NODEV (-8)        /* no HIP device with that ordinal                       */
+
+/* ---- data-structure kinds --------------------------------------------------------- */
+#define NRG_DS_HASHMAP 1u   /* NrHashMap: u64 -> u64, Put/Get                       */
+#define NRG_DS_STACK 2u     /* Stack: Vec<u32>, Push/Pop, Peek                      */
+#define NRG_DS_SYNTHETIC 3u /* AbstractDataStructure(n, 20, 5, 2, 1)                */
+
+/* ---- log record layouts (one WriteOperation each) --------------------------------- */
+/* NrHashMap WriteOperation::Put(key, val)               benches/hashmap.rs:52-56       */
+typedef struct {
+    uint64_t key;
+    uint64_t val;
+} nrg_put;
+
+/* Stack WriteOperation: op = NRG_STACK_PUSH (val used) or NRG_STACK_POP  benches/stack.rs:22-28 */
+#define NRG_STACK_POP 0u
+#define NRG_STACK_PUSH 1u
+typedef struct {
+    uint32_t val;
+    uint32_t op;
+} nrg_stack_op;
+
+/* Synthetic WriteOperation: WriteOnly/ReadWrite(tid, rnd1, rnd2)  benches/synthetic.rs:33-39 */
+#define NRG_SYNTH_WRITE_ONLY 0u
+#define NRG_SYNTH_READ_WRITE 1u
+typedef struct {
+    uint64_t tid;
+    uint64_t r1;
+    uint64_t r2;
+    uint64_t op;
+} nrg_synth_op;
+
+/* Synthetic ReadOperation::ReadOnly(tid, rnd1, rnd2)     benches/synthetic.rs:28-31       */
+typedef struct {
+    uint64_t tid;
+    uint64_t r1;
+    uint64_t r2;
+} nrg_synth_rd;
+
+/* ---- configuration ------------------------------------------------------------------ */
+typedef struct {
+    uint32_t ds_kind;         /* NRG_DS_*                                                  */
+    uint32_t log2_slots;      /* hashmap: table has 2^log2_slots 16-B slots (default 26)    */
+    uint64_t log_bytes;       /* Log::new(bytes): ring entries = bytes/64 rounded as in the
+                                 reference (min 2*GC_FROM_HEAD, power of two). 0 = 32 MiB   */
+    uint64_t max_batch;       /* largest number of log records replayed per kernel pass;
+                                 larger exec ranges are replayed in order, in chunks        */
+    uint64_t max_reads;       /* largest read batch per call                               */
+    uint64_t stack_capacity;  /* stack: maximum number of elements                          */
+    uint64_t synth_n;         /* synthetic: number of words (default 200000)               */
+    uint32_t synth_cold_reads, synth_cold_writes, synth_hot_reads, synth_hot_writes; /* 20,5,2,1 */
+    uint32_t stack_push_resp; /* 0: Push -> None (benches/stack.rs:77-80, nr/examples/stack.rs:70-73)
+                                 1: Push -> Some(v) (nr/tests/stack.rs:89-92)               */
+    uint32_t replica_id;      /* this replica's id (Log::register, ids start at 1)         */
+} nrg_config;
+
+/* Fill `cfg` with the defaults of the reference benches for `ds_kind`. */
+void nrg_config_default(nrg_config* cfg, uint32_t ds_kind);
+
+typedef struct nrg_ctx nrg_ctx;
+
+/* Replica::new(&log): allocate the replica (data structure + ring + scratch) on device
+ * `hip_device`; the data structure starts empty (NrHashMap/Stack) or initialised to
+ * storage[i] = i (synthetic, benches/synthetic.rs:97-100). */
+int nrg_open(int hip_device, const nrg_config* cfg, nrg_ctx** out);
+int nrg_close(nrg_ctx* ctx);
+
+/* Use `hip_stream` (a hipStream_t, or NULL for the context's own stream) for all further
+ * work on this context. */
+int nrg_set_stream(nrg_ctx* ctx, void* hip_stream);
+void* nrg_get_stream(nrg_ctx* ctx);
+
+/* Replica::sync analogue: wait for all queued work; report latched device errors. */
+int nrg_sync(nrg_ctx* ctx);
+
+const char* nrg_strerror(int code);
+/* Library build identifier ("nrgpu <version> gfx950"). */
+const char* nrg_version(void);
+/* Number of visible HIP devices (0 on a host without GPUs; never fails). */
+int nrg_device_count(void);
+
+/* ---- Log ------------------------------------------------------------------------------ */
+typedef struct {
+    uint64_t size;   /* ring entries (power of two)                        */
+    uint64_t head;   /* oldest live logical index (GC boundary)            */
+    uint64_t tail;   /* next logical index to be appended                  */
+    uint64_t ctail;  /* completed tail (max replayed tail)                 */
+    uint64_t ltail;  /* this replica's replay epoch (ltails[idx-1])        */
+    uint32_t replica_id;
+    uint32_t ds_kind;
+} nrg_log_info;
+
+/* Log::append(ops, idx): append `n` host records (layout per ds kind) with origin replica
+ * `origin`; returns the logical index of the first record. When fewer than GC_FROM_HEAD
+ * entries would remain, the replica first replays what it has not replayed (as append's
+ * GC path calls exec, nr/src/log.rs:364-387) and advances head to its ltail. */
+int nrg_log_append(nrg_ctx* ctx, const void* recs, uint64_t n, uint32_t origin, uint64_t* first_idx);
+/* Same, with `d_recs` a device pointer (stream ordered). */
+int nrg_log_append_async(nrg_ctx* ctx, const void* d_recs, uint64_t n, uint32_t origin,
+                         uint64_t* first_idx);
+/* Append `nseg` device segments (e.g. the output of an all-gather of per-GPU write
+ * segments): segment s starts at d_base + s*seg_stride records, holds lens[s] records and
+ * has origin origins[s]. Segments are appended in order s = 0..nseg-1, which is the global
+ * log order of the round. `first_idx[s]` receives each segment's first log index. */
+int nrg_log_append_segments_async(nrg_ctx* ctx, const void* d_base, uint32_t nseg,
+                                  uint64_t seg_stride, const uint64_t* lens,
+                                  const uint32_t* origins, uint64_t* first_idx);
+
+/* Log::exec(idx, dispatch_mut): replay [ltail, tail) into the replica in log order.
+ * Responses for log indices in [resp_lo, resp_hi) are written densely:
+ *   hashmap  : resp[u64] = previous value, some[u8] = 1 iff the key existed
+ *              (HashMap::insert's return, nr/examples/hashmap.rs:46-50)
+ *   stack    : resp[u32] = popped (or pushed, if stack_push_resp) value, some[u8]
+ *   synthetic: resp[u64] = ReadWrite sum (WriteOnly -> 0), some = 1
+ * `resp`/`some` may be NULL (no responses wanted, as benches/hashmap.rs:114-119 returns
+ * Ok(None)); the hashmap then skips the previous-value pipeline entirely. */
+int nrg_log_exec(nrg_ctx* ctx, uint64_t resp_lo, uint64_t resp_hi, void* resp, uint8_t* some);
+int nrg_log_exec_async(nrg_ctx* ctx, uint64_t resp_lo, uint64_t resp_hi, void* d_resp,
+                       uint8_t* d_some);
+
+int nrg_log_state(const nrg_ctx* ctx, nrg_log_info* out);
+/* Log::reset: head = tail = ctail = ltail = 0; the data structure is left untouched. */
+int nrg_log_reset(nrg_ctx* ctx);
+
+/* ---- NrHashMap ----------------------------------------------------------------------- */
+/* Dispatch::dispatch(Get(k)) for a batch, after sync-to-tail (NRG_E_NOT_SYNCED if the
+ * replica has unreplayed log entries): vals[i] = value or 0, found[i] = 1 iff present. */
+int nrg_hashmap_get(nrg_ctx* ctx, const uint64_t* keys, uint64_t n, uint64_t* vals, uint8_t* found);
+int nrg_hashmap_get_async(nrg_ctx* ctx, const uint64_t* d_keys, uint64_t n, uint64_t* d_vals,
+                          uint8_t* d_found);
+
+/* Replica::combine for a single-GPU replica, fused: append the W device records `d_puts`
+ * with origin `origin`, replay everything up to the new tail, then answer the R reads
+ * `d_get_keys` against the post-replay state. Previous-value responses for the appended
+ * puts go to d_prev/d_prev_found if non-NULL. */
+int nrg_hashmap_round_async(nrg_ctx* ctx, const nrg_put* d_puts, uint64_t W, uint32_t origin,
+                            const uint64_t* d_get_keys, uint64_t R, uint64_t* d_get_vals,
+                            uint8_t* d_get_found, uint64_t* d_prev, uint8_t* d_prev_found);
+
+/* NrHashMap::default(): insert (keys[i], vals[i]) directly (no log traffic). */
+int nrg_hashmap_prefill(nrg_ctx* ctx, const uint64_t* keys, const uint64_t* vals, uint64_t n);
+/* Generated on device: keys k = 0..n-1 -> k + val_offset (benches/hashmap.rs:91-100 uses
+ * n = INITIAL_CAPACITY, val_offset = 1). */
+int nrg_hashmap_prefill_range(nrg_ctx* ctx, uint64_t n, uint64_t val_offset);
+int nrg_hashmap_size(nrg_ctx* ctx, uint64_t* n);
+/* Copy out every (key, value) pair (unordered). `*n` receives the number of pairs; if it
+ * exceeds `cap`, nothing is copied and NRG_E_CAPACITY is returned. */
+int nrg_hashmap_dump(nrg_ctx* ctx, uint64_t* keys, uint64_t* vals, uint64_t cap, uint64_t* n);
+/* Order-independent digest of the contents: count, sum and xor of mix64(k ^ mix64(v)). */
+int nrg_hashmap_digest(nrg_ctx* ctx, uint64_t out[3]);
+
+/* ---- Stack --------------------------------------------------------------------------- */
+/* Stack::default(): storage = vals[0..n) (bottom first). */
+int nrg_stack_init(nrg_ctx* ctx, const uint32_t* vals, uint64_t n);
+/* Dispatch::dispatch(Peek) after sync: top of stack. */
+int nrg_stack_peek(nrg_ctx* ctx, uint32_t* val, uint8_t* some);
+int nrg_stack_len(nrg_ctx* ctx, uint64_t* n);
+int nrg_stack_dump(nrg_ctx* ctx, uint32_t* vals, uint64_t cap, uint64_t* n);
+
+/* ---- AbstractDataStructure (synthetic) ------------------------------------------------ */
+/* Dispatch::dispatch(ReadOnly(tid, r1, r2)) for a batch, after sync. */
+int nrg_synth_read(nrg_ctx* ctx, const nrg_synth_rd* ops, uint64_t n, uint64_t* sums);
+int nrg_synth_read_async(nrg_ctx* ctx, const nrg_synth_rd* d_ops, uint64_t n, uint64_t* d_sums);
+int nrg_synth_dump(nrg_ctx* ctx, uint64_t* words, uint64_t cap, uint64_t* n);
+
+/* ---- device memory helpers (for callers without their own allocator) ----------------- */
+int nrg_dev_alloc(nrg_ctx* ctx, uint64_t bytes, void** d_ptr);
+int nrg_dev_free(nrg_ctx* ctx, void* d_ptr);
+int nrg_memcpy_h2d(nrg_ctx* ctx, void* d_dst, const void* h_src, uint64_t bytes);
+int nrg_memcpy_d2h(nrg_ctx* ctx, void* h_dst, const void* d_src, uint64_t bytes);
+
+/* ---- synthetic workload generators (device side; identical streams to oracle/) -------- */
+/* keys[i] = mulhi64(splitmix64_at(seed, i), span): uniform in [0, span). */
+int nrg_gen_uniform_async(nrg_ctx* ctx, uint64_t* d_out, uint64_t n, uint64_t seed, uint64_t span);
+/* raw splitmix64_at(seed, i) (values for Puts, push values after >> 32). */
+int nrg_gen_raw_async(nrg_ctx* ctx, uint64_t* d_out, uint64_t n, uint64_t seed);
+/* interleave: puts[i] = {keys[i], vals[i]} */
+int nrg_gen_puts_async(nrg_ctx* ctx, nrg_put* d_out, const uint64_t* d_keys, const uint64_t* d_vals,
+                       uint64_t n);
+
+/* ---- timing: HIP events recorded around the dominant replay kernel -------------------- */
+/* When enabled, the context records a start/stop event pair around every launch of the
+ * kernel named `which` ("hm_apply_get", "hm_index", ...) and accumulates the elapsed time;
+ * nrg_kernel_time reads (launches, total milliseconds) after synchronising. */
+int nrg_kernel_timing(nrg_ctx* ctx, int enable);
+int nrg_kernel_time(nrg_ctx* ctx, const char* which, uint64_t* launches, double* total_ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NRGPU_H */

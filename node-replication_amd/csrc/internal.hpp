@@ -1,0 +1,131 @@
+// internal.hpp — host-side structures shared by the runtime and the kernel launchers.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/nrgpu.h"
+#include "common.hpp"
+
+namespace nrg {
+
+// Scratch for the stable LSD radix sort of (u32 key, u32 value) pairs (radix_sort.hip).
+struct SortScratch {
+    u64 cap = 0;           // max elements
+    u32* k[2] = {nullptr, nullptr};
+    u32* v[2] = {nullptr, nullptr};
+    u32* ctlmem = nullptr;  // [hist: 4*256][tickets: 64][desc: 4 * max_tiles * 256]
+    u64 max_tiles = 0;
+    u64 ctl_words = 0;
+};
+
+int sort_alloc(SortScratch& s, u64 cap);
+void sort_free(SortScratch& s);
+// Sort n pairs by the low `key_bits` bits of key (stable). vals_in == nullptr means
+// values are 0..n-1. Result pointers are returned (inside the scratch).
+hipError_t sort_pairs(SortScratch& s, const u32* keys_in, const u32* vals_in, u64 n, int key_bits,
+                      hipStream_t st, u32** out_k, u32** out_v);
+
+struct KTimer {
+    std::vector<hipEvent_t> ev;  // pairs
+    u64 pending = 0;             // recorded pairs not yet harvested
+    u64 launches = 0;
+    double total_ms = 0.0;
+};
+
+struct Staging {  // growable device scratch for the host-pointer entry points
+    void* p = nullptr;
+    uint64_t bytes = 0;
+};
+
+struct HostRun {  // origin tags of appended log ranges (the Entry::replica field)
+    u64 first, count;
+    u32 origin;
+};
+
+}  // namespace nrg
+
+struct nrg_ctx {
+    int device = 0;
+    nrg_config cfg{};
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+
+    // ---- Log (per-replica HBM ring) ----
+    uint64_t log_size = 0;  // entries (power of two), as Log::new computes it
+    uint64_t head = 0, tail = 0, ctail = 0, ltail = 0;
+    uint32_t rec_bytes = 0;
+    void* d_ring = nullptr;
+    std::vector<nrg::HostRun> origins;
+
+    nrg::DevCtl* d_ctl = nullptr;
+
+    // ---- NrHashMap ----
+    uint32_t slot_shift = 0;  // 64 - log2_slots
+    uint64_t slots = 0;
+    nrg::Slot* d_table = nullptr;
+    uint64_t blt_size = 0;
+    nrg::BltEntry* d_blt[2] = {nullptr, nullptr};
+    uint64_t* d_blt_old[2] = {nullptr, nullptr};
+    uint32_t* d_bslot[2] = {nullptr, nullptr};
+    uint64_t prev_n = 0;  // puts in the previous round (their BLT entries are cleared next round)
+    uint32_t parity = 0;
+
+    // ---- Stack ----
+    uint32_t* d_stack = nullptr;
+    uint32_t stack_key_bits = 0;
+
+    // ---- Synthetic ----
+    uint64_t* d_words = nullptr;
+    uint64_t* d_sort_aux = nullptr;  // per-touch max-scan output
+    uint32_t synth_key_bits = 0;
+
+    // ---- shared scratch ----
+    nrg::SortScratch sort;
+    uint64_t* d_tmp_u64 = nullptr;  // general scratch (max_batch words)
+    uint64_t tmp_words = 0;
+    uint32_t* d_scan_desc = nullptr;  // decoupled look-back descriptors for scans
+    uint64_t scan_desc_words = 0;
+
+    nrg::Staging stg[4];
+
+    // ---- timing ----
+    bool timing = false;
+    std::map<std::string, nrg::KTimer> timers;
+};
+
+namespace nrg {
+// timing helpers (runtime.cpp)
+void timer_begin(nrg_ctx* c, const char* name);
+void timer_end(nrg_ctx* c, const char* name);
+
+// hashmap.hip
+hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool write_ring,
+                           const u64* d_get_keys, u64 R, u64* d_get_vals, uint8_t* d_get_found,
+                           u64 resp_lo, u64 resp_hi, u64* d_prev, uint8_t* d_prev_found,
+                           bool touch_log);
+hipError_t hm_get_only(nrg_ctx* c, const u64* d_keys, u64 n, u64* d_vals, uint8_t* d_found);
+hipError_t hm_prefill_range(nrg_ctx* c, u64 n, u64 off);
+hipError_t hm_dump(nrg_ctx* c, u64* d_keys, u64* d_vals);
+hipError_t hm_digest(nrg_ctx* c, u64* d_out3);
+hipError_t gen_uniform(nrg_ctx* c, u64* d, u64 n, u64 seed, u64 span);
+hipError_t gen_raw(nrg_ctx* c, u64* d, u64 n, u64 seed);
+hipError_t gen_puts(nrg_ctx* c, nrg_put* d, const u64* k, const u64* v, u64 n);
+hipError_t copy_segments(nrg_ctx* c, const void* d_base, u32 nseg, u64 seg_stride, const u64* lens,
+                         u64 dst_lo);
+
+// stack.hip
+hipError_t st_replay_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 resp_hi, uint32_t* d_resp,
+                           uint8_t* d_some);
+
+// synthetic.hip
+hipError_t sy_init(nrg_ctx* c);
+hipError_t sy_replay_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 resp_hi, u64* d_resp,
+                           uint8_t* d_some);
+hipError_t sy_read(nrg_ctx* c, const nrg_synth_rd* d_ops, u64 n, u64* d_sums);
+hipError_t sy_maxscan(nrg_ctx* c, const u32* sk, const u32* sv, u64 n, u32* M);
+}  // namespace nrg

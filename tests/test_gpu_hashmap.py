@@ -1,0 +1,182 @@
+"""NrHashMap parity: the HIP replay (through the C ABI) vs the sequential CPU oracle.
+
+Semantics under test (SURVEY.md §8a "Round semantics"): the writes of a round are replayed
+in global log order (Put -> HashMap::insert, response = previous value,
+nr/examples/hashmap.rs:46-50), then the round's reads are answered against the post-round
+state (dispatch after sync-to-tail, nr/src/replica.rs:483-497). Bit-exact comparison of every
+response and of the final replica contents.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+EMPTY = 0xFFFFFFFFFFFFFFFF
+
+
+def _puts(keys, vals):
+    import nrgpu
+
+    r = np.zeros(len(keys), nrgpu.PUT_DTYPE)
+    r["key"] = keys
+    r["val"] = vals
+    return r
+
+
+def _check_state(dev, om):
+    gk, gv = dev.hm_dump()
+    ok, ov = om.dump_sorted()
+    assert len(gk) == len(ok) == len(om)
+    np.testing.assert_array_equal(gk, ok)
+    np.testing.assert_array_equal(gv, ov)
+    assert dev.hm_size() == len(om)
+    assert dev.hm_digest() == om.digest()
+
+
+@pytest.mark.parametrize("span,W,R,rounds", [(64, 300, 500, 6), (5000, 2000, 3000, 5), (1 << 40, 4000, 4000, 3)])
+def test_rounds_prev_and_gets(nrg, orc, span, W, R, rounds):
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=16, max_batch=8192)
+    om = orc.HashMap()
+    dev.hm_prefill_range(min(span, 1000), 1)
+    om.prefill_range(min(span, 1000), 1)
+    for r in range(rounds):
+        keys = orc.gen_uniform(W, 1000 + r, span)
+        vals = orc.gen_raw(W, 2000 + r)
+        if r % 2 == 1:
+            keys[::97] = EMPTY  # the side-slot key
+        gkeys = orc.gen_uniform(R, 3000 + r, span + span // 10 + 1)
+        gkeys[::131] = EMPTY
+        first = dev.log_append(_puts(keys, vals), 1)
+        prev, pf = dev.log_exec(first, first + W)
+        oprev, opf = om.replay(keys, vals)
+        np.testing.assert_array_equal(pf, opf)
+        np.testing.assert_array_equal(prev, oprev)
+        gv, gf = dev.hm_get(gkeys)
+        ov, of = om.get_batch(gkeys)
+        np.testing.assert_array_equal(gf, of)
+        np.testing.assert_array_equal(gv, ov)
+    _check_state(dev, om)
+    dev.close()
+
+
+def test_exec_without_responses_matches(nrg, orc):
+    """benches/hashmap.rs:114-119 returns Ok(None): no previous-value pipeline."""
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=16, max_batch=4096)
+    om = orc.HashMap()
+    for r in range(4):
+        keys = orc.gen_uniform(3000, 7 + r, 700)
+        vals = orc.gen_raw(3000, 70 + r)
+        dev.log_append(_puts(keys, vals), 1)
+        dev.log_exec()
+        om.replay(keys, vals)
+    _check_state(dev, om)
+
+
+def test_exec_chunks_longer_than_max_batch(nrg, orc):
+    """An exec range longer than max_batch is replayed in order, chunk by chunk."""
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=15, max_batch=1000)
+    om = orc.HashMap()
+    keys = orc.gen_uniform(4500, 5, 300)  # heavy duplication across chunk boundaries
+    vals = orc.gen_raw(4500, 6)
+    first = dev.log_append(_puts(keys, vals), 1)
+    prev, pf = dev.log_exec(first, first + 4500)
+    oprev, opf = om.replay(keys, vals)
+    np.testing.assert_array_equal(pf, opf)
+    np.testing.assert_array_equal(prev, oprev)
+    _check_state(dev, om)
+
+
+def test_zipf_conflicts(nrg, orc):
+    """Zipf 0.99 stream: hot keys stress last-writer-wins ordering and CAS contention."""
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=20, max_batch=1 << 17)
+    om = orc.HashMap()
+    dev.hm_prefill_range(10000, 1)
+    om.prefill_range(10000, 1)
+    for r in range(3):
+        W = 100_000
+        keys = orc.gen_zipf(W, 11 + r, 100_000, 0.99, scramble=(r == 1))
+        vals = orc.gen_raw(W, 12 + r)
+        first = dev.log_append(_puts(keys, vals), 1)
+        prev, pf = dev.log_exec(first, first + W)
+        oprev, opf = om.replay(keys, vals)
+        np.testing.assert_array_equal(pf, opf)
+        np.testing.assert_array_equal(prev, oprev)
+    _check_state(dev, om)
+
+
+def test_fused_round_device(nrg, orc):
+    """nrg_hashmap_round_async: append + replay + reads in one call on device buffers."""
+    import torch
+
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=18, max_batch=1 << 14)
+    dev.use_torch_stream()
+    om = orc.HashMap()
+    dev.hm_prefill_range(20000, 1)
+    om.prefill_range(20000, 1)
+    W, R = 10000, 30000
+    for r in range(4):
+        keys = orc.gen_uniform(W, 40 + r, 25000)
+        vals = orc.gen_raw(W, 50 + r)
+        gk = orc.gen_uniform(R, 60 + r, 26000)
+        d_puts = torch.from_numpy(_puts(keys, vals).view(np.int64).copy()).cuda()
+        d_gk = torch.from_numpy(gk.view(np.int64)).cuda()
+        d_gv = torch.empty(R, dtype=torch.int64, device="cuda")
+        d_gf = torch.empty(R, dtype=torch.uint8, device="cuda")
+        d_pv = torch.empty(W, dtype=torch.int64, device="cuda")
+        d_pf = torch.empty(W, dtype=torch.uint8, device="cuda")
+        dev.hm_round_device(d_puts, W, 1, d_gk, R, d_gv, d_gf, d_pv, d_pf)
+        torch.cuda.synchronize()
+        oprev, opf = om.replay(keys, vals)
+        ov, of = om.get_batch(gk)
+        np.testing.assert_array_equal(d_pf.cpu().numpy(), opf)
+        np.testing.assert_array_equal(d_pv.cpu().numpy().view(np.uint64), oprev)
+        np.testing.assert_array_equal(d_gf.cpu().numpy(), of)
+        np.testing.assert_array_equal(d_gv.cpu().numpy().view(np.uint64), ov)
+    dev.sync()
+    _check_state(dev, om)
+
+
+def test_device_generator_matches_oracle(nrg, orc):
+    import torch
+
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=10, max_batch=1024)
+    dev.use_torch_stream()
+    d = torch.empty(100_000, dtype=torch.int64, device="cuda")
+    dev.gen_uniform_device(d, 100_000, 1234, 10_000_000)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(d.cpu().numpy().view(np.uint64), orc.gen_uniform(100_000, 1234, 10_000_000))
+    dev.gen_raw_device(d, 100_000, 99)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(d.cpu().numpy().view(np.uint64), orc.gen_raw(100_000, 99))
+
+
+def test_not_synced_read_is_refused(nrg, orc):
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=10, max_batch=1024)
+    dev.log_append(_puts(np.array([1], np.uint64), np.array([2], np.uint64)), 1)
+    with pytest.raises(nrg.NrgError) as e:
+        dev.hm_get(np.array([1], np.uint64))
+    assert e.value.code == nrg._lib.NRG_E_NOT_SYNCED
+    dev.log_exec()
+    v, f = dev.hm_get(np.array([1, 3], np.uint64))
+    assert list(f) == [1, 0] and int(v[0]) == 2
+
+
+def test_ring_wrap_and_gc(nrg, orc):
+    """Many appends through a minimum-size log (16384 entries): ring wrap-around and the GC
+    path of Log::append (exec before advancing head, nr/src/log.rs:364-387)."""
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=16, max_batch=4096, log_bytes=1024)
+    st = dev.log_state()
+    assert st["size"] == 16384
+    om = orc.HashMap()
+    total = 0
+    for r in range(12):
+        n = 3000 + 17 * r
+        keys = orc.gen_uniform(n, 300 + r, 5000)
+        vals = orc.gen_raw(n, 400 + r)
+        dev.log_append(_puts(keys, vals), 1)  # no exec: append's GC path replays when needed
+        om.replay(keys, vals)
+        total += n
+    dev.log_exec()
+    st = dev.log_state()
+    assert st["tail"] == total and st["ltail"] == total and st["ctail"] == total
+    _check_state(dev, om)

@@ -1,0 +1,64 @@
+"""Stack parity: HIP depth-scan replay vs the sequential Vec<u32> oracle.
+
+Mirrors nr/tests/stack.rs `sequential_test` (:102-168: random push/pop/peek vs a Vec
+model, then verify storage and popped values) and benches/stack.rs (50/50 push/pop over
+an initial 50,000-element stack, :50-63, :87-102), with seeded streams.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _ops(vals, ops):
+    import nrgpu
+
+    r = np.zeros(len(ops), nrgpu.STACK_OP_DTYPE)
+    r["val"] = vals
+    r["op"] = ops
+    return r
+
+
+@pytest.mark.parametrize("init_n,n,rounds,push_resp", [(0, 50, 3, 1), (1000, 5000, 4, 0), (50000, 200000, 3, 0),
+                                                       (3, 20000, 2, 1)])
+def test_stack_rounds(nrg, orc, init_n, n, rounds, push_resp):
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_STACK, 0, max_batch=1 << 18, stack_capacity=1 << 20,
+                            stack_push_resp=push_resp)
+    init = np.arange(init_n, dtype=np.uint32)
+    dev.st_init(init)
+    os_ = orc.Stack(init)
+    for r in range(rounds):
+        vals, ops = orc.gen_stack_ops(n, 77 + r)
+        if init_n == 3:
+            ops[: n // 2] = 0  # long runs of pops on an empty stack (saturating depth)
+        first = dev.log_append(_ops(vals, ops), 1)
+        resp, some = dev.log_exec(first, first + n)
+        oresp, osome = os_.replay(vals, ops, push_resp=bool(push_resp))
+        np.testing.assert_array_equal(some, osome)
+        np.testing.assert_array_equal(resp, oresp)
+        assert dev.st_len() == len(os_)
+        assert dev.st_peek() == os_.peek()
+    np.testing.assert_array_equal(dev.st_dump(), os_.dump())
+
+
+def test_stack_chunked_exec(nrg, orc):
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_STACK, 0, max_batch=3000, stack_capacity=1 << 16)
+    init = np.arange(100, dtype=np.uint32)
+    dev.st_init(init)
+    os_ = orc.Stack(init)
+    vals, ops = orc.gen_stack_ops(10000, 5)
+    first = dev.log_append(_ops(vals, ops), 1)
+    resp, some = dev.log_exec(first, first + 10000)
+    oresp, osome = os_.replay(vals, ops)
+    np.testing.assert_array_equal(some, osome)
+    np.testing.assert_array_equal(resp, oresp)
+    np.testing.assert_array_equal(dev.st_dump(), os_.dump())
+
+
+def test_stack_capacity_error(nrg, orc):
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_STACK, 0, max_batch=1024, stack_capacity=100)
+    dev.st_init(np.arange(90, dtype=np.uint32))
+    dev.log_append(_ops(np.arange(20, dtype=np.uint32), np.ones(20, np.uint32)), 1)
+    with pytest.raises(nrg.NrgError) as e:
+        dev.log_exec()
+    assert e.value.code == nrg._lib.NRG_E_CAPACITY
