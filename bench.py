@@ -1,0 +1,301 @@
+#!/usr/bin/env python3
+"""bench.py — NR log-replay throughput on MI355X (BASELINE.json metric).
+
+Metric: whole-node Mops/s of an NrHashMap replica group at 10% writes (BASELINE.json
+"Mops/s whole node, NrHashMap 10% writes, 1/2/4/8 GPUs; replay HBM GB/s vs peak").
+
+Workload (N = 1: BASELINE.json configs[1], "B1" in SURVEY.md §8d): one GPU replica with a
+2^26-slot open-addressing u64->u64 table (1 GiB), prefilled with keys [0, 2^23) -> k+1
+(NrHashMap::default, benches/hashmap.rs:91-100), uniform keys over a 10M key space, rounds
+of 1M ops = 100k Put + 900k Get per GPU. One step = one NR round on every GPU:
+  Log::append of the rank's write segment (RCCL all-gather of all ranks' segments for N > 1)
+  -> Log::exec of the round's global writes -> dispatch of the rank's reads after sync
+  (nr/src/replica.rs:544-595, :483-497), fused into nrg_hashmap_round[_segments]_async.
+Put responses follow benches/hashmap.rs:114-119 (Ok(None)); the variant with HashMap::insert's
+previous-value responses (nr/examples/hashmap.rs:46-50) is measured beside it.
+Inputs are generated on device before the timed region (a pool of distinct batches, cycled).
+For N > 1 every rank adds 1M ops per round (weak scaling); the value counts all ranks' ops.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(ROOT, "node-replication_amd"), os.path.join(ROOT, "oracle")]
+
+METRIC = "Mops/s whole node, NrHashMap 10% writes, 1/2/4/8 GPUs; replay HBM GB/s vs peak"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def log(msg):
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def numa_groups(cpus):
+    """Group the CPUs we may run on by NUMA node (/sys/devices/system/node)."""
+    groups = {}
+    base = "/sys/devices/system/node"
+    node_of = {}
+    try:
+        for d in os.listdir(base):
+            if not d.startswith("node") or not d[4:].isdigit():
+                continue
+            with open(os.path.join(base, d, "cpulist")) as f:
+                for part in f.read().strip().split(","):
+                    if not part:
+                        continue
+                    a, _, b = part.partition("-")
+                    for c in range(int(a), int(b or a) + 1):
+                        node_of[c] = int(d[4:])
+    except OSError:
+        pass
+    for c in cpus:
+        groups.setdefault(node_of.get(c, 0), []).append(c)
+    return [groups[k] for k in sorted(groups)]
+
+
+def cpu_budget(n_affinity: int) -> int:
+    """CPUs this job may really use: the affinity mask, capped by the cgroup CPU quota and by
+    OMP_NUM_THREADS (the GPU box gives one GPU's job a 16-CPU share of a larger host)."""
+    n = n_affinity
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()
+            if q != "max":
+                n = min(n, max(1, int(int(q) / int(p))))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit():
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def cpu_baseline(seconds: float, write_ratio: int, key_space: int, prefill: int):
+    """C++ restatement of nr (flat combining + shared log + per-replica RwLock) timed on this
+    host's cores, one Replica per NUMA node (oracle/nr_cpu.cpp)."""
+    import oracle
+
+    cpus = sorted(os.sched_getaffinity(0))
+    budget = cpu_budget(len(cpus))
+    nodes = numa_groups(cpus)
+    # spread the thread budget evenly over the NUMA nodes (lowest-numbered CPUs of each node are
+    # physical cores; their SMT siblings come later), one Replica per node
+    per = max(1, budget // len(nodes))
+    groups = [g[:per] for g in nodes][: max(1, min(len(nodes), budget))]
+    cpu_list, rep = [], []
+    for r, g in enumerate(groups):
+        cpu_list += g
+        rep += [r] * len(g)
+    res = oracle.nr_hashmap_bench(cpu_list, rep, seconds, write_ratio, key_space, prefill, 2_500_000, 0xC0FFEE)
+    return {
+        "value": round(res.ops / res.seconds / 1e6, 3),
+        "unit": "Mops/s",
+        "cores": len(cpu_list),
+        "kind": "port",
+        "sample": (f"{res.seconds:.1f} s of the same NrHashMap stream (uniform over {key_space} keys, prefill "
+                   f"[0,{prefill}), {write_ratio}% writes, 2.5M-op per-thread shuffles, 128 ops per clock check) "
+                   f"through the C++ restatement of nr on {len(cpu_list)} threads, {len(groups)} replica(s) "
+                   f"(one per NUMA node); {res.ops} ops"),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--warmup", type=int, default=40)
+    ap.add_argument("--write-ratio", type=int, default=10)
+    ap.add_argument("--ops-per-gpu", type=int, default=1_000_000)
+    ap.add_argument("--key-space", type=int, default=10_000_000)
+    ap.add_argument("--prefill", type=int, default=1 << 23)
+    ap.add_argument("--log2-slots", type=int, default=26)
+    ap.add_argument("--pool", type=int, default=64, help="distinct pre-generated input batches")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-prev-variant", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dev_t = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev_t)
+
+    import nrgpu
+    from nrgpu import _lib as L
+
+    W = args.ops_per_gpu * args.write_ratio // 100
+    R = args.ops_per_gpu - W
+    Wg = W * world
+    rep = nrgpu.DeviceReplica(L.NRG_DS_HASHMAP, local, log2_slots=args.log2_slots, max_batch=max(Wg, 1),
+                              log_bytes=64 * 4 * max(Wg, 8192), replica_id=rank + 1)
+    rep.use_torch_stream()
+    t0 = time.time()
+    rep.hm_prefill_range(args.prefill, 1)
+    log(f"rank {rank}: prefill {args.prefill} keys in {time.time() - t0:.2f}s")
+
+    # ---- inputs: a pool of distinct batches generated on device (seeds per rank/batch) ----
+    P = max(1, min(args.pool, args.steps + args.warmup))
+    puts = torch.empty((P, max(W, 1), 2), dtype=torch.int64, device=dev_t)
+    gkeys = torch.empty((P, max(R, 1)), dtype=torch.int64, device=dev_t)
+    tmp_k = torch.empty(max(W, 1), dtype=torch.int64, device=dev_t)
+    tmp_v = torch.empty(max(W, 1), dtype=torch.int64, device=dev_t)
+    seed0 = 0x4E52475055310001 + rank * 0x1000193
+    for p in range(P):
+        if W:
+            rep.gen_uniform_device(tmp_k, W, seed0 + 3 * p, args.key_space)
+            rep.gen_raw_device(tmp_v, W, seed0 + 3 * p + 1)
+            rep.gen_puts_device(puts[p], tmp_k, tmp_v, W)
+        if R:
+            rep.gen_uniform_device(gkeys[p], R, seed0 + 3 * p + 2, args.key_space)
+    gvals = torch.empty(max(R, 1), dtype=torch.int64, device=dev_t)
+    gfound = torch.empty(max(R, 1), dtype=torch.uint8, device=dev_t)
+    pvals = torch.empty(max(W, 1), dtype=torch.int64, device=dev_t)
+    pfound = torch.empty(max(W, 1), dtype=torch.uint8, device=dev_t)
+    torch.cuda.synchronize()
+
+    # distinct keys per batch (for the algorithmic byte count), outside the timed region
+    u_r = sum(int(torch.unique(gkeys[p, :R]).numel()) for p in range(min(P, 8))) / min(P, 8) if R else 0
+    u_w_local = sum(int(torch.unique(puts[p, :W, 0]).numel()) for p in range(min(P, 8))) / min(P, 8) if W else 0
+
+    group = None
+    if world > 1:
+        from nrgpu.parallel import ReplicatedHashMap
+
+        group = ReplicatedHashMap(rep, device=dev_t)
+
+    def step(i, prev=False):
+        p = i % P
+        pv = pvals if prev else None
+        pf = pfound if prev else None
+        if group is None:
+            rep.hm_round_device(puts[p], W, rank + 1, gkeys[p], R, gvals, gfound, pv, pf)
+        else:
+            group.round(puts[p, :W], gkeys[p, :R], gvals, gfound, pv, pf, stride=W)
+
+    def timed(n, prev=False):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for i in range(n):
+            step(i, prev)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t
+        if world > 1:
+            x = torch.tensor([el], dtype=torch.float64, device=dev_t)
+            dist.all_reduce(x, op=dist.ReduceOp.MAX)
+            el = float(x.item())
+        return el
+
+    for i in range(args.warmup):
+        step(i)
+    rep.sync()
+    log(f"rank {rank}: warmup {args.warmup} rounds done")
+
+    rep.kernel_timing(True)
+    elapsed = timed(args.steps)
+    k2_n, k2_ms = rep.kernel_time("hm_apply_get")
+    k1_n, k1_ms = rep.kernel_time("hm_index")
+    rep.kernel_timing(False)
+    rep.sync()
+    ms_per_step = elapsed * 1e3 / args.steps
+    total_ops = world * args.ops_per_gpu * args.steps
+    value = total_ops / elapsed / 1e6
+
+    prev_value = None
+    if not args.no_prev_variant and world == 1:
+        n2 = max(args.steps // 4, 10)
+        e2 = timed(n2, prev=True)
+        prev_value = world * args.ops_per_gpu * n2 / e2 / 1e6
+    rep.sync()
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    # ---- roofline of the dominant kernel (hm_apply_get = K2) --------------------------------
+    # algorithmic bytes per launch: 16 B per Get (key in, value out) + one 64-B sector per
+    # distinct key read + 8 B per replayed Put value + one 64-B sector written back per distinct
+    # key written (found bytes ignored)
+    u_w = u_w_local * world
+    k2_bytes = 16 * R + 64 * u_r + 8 * Wg + 64 * u_w
+    k2_avg_s = (k2_ms / 1e3 / k2_n) if k2_n else float("nan")
+    achieved = k2_bytes / k2_avg_s / 1e9 if k2_n else None
+    round_bytes = 16 * R + 16 * Wg + 64 * u_r + 128 * u_w
+    res = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "Mops/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic",
+        "config": {
+            "workload": ("B1 NrHashMap replica per GPU: 2^%d-slot table, uniform keys over %d, prefill [0,%d)->k+1, "
+                         "rounds of %d ops/GPU = %d Put + %d Get%s" % (
+                             args.log2_slots, args.key_space, args.prefill, args.ops_per_gpu, W, R,
+                             "; write segments all-gathered over RCCL, every replica replays all %d Puts" % Wg
+                             if world > 1 else "")),
+            "write_ratio_pct": args.write_ratio,
+            "ops_per_gpu_per_round": args.ops_per_gpu,
+            "put_responses": "Ok(None) as benches/hashmap.rs:114-119",
+            "parallelism": "replicas%d" % world,
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "hm_apply_get",
+            "achieved": round(achieved, 1) if achieved else None,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+            "traffic": None,
+            "bytes_per_launch": int(k2_bytes),
+            "avg_launch_us": round(k2_avg_s * 1e6, 3) if k2_n else None,
+            "launches": k2_n,
+        },
+        "round": {
+            "algorithmic_bytes": int(round_bytes),
+            "achieved_GBps": round(round_bytes / (elapsed / args.steps) / 1e9, 1),
+            "hm_index_avg_us": round(k1_ms * 1e3 / k1_n, 3) if k1_n else None,
+            "distinct_get_keys": int(u_r),
+            "distinct_put_keys": int(u_w),
+        },
+    }
+    if prev_value is not None:
+        res["variants"] = {"prev_value_responses_Mops": round(prev_value, 3)}
+    if not args.no_cpu_baseline and world == 1:
+        log(f"cpu baseline: {args.cpu_seconds}s ...")
+        try:
+            res["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.write_ratio, args.key_space, args.prefill)
+        except Exception as e:  # noqa: BLE001
+            res["cpu_baseline"] = {"error": str(e)}
+    print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

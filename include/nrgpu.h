@@ -195,6 +195,19 @@ int nrg_hashmap_round_async(nrg_ctx* ctx, const nrg_put* d_puts, uint64_t W, uin
                             const uint64_t* d_get_keys, uint64_t R, uint64_t* d_get_vals,
                             uint8_t* d_get_found, uint64_t* d_prev, uint8_t* d_prev_found);
 
+/* Multi-GPU round on one replica: the write segments of every replica (e.g. the output of
+ * an RCCL all-gather, segment s at d_base + s*seg_stride records, lens[s] records, origin
+ * origins[s]) are appended in order s = 0..nseg-1 (the round's global log order), the log is
+ * replayed, and the R local reads are answered against the post-round state. Previous-value
+ * responses are produced for segment `resp_seg` (this replica's own writes) if d_prev is
+ * non-NULL. When every segment but the last is full (lens[s] == seg_stride) the gathered
+ * buffer is replayed in place and the log copy is written by the replay itself. */
+int nrg_hashmap_round_segments_async(nrg_ctx* ctx, const nrg_put* d_base, uint32_t nseg,
+                                     uint64_t seg_stride, const uint64_t* lens,
+                                     const uint32_t* origins, uint32_t resp_seg,
+                                     const uint64_t* d_get_keys, uint64_t R, uint64_t* d_get_vals,
+                                     uint8_t* d_get_found, uint64_t* d_prev, uint8_t* d_prev_found);
+
 /* NrHashMap::default(): insert (keys[i], vals[i]) directly (no log traffic). */
 int nrg_hashmap_prefill(nrg_ctx* ctx, const uint64_t* keys, const uint64_t* vals, uint64_t n);
 /* Generated on device: keys k = 0..n-1 -> k + val_offset (benches/hashmap.rs:91-100 uses

@@ -1,0 +1,140 @@
+// random_gather.hip — how fast can MI355X serve random small reads from a table far larger
+// than the Infinity Cache? Calibrates the roofline of the NrHashMap lookup (SURVEY.md §8d
+// "sector-size check"): each Get is one random 16-B slot read from a 1 GiB table.
+//
+// Variants (all read a 2^26 x 16 B = 1 GiB table at splitmix-random slots):
+//   g16xK : each lane issues K independent 16-B loads (K = 1, 2, 4, 8) -> MLP per lane
+//   g8xK  : 8-B loads (key only)
+//   g64   : 4 lanes cooperatively read one 64-B line (one dwordx4 each)
+// Prints per variant: lookups/s, useful GB/s, and GB/s if every access moved a 64-B / 128-B
+// sector. Run under rocprofv3 --pmc FETCH_SIZE to see the bytes the L2 actually fetched.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CHK(x)                                                                          \
+    do {                                                                                \
+        hipError_t e = (x);                                                             \
+        if (e != hipSuccess) {                                                          \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e));    \
+            exit(1);                                                                    \
+        }                                                                               \
+    } while (0)
+
+typedef unsigned long long u64;
+
+__device__ __forceinline__ u64 mix64(u64 z) {
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+struct __attribute__((aligned(16))) Slot {
+    u64 k, v;
+};
+
+template <int K>
+__global__ __launch_bounds__(256) void g16(const Slot* __restrict__ t, u64 mask, u64 n, u64 seed, u64* out) {
+    const u64 base = (blockIdx.x * 256ull + threadIdx.x) * K;
+    Slot s[K];
+#pragma unroll
+    for (int j = 0; j < K; j++) {
+        const u64 i = base + j;
+        s[j] = i < n ? t[mix64(seed + i) & mask] : Slot{0, 0};
+    }
+    u64 acc = 0;
+#pragma unroll
+    for (int j = 0; j < K; j++) acc += s[j].k ^ s[j].v;
+    if (acc == 0x12345) out[0] = acc;
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void g8(const u64* __restrict__ t, u64 mask, u64 n, u64 seed, u64* out) {
+    const u64 base = (blockIdx.x * 256ull + threadIdx.x) * K;
+    u64 s[K];
+#pragma unroll
+    for (int j = 0; j < K; j++) {
+        const u64 i = base + j;
+        s[j] = i < n ? t[2 * (mix64(seed + i) & mask)] : 0;
+    }
+    u64 acc = 0;
+#pragma unroll
+    for (int j = 0; j < K; j++) acc += s[j];
+    if (acc == 0x12345) out[0] = acc;
+}
+
+// 4 lanes read one 64-B line (4 consecutive slots), K lines per group
+template <int K>
+__global__ __launch_bounds__(256) void g64(const Slot* __restrict__ t, u64 mask, u64 n, u64 seed, u64* out) {
+    const u64 grp = (blockIdx.x * 256ull + threadIdx.x) >> 2;
+    const int sub = threadIdx.x & 3;
+    Slot s[K];
+#pragma unroll
+    for (int j = 0; j < K; j++) {
+        const u64 i = grp * K + j;
+        s[j] = i < n ? t[((mix64(seed + i) & mask) & ~3ull) + sub] : Slot{0, 0};
+    }
+    u64 acc = 0;
+#pragma unroll
+    for (int j = 0; j < K; j++) acc += s[j].k ^ s[j].v;
+    if (acc == 0x12345) out[0] = acc;
+}
+
+template <typename F>
+float time_it(F f, int reps) {
+    hipEvent_t a, b;
+    CHK(hipEventCreate(&a));
+    CHK(hipEventCreate(&b));
+    f();
+    CHK(hipDeviceSynchronize());
+    CHK(hipEventRecord(a));
+    for (int r = 0; r < reps; r++) f();
+    CHK(hipEventRecord(b));
+    CHK(hipEventSynchronize(b));
+    float ms;
+    CHK(hipEventElapsedTime(&ms, a, b));
+    return ms / reps;
+}
+
+int main(int argc, char** argv) {
+    const int log2 = argc > 1 ? atoi(argv[1]) : 26;
+    const u64 slots = 1ull << log2, mask = slots - 1;
+    const u64 n = argc > 2 ? strtoull(argv[2], 0, 10) : (1ull << 22);
+    const int reps = 20;
+    Slot* t;
+    u64* out;
+    CHK(hipMalloc(&t, slots * sizeof(Slot)));
+    CHK(hipMemset(t, 1, slots * sizeof(Slot)));
+    CHK(hipMalloc(&out, 64));
+    printf("table %llu slots (%.2f GiB), %llu lookups per launch\n", slots, slots * 16.0 / (1 << 30), n);
+    auto report = [&](const char* name, float ms, double useful_bytes) {
+        double s = ms / 1e3;
+        printf("%-8s %8.2f us  %8.2f Glookups/s  useful %7.1f GB/s  @64B %7.1f GB/s  @128B %7.1f GB/s\n", name,
+               ms * 1e3, n / s / 1e9, n * useful_bytes / s / 1e9, n * 64.0 / s / 1e9, n * 128.0 / s / 1e9);
+    };
+#define RUN16(K)                                                                                        \
+    {                                                                                                   \
+        u64 g = (n + 256 * K - 1) / (256 * K);                                                          \
+        float ms = time_it([&] { g16<K><<<(unsigned)g, 256>>>(t, mask, n, 77 + K, out); }, reps);      \
+        report("g16x" #K, ms, 16);                                                                      \
+    }
+#define RUN8(K)                                                                                         \
+    {                                                                                                   \
+        u64 g = (n + 256 * K - 1) / (256 * K);                                                          \
+        float ms = time_it([&] { g8<K><<<(unsigned)g, 256>>>((const u64*)t, mask, n, 99 + K, out); }, reps); \
+        report("g8x" #K, ms, 8);                                                                        \
+    }
+#define RUN64(K)                                                                                        \
+    {                                                                                                   \
+        u64 g = (n * 4 + 256 * K - 1) / (256 * K);                                                      \
+        float ms = time_it([&] { g64<K><<<(unsigned)g, 256>>>(t, mask, n, 55 + K, out); }, reps);      \
+        report("g64x" #K, ms, 64);                                                                      \
+    }
+    RUN16(1) RUN16(2) RUN16(4) RUN16(8)
+    RUN8(1) RUN8(4)
+    RUN64(1) RUN64(4)
+    CHK(hipFree(t));
+    return 0;
+}

@@ -521,6 +521,66 @@ int nrg_hashmap_round_async(nrg_ctx* c, const nrg_put* d_puts, uint64_t W, uint3
     return NRG_OK;
 }
 
+// replay [ltail, tail) and answer R reads against the final state, fused into the last chunk
+static int hm_exec_with_gets(nrg_ctx* c, uint64_t resp_lo, uint64_t resp_hi, uint64_t* d_prev, uint8_t* d_prevf,
+                             const uint64_t* d_get_keys, uint64_t R, uint64_t* d_get_vals, uint8_t* d_get_found) {
+    if (c->ltail == c->tail) return hip_fail(hm_get_only(c, d_get_keys, R, d_get_vals, d_get_found));
+    while (c->ltail < c->tail) {
+        uint64_t n = c->tail - c->ltail;
+        if (n > c->cfg.max_batch) n = c->cfg.max_batch;
+        const uint64_t lo = c->ltail;
+        const bool last = lo + n == c->tail;
+        HIPCHK(hm_replay_chunk(c, nullptr, lo, n, false, last ? d_get_keys : nullptr, last ? R : 0,
+                               last ? d_get_vals : nullptr, last ? d_get_found : nullptr, resp_lo, resp_hi, d_prev,
+                               d_prevf, true));
+        c->ltail = lo + n;
+    }
+    if (c->ctail < c->ltail) c->ctail = c->ltail;
+    return NRG_OK;
+}
+
+int nrg_hashmap_round_segments_async(nrg_ctx* c, const nrg_put* d_base, uint32_t nseg, uint64_t seg_stride,
+                                     const uint64_t* lens, const uint32_t* origins, uint32_t resp_seg,
+                                     const uint64_t* d_get_keys, uint64_t R, uint64_t* d_get_vals,
+                                     uint8_t* d_get_found, uint64_t* d_prev, uint8_t* d_prev_found) {
+    int r = need(c, NRG_DS_HASHMAP);
+    if (r) return r;
+    if (!lens || nseg == 0 || nseg > 64 || !d_base) return NRG_E_INVAL;
+    if (R && (!d_get_keys || !d_get_vals || !d_get_found)) return NRG_E_INVAL;
+    if (!d_prev || !d_prev_found) d_prev = nullptr, d_prev_found = nullptr;
+    uint64_t total = 0, own_off = 0;
+    bool dense = true;
+    for (uint32_t s = 0; s < nseg; s++) {
+        if (lens[s] > seg_stride) return NRG_E_INVAL;
+        if (s == resp_seg) own_off = total;
+        if (s + 1 < nseg && lens[s] != seg_stride) dense = false;
+        total += lens[s];
+    }
+    if ((r = exec_range(c, 0, 0, nullptr, nullptr))) return r;
+    if ((r = reserve(c, total))) return r;
+    const uint64_t lo = c->tail;
+    const uint64_t rlo = resp_seg < nseg ? lo + own_off : 0;
+    const uint64_t rhi = resp_seg < nseg ? rlo + lens[resp_seg] : 0;
+    if (dense && total <= c->cfg.max_batch) {
+        // the gathered segments are already the contiguous round W_0 || W_1 || ...: replay them
+        // in place while K1 writes the log copy (no separate append pass)
+        HIPCHK(hm_replay_chunk(c, d_base, lo, total, true, d_get_keys, R, d_get_vals, d_get_found, rlo, rhi, d_prev,
+                               d_prev_found, true));
+        for (uint32_t s = 0, off = 0; s < nseg; off += (uint32_t)lens[s], s++)
+            if (lens[s]) note_origin(c, lo + off, lens[s], origins ? origins[s] : s + 1);
+        c->tail = lo + total;
+        c->ltail = c->tail;
+        if (c->ctail < c->tail) c->ctail = c->tail;
+        return NRG_OK;
+    }
+    HIPCHK(copy_segments(c, d_base, nseg, seg_stride, lens, lo));
+    for (uint32_t s = 0; s < nseg; s++) {
+        if (lens[s]) note_origin(c, c->tail, lens[s], origins ? origins[s] : s + 1);
+        c->tail += lens[s];
+    }
+    return hm_exec_with_gets(c, rlo, rhi, d_prev, d_prev_found, d_get_keys, R, d_get_vals, d_get_found);
+}
+
 int nrg_hashmap_prefill(nrg_ctx* c, const uint64_t* keys, const uint64_t* vals, uint64_t n) {
     int r = need(c, NRG_DS_HASHMAP);
     if (r) return r;

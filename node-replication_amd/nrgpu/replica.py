@@ -155,6 +155,15 @@ class DeviceReplica:
                                                   _dptr(d_get_vals), _dptr(d_get_found), _dptr(d_prev),
                                                   _dptr(d_prev_found)), "round")
 
+    def hm_round_segments_device(self, d_base, seg_stride, lens, origins, resp_seg, d_get_keys, R, d_get_vals,
+                                 d_get_found, d_prev=None, d_prev_found=None):
+        nseg = len(lens)
+        la = (C.c_uint64 * nseg)(*lens)
+        oa = (C.c_uint32 * nseg)(*origins)
+        L.check(self._lib.nrg_hashmap_round_segments_async(
+            self._h, _dptr(d_base), nseg, seg_stride, la, oa, resp_seg, _dptr(d_get_keys), R, _dptr(d_get_vals),
+            _dptr(d_get_found), _dptr(d_prev), _dptr(d_prev_found)), "round_segments")
+
     def hm_prefill(self, keys: np.ndarray, vals: np.ndarray):
         keys = np.ascontiguousarray(keys, np.uint64)
         vals = np.ascontiguousarray(vals, np.uint64)
