@@ -82,6 +82,42 @@ __global__ __launch_bounds__(256) void g64(const Slot* __restrict__ t, u64 mask,
     if (acc == 0x12345) out[0] = acc;
 }
 
+// 32-B slots: key+val (16 B) and stamp (8 B) of one slot, two loads from one 128-B line
+struct __attribute__((aligned(32))) Slot32 {
+    u64 k, v, st, pad;
+};
+__global__ __launch_bounds__(256) void g32(const Slot32* __restrict__ t, u64 mask, u64 n, u64 seed, u64* out) {
+    const u64 i = blockIdx.x * 256ull + threadIdx.x;
+    if (i >= n) return;
+    const Slot32* p = &t[mix64(seed + i) & mask];
+    const u64 k = p->k, v = p->v, st = p->st;
+    if ((k ^ v ^ st) == 0x12345) out[0] = k;
+}
+
+// scattered device-scope atomics / plain stores over a small (L2/MALL-sized) array
+__global__ __launch_bounds__(256) void a_cas(u64* a, u64 mask, u64 n, u64 seed, u64* out) {
+    const u64 i = blockIdx.x * 256ull + threadIdx.x;
+    if (i >= n) return;
+    const u64 h = mix64(seed + i);
+    const u64 old = atomicCAS(&a[h & mask], 0ull, h | 1);
+    if (old == 0x12345) out[0] = old;
+}
+__global__ __launch_bounds__(256) void a_max(unsigned* a, u64 mask, u64 n, u64 seed) {
+    const u64 i = blockIdx.x * 256ull + threadIdx.x;
+    if (i >= n) return;
+    atomicMax(&a[mix64(seed + i) & mask], (unsigned)i);
+}
+__global__ __launch_bounds__(256) void s_byte(unsigned char* a, u64 mask, u64 n, u64 seed) {
+    const u64 i = blockIdx.x * 256ull + threadIdx.x;
+    if (i >= n) return;
+    a[mix64(seed + i) & mask] = 1;
+}
+__global__ __launch_bounds__(256) void s_16(Slot* a, u64 mask, u64 n, u64 seed) {
+    const u64 i = blockIdx.x * 256ull + threadIdx.x;
+    if (i >= n) return;
+    a[mix64(seed + i) & mask] = Slot{i, i};
+}
+
 template <typename F>
 float time_it(F f, int reps) {
     hipEvent_t a, b;
@@ -135,6 +171,27 @@ int main(int argc, char** argv) {
     RUN16(1) RUN16(2) RUN16(4) RUN16(8)
     RUN8(1) RUN8(4)
     RUN64(1) RUN64(4)
+    {  // 32-B slots over the same bytes (half as many slots)
+        const unsigned g = (unsigned)((n + 255) / 256);
+        float ms = time_it([&] { g32<<<g, 256>>>((const Slot32*)t, mask >> 1, n, 31, out); }, reps);
+        report("g32x1", ms, 24);
+    }
+    // scattered atomics / stores: 100k and 1M ops over a 4 MiB array (the BLT's size at B1)
+    for (u64 m : {100000ull, 1000000ull}) {
+        const u64 amask = (4ull << 20) / 8 - 1;
+        const unsigned g = (unsigned)((m + 255) / 256);
+        float ms;
+        ms = time_it([&] { CHK(hipMemsetAsync(t, 0, 4 << 20)); a_cas<<<g, 256>>>((u64*)t, amask, m, 5, out); }, reps);
+        printf("cas64   n=%7llu  %8.2f us (incl. 4 MiB memset)  %6.2f Gops/s\n", m, ms * 1e3, m / (ms / 1e3) / 1e9);
+        ms = time_it([&] { a_max<<<g, 256>>>((unsigned*)t, amask * 2 + 1, m, 6); }, reps);
+        printf("max32   n=%7llu  %8.2f us  %6.2f Gops/s\n", m, ms * 1e3, m / (ms / 1e3) / 1e9);
+        ms = time_it([&] { s_byte<<<g, 256>>>((unsigned char*)t, (1ull << 20) - 1, m, 7); }, reps);
+        printf("byte1MB n=%7llu  %8.2f us  %6.2f Gops/s\n", m, ms * 1e3, m / (ms / 1e3) / 1e9);
+        ms = time_it([&] { s_16<<<g, 256>>>(t, (4ull << 20) / 16 - 1, m, 8); }, reps);
+        printf("st16    n=%7llu  %8.2f us  %6.2f Gops/s\n", m, ms * 1e3, m / (ms / 1e3) / 1e9);
+        ms = time_it([&] { CHK(hipMemsetAsync(t, 0, 4 << 20)); }, reps);
+        printf("memset 4MiB        %8.2f us\n", ms * 1e3);
+    }
     CHK(hipFree(t));
     return 0;
 }

@@ -43,26 +43,20 @@ struct DevCtl {
     u64 nkeys;           // hashmap: number of keys (including the side-slot key)
     u64 sp_present;      // side slot for key == EMPTY_KEY
     u64 sp_val;
-    u64 sp_old_present;  // side slot before the current round (previous-value responses)
-    u64 sp_old_val;
-    u32 sp_last[2];      // per round parity: 1 + last log offset of a Put to EMPTY_KEY
+    u64 sp_stamp;        // epoch << 32 | 1 + round offset of the last Put to EMPTY_KEY
     long long depth;     // stack: current length
     u64 counter;         // scratch counter (dump compaction)
-    u64 pad1[6];
+    u64 pad1[8];
 };
 
-// 16-byte table slot {key, value}: one dwordx4 load fetches both (AoS keeps Get at one
-// random 64-B sector).
-struct __attribute__((aligned(16))) Slot {
-    u64 key;
+// 32-byte table slot; a random 16-B read costs a whole 128-B line on MI355X anyway, so the
+// last-writer stamp and creation epoch ride in the same line as key and value.
+struct __attribute__((aligned(32))) Slot {
+    u64 key;      // EMPTY_KEY when free
     u64 val;
-};
-
-// Batch-local table entry: one per distinct key written in a round.
-struct __attribute__((aligned(16))) BltEntry {
-    u64 key;   // EMPTY_KEY when free
-    u32 last;  // 1 + log offset (within the round) of the last Put to key  (last-writer-wins)
-    u32 info;  // main-table slot of key before the round, or NEW_SLOT
+    u64 stamp;    // epoch << 32 | 1 + offset of the round's last Put to key (atomicMax)
+    u32 created;  // epoch of the round that inserted key
+    u32 pad;
 };
 
 __device__ __forceinline__ u64 ld_relaxed(const u64* p) {

@@ -4,28 +4,32 @@
 // benches/hashmap.rs:114-119, nr/examples/hashmap.rs:46-50) and the read path
 // Replica::read_only -> dispatch (nr/src/replica.rs:483-497, benches/hashmap.rs:107-111).
 //
-// A replay "round" covers the log records [lo, lo+n) (one combined batch, or one chunk of
-// a longer exec range) followed by a batch of R reads answered against the post-round state
-// (the reads' sync-to-ctail contract: every write appended before the read is visible).
+// Table: 2^k open-addressing slots of 32 B {key, val, stamp, created}; four slots per 128-B
+// line, the HBM access granule for random reads on MI355X (microbench/random_gather.hip,
+// profiles/r01_random_gather_fetch_size.txt). A replay "round" covers the log records
+// [lo, lo+n) with a fresh epoch e (one per round, never reused):
 //
-//   K1 hm_index     one thread per Put: claim the key's entry in a batch-local table (BLT,
-//                   ~2n entries, L2/MALL resident) with a 64-bit CAS; atomicMax(last, i+1)
-//                   selects the last writer in log order (= HashMap::insert sequence
-//                   semantics for the final value); the entry's owner probes the main table
-//                   once (read-only) and records the key's slot and pre-round value.
-//                   Also clears the previous round's BLT entries (double-buffered BLT).
-//   K2 hm_apply_get one launch, two roles: Put threads whose i+1 == last write the final
-//                   value (update in place, or a CAS insert for new keys); Get threads
-//                   probe BLT and main table concurrently (two independent loads in flight)
-//                   and answer from the round's last writer when the key was written.
-//   prev path       (only when previous-value responses are requested): stable radix sort
-//                   of (BLT entry, i) pairs → each Put's previous value is its in-group
-//                   predecessor's value, or the pre-round value captured by K1.
+//   K1 hm_index     one thread per Put (4 per thread): probe the key's slot (read-only), or
+//                   claim an empty one with a 64-bit CAS (new key, created = e); the last
+//                   writer in log order is elected by atomicMax(slot.stamp, e<<32 | i+1),
+//                   pre-combined per block in LDS so a hot key costs one global atomic per
+//                   block (Zipf streams). Writes the log copy when the round is appended here.
+//   prev path       only when previous-value responses are requested: stable radix sort of
+//                   (slot, i) -> a Put's previous value is its in-group predecessor's value,
+//                   or the slot's pre-round value (absent if created == e). Runs before K2.
+//   K2 hm_apply_get one launch, two roles: Put threads whose stamp is (e, i+1) store the
+//                   final value; Get threads probe the table once and read the value from
+//                   the round's log record when the slot's stamp carries epoch e.
+// The result equals the sequential replay: last-writer-wins per key in log order, reads
+// after the round's writes (SURVEY.md §8a round semantics).
 #include "internal.hpp"
 
 namespace nrg {
 
 constexpr int TPB = 256;
+constexpr int K1_ITEMS = 4;              // puts per thread in K1
+constexpr int K1_TILE = TPB * K1_ITEMS;  // puts per block
+constexpr int K1_LDS = 2 * K1_TILE;      // LDS combining table entries (power of two)
 
 // record i of the round: from the caller's segment when given (fused append), else the ring
 __device__ __forceinline__ nrg_put rec_at(const nrg_put* __restrict__ src, const nrg_put* ring, u64 ring_mask,
@@ -33,128 +37,143 @@ __device__ __forceinline__ nrg_put rec_at(const nrg_put* __restrict__ src, const
     return src ? src[i] : ring[(lo + i) & ring_mask];
 }
 
-__device__ __forceinline__ bool table_probe(const Slot* __restrict__ table, u64 k, u32 shift, u64 tmask,
-                                            u64* slot, u64* val) {
-    u64 s = table_home(k, shift);
-    for (u64 pr = 0; pr <= tmask; pr++) {
-        const Slot sl = table[s];
-        if (sl.key == k) {
-            *slot = s;
-            *val = sl.val;
-            return true;
-        }
-        if (sl.key == EMPTY_KEY) return false;
-        s = (s + 1) & tmask;
-    }
-    return false;
+__device__ __forceinline__ u64 stamp_of(u32 epoch, u64 i) { return ((u64)epoch << 32) | (i + 1); }
+
+// Load a whole slot with two 16-B loads issued together. The empty asm pins both values at
+// this point: otherwise hipcc sinks the {val, stamp} load below the key compare of the probe
+// loop, turning every Get into two dependent accesses to its line.
+__device__ __forceinline__ Slot load_slot(const Slot* p) {
+    typedef u64 u64x2 __attribute__((ext_vector_type(2)));
+    const u64x2 a = *(const u64x2*)p;
+    const u64x2 b = *((const u64x2*)p + 1);
+    u64 k = a.x, v = a.y, st = b.x;
+    asm volatile("" : "+v"(k), "+v"(v), "+v"(st));
+    Slot s;
+    s.key = k;
+    s.val = v;
+    s.stamp = st;
+    s.created = (u32)b.y;
+    s.pad = 0;
+    return s;
 }
 
-// insert a key known to be absent (or overwrite if present); returns true if newly inserted
-__device__ __forceinline__ int table_insert(Slot* table, u64 k, u64 v, u32 shift, u64 tmask) {
-    u64 s = table_home(k, shift);
+// Read-only probe from slot s whose contents `sl` the caller already loaded: slot or -1.
+__device__ __forceinline__ long long probe_from(const Slot* __restrict__ table, u64 k, u64 s, u64 tmask, Slot sl,
+                                                Slot* out) {
     for (u64 pr = 0; pr <= tmask; pr++) {
-        const u64 old = atomicCAS(&table[s].key, EMPTY_KEY, k);
-        if (old == EMPTY_KEY) {
-            table[s].val = v;
-            return 1;
+        if (sl.key == k) {
+            *out = sl;
+            return (long long)s;
         }
-        if (old == k) {
-            table[s].val = v;
-            return 0;
+        if (sl.key == EMPTY_KEY) return -1;
+        s = (s + 1) & tmask;
+        sl = load_slot(&table[s]);
+    }
+    return -2;
+}
+
+// find-or-claim k from slot s (its key already loaded as key0); returns slot or -1 if full
+__device__ __forceinline__ long long find_or_claim(Slot* table, u64 k, u64 s, u64 tmask, u64 key0, u32 epoch,
+                                                   u32* created) {
+    u64 key = key0;
+    for (u64 pr = 0; pr <= tmask; pr++) {
+        if (key == k) return (long long)s;
+        if (key == EMPTY_KEY) {
+            const u64 old = atomicCAS(&table[s].key, EMPTY_KEY, k);
+            if (old == EMPTY_KEY) {
+                table[s].created = epoch;
+                *created += 1;
+                return (long long)s;
+            }
+            if (old == k) return (long long)s;
         }
         s = (s + 1) & tmask;
+        key = ld_relaxed(&table[s].key);
     }
     return -1;
 }
 
-__global__ __launch_bounds__(TPB) void hm_index_kernel(
-    const nrg_put* __restrict__ src, nrg_put* ring, u64 ring_mask, u64 lo, u64 n, int write_ring,
-    BltEntry* blt, u64* __restrict__ blt_old, u64 bmask, u32* __restrict__ bslot,
-    const Slot* __restrict__ table, u32 shift, u64 tmask, BltEntry* blt_prev, const u32* __restrict__ bslot_prev,
-    u64 n_prev, DevCtl* ctl, u32 par, u32 special) {
-    const u64 gid = blockIdx.x * (u64)TPB + threadIdx.x;
-    const u64 stride = (u64)gridDim.x * TPB;
-    if (gid == 0) {
-        ctl->sp_last[par ^ 1u] = 0;
-        ctl->sp_old_present = ctl->sp_present;
-        ctl->sp_old_val = ctl->sp_val;
+__global__ __launch_bounds__(TPB) void hm_index_kernel(const nrg_put* __restrict__ src, nrg_put* ring, u64 ring_mask,
+                                                       u64 lo, u64 n, int write_ring, Slot* table, u32 shift,
+                                                       u64 tmask, u32* __restrict__ put_slot, DevCtl* ctl, u32 epoch) {
+    __shared__ u32 s_slot[K1_LDS];
+    __shared__ u32 s_max[K1_LDS];
+    for (int q = threadIdx.x; q < K1_LDS; q += TPB) {
+        s_slot[q] = 0xFFFFFFFFu;
+        s_max[q] = 0;
     }
-    for (u64 j = gid; j < n_prev; j += stride) {
-        const u32 b = bslot_prev[j];
-        if (b != special) {
-            BltEntry z;
-            z.key = EMPTY_KEY;
-            z.last = 0;
-            z.info = 0;
-            blt_prev[b] = z;
-        }
+    __syncthreads();
+    const u64 base = (u64)blockIdx.x * K1_TILE;
+    u32 created = 0;
+    u64 sl_idx[K1_ITEMS];
+    u64 key0[K1_ITEMS];
+    nrg_put rec[K1_ITEMS];
+    // issue every record load and every first probe before waiting on any of them
+#pragma unroll
+    for (int j = 0; j < K1_ITEMS; j++) {
+        const u64 i = base + (u64)j * TPB + threadIdx.x;
+        rec[j] = i < n ? rec_at(src, ring, ring_mask, lo, i) : nrg_put{EMPTY_KEY, 0};
     }
-    for (u64 i = gid; i < n; i += stride) {
-        const nrg_put rec = rec_at(src, ring, ring_mask, lo, i);
-        if (write_ring) ring[(lo + i) & ring_mask] = rec;
-        const u64 k = rec.key;
-        if (k == EMPTY_KEY) {
-            atomicMax(&ctl->sp_last[par], (u32)(i + 1));
-            bslot[i] = special;
+#pragma unroll
+    for (int j = 0; j < K1_ITEMS; j++) {
+        const u64 i = base + (u64)j * TPB + threadIdx.x;
+        if (i < n && write_ring) ring[(lo + i) & ring_mask] = rec[j];
+        sl_idx[j] = table_home(rec[j].key, shift);
+        key0[j] = rec[j].key != EMPTY_KEY ? table[sl_idx[j]].key : EMPTY_KEY;
+    }
+#pragma unroll
+    for (int j = 0; j < K1_ITEMS; j++) {
+        const u64 i = base + (u64)j * TPB + threadIdx.x;
+        if (i >= n) continue;
+        const u64 k = rec[j].key;
+        if (k == EMPTY_KEY) {  // the side-slot key
+            atomicMax(&ctl->sp_stamp, stamp_of(epoch, i));
+            put_slot[i] = 0xFFFFFFFFu;
             continue;
         }
-        u64 b = blt_home(k) & bmask;
-        bool owner = false;
-        for (u64 probes = 0;; probes++) {
-            const u64 cur = ld_relaxed(&blt[b].key);
-            if (cur == k) break;
-            if (cur == EMPTY_KEY) {
-                const u64 old = atomicCAS(&blt[b].key, EMPTY_KEY, k);
-                if (old == EMPTY_KEY) {
-                    owner = true;
-                    break;
-                }
-                if (old == k) break;
-            }
-            b = (b + 1) & bmask;
-            if (probes > bmask) {
-                atomicOr(&ctl->err, ERR_BLT_FULL);
-                break;
-            }
+        const long long s = find_or_claim(table, k, sl_idx[j], tmask, key0[j], epoch, &created);
+        if (s < 0) {
+            atomicOr(&ctl->err, ERR_TABLE_FULL);
+            put_slot[i] = 0xFFFFFFFEu;
+            continue;
         }
-        atomicMax(&blt[b].last, (u32)(i + 1));
-        bslot[i] = (u32)b;
-        if (owner) {
-            u64 s = 0, v = 0;
-            const bool f = table_probe(table, k, shift, tmask, &s, &v);
-            blt[b].info = f ? (u32)s : NEW_SLOT;
-            blt_old[b] = f ? v : 0;
+        put_slot[i] = (u32)s;
+        // combine in LDS: max (i+1) per slot within the block
+        u32 h = (u32)(mix64((u64)s) & (K1_LDS - 1));
+        for (;;) {
+            const u32 old = atomicCAS(&s_slot[h], 0xFFFFFFFFu, (u32)s);
+            if (old == 0xFFFFFFFFu || old == (u32)s) break;
+            h = (h + 1) & (K1_LDS - 1);
         }
+        atomicMax(&s_max[h], (u32)(i + 1));
+    }
+    if (created) atomicAdd(&ctl->nkeys, (u64)created);
+    __syncthreads();
+    for (int q = threadIdx.x; q < K1_LDS; q += TPB) {
+        const u32 s = s_slot[q];
+        if (s != 0xFFFFFFFFu) atomicMax(&table[s].stamp, ((u64)epoch << 32) | s_max[q]);
     }
 }
 
 __global__ __launch_bounds__(TPB) void hm_apply_get_kernel(
     const nrg_put* __restrict__ src, const nrg_put* __restrict__ ring, u64 ring_mask, u64 lo, u64 n, u32 put_blocks,
-    const BltEntry* __restrict__ blt, u64 bmask, const u32* __restrict__ bslot, Slot* table, u32 shift,
-    u64 tmask, DevCtl* ctl, u32 par, u32 special, const u64* __restrict__ gkeys, u64 R,
-    u64* __restrict__ gvals, uint8_t* __restrict__ gfound, int use_blt) {
+    const u32* __restrict__ put_slot, Slot* table, u32 shift, u64 tmask, DevCtl* ctl, u32 epoch,
+    const u64* __restrict__ gkeys, u64 R, u64* __restrict__ gvals, uint8_t* __restrict__ gfound, int round_live) {
     if (blockIdx.x < put_blocks) {
         u32 inserted = 0;
         for (u64 i = blockIdx.x * (u64)TPB + threadIdx.x; i < n; i += (u64)put_blocks * TPB) {
-            const u32 b = bslot[i];
-            if (b == special) {
-                if (ctl->sp_last[par] == (u32)(i + 1)) {
+            const u32 s = put_slot[i];
+            const u64 want = stamp_of(epoch, i);
+            if (s == 0xFFFFFFFFu) {  // side-slot key
+                if (ctl->sp_stamp == want) {
                     if (!ctl->sp_present) inserted++;
                     ctl->sp_val = rec_at(src, ring, ring_mask, lo, i).val;
                     ctl->sp_present = 1;
                 }
                 continue;
             }
-            const BltEntry e = blt[b];
-            if (e.last != (u32)(i + 1)) continue;
-            const nrg_put rec = rec_at(src, ring, ring_mask, lo, i);
-            if (e.info != NEW_SLOT) {
-                table[e.info].val = rec.val;
-            } else {
-                const int r = table_insert(table, rec.key, rec.val, shift, tmask);
-                if (r < 0) atomicOr(&ctl->err, ERR_TABLE_FULL);
-                if (r > 0) inserted++;
-            }
+            if (s == 0xFFFFFFFEu) continue;  // table full (reported)
+            if (table[s].stamp == want) table[s].val = rec_at(src, ring, ring_mask, lo, i).val;
         }
         if (inserted) atomicAdd(&ctl->nkeys, (u64)inserted);
         return;
@@ -165,43 +184,23 @@ __global__ __launch_bounds__(TPB) void hm_apply_get_kernel(
     u64 v = 0;
     uint8_t f = 0;
     if (k == EMPTY_KEY) {
-        const u32 last = use_blt ? ctl->sp_last[par] : 0u;
-        if (last) {
-            v = rec_at(src, ring, ring_mask, lo, last - 1).val;
+        const u64 st = ctl->sp_stamp;
+        if (round_live && (u32)(st >> 32) == epoch) {
+            v = rec_at(src, ring, ring_mask, lo, (u32)st - 1).val;
             f = 1;
         } else if (ctl->sp_present) {
             v = ctl->sp_val;
             f = 1;
         }
     } else {
-        u64 s = table_home(k, shift);
-        Slot sl = table[s];
-        bool done = false;
-        if (use_blt) {
-            u64 b = blt_home(k) & bmask;
-            BltEntry e = blt[b];
-            while (e.key != EMPTY_KEY) {
-                if (e.key == k) {
-                    v = rec_at(src, ring, ring_mask, lo, e.last - 1).val;
-                    f = 1;
-                    done = true;
-                    break;
-                }
-                b = (b + 1) & bmask;
-                e = blt[b];
-            }
-        }
-        if (!done) {
-            for (u64 pr = 0; pr <= tmask; pr++) {
-                if (sl.key == k) {
-                    v = sl.val;
-                    f = 1;
-                    break;
-                }
-                if (sl.key == EMPTY_KEY) break;
-                s = (s + 1) & tmask;
-                sl = table[s];
-            }
+        const u64 s0 = table_home(k, shift);
+        Slot sl;
+        const long long s = probe_from(table, k, s0, tmask, load_slot(&table[s0]), &sl);
+        if (s >= 0) {
+            f = 1;
+            v = (round_live && (u32)(sl.stamp >> 32) == epoch)
+                    ? rec_at(src, ring, ring_mask, lo, (u32)sl.stamp - 1).val
+                    : sl.val;
         }
     }
     gvals[j] = v;
@@ -209,39 +208,60 @@ __global__ __launch_bounds__(TPB) void hm_apply_get_kernel(
 }
 
 __global__ __launch_bounds__(TPB) void hm_prev_kernel(const u32* __restrict__ sk, const u32* __restrict__ sv, u64 n,
-                                                      const nrg_put* __restrict__ src, const nrg_put* __restrict__ ring, u64 ring_mask, u64 lo,
-                                                      const BltEntry* __restrict__ blt,
-                                                      const u64* __restrict__ blt_old, const DevCtl* ctl,
-                                                      u32 special, u64 resp_lo, u64 resp_hi,
+                                                      const nrg_put* __restrict__ src, const nrg_put* __restrict__ ring,
+                                                      u64 ring_mask, u64 lo, const Slot* __restrict__ table,
+                                                      const DevCtl* ctl, u32 epoch, u64 resp_lo, u64 resp_hi,
                                                       u64* __restrict__ prev, uint8_t* __restrict__ prevf) {
     const u64 p = blockIdx.x * (u64)TPB + threadIdx.x;
     if (p >= n) return;
-    const u32 b = sk[p];
+    const u32 s = sk[p];
     const u64 gidx = lo + sv[p];
     if (gidx < resp_lo || gidx >= resp_hi) return;
     u64 v = 0;
     uint8_t f = 0;
-    if (p > 0 && sk[p - 1] == b) {
+    const bool has_pred = p > 0 && sk[p - 1] == s;
+    if (has_pred) {
         v = rec_at(src, ring, ring_mask, lo, sv[p - 1]).val;
         f = 1;
-    } else if (b == special) {
-        f = (uint8_t)(ctl->sp_old_present != 0);
-        v = f ? ctl->sp_old_val : 0;
-    } else if (blt[b].info != NEW_SLOT) {
-        v = blt_old[b];
+    } else if (s == 0xFFFFFFFFu) {  // side slot, before K2 of this round: pre-round state
+        f = (uint8_t)(ctl->sp_present != 0);
+        v = f ? ctl->sp_val : 0;
+    } else if (s != 0xFFFFFFFEu && table[s].created != epoch) {  // existed before; K2 not run yet
+        v = table[s].val;
         f = 1;
     }
     prev[gidx - resp_lo] = v;
     prevf[gidx - resp_lo] = f;
 }
 
+__global__ __launch_bounds__(TPB) void hm_init_table_kernel(Slot* table, u64 slots) {
+    for (u64 s = blockIdx.x * (u64)TPB + threadIdx.x; s < slots; s += (u64)gridDim.x * TPB) {
+        Slot z;
+        z.key = EMPTY_KEY;
+        z.val = 0;
+        z.stamp = 0;
+        z.created = 0;
+        z.pad = 0;
+        table[s] = z;
+    }
+}
+
 __global__ __launch_bounds__(TPB) void hm_prefill_range_kernel(Slot* table, u64 n, u64 off, u32 shift, u64 tmask,
                                                                DevCtl* ctl) {
     u32 inserted = 0;
     for (u64 k = blockIdx.x * (u64)TPB + threadIdx.x; k < n; k += (u64)gridDim.x * TPB) {
-        const int r = table_insert(table, k, k + off, shift, tmask);
-        if (r < 0) atomicOr(&ctl->err, ERR_TABLE_FULL);
-        if (r > 0) inserted++;
+        u64 s = table_home(k, shift);
+        bool done = false;
+        for (u64 pr = 0; pr <= tmask && !done; pr++) {
+            const u64 old = atomicCAS(&table[s].key, EMPTY_KEY, k);
+            if (old == EMPTY_KEY || old == k) {
+                table[s].val = k + off;
+                inserted += old == EMPTY_KEY;
+                done = true;
+            }
+            s = (s + 1) & tmask;
+        }
+        if (!done) atomicOr(&ctl->err, ERR_TABLE_FULL);
     }
     if (inserted) atomicAdd(&ctl->nkeys, (u64)inserted);
 }
@@ -255,11 +275,11 @@ __global__ __launch_bounds__(TPB) void hm_dump_kernel(const Slot* __restrict__ t
         ov[i] = ctl->sp_val;
     }
     for (u64 s = gid; s < slots; s += (u64)gridDim.x * TPB) {
-        const Slot sl = table[s];
-        if (sl.key != EMPTY_KEY) {
+        const u64 k = table[s].key;
+        if (k != EMPTY_KEY) {
             const u64 i = atomicAdd(&ctl->counter, 1ull);
-            ok[i] = sl.key;
-            ov[i] = sl.val;
+            ok[i] = k;
+            ov[i] = table[s].val;
         }
     }
 }
@@ -276,9 +296,9 @@ __global__ __launch_bounds__(TPB) void hm_digest_kernel(const Slot* __restrict__
         x ^= h;
     }
     for (u64 s = gid; s < slots; s += (u64)gridDim.x * TPB) {
-        const Slot sl = table[s];
-        if (sl.key != EMPTY_KEY) {
-            const u64 h = mix64(sl.key ^ mix64(sl.val));
+        const u64 k = table[s].key;
+        if (k != EMPTY_KEY) {
+            const u64 h = mix64(k ^ mix64(table[s].val));
             c++;
             sm += h;
             x ^= h;
@@ -335,9 +355,9 @@ __global__ __launch_bounds__(TPB) void copy_segments_kernel(const u64* __restric
         u32 s = 0;
         while (s + 1 < a.nseg && a.start[s + 1] <= r) s++;
         const u64 j = r - a.start[s];
-        const u64* src = base + s * seg_stride_words + j * a.words;
+        const u64* srcp = base + s * seg_stride_words + j * a.words;
         u64* dst = ring + ((dst_lo + r) & ring_mask) * a.words;
-        for (u32 q = 0; q < a.words; q++) dst[q] = src[q];
+        for (u32 q = 0; q < a.words; q++) dst[q] = srcp[q];
     }
 }
 
@@ -348,50 +368,47 @@ static inline unsigned grid_for(u64 n, u64 cap = 4096) {
     return (unsigned)g;
 }
 
+hipError_t hm_init(nrg_ctx* c) {
+    hm_init_table_kernel<<<grid_for(c->slots, 16384), TPB, 0, c->stream>>>(c->d_table, c->slots);
+    return hipGetLastError();
+}
+
 hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool write_ring,
                            const u64* d_get_keys, u64 R, u64* d_get_vals, uint8_t* d_get_found, u64 resp_lo,
                            u64 resp_hi, u64* d_prev, uint8_t* d_prev_found, bool touch_log) {
     hipStream_t st = c->stream;
     const u64 ring_mask = c->log_size - 1;
-    const u64 bmask = c->blt_size - 1;
-    const u32 special = (u32)c->blt_size;
     const u64 tmask = c->slots - 1;
     nrg_put* ring = (nrg_put*)c->d_ring;
-    const u32 par = c->parity;
+    const nrg_put* src = (const nrg_put*)src_recs;
     (void)touch_log;
+    const u32 epoch = n > 0 ? ++c->epoch : c->epoch;
     if (n > 0) {
-        const u64 work = n > c->prev_n ? n : c->prev_n;
         timer_begin(c, "hm_index");
-        hm_index_kernel<<<grid_for(work), TPB, 0, st>>>(
-            (const nrg_put*)src_recs, ring, ring_mask, lo, n, write_ring ? 1 : 0, c->d_blt[par], c->d_blt_old[par],
-            bmask, c->d_bslot[par], c->d_table, c->slot_shift, tmask, c->d_blt[par ^ 1], c->d_bslot[par ^ 1],
-            c->prev_n, c->d_ctl, par, special);
+        hm_index_kernel<<<(unsigned)((n + K1_TILE - 1) / K1_TILE), TPB, 0, st>>>(
+            src, ring, ring_mask, lo, n, write_ring ? 1 : 0, c->d_table, c->slot_shift, tmask, c->d_put_slot, c->d_ctl,
+            epoch);
         timer_end(c, "hm_index");
+        if (d_prev && resp_lo < lo + n && resp_hi > lo) {
+            u32 *sk = nullptr, *sv = nullptr;
+            timer_begin(c, "hm_prev");
+            // slot ids < 2^log2_slots; the side-slot key (0xFFFFFFFF) sorts last
+            hipError_t e = sort_pairs(c->sort, c->d_put_slot, nullptr, n, 32, st, &sk, &sv);
+            if (e != hipSuccess) return e;
+            hm_prev_kernel<<<(unsigned)((n + TPB - 1) / TPB), TPB, 0, st>>>(
+                sk, sv, n, src, ring, ring_mask, lo, c->d_table, c->d_ctl, epoch, resp_lo, resp_hi, d_prev,
+                d_prev_found);
+            timer_end(c, "hm_prev");
+        }
     }
     const u32 put_blocks = n ? grid_for(n, 1024) : 0;
     const u64 get_blocks = (R + TPB - 1) / TPB;
     if (put_blocks + get_blocks > 0) {
         timer_begin(c, "hm_apply_get");
         hm_apply_get_kernel<<<(unsigned)(put_blocks + get_blocks), TPB, 0, st>>>(
-            (const nrg_put*)src_recs, ring, ring_mask, lo, n, put_blocks, c->d_blt[par], bmask, c->d_bslot[par], c->d_table, c->slot_shift,
-            tmask, c->d_ctl, par, special, d_get_keys, R, d_get_vals, d_get_found, n > 0 ? 1 : 0);
+            src, ring, ring_mask, lo, n, put_blocks, c->d_put_slot, c->d_table, c->slot_shift, tmask, c->d_ctl, epoch,
+            d_get_keys, R, d_get_vals, d_get_found, n > 0 ? 1 : 0);
         timer_end(c, "hm_apply_get");
-    }
-    if (n > 0 && d_prev && resp_lo < lo + n && resp_hi > lo) {
-        u32 *sk = nullptr, *sv = nullptr;
-        int bits = 1;
-        while ((1ull << bits) <= c->blt_size) bits++;  // keys in [0, blt_size]
-        timer_begin(c, "hm_prev");
-        hipError_t e = sort_pairs(c->sort, c->d_bslot[par], nullptr, n, bits, st, &sk, &sv);
-        if (e != hipSuccess) return e;
-        hm_prev_kernel<<<(unsigned)((n + TPB - 1) / TPB), TPB, 0, st>>>(
-            sk, sv, n, (const nrg_put*)src_recs, ring, ring_mask, lo, c->d_blt[par], c->d_blt_old[par], c->d_ctl, special, resp_lo, resp_hi,
-            d_prev, d_prev_found);
-        timer_end(c, "hm_prev");
-    }
-    if (n > 0) {
-        c->prev_n = n;
-        c->parity ^= 1u;
     }
     return hipGetLastError();
 }

@@ -68,12 +68,8 @@ struct nrg_ctx {
     uint32_t slot_shift = 0;  // 64 - log2_slots
     uint64_t slots = 0;
     nrg::Slot* d_table = nullptr;
-    uint64_t blt_size = 0;
-    nrg::BltEntry* d_blt[2] = {nullptr, nullptr};
-    uint64_t* d_blt_old[2] = {nullptr, nullptr};
-    uint32_t* d_bslot[2] = {nullptr, nullptr};
-    uint64_t prev_n = 0;  // puts in the previous round (their BLT entries are cleared next round)
-    uint32_t parity = 0;
+    uint32_t* d_put_slot = nullptr;  // per Put of the round: its table slot
+    uint32_t epoch = 0;              // replay rounds so far (stamps carry the round's epoch)
 
     // ---- Stack ----
     uint32_t* d_stack = nullptr;
@@ -109,6 +105,7 @@ hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool
                            u64 resp_lo, u64 resp_hi, u64* d_prev, uint8_t* d_prev_found,
                            bool touch_log);
 hipError_t hm_get_only(nrg_ctx* c, const u64* d_keys, u64 n, u64* d_vals, uint8_t* d_found);
+hipError_t hm_init(nrg_ctx* c);
 hipError_t hm_prefill_range(nrg_ctx* c, u64 n, u64 off);
 hipError_t hm_dump(nrg_ctx* c, u64* d_keys, u64* d_vals);
 hipError_t hm_digest(nrg_ctx* c, u64* d_out3);

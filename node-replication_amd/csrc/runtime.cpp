@@ -276,20 +276,13 @@ int nrg_open(int dev, const nrg_config* cfg_in, nrg_ctx** out) {
 
     const uint64_t mb = cf.max_batch;
     if (cf.ds_kind == NRG_DS_HASHMAP) {
-        if (cf.log2_slots < 4 || cf.log2_slots > 32) { nrg_close(c); return NRG_E_INVAL; }
+        // slot ids are u32 with two reserved values: at most 2^31 slots (64 GiB)
+        if (cf.log2_slots < 4 || cf.log2_slots > 31) { nrg_close(c); return NRG_E_INVAL; }
         c->slots = 1ull << cf.log2_slots;
         c->slot_shift = 64 - cf.log2_slots;
         OPEN_CHK(hipMalloc(&c->d_table, c->slots * sizeof(Slot)));
-        OPEN_CHK(hipMemsetAsync(c->d_table, 0xFF, c->slots * sizeof(Slot), c->stream));
-        c->blt_size = pow2_at_least(2 * mb < 1024 ? 1024 : 2 * mb);
-        for (int p = 0; p < 2; p++) {
-            OPEN_CHK(hipMalloc(&c->d_blt[p], c->blt_size * sizeof(BltEntry)));
-            OPEN_CHK(hipMalloc(&c->d_blt_old[p], c->blt_size * sizeof(uint64_t)));
-            OPEN_CHK(hipMalloc(&c->d_bslot[p], mb * sizeof(uint32_t)));
-            // {key = EMPTY, last = 0, info = 0}: key words 0xFF.., last/info 0
-            OPEN_CHK(hipMemset2DAsync(c->d_blt[p], 16, 0xFF, 8, c->blt_size, c->stream));
-            OPEN_CHK(hipMemset2DAsync((char*)c->d_blt[p] + 8, 16, 0, 8, c->blt_size, c->stream));
-        }
+        OPEN_CHK(hm_init(c));
+        OPEN_CHK(hipMalloc(&c->d_put_slot, mb * sizeof(uint32_t)));
         if (sort_alloc(c->sort, mb) != NRG_OK) { nrg_close(c); return NRG_E_NOMEM; }
     } else if (cf.ds_kind == NRG_DS_STACK) {
         if (!cf.stack_capacity || cf.stack_capacity >= (1ull << 31)) { nrg_close(c); return NRG_E_INVAL; }
@@ -329,9 +322,8 @@ int nrg_close(nrg_ctx* c) {
     g_dev_set = c->device;
     if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
     if (c->stream && c->stream != c->own_stream) (void)hipStreamSynchronize(c->stream);
-    void* ptrs[] = {c->d_ring,   c->d_ctl,      c->d_table,    c->d_blt[0],  c->d_blt[1],    c->d_blt_old[0],
-                    c->d_blt_old[1], c->d_bslot[0], c->d_bslot[1], c->d_stack, c->d_words,   c->d_sort_aux,
-                    c->d_tmp_u64, c->d_scan_desc};
+    void* ptrs[] = {c->d_ring,  c->d_ctl,      c->d_table,   c->d_put_slot, c->d_stack,
+                    c->d_words, c->d_sort_aux, c->d_tmp_u64, c->d_scan_desc};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     sort_free(c->sort);
