@@ -98,7 +98,7 @@ typedef struct {
 /* ---- configuration ------------------------------------------------------------------ */
 typedef struct {
     uint32_t ds_kind;         /* NRG_DS_*                                                  */
-    uint32_t log2_slots;      /* hashmap: table has 2^log2_slots 16-B slots (default 26)    */
+    uint32_t log2_slots;      /* hashmap: table has 2^log2_slots 32-B slots (default 26)    */
     uint64_t log_bytes;       /* Log::new(bytes): ring entries = bytes/64 rounded as in the
                                  reference (min 2*GC_FROM_HEAD, power of two). 0 = 32 MiB   */
     uint64_t max_batch;       /* largest number of log records replayed per kernel pass;
@@ -110,6 +110,13 @@ typedef struct {
     uint32_t stack_push_resp; /* 0: Push -> None (benches/stack.rs:77-80, nr/examples/stack.rs:70-73)
                                  1: Push -> Some(v) (nr/tests/stack.rs:89-92)               */
     uint32_t replica_id;      /* this replica's id (Log::register, ids start at 1)         */
+    uint32_t pipeline;        /* hashmap, opt-in (default 0). 0: every output of an *_async call
+                                 is ordered on the context's stream. 1: the reads of an async
+                                 round run on an internal side stream, overlapping the next
+                                 round's index pass; their outputs (and their key buffer) are
+                                 ordered on the context's stream only after nrg_join(), the
+                                 next call that replays writes on this context, or nrg_sync(). Synchronous
+                                 calls are unaffected (their outputs are complete on return). */
 } nrg_config;
 
 /* Fill `cfg` with the defaults of the reference benches for `ds_kind`. */
@@ -130,6 +137,9 @@ void* nrg_get_stream(nrg_ctx* ctx);
 
 /* Replica::sync analogue: wait for all queued work; report latched device errors. */
 int nrg_sync(nrg_ctx* ctx);
+/* Order outstanding side-stream reads (config.pipeline = 1) on the context's stream without
+ * blocking the host; a no-op when nothing is outstanding. */
+int nrg_join(nrg_ctx* ctx);
 
 const char* nrg_strerror(int code);
 /* Library build identifier ("nrgpu <version> gfx950"). */
@@ -254,6 +264,8 @@ int nrg_gen_puts_async(nrg_ctx* ctx, nrg_put* d_out, const uint64_t* d_keys, con
  * kernel named `which` ("hm_apply_get", "hm_index", ...) and accumulates the elapsed time;
  * nrg_kernel_time reads (launches, total milliseconds) after synchronising. */
 int nrg_kernel_timing(nrg_ctx* ctx, int enable);
+/* Restrict timing to one kernel name (NULL or "" = all). */
+int nrg_kernel_timing_only(nrg_ctx* ctx, const char* which);
 int nrg_kernel_time(nrg_ctx* ctx, const char* which, uint64_t* launches, double* total_ms);
 
 #ifdef __cplusplus

@@ -27,9 +27,7 @@
 namespace nrg {
 
 constexpr int TPB = 256;
-constexpr int K1_ITEMS = 4;              // puts per thread in K1
-constexpr int K1_TILE = TPB * K1_ITEMS;  // puts per block
-constexpr int K1_LDS = 2 * K1_TILE;      // LDS combining table entries (power of two)
+// K1 geometry: ITEMS puts per thread, an LDS combining table of 2*TPB*ITEMS entries per block
 
 // record i of the round: from the caller's segment when given (fused append), else the ring
 __device__ __forceinline__ nrg_put rec_at(const nrg_put* __restrict__ src, const nrg_put* ring, u64 ring_mask,
@@ -93,9 +91,12 @@ __device__ __forceinline__ long long find_or_claim(Slot* table, u64 k, u64 s, u6
     return -1;
 }
 
+template <int K1_ITEMS>
 __global__ __launch_bounds__(TPB) void hm_index_kernel(const nrg_put* __restrict__ src, nrg_put* ring, u64 ring_mask,
                                                        u64 lo, u64 n, int write_ring, Slot* table, u32 shift,
                                                        u64 tmask, u32* __restrict__ put_slot, DevCtl* ctl, u32 epoch) {
+    constexpr int K1_TILE = TPB * K1_ITEMS;
+    constexpr int K1_LDS = 2 * K1_TILE;
     __shared__ u32 s_slot[K1_LDS];
     __shared__ u32 s_max[K1_LDS];
     for (int q = threadIdx.x; q < K1_LDS; q += TPB) {
@@ -155,56 +156,69 @@ __global__ __launch_bounds__(TPB) void hm_index_kernel(const nrg_put* __restrict
     }
 }
 
-__global__ __launch_bounds__(TPB) void hm_apply_get_kernel(
-    const nrg_put* __restrict__ src, const nrg_put* __restrict__ ring, u64 ring_mask, u64 lo, u64 n, u32 put_blocks,
-    const u32* __restrict__ put_slot, Slot* table, u32 shift, u64 tmask, DevCtl* ctl, u32 epoch,
-    const u64* __restrict__ gkeys, u64 R, u64* __restrict__ gvals, uint8_t* __restrict__ gfound, int round_live) {
-    if (blockIdx.x < put_blocks) {
-        u32 inserted = 0;
-        for (u64 i = blockIdx.x * (u64)TPB + threadIdx.x; i < n; i += (u64)put_blocks * TPB) {
-            const u32 s = put_slot[i];
-            const u64 want = stamp_of(epoch, i);
-            if (s == 0xFFFFFFFFu) {  // side-slot key
-                if (ctl->sp_stamp == want) {
-                    if (!ctl->sp_present) inserted++;
-                    ctl->sp_val = rec_at(src, ring, ring_mask, lo, i).val;
-                    ctl->sp_present = 1;
-                }
-                continue;
+// K2a: the round's last writer of each key (stamp == (e, i+1)) stores the final value.
+__global__ __launch_bounds__(TPB) void hm_apply_kernel(const nrg_put* __restrict__ src, const nrg_put* __restrict__ ring,
+                                                       u64 ring_mask, u64 lo, u64 n, const u32* __restrict__ put_slot,
+                                                       Slot* table, DevCtl* ctl, u32 epoch) {
+    u32 inserted = 0;
+    for (u64 i = blockIdx.x * (u64)TPB + threadIdx.x; i < n; i += (u64)gridDim.x * TPB) {
+        const u32 s = put_slot[i];
+        const u64 want = stamp_of(epoch, i);
+        if (s == 0xFFFFFFFFu) {  // side-slot key
+            if (ctl->sp_stamp == want) {
+                if (!ctl->sp_present) inserted++;
+                ctl->sp_val = rec_at(src, ring, ring_mask, lo, i).val;
+                ctl->sp_present = 1;
             }
-            if (s == 0xFFFFFFFEu) continue;  // table full (reported)
-            if (table[s].stamp == want) table[s].val = rec_at(src, ring, ring_mask, lo, i).val;
+            continue;
         }
-        if (inserted) atomicAdd(&ctl->nkeys, (u64)inserted);
-        return;
+        if (s == 0xFFFFFFFEu) continue;  // table full (reported)
+        if (table[s].stamp == want) table[s].val = rec_at(src, ring, ring_mask, lo, i).val;
     }
-    const u64 j = (u64)(blockIdx.x - put_blocks) * TPB + threadIdx.x;
-    if (j >= R) return;
-    const u64 k = gkeys[j];
-    u64 v = 0;
-    uint8_t f = 0;
-    if (k == EMPTY_KEY) {
-        const u64 st = ctl->sp_stamp;
-        if (round_live && (u32)(st >> 32) == epoch) {
-            v = rec_at(src, ring, ring_mask, lo, (u32)st - 1).val;
-            f = 1;
-        } else if (ctl->sp_present) {
-            v = ctl->sp_val;
-            f = 1;
-        }
-    } else {
-        const u64 s0 = table_home(k, shift);
-        Slot sl;
-        const long long s = probe_from(table, k, s0, tmask, load_slot(&table[s0]), &sl);
-        if (s >= 0) {
-            f = 1;
-            v = (round_live && (u32)(sl.stamp >> 32) == epoch)
-                    ? rec_at(src, ring, ring_mask, lo, (u32)sl.stamp - 1).val
-                    : sl.val;
-        }
+    if (inserted) atomicAdd(&ctl->nkeys, (u64)inserted);
+}
+
+// K2b: Gets against the state after round `epoch` (dispatch after sync-to-tail). A slot
+// counts only if 0 < created <= epoch: with rounds pipelined, the next round's hm_index may
+// already be claiming slots for its new keys (created is 0 until its claimer writes it, then
+// epoch+1), and those keys do not exist yet for these reads.
+template <int G>
+__global__ __launch_bounds__(TPB) void hm_get_kernel(const Slot* __restrict__ table, u32 shift, u64 tmask,
+                                                     const DevCtl* ctl, u32 epoch, const u64* __restrict__ gkeys, u64 R,
+                                                     u64* __restrict__ gvals, uint8_t* __restrict__ gfound) {
+    // G Gets per thread: all key loads, then all first-slot loads, are in flight together
+    const u64 jb = (u64)blockIdx.x * TPB * G + threadIdx.x;
+    u64 k[G];
+    Slot first[G];
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+        const u64 j = jb + (u64)g * TPB;
+        k[g] = j < R ? gkeys[j] : EMPTY_KEY;
     }
-    gvals[j] = v;
-    gfound[j] = f;
+#pragma unroll
+    for (int g = 0; g < G; g++) first[g] = load_slot(&table[table_home(k[g], shift)]);
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+        const u64 j = jb + (u64)g * TPB;
+        if (j >= R) break;
+        u64 v = 0;
+        uint8_t f = 0;
+        if (k[g] == EMPTY_KEY) {
+            if (ctl->sp_present) {
+                v = ctl->sp_val;
+                f = 1;
+            }
+        } else {
+            Slot sl;
+            const long long s = probe_from(table, k[g], table_home(k[g], shift), tmask, first[g], &sl);
+            if (s >= 0 && sl.created != 0 && sl.created <= epoch) {
+                f = 1;
+                v = sl.val;
+            }
+        }
+        gvals[j] = v;
+        gfound[j] = f;
+    }
 }
 
 __global__ __launch_bounds__(TPB) void hm_prev_kernel(const u32* __restrict__ sk, const u32* __restrict__ sv, u64 n,
@@ -247,7 +261,7 @@ __global__ __launch_bounds__(TPB) void hm_init_table_kernel(Slot* table, u64 slo
 }
 
 __global__ __launch_bounds__(TPB) void hm_prefill_range_kernel(Slot* table, u64 n, u64 off, u32 shift, u64 tmask,
-                                                               DevCtl* ctl) {
+                                                               DevCtl* ctl, u32 epoch) {
     u32 inserted = 0;
     for (u64 k = blockIdx.x * (u64)TPB + threadIdx.x; k < n; k += (u64)gridDim.x * TPB) {
         u64 s = table_home(k, shift);
@@ -256,6 +270,7 @@ __global__ __launch_bounds__(TPB) void hm_prefill_range_kernel(Slot* table, u64 
             const u64 old = atomicCAS(&table[s].key, EMPTY_KEY, k);
             if (old == EMPTY_KEY || old == k) {
                 table[s].val = k + off;
+                if (old == EMPTY_KEY) table[s].created = epoch;
                 inserted += old == EMPTY_KEY;
                 done = true;
             }
@@ -384,33 +399,75 @@ hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool
     (void)touch_log;
     const u32 epoch = n > 0 ? ++c->epoch : c->epoch;
     if (n > 0) {
-        timer_begin(c, "hm_index");
-        hm_index_kernel<<<(unsigned)((n + K1_TILE - 1) / K1_TILE), TPB, 0, st>>>(
-            src, ring, ring_mask, lo, n, write_ring ? 1 : 0, c->d_table, c->slot_shift, tmask, c->d_put_slot, c->d_ctl,
-            epoch);
-        timer_end(c, "hm_index");
+        timer_begin(c, "hm_index", st);
+#define NRG_K1(IT)                                                                                            \
+    hm_index_kernel<IT><<<(unsigned)((n + TPB * IT - 1) / (TPB * IT)), TPB, 0, st>>>(                           \
+        src, ring, ring_mask, lo, n, write_ring ? 1 : 0, c->d_table, c->slot_shift, tmask, c->d_put_slot, c->d_ctl, \
+        epoch)
+        if (c->k1_items >= 4)
+            NRG_K1(4);
+        else if (c->k1_items == 2)
+            NRG_K1(2);
+        else
+            NRG_K1(1);
+#undef NRG_K1
+        timer_end(c, "hm_index", st);
         if (d_prev && resp_lo < lo + n && resp_hi > lo) {
             u32 *sk = nullptr, *sv = nullptr;
-            timer_begin(c, "hm_prev");
+            timer_begin(c, "hm_prev", st);
             // slot ids < 2^log2_slots; the side-slot key (0xFFFFFFFF) sorts last
             hipError_t e = sort_pairs(c->sort, c->d_put_slot, nullptr, n, 32, st, &sk, &sv);
             if (e != hipSuccess) return e;
             hm_prev_kernel<<<(unsigned)((n + TPB - 1) / TPB), TPB, 0, st>>>(
                 sk, sv, n, src, ring, ring_mask, lo, c->d_table, c->d_ctl, epoch, resp_lo, resp_hi, d_prev,
                 d_prev_found);
-            timer_end(c, "hm_prev");
+            timer_end(c, "hm_prev", st);
         }
     }
-    const u32 put_blocks = n ? grid_for(n, 1024) : 0;
-    const u64 get_blocks = (R + TPB - 1) / TPB;
-    if (put_blocks + get_blocks > 0) {
-        timer_begin(c, "hm_apply_get");
-        hm_apply_get_kernel<<<(unsigned)(put_blocks + get_blocks), TPB, 0, st>>>(
-            src, ring, ring_mask, lo, n, put_blocks, c->d_put_slot, c->d_table, c->slot_shift, tmask, c->d_ctl, epoch,
-            d_get_keys, R, d_get_vals, d_get_found, n > 0 ? 1 : 0);
-        timer_end(c, "hm_apply_get");
+    hipError_t e;
+    if (n > 0) {
+        // values of this round may only be stored once the previous round's reads (possibly
+        // still running on the side stream) are done with the old ones
+        if ((e = side_join(c)) != hipSuccess) return e;
+        timer_begin(c, "hm_apply", st);
+        hm_apply_kernel<<<grid_for(n, 1024), TPB, 0, st>>>(src, ring, ring_mask, lo, n, c->d_put_slot, c->d_table,
+                                                           c->d_ctl, epoch);
+        timer_end(c, "hm_apply", st);
+    }
+    if (R > 0) {
+        // Reads of this round run on the side stream when pipelining, so that they overlap the
+        // next round's hm_index (which only claims slots and raises stamps, see hm_get_kernel).
+        hipStream_t gs = st;
+        if (c->pipeline) {
+            if ((e = hipEventRecord(c->ev_applied, st)) != hipSuccess) return e;
+            if ((e = hipStreamWaitEvent(c->side_stream, c->ev_applied, 0)) != hipSuccess) return e;
+            gs = c->side_stream;
+        }
+        const u32 G = c->gets_per_thread >= 4 ? 4 : (c->gets_per_thread == 2 ? 2 : 1);
+        const unsigned gb = (unsigned)((R + TPB * G - 1) / (TPB * G));
+        timer_begin(c, "hm_get", gs);
+        if (G == 4)
+            hm_get_kernel<4><<<gb, TPB, 0, gs>>>(c->d_table, c->slot_shift, tmask, c->d_ctl, epoch, d_get_keys, R,
+                                                d_get_vals, d_get_found);
+        else if (G == 2)
+            hm_get_kernel<2><<<gb, TPB, 0, gs>>>(c->d_table, c->slot_shift, tmask, c->d_ctl, epoch, d_get_keys, R,
+                                                d_get_vals, d_get_found);
+        else
+            hm_get_kernel<1><<<gb, TPB, 0, gs>>>(c->d_table, c->slot_shift, tmask, c->d_ctl, epoch, d_get_keys, R,
+                                                d_get_vals, d_get_found);
+        timer_end(c, "hm_get", gs);
+        if (c->pipeline) {
+            if ((e = hipEventRecord(c->ev_reads_done, gs)) != hipSuccess) return e;
+            c->side_pending = true;
+        }
     }
     return hipGetLastError();
+}
+
+hipError_t side_join(nrg_ctx* c) {
+    if (!c->side_pending) return hipSuccess;
+    c->side_pending = false;
+    return hipStreamWaitEvent(c->stream, c->ev_reads_done, 0);
 }
 
 hipError_t hm_get_only(nrg_ctx* c, const u64* d_keys, u64 n, u64* d_vals, uint8_t* d_found) {
@@ -419,8 +476,10 @@ hipError_t hm_get_only(nrg_ctx* c, const u64* d_keys, u64 n, u64* d_vals, uint8_
 }
 
 hipError_t hm_prefill_range(nrg_ctx* c, u64 n, u64 off) {
+    hipError_t e = side_join(c);
+    if (e != hipSuccess) return e;
     hm_prefill_range_kernel<<<grid_for(n, 8192), TPB, 0, c->stream>>>(c->d_table, n, off, c->slot_shift,
-                                                                      c->slots - 1, c->d_ctl);
+                                                                      c->slots - 1, c->d_ctl, c->epoch);
     return hipGetLastError();
 }
 

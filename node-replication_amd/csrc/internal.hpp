@@ -70,6 +70,14 @@ struct nrg_ctx {
     nrg::Slot* d_table = nullptr;
     uint32_t* d_put_slot = nullptr;  // per Put of the round: its table slot
     uint32_t epoch = 0;              // replay rounds so far (stamps carry the round's epoch)
+    uint32_t k1_items = 1;           // Puts per thread in hm_index (tuning knob NRG_K1_ITEMS)
+    uint32_t gets_per_thread = 1;    // Gets per thread in hm_get (tuning knob NRG_GETS)
+    // round pipelining: a round's reads run on side_stream, overlapping the next round's index
+    bool pipeline = false;
+    hipStream_t side_stream = nullptr;
+    hipEvent_t ev_applied = nullptr;     // main stream: round's values stored
+    hipEvent_t ev_reads_done = nullptr;  // side stream: round's reads finished
+    bool side_pending = false;           // ev_reads_done not yet joined into the main stream
 
     // ---- Stack ----
     uint32_t* d_stack = nullptr;
@@ -91,13 +99,16 @@ struct nrg_ctx {
 
     // ---- timing ----
     bool timing = false;
+    std::string timing_only;  // if non-empty, only this kernel is timed
     std::map<std::string, nrg::KTimer> timers;
 };
 
 namespace nrg {
 // timing helpers (runtime.cpp)
-void timer_begin(nrg_ctx* c, const char* name);
-void timer_end(nrg_ctx* c, const char* name);
+void timer_begin(nrg_ctx* c, const char* name, hipStream_t s = nullptr);
+void timer_end(nrg_ctx* c, const char* name, hipStream_t s = nullptr);
+// make the main stream wait for reads still running on the side stream
+hipError_t side_join(nrg_ctx* c);
 
 // hashmap.hip
 hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool write_ring,

@@ -68,14 +68,21 @@ int use_device(nrg_ctx* c) {
     return NRG_OK;
 }
 
+// wait for everything queued on this replica, including reads on the side stream
+hipError_t sync_all(nrg_ctx* c) {
+    hipError_t e = side_join(c);
+    if (e != hipSuccess) return e;
+    return hipStreamSynchronize(c->stream);
+}
+
 int check_err(nrg_ctx* c) {
     uint32_t err = 0;
     HIPCHK(hipMemcpyAsync(&err, &c->d_ctl->err, sizeof(err), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(sync_all(c));
     if (err) {
         uint32_t z = 0;
         HIPCHK(hipMemcpyAsync(&c->d_ctl->err, &z, sizeof(z), hipMemcpyHostToDevice, c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
+        HIPCHK(sync_all(c));
         if (err & ERR_TABLE_FULL) return NRG_E_TABLE_FULL;
         if (err & ERR_BLT_FULL) return NRG_E_CAPACITY;
         if (err & ERR_CAPACITY) return NRG_E_CAPACITY;
@@ -167,8 +174,10 @@ int staging(nrg_ctx* c, Staging& st, uint64_t bytes) {
 }  // namespace
 
 namespace nrg {
-void timer_begin(nrg_ctx* c, const char* name) {
-    if (!c->timing) return;
+// HIP events around a kernel, recorded on the stream that kernel is launched on. When
+// c->timing_only is set, only that kernel is bracketed (keeps event packets off the others).
+void timer_begin(nrg_ctx* c, const char* name, hipStream_t s) {
+    if (!c->timing || (!c->timing_only.empty() && c->timing_only != name)) return;
     KTimer& t = c->timers[name];
     const size_t idx = t.pending * 2;
     while (t.ev.size() < idx + 2) {
@@ -176,14 +185,14 @@ void timer_begin(nrg_ctx* c, const char* name) {
         if (hipEventCreate(&e) != hipSuccess) return;
         t.ev.push_back(e);
     }
-    (void)hipEventRecord(t.ev[idx], c->stream);
+    (void)hipEventRecord(t.ev[idx], s ? s : c->stream);
 }
-void timer_end(nrg_ctx* c, const char* name) {
-    if (!c->timing) return;
+void timer_end(nrg_ctx* c, const char* name, hipStream_t s) {
+    if (!c->timing || (!c->timing_only.empty() && c->timing_only != name)) return;
     KTimer& t = c->timers[name];
     const size_t idx = t.pending * 2;
     if (t.ev.size() < idx + 2) return;
-    (void)hipEventRecord(t.ev[idx + 1], c->stream);
+    (void)hipEventRecord(t.ev[idx + 1], s ? s : c->stream);
     t.pending++;
 }
 }  // namespace nrg
@@ -207,6 +216,7 @@ void nrg_config_default(nrg_config* cfg, uint32_t ds_kind) {
     cfg->synth_hot_writes = 1;
     cfg->stack_push_resp = 0;
     cfg->replica_id = 1;
+    cfg->pipeline = 0;  // opt-in: see nrg_config.pipeline
 }
 
 const char* nrg_strerror(int code) {
@@ -283,6 +293,16 @@ int nrg_open(int dev, const nrg_config* cfg_in, nrg_ctx** out) {
         OPEN_CHK(hipMalloc(&c->d_table, c->slots * sizeof(Slot)));
         OPEN_CHK(hm_init(c));
         OPEN_CHK(hipMalloc(&c->d_put_slot, mb * sizeof(uint32_t)));
+        if (const char* e = std::getenv("NRG_K1_ITEMS")) c->k1_items = (uint32_t)std::atoi(e);
+        if (const char* e = std::getenv("NRG_GETS")) c->gets_per_thread = (uint32_t)std::atoi(e);
+        c->pipeline = cf.pipeline != 0;
+        if (const char* e = std::getenv("NRG_PIPELINE")) c->pipeline = std::atoi(e) != 0;
+        if (c->pipeline) {
+            OPEN_CHK(hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking));
+            OPEN_CHK(hipEventCreateWithFlags(&c->ev_applied, hipEventDisableTiming));
+            OPEN_CHK(hipEventCreateWithFlags(&c->ev_reads_done, hipEventDisableTiming));
+        }
+        c->epoch = 1;  // epoch 1 = the state built by prefill; replay rounds start at 2
         if (sort_alloc(c->sort, mb) != NRG_OK) { nrg_close(c); return NRG_E_NOMEM; }
     } else if (cf.ds_kind == NRG_DS_STACK) {
         if (!cf.stack_capacity || cf.stack_capacity >= (1ull << 31)) { nrg_close(c); return NRG_E_INVAL; }
@@ -322,6 +342,12 @@ int nrg_close(nrg_ctx* c) {
     g_dev_set = c->device;
     if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
     if (c->stream && c->stream != c->own_stream) (void)hipStreamSynchronize(c->stream);
+    if (c->side_stream) {
+        (void)hipStreamSynchronize(c->side_stream);
+        (void)hipStreamDestroy(c->side_stream);
+    }
+    if (c->ev_applied) (void)hipEventDestroy(c->ev_applied);
+    if (c->ev_reads_done) (void)hipEventDestroy(c->ev_reads_done);
     void* ptrs[] = {c->d_ring,  c->d_ctl,      c->d_table,   c->d_put_slot, c->d_stack,
                     c->d_words, c->d_sort_aux, c->d_tmp_u64, c->d_scan_desc};
     for (void* p : ptrs)
@@ -340,7 +366,7 @@ int nrg_close(nrg_ctx* c) {
 int nrg_set_stream(nrg_ctx* c, void* s) {
     if (!c) return NRG_E_INVAL;
     c->stream = s ? (hipStream_t)s : c->own_stream;
-    return NRG_OK;
+    return hip_fail(side_join(c));  // the new stream inherits reads still in flight
 }
 
 void* nrg_get_stream(nrg_ctx* c) { return c ? (void*)c->stream : nullptr; }
@@ -349,8 +375,16 @@ int nrg_sync(nrg_ctx* c) {
     if (!c) return NRG_E_INVAL;
     int r = use_device(c);
     if (r) return r;
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(sync_all(c));
     return check_err(c);
+}
+
+int nrg_join(nrg_ctx* c) {
+    if (!c) return NRG_E_INVAL;
+    int r = use_device(c);
+    if (r) return r;
+    HIPCHK(side_join(c));
+    return NRG_OK;
 }
 
 // ---- Log -------------------------------------------------------------------------------
@@ -374,7 +408,7 @@ static int append_common(nrg_ctx* c, const void* recs, uint64_t n, uint32_t orig
 int nrg_log_append(nrg_ctx* c, const void* recs, uint64_t n, uint32_t origin, uint64_t* first_idx) {
     int r = append_common(c, recs, n, origin, first_idx, hipMemcpyHostToDevice);
     if (r) return r;
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(sync_all(c));
     return NRG_OK;
 }
 
@@ -439,7 +473,7 @@ int nrg_log_exec(nrg_ctx* c, uint64_t resp_lo, uint64_t resp_hi, void* resp, uin
         HIPCHK(hipMemcpyAsync(resp, dr, w * resp_elem_bytes(c), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipMemcpyAsync(some, ds, w, hipMemcpyDeviceToHost, c->stream));
     }
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(sync_all(c));
     return check_err(c);
 }
 
@@ -486,9 +520,10 @@ int nrg_hashmap_get(nrg_ctx* c, const uint64_t* keys, uint64_t n, uint64_t* vals
     if ((r = staging(c, s[0], n * 8)) || (r = staging(c, s[1], n * 8)) || (r = staging(c, s[2], n))) return r;
     HIPCHK(hipMemcpyAsync(s[0].p, keys, n * 8, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hm_get_only(c, (u64*)s[0].p, n, (u64*)s[1].p, (uint8_t*)s[2].p));
+    HIPCHK(side_join(c));  // the reads may have run on the side stream (config.pipeline)
     HIPCHK(hipMemcpyAsync(vals, s[1].p, n * 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipMemcpyAsync(found, s[2].p, n, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(sync_all(c));
     return check_err(c);
 }
 
@@ -595,7 +630,7 @@ int nrg_hashmap_prefill(nrg_ctx* c, const uint64_t* keys, const uint64_t* vals, 
                                false));
         done += m;
     }
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(sync_all(c));
     return check_err(c);
 }
 
@@ -603,7 +638,7 @@ int nrg_hashmap_prefill_range(nrg_ctx* c, uint64_t n, uint64_t off) {
     int r = need(c, NRG_DS_HASHMAP);
     if (r) return r;
     HIPCHK(hm_prefill_range(c, n, off));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(sync_all(c));
     return check_err(c);
 }
 
@@ -611,7 +646,7 @@ int nrg_hashmap_size(nrg_ctx* c, uint64_t* n) {
     int r = need(c, NRG_DS_HASHMAP);
     if (r) return r;
     HIPCHK(hipMemcpyAsync(n, &c->d_ctl->nkeys, 8, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(sync_all(c));
     return check_err(c);
 }
 
@@ -625,7 +660,7 @@ int nrg_hashmap_dump(nrg_ctx* c, uint64_t* keys, uint64_t* vals, uint64_t cap, u
     HIPCHK(hm_dump(c, (u64*)s[0].p, (u64*)s[1].p));
     HIPCHK(hipMemcpyAsync(keys, s[0].p, *n * 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipMemcpyAsync(vals, s[1].p, *n * 8, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(sync_all(c));
     return check_err(c);
 }
 
@@ -636,7 +671,7 @@ int nrg_hashmap_digest(nrg_ctx* c, uint64_t out[3]) {
     if ((r = staging(c, s[3], 64))) return r;
     HIPCHK(hm_digest(c, (u64*)s[3].p));
     HIPCHK(hipMemcpyAsync(out, s[3].p, 24, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(sync_all(c));
     return check_err(c);
 }
 
@@ -648,7 +683,7 @@ int nrg_stack_init(nrg_ctx* c, const uint32_t* vals, uint64_t n) {
     if (n) HIPCHK(hipMemcpyAsync(c->d_stack, vals, n * 4, hipMemcpyHostToDevice, c->stream));
     long long d = (long long)n;
     HIPCHK(hipMemcpyAsync(&c->d_ctl->depth, &d, sizeof(d), hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(sync_all(c));
     return NRG_OK;
 }
 
@@ -657,7 +692,7 @@ int nrg_stack_len(nrg_ctx* c, uint64_t* n) {
     if (r) return r;
     long long d = 0;
     HIPCHK(hipMemcpyAsync(&d, &c->d_ctl->depth, sizeof(d), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(sync_all(c));
     *n = (uint64_t)d;
     return check_err(c);
 }
@@ -672,7 +707,7 @@ int nrg_stack_peek(nrg_ctx* c, uint32_t* val, uint8_t* some) {
     *val = 0;
     if (n) {
         HIPCHK(hipMemcpyAsync(val, c->d_stack + (n - 1), 4, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
+        HIPCHK(sync_all(c));
     }
     return NRG_OK;
 }
@@ -683,7 +718,7 @@ int nrg_stack_dump(nrg_ctx* c, uint32_t* vals, uint64_t cap, uint64_t* n) {
     if (*n > cap) return NRG_E_CAPACITY;
     if (*n) {
         HIPCHK(hipMemcpyAsync(vals, c->d_stack, *n * 4, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
+        HIPCHK(sync_all(c));
     }
     return NRG_OK;
 }
@@ -706,7 +741,7 @@ int nrg_synth_read(nrg_ctx* c, const nrg_synth_rd* ops, uint64_t n, uint64_t* su
     HIPCHK(hipMemcpyAsync(s[0].p, ops, n * sizeof(nrg_synth_rd), hipMemcpyHostToDevice, c->stream));
     HIPCHK(sy_read(c, (const nrg_synth_rd*)s[0].p, n, (u64*)s[1].p));
     HIPCHK(hipMemcpyAsync(sums, s[1].p, n * 8, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(sync_all(c));
     return check_err(c);
 }
 
@@ -716,7 +751,7 @@ int nrg_synth_dump(nrg_ctx* c, uint64_t* words, uint64_t cap, uint64_t* n) {
     *n = c->cfg.synth_n;
     if (*n > cap) return NRG_E_CAPACITY;
     HIPCHK(hipMemcpyAsync(words, c->d_words, *n * 8, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(sync_all(c));
     return check_err(c);
 }
 
@@ -732,7 +767,7 @@ int nrg_dev_free(nrg_ctx* c, void* p) {
     if (!c) return NRG_E_INVAL;
     int r = use_device(c);
     if (r) return r;
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(sync_all(c));
     HIPCHK(hipFree(p));
     return NRG_OK;
 }
@@ -741,7 +776,7 @@ int nrg_memcpy_h2d(nrg_ctx* c, void* d, const void* h, uint64_t bytes) {
     int r = use_device(c);
     if (r) return r;
     HIPCHK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(sync_all(c));
     return NRG_OK;
 }
 int nrg_memcpy_d2h(nrg_ctx* c, void* h, const void* d, uint64_t bytes) {
@@ -749,7 +784,7 @@ int nrg_memcpy_d2h(nrg_ctx* c, void* h, const void* d, uint64_t bytes) {
     int r = use_device(c);
     if (r) return r;
     HIPCHK(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(sync_all(c));
     return NRG_OK;
 }
 
@@ -780,11 +815,17 @@ int nrg_kernel_timing(nrg_ctx* c, int enable) {
     return NRG_OK;
 }
 
+int nrg_kernel_timing_only(nrg_ctx* c, const char* which) {
+    if (!c) return NRG_E_INVAL;
+    c->timing_only = which ? which : "";
+    return NRG_OK;
+}
+
 int nrg_kernel_time(nrg_ctx* c, const char* which, uint64_t* launches, double* total_ms) {
     if (!c || !which) return NRG_E_INVAL;
     int r = use_device(c);
     if (r) return r;
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(sync_all(c));
     auto it = c->timers.find(which);
     if (it == c->timers.end()) {
         *launches = 0;
@@ -818,7 +859,7 @@ extern "C" int nrg_test_sort_pairs(nrg_ctx* c, const uint32_t* d_keys, const uin
         HIPCHK(hipMemcpyAsync(d_ok, sk, n * 4, hipMemcpyDeviceToDevice, c->stream));
         HIPCHK(hipMemcpyAsync(d_ov, sv, n * 4, hipMemcpyDeviceToDevice, c->stream));
     }
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(sync_all(c));
     return NRG_OK;
 }
 
@@ -828,6 +869,6 @@ extern "C" int nrg_test_maxscan(nrg_ctx* c, const uint32_t* d_keys, const uint32
     int r = use_device(c);
     if (r) return r;
     HIPCHK(sy_maxscan(c, d_keys, d_vals, n, d_out));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(sync_all(c));
     return NRG_OK;
 }

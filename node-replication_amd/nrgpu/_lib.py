@@ -61,6 +61,7 @@ class Config(C.Structure):
         ("synth_hot_writes", C.c_uint32),
         ("stack_push_resp", C.c_uint32),
         ("replica_id", C.c_uint32),
+        ("pipeline", C.c_uint32),
     ]
 
 
@@ -89,6 +90,7 @@ SIGNATURES = {
     "nrg_set_stream": (C.c_int, [vp, vp]),
     "nrg_get_stream": (vp, [vp]),
     "nrg_sync": (C.c_int, [vp]),
+    "nrg_join": (C.c_int, [vp]),
     "nrg_strerror": (C.c_char_p, [C.c_int]),
     "nrg_version": (C.c_char_p, []),
     "nrg_device_count": (C.c_int, []),
@@ -124,6 +126,7 @@ SIGNATURES = {
     "nrg_gen_raw_async": (C.c_int, [vp, vp, u64, u64]),
     "nrg_gen_puts_async": (C.c_int, [vp, vp, vp, vp, u64]),
     "nrg_kernel_timing": (C.c_int, [vp, C.c_int]),
+    "nrg_kernel_timing_only": (C.c_int, [vp, C.c_char_p]),
     "nrg_kernel_time": (C.c_int, [vp, C.c_char_p, u64p, C.POINTER(C.c_double)]),
 }
 

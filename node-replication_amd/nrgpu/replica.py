@@ -92,6 +92,10 @@ class DeviceReplica:
     def sync(self):
         L.check(self._lib.nrg_sync(self._h), "nrg_sync")
 
+    def join(self):
+        """Order outstanding side-stream reads (pipeline=1) on this replica's stream."""
+        L.check(self._lib.nrg_join(self._h), "nrg_join")
+
     # -- log -----------------------------------------------------------------------
     def log_state(self) -> dict:
         info = L.LogInfo()
@@ -240,7 +244,8 @@ class DeviceReplica:
     def gen_puts_device(self, d_out, d_keys, d_vals, n):
         L.check(self._lib.nrg_gen_puts_async(self._h, _dptr(d_out), _dptr(d_keys), _dptr(d_vals), n))
 
-    def kernel_timing(self, enable: bool = True):
+    def kernel_timing(self, enable: bool = True, only: Optional[str] = None):
+        L.check(self._lib.nrg_kernel_timing_only(self._h, (only or "").encode()))
         L.check(self._lib.nrg_kernel_timing(self._h, int(enable)))
 
     def kernel_time(self, name: str):

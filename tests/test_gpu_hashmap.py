@@ -136,6 +136,43 @@ def test_fused_round_device(nrg, orc):
     _check_state(dev, om)
 
 
+def test_pipelined_rounds_back_to_back(nrg, orc):
+    """config.pipeline = 1: rounds enqueued back to back, no host sync in between. Each
+    round's reads run on the side stream overlapping the next round's index pass and must
+    still see exactly their own round's state (keys created by later rounds invisible,
+    values overwritten by later rounds not yet applied)."""
+    import torch
+
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=17, max_batch=1 << 14, pipeline=1)
+    dev.use_torch_stream()
+    om = orc.HashMap()
+    dev.hm_prefill_range(3000, 1)
+    om.prefill_range(3000, 1)
+    W, R, rounds = 6000, 20000, 8
+    outs, want = [], []
+    for r in range(rounds):
+        keys = orc.gen_uniform(W, 140 + r, 9000)  # ~1/3 of each round's keys are new
+        vals = orc.gen_raw(W, 150 + r)
+        keys[::89] = EMPTY
+        gk = orc.gen_uniform(R, 160 + r, 9500)
+        gk[::101] = EMPTY
+        d_puts = torch.from_numpy(_puts(keys, vals).view(np.int64).copy()).cuda()
+        d_gk = torch.from_numpy(gk.view(np.int64)).cuda()
+        d_gv = torch.full((R,), -1, dtype=torch.int64, device="cuda")
+        d_gf = torch.full((R,), 7, dtype=torch.uint8, device="cuda")
+        dev.hm_round_device(d_puts, W, 1, d_gk, R, d_gv, d_gf, None, None)
+        outs.append((d_puts, d_gk, d_gv, d_gf))
+        om.replay(keys, vals)
+        want.append(om.get_batch(gk))
+    dev.join()  # orders the last round's reads on the torch stream
+    got = [(gv.cpu().numpy().view(np.uint64), gf.cpu().numpy()) for (_, _, gv, gf) in outs]
+    for r in range(rounds):
+        np.testing.assert_array_equal(got[r][1], want[r][1], err_msg=f"round {r} found")
+        np.testing.assert_array_equal(got[r][0], want[r][0], err_msg=f"round {r} vals")
+    dev.sync()
+    _check_state(dev, om)
+
+
 def test_device_generator_matches_oracle(nrg, orc):
     import torch
 
