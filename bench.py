@@ -106,6 +106,27 @@ def cpu_baseline(seconds: float, write_ratio: int, key_space: int, prefill: int)
     }
 
 
+def traffic_key(args):
+    return "w%d_ops%d_ks%d_pf%d_s%d_n%d" % (args.write_ratio, args.ops_per_gpu, args.key_space, args.prefill,
+                                           args.log2_slots, int(os.environ.get("WORLD_SIZE", "1")))
+
+
+def measured_traffic(args):
+    """HBM bytes per hm_round launch from the PMC passes of tools/profile.sh (FETCH_SIZE x2 +
+    WRITE_SIZE, gfx950 correction per MI355X_MICROARCH.md), as committed by
+    tools/prof_summary.py for this exact workload; None when no matching profile exists."""
+    path = os.path.join(ROOT, "profiles", "traffic_hm_round.json")
+    try:
+        with open(path) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    e = t.get(traffic_key(args))
+    if not e:
+        return None
+    return {"bytes_per_launch": e["bytes_per_launch"], "source": e["source"]}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -120,8 +141,11 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-prev-variant", action="store_true")
-    ap.add_argument("--pipeline", type=int, default=0,
-                    help="1: a round's reads overlap the next round's index pass (nrg_config.pipeline)")
+    ap.add_argument("--no-kernel-timing", action="store_true", help="diagnostic: no HIP events in the timed region")
+    ap.add_argument("--timing-every", type=int, default=8, help="event-stamp every n-th hm_round launch")
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="1: a round's apply+reads ride in the next round's launch (nrg_config.pipeline); "
+                         "0: every round call completes its own reads")
     args = ap.parse_args()
 
     import torch
@@ -180,14 +204,25 @@ def main():
 
         group = ReplicatedHashMap(rep, device=dev_t)
 
+    # raw device pointers per pool entry, resolved once: the per-round host path is then one
+    # C-ABI call (Replica::combine's batch hand-off), not tensor indexing + marshalling
+    round_fn, h = rep._lib.nrg_hashmap_round_async, rep._h
+    ptrs = [(puts[p].data_ptr(), gkeys[p].data_ptr()) for p in range(P)]
+    gv_p, gf_p, pv_p, pf_p = gvals.data_ptr(), gfound.data_ptr(), pvals.data_ptr(), pfound.data_ptr()
+
     def step(i, prev=False):
         p = i % P
-        pv = pvals if prev else None
-        pf = pfound if prev else None
         if group is None:
-            rep.hm_round_device(puts[p], W, rank + 1, gkeys[p], R, gvals, gfound, pv, pf)
+            pp, gp = ptrs[p]
+            rc = round_fn(h, pp, W, rank + 1, gp, R, gv_p, gf_p, pv_p if prev else None, pf_p if prev else None)
+            if rc:
+                L.check(rc, "nrg_hashmap_round_async")
         else:
+            pv = pvals if prev else None
+            pf = pfound if prev else None
             group.round(puts[p, :W], gkeys[p, :R], gvals, gfound, pv, pf, stride=W)
+
+    host_s = [0.0]
 
     def timed(n, prev=False):
         if world > 1:
@@ -196,6 +231,8 @@ def main():
         t = time.perf_counter()
         for i in range(n):
             step(i, prev)
+        rep.join()  # launches the last round's deferred apply + reads: inside the timed region
+        host_s[0] = time.perf_counter() - t
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -211,27 +248,20 @@ def main():
     rep.sync()
     log(f"rank {rank}: warmup {args.warmup} rounds done")
 
-    # timed region: HIP events only around the dominant kernel (hm_get), on its own stream
-    rep.kernel_timing(True, only="hm_get")
+    # timed region. The dominant (and only per-round) kernel, hm_round, is timed with HIP events
+    # stamped from its own dispatch packets (hipExtLaunchKernelGGL start/stop events on the
+    # stream it runs on). An event-stamped dispatch costs ~5 us of command-processor time, so
+    # only every TIMING_EVERY-th launch is stamped (steady-state launches: round e's index plus
+    # round e-1's apply and reads, i.e. one round of work each).
+    rep.kernel_timing(not args.no_kernel_timing, only="hm_round", every=args.timing_every)
     elapsed = timed(args.steps)
-    k2_n, k2_ms = rep.kernel_time("hm_get")
+    host_enqueue_us = host_s[0] * 1e6 / args.steps
+    k_n, k_ms = rep.kernel_time("hm_round")
     rep.kernel_timing(False)
     rep.sync()
     ms_per_step = elapsed * 1e3 / args.steps
     total_ops = world * args.ops_per_gpu * args.steps
     value = total_ops / elapsed / 1e6
-
-    # breakdown pass (not the measurement): every kernel bracketed by events
-    nb = max(args.steps // 4, 10)
-    rep.kernel_timing(True)
-    timed(nb)
-    parts = {}
-    for k in ("hm_index", "hm_apply", "hm_get"):
-        n_, ms_ = rep.kernel_time(k)
-        n0 = k2_n if k == "hm_get" else 0
-        ms0 = k2_ms if k == "hm_get" else 0.0
-        parts[k + "_avg_us"] = round((ms_ - ms0) * 1e3 / (n_ - n0), 3) if n_ > n0 else None
-    rep.kernel_timing(False)
 
     prev_value = None
     if not args.no_prev_variant and world == 1:
@@ -245,14 +275,17 @@ def main():
             dist.destroy_process_group()
         return
 
-    # ---- roofline of the dominant kernel (hm_get: the round's reads) -------------------------
-    # algorithmic bytes per launch (per-unit figures): 16 B per Get (8-B key in,
-    # 8-B value out) + one 64-B sector per distinct key read; found bytes ignored
+    # ---- roofline of the dominant kernel (hm_round: index of round e + apply/reads of e-1) ----
+    # Algorithmic bytes per round: B = 16 R + 16 W_glob + 64 U_r + 128 U_w
+    # (8-B key in + 8-B value out per Get, the 16-B records replayed, one 64-B sector per
+    # distinct key read, read + write-back per distinct key written; Put responses are
+    # Ok(None) here, so no 8 W_own term). Every sampled launch carries one round of work.
     u_w = u_w_local * world
-    k2_bytes = 16 * R + 64 * u_r
-    k2_avg_s = (k2_ms / 1e3 / k2_n) if k2_n else float("nan")
-    achieved = k2_bytes / k2_avg_s / 1e9 if k2_n else None
     round_bytes = 16 * R + 16 * Wg + 64 * u_r + 128 * u_w
+    k_bytes = round_bytes
+    k_avg_s = (k_ms / 1e3 / k_n) if k_n else float("nan")
+    achieved = k_bytes / k_avg_s / 1e9 if k_n else None
+    traffic = measured_traffic(args)
     res = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -279,20 +312,23 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "hm_get",
+            "kernel": "hm_round",
             "achieved": round(achieved, 1) if achieved else None,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-            "traffic": None,
-            "bytes_per_launch": int(k2_bytes),
-            "avg_launch_us": round(k2_avg_s * 1e6, 3) if k2_n else None,
-            "launches": k2_n,
+            "traffic": traffic.get("bytes_per_launch") if traffic else None,
+            "traffic_source": traffic.get("source") if traffic else None,
+            "bytes_per_launch": int(k_bytes),
+            "sampled_every": args.timing_every,
+            "traffic_key": traffic_key(args),
+            "avg_launch_us": round(k_avg_s * 1e6, 3) if k_n else None,
+            "launches": k_n,
         },
         "round": {
             "algorithmic_bytes": int(round_bytes),
             "achieved_GBps": round(round_bytes / (elapsed / args.steps) / 1e9, 1),
-            **parts,
+            "host_enqueue_us": round(host_enqueue_us, 2),
             "distinct_get_keys": int(u_r),
             "distinct_put_keys": int(u_w),
         },

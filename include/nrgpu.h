@@ -260,9 +260,11 @@ int nrg_gen_puts_async(nrg_ctx* ctx, nrg_put* d_out, const uint64_t* d_keys, con
                        uint64_t n);
 
 /* ---- timing: HIP events recorded around the dominant replay kernel -------------------- */
-/* When enabled, the context records a start/stop event pair around every launch of the
- * kernel named `which` ("hm_apply_get", "hm_index", ...) and accumulates the elapsed time;
- * nrg_kernel_time reads (launches, total milliseconds) after synchronising. */
+/* enable = 0: off; 1: every launch; n > 1: every n-th launch (sampling keeps the timed stream
+ * unperturbed). The main replay kernel ("hm_round") is timed with start/stop events stamped
+ * from its own dispatch (hipExtLaunchKernelGGL); other kernels ("hm_prev", "st_scan",
+ * "st_sort", "sy_replay") with event records around them. nrg_kernel_time reads (timed
+ * launches, their total milliseconds) after synchronising. */
 int nrg_kernel_timing(nrg_ctx* ctx, int enable);
 /* Restrict timing to one kernel name (NULL or "" = all). */
 int nrg_kernel_timing_only(nrg_ctx* ctx, const char* which);

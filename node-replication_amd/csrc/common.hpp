@@ -11,13 +11,11 @@ typedef unsigned int u32;
 
 // Empty-slot marker of the open-addressing tables. Keys span all of u64 (key 0 is used by
 // benches/hashmap.rs:95-96,150), so the one key equal to the marker lives in a side slot
-// (DevCtl::sp_*), giving the full HashMap<u64,u64> key domain (SURVEY.md §7 "Sentinels").
+// (DevCtl::sp), giving the full HashMap<u64,u64> key domain (SURVEY.md §7 "Sentinels").
 constexpr u64 EMPTY_KEY = ~0ull;
-constexpr u32 NEW_SLOT = 0xFFFFFFFFu;  // BLT info: key absent from the table before the round
 
 // Device error bits latched in DevCtl::err and reported by nrg_sync.
 constexpr u32 ERR_TABLE_FULL = 1u;
-constexpr u32 ERR_BLT_FULL = 2u;
 constexpr u32 ERR_CAPACITY = 4u;
 
 // splitmix64 finaliser — identical constants to oracle/nr_oracle.c (orc_mix64) so that
@@ -32,31 +30,42 @@ __host__ __device__ __forceinline__ u64 sm64_at(u64 seed, u64 i) {
 }
 __device__ __forceinline__ u64 mulhi64(u64 a, u64 b) { return __umul64hi(a, b); }
 
-// Main-table home slot: top bits of the mixed key. BLT home slot: low bits (independent).
+// Home slot of a key: top bits of the mixed key.
 __device__ __forceinline__ u64 table_home(u64 key, u32 shift) { return mix64(key) >> shift; }
-__device__ __forceinline__ u64 blt_home(u64 key) { return mix64(key ^ 0x5bd1e9955bd1e995ull); }
+
+// 64-byte table slot, two per 128-B line. A random read costs one 128-B line at the memory
+// side whatever its width (TCC_EA0_RDREQ_128B = 1 per lookup, profiles/r01_rdreq_size.txt),
+// so the replay's bookkeeping rides in the same line as key and value:
+//   stamp of parity p  last writer of the key in the most recent round of epoch parity p:
+//             epoch << 32 | 1 + offset in that round (raised with atomicMax). Two words so a
+//             round's index pass (parity e&1) can run while the previous round's apply and
+//             reads (parity (e-1)&1) are still in flight.
+//   created   epoch of the round that inserted the key (0 while a claim is in progress).
+// Layout: a read needs {key, val} and {created, stamp of its parity}; `created` sits between
+// the two stamps so that both pairs are one 16-B load (bytes 16-31 or 24-39).
+struct __attribute__((aligned(64))) Slot {
+    u64 key;     // EMPTY_KEY when free
+    u64 val;
+    u64 stamp1;  // odd epochs
+    u32 created;
+    u32 pad;
+    u64 stamp0;  // even epochs
+    u64 pad2[3];
+};
+__host__ __device__ __forceinline__ u64* slot_stamp(Slot* s, u32 par) { return par ? &s->stamp1 : &s->stamp0; }
+__host__ __device__ __forceinline__ const u64* slot_stamp(const Slot* s, u32 par) {
+    return par ? &s->stamp1 : &s->stamp0;
+}
 
 // One replica-wide control block in HBM.
-struct DevCtl {
-    u32 err;             // latched ERR_* bits
+struct __attribute__((aligned(64))) DevCtl {
+    u32 err;          // latched ERR_* bits
     u32 pad0;
-    u64 nkeys;           // hashmap: number of keys (including the side-slot key)
-    u64 sp_present;      // side slot for key == EMPTY_KEY
-    u64 sp_val;
-    u64 sp_stamp;        // epoch << 32 | 1 + round offset of the last Put to EMPTY_KEY
-    long long depth;     // stack: current length
-    u64 counter;         // scratch counter (dump compaction)
-    u64 pad1[8];
-};
-
-// 32-byte table slot; a random 16-B read costs a whole 128-B line on MI355X anyway, so the
-// last-writer stamp and creation epoch ride in the same line as key and value.
-struct __attribute__((aligned(32))) Slot {
-    u64 key;      // EMPTY_KEY when free
-    u64 val;
-    u64 stamp;    // epoch << 32 | 1 + offset of the round's last Put to key (atomicMax)
-    u32 created;  // epoch of the round that inserted key
-    u32 pad;
+    u64 nkeys;        // hashmap: number of keys (including the side-slot key)
+    long long depth;  // stack: current length
+    u64 counter;      // scratch counter (dump compaction)
+    u64 pad1[4];
+    Slot sp;          // side slot for key == EMPTY_KEY (present iff sp.created != 0)
 };
 
 __device__ __forceinline__ u64 ld_relaxed(const u64* p) {

@@ -4,70 +4,102 @@
 // benches/hashmap.rs:114-119, nr/examples/hashmap.rs:46-50) and the read path
 // Replica::read_only -> dispatch (nr/src/replica.rs:483-497, benches/hashmap.rs:107-111).
 //
-// Table: 2^k open-addressing slots of 32 B {key, val, stamp, created}; four slots per 128-B
-// line, the HBM access granule for random reads on MI355X (microbench/random_gather.hip,
-// profiles/r01_random_gather_fetch_size.txt). A replay "round" covers the log records
-// [lo, lo+n) with a fresh epoch e (one per round, never reused):
+// Table: 2^k open-addressing slots of 64 B (common.hpp), linear probing from
+// mix64(key) >> (64 - k). A replay round covers the log records [lo, lo+n) and gets a fresh
+// epoch e (never reused). Its work splits into two halves:
 //
-//   K1 hm_index     one thread per Put (4 per thread): probe the key's slot (read-only), or
-//                   claim an empty one with a 64-bit CAS (new key, created = e); the last
-//                   writer in log order is elected by atomicMax(slot.stamp, e<<32 | i+1),
-//                   pre-combined per block in LDS so a hot key costs one global atomic per
-//                   block (Zipf streams). Writes the log copy when the round is appended here.
-//   prev path       only when previous-value responses are requested: stable radix sort of
-//                   (slot, i) -> a Put's previous value is its in-group predecessor's value,
-//                   or the slot's pre-round value (absent if created == e). Runs before K2.
-//   K2 hm_apply_get one launch, two roles: Put threads whose stamp is (e, i+1) store the
-//                   final value; Get threads probe the table once and read the value from
-//                   the round's log record when the slot's stamp carries epoch e.
-// The result equals the sequential replay: last-writer-wins per key in log order, reads
+//   index(e)   per Put: find the key's slot, or claim an empty one with a 64-bit CAS
+//              (created = e); elect the round's last writer of every key with
+//              atomicMax(slot.stamp[e&1], e<<32 | i+1), pre-combined per block in LDS so a
+//              hot key costs one global atomic per block (Zipf streams). Writes put_slot[i]
+//              and, when the round is appended here, the log copy.
+//   apply(e)   per Put: the elected writer (stamp[e&1] == (e, i+1)) stores its value.
+//   reads(e)   per Get, against the state after round e: a key counts iff 0 < created <= e;
+//              its value is the round's elected record when stamp[e&1] carries epoch e
+//              (apply(e) may still be storing it), else the slot's value.
+//
+// All three roles live in ONE kernel (hm_round_kernel, disjoint block ranges), launched as
+// {index(e) | apply(e-1) + reads(e-1)}: the latency-bound index pass of a round overlaps the
+// bandwidth-bound reads of the previous one. This is race-free because index(e) only claims
+// empty slots (invisible to reads(e-1): created is 0 or e) and raises stamp[e&1], while
+// apply(e-1)/reads(e-1) only look at stamp[(e-1)&1] and at values that index never writes.
+// The result equals the sequential replay: last-writer-wins per key in log order, and reads
 // after the round's writes (SURVEY.md §8a round semantics).
 #include "internal.hpp"
 
 namespace nrg {
 
 constexpr int TPB = 256;
-// K1 geometry: ITEMS puts per thread, an LDS combining table of 2*TPB*ITEMS entries per block
-
-// record i of the round: from the caller's segment when given (fused append), else the ring
-__device__ __forceinline__ nrg_put rec_at(const nrg_put* __restrict__ src, const nrg_put* ring, u64 ring_mask,
-                                          u64 lo, u64 i) {
-    return src ? src[i] : ring[(lo + i) & ring_mask];
-}
+constexpr u32 SIDE_SLOT = 0xFFFFFFFFu;   // put_slot value of the EMPTY_KEY key (side slot)
+constexpr u32 FULL_SLOT = 0xFFFFFFFEu;   // put_slot value of a Put that found no slot
 
 __device__ __forceinline__ u64 stamp_of(u32 epoch, u64 i) { return ((u64)epoch << 32) | (i + 1); }
 
-// Load a whole slot with two 16-B loads issued together. The empty asm pins both values at
-// this point: otherwise hipcc sinks the {val, stamp} load below the key compare of the probe
-// loop, turning every Get into two dependent accesses to its line.
-__device__ __forceinline__ Slot load_slot(const Slot* p) {
+// record i of a round: from a caller's buffer when given, else from the log ring
+struct RecSrc {
+    const nrg_put* src;
+    const nrg_put* ring;
+    u64 mask, lo;
+    __device__ __forceinline__ nrg_put at(u64 i) const { return src ? src[i] : ring[(lo + i) & mask]; }
+};
+
+struct IndexJob {
+    RecSrc rec;
+    nrg_put* ring_out;  // log copy to write (nullptr: records already in the ring)
+    u64 n;
+    u32* put_slot;
+    u32 epoch;
+    u32 nblocks;
+};
+struct ApplyJob {
+    RecSrc rec;
+    u64 n;
+    const u32* put_slot;
+    u32 epoch;
+    u32 nblocks;
+};
+struct ReadJob {
+    RecSrc rec;  // records of round `epoch` (used while its apply may be in flight); src=ring=0: none
+    const u64* keys;
+    u64 R;
+    u64* vals;
+    uint8_t* found;
+    u32 epoch;
+    u32 nblocks;
+};
+
+// What a read needs of a slot: two 16-B loads to the same 128-B line, {key, val} and
+// {stamp1, created} (odd epochs) or {created, stamp0} (even epochs), issued together. The
+// empty asm pins the values at this point: otherwise hipcc sinks the second load below the
+// key compare of the probe loop, turning a Get into two dependent accesses.
+struct View {
+    u64 key, val, st;
+    u32 created;
+};
+__device__ __forceinline__ View load_view(const Slot* p, u32 par) {
     typedef u64 u64x2 __attribute__((ext_vector_type(2)));
     const u64x2 a = *(const u64x2*)p;
-    const u64x2 b = *((const u64x2*)p + 1);
-    u64 k = a.x, v = a.y, st = b.x;
-    asm volatile("" : "+v"(k), "+v"(v), "+v"(st));
-    Slot s;
-    s.key = k;
-    s.val = v;
-    s.stamp = st;
-    s.created = (u32)b.y;
-    s.pad = 0;
-    return s;
+    const u64x2 b = *(const u64x2*)((const char*)p + (par ? 16 : 24));
+    u64 k = a.x, v = a.y;
+    u64 st = par ? b.x : b.y;
+    u32 cr = (u32)(par ? b.y : b.x);
+    asm volatile("" : "+v"(k), "+v"(v), "+v"(st), "+v"(cr));
+    View w;
+    w.key = k;
+    w.val = v;
+    w.st = st;
+    w.created = cr;
+    return w;
 }
 
-// Read-only probe from slot s whose contents `sl` the caller already loaded: slot or -1.
-__device__ __forceinline__ long long probe_from(const Slot* __restrict__ table, u64 k, u64 s, u64 tmask, Slot sl,
-                                                Slot* out) {
-    for (u64 pr = 0; pr <= tmask; pr++) {
-        if (sl.key == k) {
-            *out = sl;
-            return (long long)s;
-        }
-        if (sl.key == EMPTY_KEY) return -1;
-        s = (s + 1) & tmask;
-        sl = load_slot(&table[s]);
-    }
-    return -2;
+// The value a read of epoch ep sees in a slot (or side slot) holding its key.
+__device__ __forceinline__ bool resolve(View w, u32 ep, RecSrc rec, bool use_rec, u64* v) {
+    if (w.created == 0 || w.created > ep) return false;  // inserted by a later round (or claiming)
+    if (use_rec && (u32)(w.st >> 32) == ep)
+        *v = rec.at((u64)(u32)w.st - 1).val;  // written in round ep; apply(ep) may be in flight
+    else
+        *v = w.val;
+    return true;
 }
 
 // find-or-claim k from slot s (its key already loaded as key0); returns slot or -1 if full
@@ -91,54 +123,58 @@ __device__ __forceinline__ long long find_or_claim(Slot* table, u64 k, u64 s, u6
     return -1;
 }
 
+// ---- role: index(e) -------------------------------------------------------------------------
 template <int K1_ITEMS>
-__global__ __launch_bounds__(TPB) void hm_index_kernel(const nrg_put* __restrict__ src, nrg_put* ring, u64 ring_mask,
-                                                       u64 lo, u64 n, int write_ring, Slot* table, u32 shift,
-                                                       u64 tmask, u32* __restrict__ put_slot, DevCtl* ctl, u32 epoch) {
+__device__ __forceinline__ void index_role(IndexJob j, u32 blk, Slot* table, u32 shift, u64 tmask,
+                                           DevCtl* ctl) {
     constexpr int K1_TILE = TPB * K1_ITEMS;
     constexpr int K1_LDS = 2 * K1_TILE;
     __shared__ u32 s_slot[K1_LDS];
     __shared__ u32 s_max[K1_LDS];
+    __shared__ u32 s_created;
     for (int q = threadIdx.x; q < K1_LDS; q += TPB) {
         s_slot[q] = 0xFFFFFFFFu;
         s_max[q] = 0;
     }
+    if (threadIdx.x == 0) s_created = 0;
     __syncthreads();
-    const u64 base = (u64)blockIdx.x * K1_TILE;
+    const u32 par = j.epoch & 1;
+    const u64 base = (u64)blk * K1_TILE;
     u32 created = 0;
     u64 sl_idx[K1_ITEMS];
     u64 key0[K1_ITEMS];
     nrg_put rec[K1_ITEMS];
     // issue every record load and every first probe before waiting on any of them
 #pragma unroll
-    for (int j = 0; j < K1_ITEMS; j++) {
-        const u64 i = base + (u64)j * TPB + threadIdx.x;
-        rec[j] = i < n ? rec_at(src, ring, ring_mask, lo, i) : nrg_put{EMPTY_KEY, 0};
+    for (int q = 0; q < K1_ITEMS; q++) {
+        const u64 i = base + (u64)q * TPB + threadIdx.x;
+        rec[q] = i < j.n ? j.rec.at(i) : nrg_put{EMPTY_KEY, 0};
     }
 #pragma unroll
-    for (int j = 0; j < K1_ITEMS; j++) {
-        const u64 i = base + (u64)j * TPB + threadIdx.x;
-        if (i < n && write_ring) ring[(lo + i) & ring_mask] = rec[j];
-        sl_idx[j] = table_home(rec[j].key, shift);
-        key0[j] = rec[j].key != EMPTY_KEY ? table[sl_idx[j]].key : EMPTY_KEY;
+    for (int q = 0; q < K1_ITEMS; q++) {
+        const u64 i = base + (u64)q * TPB + threadIdx.x;
+        if (i < j.n && j.ring_out) j.ring_out[(j.rec.lo + i) & j.rec.mask] = rec[q];
+        sl_idx[q] = table_home(rec[q].key, shift);
+        key0[q] = rec[q].key != EMPTY_KEY ? table[sl_idx[q]].key : EMPTY_KEY;
     }
 #pragma unroll
-    for (int j = 0; j < K1_ITEMS; j++) {
-        const u64 i = base + (u64)j * TPB + threadIdx.x;
-        if (i >= n) continue;
-        const u64 k = rec[j].key;
+    for (int q = 0; q < K1_ITEMS; q++) {
+        const u64 i = base + (u64)q * TPB + threadIdx.x;
+        if (i >= j.n) continue;
+        const u64 k = rec[q].key;
         if (k == EMPTY_KEY) {  // the side-slot key
-            atomicMax(&ctl->sp_stamp, stamp_of(epoch, i));
-            put_slot[i] = 0xFFFFFFFFu;
+            if (ld_relaxed32(&ctl->sp.created) == 0 && atomicCAS(&ctl->sp.created, 0u, j.epoch) == 0u) created++;
+            atomicMax(slot_stamp(&ctl->sp, par), stamp_of(j.epoch, i));
+            j.put_slot[i] = SIDE_SLOT;
             continue;
         }
-        const long long s = find_or_claim(table, k, sl_idx[j], tmask, key0[j], epoch, &created);
+        const long long s = find_or_claim(table, k, sl_idx[q], tmask, key0[q], j.epoch, &created);
         if (s < 0) {
             atomicOr(&ctl->err, ERR_TABLE_FULL);
-            put_slot[i] = 0xFFFFFFFEu;
+            j.put_slot[i] = FULL_SLOT;
             continue;
         }
-        put_slot[i] = (u32)s;
+        j.put_slot[i] = (u32)s;
         // combine in LDS: max (i+1) per slot within the block
         u32 h = (u32)(mix64((u64)s) & (K1_LDS - 1));
         for (;;) {
@@ -148,99 +184,119 @@ __global__ __launch_bounds__(TPB) void hm_index_kernel(const nrg_put* __restrict
         }
         atomicMax(&s_max[h], (u32)(i + 1));
     }
-    if (created) atomicAdd(&ctl->nkeys, (u64)created);
+    // one key-count atomic per block: a same-address atomic per thread serialises at the
+    // memory side (16k new keys cost ~16 us that way)
+    if (created) atomicAdd(&s_created, created);
     __syncthreads();
     for (int q = threadIdx.x; q < K1_LDS; q += TPB) {
         const u32 s = s_slot[q];
-        if (s != 0xFFFFFFFFu) atomicMax(&table[s].stamp, ((u64)epoch << 32) | s_max[q]);
+        if (s != 0xFFFFFFFFu) atomicMax(slot_stamp(&table[s], par), ((u64)j.epoch << 32) | s_max[q]);
+    }
+    if (threadIdx.x == 0 && s_created) atomicAdd(&ctl->nkeys, (u64)s_created);
+}
+
+// ---- role: apply(e) -------------------------------------------------------------------------
+__device__ __forceinline__ void apply_role(ApplyJob j, u32 blk, Slot* table, DevCtl* ctl) {
+    const u64 i = (u64)blk * TPB + threadIdx.x;
+    if (i >= j.n) return;
+    const u32 par = j.epoch & 1;
+    const u32 s = j.put_slot[i];
+    const u64 want = stamp_of(j.epoch, i);
+    if (s == SIDE_SLOT) {
+        if (*slot_stamp(&ctl->sp, par) == want) ctl->sp.val = j.rec.at(i).val;
+    } else if (s != FULL_SLOT) {
+        if (*slot_stamp(&table[s], par) == want) table[s].val = j.rec.at(i).val;
     }
 }
 
-// K2a: the round's last writer of each key (stamp == (e, i+1)) stores the final value.
-__global__ __launch_bounds__(TPB) void hm_apply_kernel(const nrg_put* __restrict__ src, const nrg_put* __restrict__ ring,
-                                                       u64 ring_mask, u64 lo, u64 n, const u32* __restrict__ put_slot,
-                                                       Slot* table, DevCtl* ctl, u32 epoch) {
-    u32 inserted = 0;
-    for (u64 i = blockIdx.x * (u64)TPB + threadIdx.x; i < n; i += (u64)gridDim.x * TPB) {
-        const u32 s = put_slot[i];
-        const u64 want = stamp_of(epoch, i);
-        if (s == 0xFFFFFFFFu) {  // side-slot key
-            if (ctl->sp_stamp == want) {
-                if (!ctl->sp_present) inserted++;
-                ctl->sp_val = rec_at(src, ring, ring_mask, lo, i).val;
-                ctl->sp_present = 1;
-            }
-            continue;
-        }
-        if (s == 0xFFFFFFFEu) continue;  // table full (reported)
-        if (table[s].stamp == want) table[s].val = rec_at(src, ring, ring_mask, lo, i).val;
-    }
-    if (inserted) atomicAdd(&ctl->nkeys, (u64)inserted);
-}
-
-// K2b: Gets against the state after round `epoch` (dispatch after sync-to-tail). A slot
-// counts only if 0 < created <= epoch: with rounds pipelined, the next round's hm_index may
-// already be claiming slots for its new keys (created is 0 until its claimer writes it, then
-// epoch+1), and those keys do not exist yet for these reads.
+// ---- role: reads(e) -------------------------------------------------------------------------
 template <int G>
-__global__ __launch_bounds__(TPB) void hm_get_kernel(const Slot* __restrict__ table, u32 shift, u64 tmask,
-                                                     const DevCtl* ctl, u32 epoch, const u64* __restrict__ gkeys, u64 R,
-                                                     u64* __restrict__ gvals, uint8_t* __restrict__ gfound) {
+__device__ __forceinline__ void read_role(ReadJob j, u32 blk, const Slot* table, u32 shift, u64 tmask,
+                                          const DevCtl* ctl) {
     // G Gets per thread: all key loads, then all first-slot loads, are in flight together
-    const u64 jb = (u64)blockIdx.x * TPB * G + threadIdx.x;
+    const u32 par = j.epoch & 1;
+    const bool use_rec = j.rec.src != nullptr || j.rec.ring != nullptr;
+    const u64 jb = (u64)blk * TPB * G + threadIdx.x;
     u64 k[G];
-    Slot first[G];
+    View first[G];
 #pragma unroll
     for (int g = 0; g < G; g++) {
-        const u64 j = jb + (u64)g * TPB;
-        k[g] = j < R ? gkeys[j] : EMPTY_KEY;
+        const u64 q = jb + (u64)g * TPB;
+        k[g] = q < j.R ? j.keys[q] : EMPTY_KEY;
     }
 #pragma unroll
-    for (int g = 0; g < G; g++) first[g] = load_slot(&table[table_home(k[g], shift)]);
+    for (int g = 0; g < G; g++) first[g] = load_view(k[g] == EMPTY_KEY ? &ctl->sp : &table[table_home(k[g], shift)], par);
 #pragma unroll
     for (int g = 0; g < G; g++) {
-        const u64 j = jb + (u64)g * TPB;
-        if (j >= R) break;
+        const u64 q = jb + (u64)g * TPB;
+        if (q >= j.R) break;
         u64 v = 0;
-        uint8_t f = 0;
+        bool f = false;
         if (k[g] == EMPTY_KEY) {
-            if (ctl->sp_present) {
-                v = ctl->sp_val;
-                f = 1;
-            }
+            f = resolve(first[g], j.epoch, j.rec, use_rec, &v);
         } else {
-            Slot sl;
-            const long long s = probe_from(table, k[g], table_home(k[g], shift), tmask, first[g], &sl);
-            if (s >= 0 && sl.created != 0 && sl.created <= epoch) {
-                f = 1;
-                v = sl.val;
+            u64 s = table_home(k[g], shift);
+            View w = first[g];
+            for (u64 pr = 0; pr <= tmask; pr++) {
+                if (w.key == k[g]) {
+                    f = resolve(w, j.epoch, j.rec, use_rec, &v);
+                    break;
+                }
+                if (w.key == EMPTY_KEY) break;
+                s = (s + 1) & tmask;
+                w = load_view(&table[s], par);
             }
         }
-        gvals[j] = v;
-        gfound[j] = f;
+        if (!f) v = 0;
+        j.vals[q] = v;
+        j.found[q] = f ? 1 : 0;
     }
 }
 
+// One launch = {index(e)} + {apply(p)} + {reads(p)} over disjoint block ranges (any may be
+// empty). Index blocks come first so the latency-bound pass is dispatched first.
+template <int K1_ITEMS, int G>
+__global__ __launch_bounds__(TPB) void hm_round_kernel(IndexJob ij, ApplyJob aj, ReadJob rj, Slot* table, u32 shift,
+                                                       u64 tmask, DevCtl* ctl) {
+    u32 b = blockIdx.x;
+    if (b < ij.nblocks) {
+        index_role<K1_ITEMS>(ij, b, table, shift, tmask, ctl);
+        return;
+    }
+    b -= ij.nblocks;
+    if (b < aj.nblocks) {
+        apply_role(aj, b, table, ctl);
+        return;
+    }
+    b -= aj.nblocks;
+    read_role<G>(rj, b, table, shift, tmask, ctl);
+}
+
+// Previous-value responses (HashMap::insert's return, nr/examples/hashmap.rs:46-50): with the
+// round's Puts stably sorted by slot, a Put's previous value is its in-group predecessor's
+// value, or the slot's value before the round (absent if the key was created in it). Runs
+// after index(e) and before apply(e), so slot values are still the pre-round ones.
 __global__ __launch_bounds__(TPB) void hm_prev_kernel(const u32* __restrict__ sk, const u32* __restrict__ sv, u64 n,
-                                                      const nrg_put* __restrict__ src, const nrg_put* __restrict__ ring,
-                                                      u64 ring_mask, u64 lo, const Slot* __restrict__ table,
-                                                      const DevCtl* ctl, u32 epoch, u64 resp_lo, u64 resp_hi,
-                                                      u64* __restrict__ prev, uint8_t* __restrict__ prevf) {
+                                                      RecSrc rec, const Slot* __restrict__ table, const DevCtl* ctl,
+                                                      u32 epoch, u64 resp_lo, u64 resp_hi, u64* __restrict__ prev,
+                                                      uint8_t* __restrict__ prevf) {
     const u64 p = blockIdx.x * (u64)TPB + threadIdx.x;
     if (p >= n) return;
     const u32 s = sk[p];
-    const u64 gidx = lo + sv[p];
+    const u64 gidx = rec.lo + sv[p];
     if (gidx < resp_lo || gidx >= resp_hi) return;
     u64 v = 0;
     uint8_t f = 0;
-    const bool has_pred = p > 0 && sk[p - 1] == s;
-    if (has_pred) {
-        v = rec_at(src, ring, ring_mask, lo, sv[p - 1]).val;
+    if (p > 0 && sk[p - 1] == s) {
+        v = rec.at(sv[p - 1]).val;
         f = 1;
-    } else if (s == 0xFFFFFFFFu) {  // side slot, before K2 of this round: pre-round state
-        f = (uint8_t)(ctl->sp_present != 0);
-        v = f ? ctl->sp_val : 0;
-    } else if (s != 0xFFFFFFFEu && table[s].created != epoch) {  // existed before; K2 not run yet
+    } else if (s == SIDE_SLOT) {
+        const u32 cr = ctl->sp.created;
+        if (cr != 0 && cr != epoch) {
+            v = ctl->sp.val;
+            f = 1;
+        }
+    } else if (s != FULL_SLOT && table[s].created != epoch) {  // existed before the round
         v = table[s].val;
         f = 1;
     }
@@ -250,18 +306,18 @@ __global__ __launch_bounds__(TPB) void hm_prev_kernel(const u32* __restrict__ sk
 
 __global__ __launch_bounds__(TPB) void hm_init_table_kernel(Slot* table, u64 slots) {
     for (u64 s = blockIdx.x * (u64)TPB + threadIdx.x; s < slots; s += (u64)gridDim.x * TPB) {
-        Slot z;
+        Slot z = {};
         z.key = EMPTY_KEY;
-        z.val = 0;
-        z.stamp = 0;
-        z.created = 0;
-        z.pad = 0;
         table[s] = z;
     }
 }
 
+// NrHashMap::default (benches/hashmap.rs:91-100): keys 0..n-1 -> k + off, inserted directly.
 __global__ __launch_bounds__(TPB) void hm_prefill_range_kernel(Slot* table, u64 n, u64 off, u32 shift, u64 tmask,
                                                                DevCtl* ctl, u32 epoch) {
+    __shared__ u32 s_ins;
+    if (threadIdx.x == 0) s_ins = 0;
+    __syncthreads();
     u32 inserted = 0;
     for (u64 k = blockIdx.x * (u64)TPB + threadIdx.x; k < n; k += (u64)gridDim.x * TPB) {
         u64 s = table_home(k, shift);
@@ -278,16 +334,18 @@ __global__ __launch_bounds__(TPB) void hm_prefill_range_kernel(Slot* table, u64 
         }
         if (!done) atomicOr(&ctl->err, ERR_TABLE_FULL);
     }
-    if (inserted) atomicAdd(&ctl->nkeys, (u64)inserted);
+    if (inserted) atomicAdd(&s_ins, inserted);
+    __syncthreads();
+    if (threadIdx.x == 0 && s_ins) atomicAdd(&ctl->nkeys, (u64)s_ins);
 }
 
 __global__ __launch_bounds__(TPB) void hm_dump_kernel(const Slot* __restrict__ table, u64 slots, DevCtl* ctl,
                                                       u64* __restrict__ ok, u64* __restrict__ ov) {
     const u64 gid = blockIdx.x * (u64)TPB + threadIdx.x;
-    if (gid == 0 && ctl->sp_present) {
+    if (gid == 0 && ctl->sp.created) {
         const u64 i = atomicAdd(&ctl->counter, 1ull);
         ok[i] = EMPTY_KEY;
-        ov[i] = ctl->sp_val;
+        ov[i] = ctl->sp.val;
     }
     for (u64 s = gid; s < slots; s += (u64)gridDim.x * TPB) {
         const u64 k = table[s].key;
@@ -304,8 +362,8 @@ __global__ __launch_bounds__(TPB) void hm_digest_kernel(const Slot* __restrict__
     __shared__ u64 s_c[4], s_s[4], s_x[4];
     const u64 gid = blockIdx.x * (u64)TPB + threadIdx.x;
     u64 c = 0, sm = 0, x = 0;
-    if (gid == 0 && ctl->sp_present) {
-        const u64 h = mix64(EMPTY_KEY ^ mix64(ctl->sp_val));
+    if (gid == 0 && ctl->sp.created) {
+        const u64 h = mix64(EMPTY_KEY ^ mix64(ctl->sp.val));
         c++;
         sm += h;
         x ^= h;
@@ -383,115 +441,167 @@ static inline unsigned grid_for(u64 n, u64 cap = 4096) {
     return (unsigned)g;
 }
 
+// ---- host side ----------------------------------------------------------------------------
+static RecSrc ring_src(nrg_ctx* c, const nrg_put* src, u64 lo) {
+    RecSrc r;
+    r.src = src;
+    r.ring = (const nrg_put*)c->d_ring;
+    r.mask = c->log_size - 1;
+    r.lo = lo;
+    return r;
+}
+
+template <int K1, int G>
+static void launch_round(nrg_ctx* c, const IndexJob& ij, const ApplyJob& aj, const ReadJob& rj) {
+    const u32 blocks = ij.nblocks + aj.nblocks + rj.nblocks;
+    NRG_LAUNCH(c, "hm_round", (hm_round_kernel<K1, G>), blocks, TPB, 0, c->stream, ij, aj, rj, c->d_table,
+               c->slot_shift, (u64)(c->slots - 1), c->d_ctl);
+}
+
+static hipError_t launch(nrg_ctx* c, IndexJob& ij, ApplyJob& aj, ReadJob& rj) {
+    const u32 K1 = c->k1_items >= 4 ? 4 : (c->k1_items == 2 ? 2 : 1);
+    const u32 G = c->gets_per_thread >= 4 ? 4 : (c->gets_per_thread == 2 ? 2 : 1);
+    ij.nblocks = (u32)((ij.n + TPB * K1 - 1) / (TPB * K1));
+    aj.nblocks = (u32)((aj.n + TPB - 1) / TPB);
+    rj.nblocks = (u32)((rj.R + TPB * G - 1) / (TPB * G));
+    if (ij.nblocks + aj.nblocks + rj.nblocks == 0) return hipSuccess;
+#define NRG_RK(A, B) \
+    if (K1 == A && G == B) launch_round<A, B>(c, ij, aj, rj)
+    NRG_RK(1, 1); else NRG_RK(1, 2); else NRG_RK(1, 4); else NRG_RK(2, 1); else NRG_RK(2, 2); else NRG_RK(2, 4);
+    else NRG_RK(4, 1); else NRG_RK(4, 2); else NRG_RK(4, 4);
+#undef NRG_RK
+    return hipGetLastError();
+}
+
+static void deferred_jobs(nrg_ctx* c, ApplyJob& aj, ReadJob& rj) {
+    aj = ApplyJob{};
+    rj = ReadJob{};
+    const HmDeferred& p = c->pend;
+    if (!p.valid) return;
+    aj.rec = ring_src(c, p.src, p.lo);
+    aj.n = p.n;
+    aj.put_slot = c->d_put_slot[p.epoch & 1];
+    aj.epoch = p.epoch;
+    rj.rec = aj.rec;
+    rj.keys = p.keys;
+    rj.R = p.R;
+    rj.vals = p.vals;
+    rj.found = p.found;
+    rj.epoch = p.epoch;
+}
+
+hipError_t hm_flush(nrg_ctx* c) {
+    if (!c->pend.valid) return hipSuccess;
+    IndexJob ij{};
+    ApplyJob aj;
+    ReadJob rj;
+    deferred_jobs(c, aj, rj);
+    c->pend.valid = false;
+    return launch(c, ij, aj, rj);
+}
+
+// Reads against the current state (no writes): attached to the deferred round if it has none.
+static hipError_t hm_reads(nrg_ctx* c, const u64* keys, u64 R, u64* vals, uint8_t* found) {
+    if (R == 0) return hipSuccess;
+    if (c->pend.valid && c->pend.R == 0) {
+        c->pend.keys = keys;
+        c->pend.R = R;
+        c->pend.vals = vals;
+        c->pend.found = found;
+        return hm_flush(c);
+    }
+    hipError_t e = hm_flush(c);
+    if (e != hipSuccess) return e;
+    IndexJob ij{};
+    ApplyJob aj{};
+    ReadJob rj{};
+    rj.keys = keys;
+    rj.R = R;
+    rj.vals = vals;
+    rj.found = found;
+    rj.epoch = c->epoch;  // every earlier round is applied: values come from the slots
+    return launch(c, ij, aj, rj);
+}
+
 hipError_t hm_init(nrg_ctx* c) {
     hm_init_table_kernel<<<grid_for(c->slots, 16384), TPB, 0, c->stream>>>(c->d_table, c->slots);
     return hipGetLastError();
 }
 
-hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool write_ring,
-                           const u64* d_get_keys, u64 R, u64* d_get_vals, uint8_t* d_get_found, u64 resp_lo,
-                           u64 resp_hi, u64* d_prev, uint8_t* d_prev_found, bool touch_log) {
-    hipStream_t st = c->stream;
-    const u64 ring_mask = c->log_size - 1;
-    const u64 tmask = c->slots - 1;
-    nrg_put* ring = (nrg_put*)c->d_ring;
-    const nrg_put* src = (const nrg_put*)src_recs;
+// Replay the records [lo, lo+n) (from `src_recs` if given, else from the ring; writing the
+// ring copy if write_ring) and answer R reads against the state after them.
+hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool write_ring, const u64* d_get_keys,
+                           u64 R, u64* d_get_vals, uint8_t* d_get_found, u64 resp_lo, u64 resp_hi, u64* d_prev,
+                           uint8_t* d_prev_found, bool touch_log) {
     (void)touch_log;
-    const u32 epoch = n > 0 ? ++c->epoch : c->epoch;
-    if (n > 0) {
-        timer_begin(c, "hm_index", st);
-#define NRG_K1(IT)                                                                                            \
-    hm_index_kernel<IT><<<(unsigned)((n + TPB * IT - 1) / (TPB * IT)), TPB, 0, st>>>(                           \
-        src, ring, ring_mask, lo, n, write_ring ? 1 : 0, c->d_table, c->slot_shift, tmask, c->d_put_slot, c->d_ctl, \
-        epoch)
-        if (c->k1_items >= 4)
-            NRG_K1(4);
-        else if (c->k1_items == 2)
-            NRG_K1(2);
-        else
-            NRG_K1(1);
-#undef NRG_K1
-        timer_end(c, "hm_index", st);
-        if (d_prev && resp_lo < lo + n && resp_hi > lo) {
-            u32 *sk = nullptr, *sv = nullptr;
-            timer_begin(c, "hm_prev", st);
-            // slot ids < 2^log2_slots; the side-slot key (0xFFFFFFFF) sorts last
-            hipError_t e = sort_pairs(c->sort, c->d_put_slot, nullptr, n, 32, st, &sk, &sv);
-            if (e != hipSuccess) return e;
-            hm_prev_kernel<<<(unsigned)((n + TPB - 1) / TPB), TPB, 0, st>>>(
-                sk, sv, n, src, ring, ring_mask, lo, c->d_table, c->d_ctl, epoch, resp_lo, resp_hi, d_prev,
-                d_prev_found);
-            timer_end(c, "hm_prev", st);
-        }
+    if (n == 0) return hm_reads(c, d_get_keys, R, d_get_vals, d_get_found);
+    const nrg_put* src = (const nrg_put*)src_recs;
+    const u32 epoch = ++c->epoch;
+    IndexJob ij{};
+    ij.rec = ring_src(c, src, lo);
+    ij.ring_out = write_ring ? (nrg_put*)c->d_ring : nullptr;
+    ij.n = n;
+    ij.put_slot = c->d_put_slot[epoch & 1];
+    ij.epoch = epoch;
+    ApplyJob aj;
+    ReadJob rj;
+    deferred_jobs(c, aj, rj);  // the previous round's second half rides along
+    c->pend.valid = false;
+    hipError_t e = launch(c, ij, aj, rj);
+    if (e != hipSuccess) return e;
+    // records of this round for its deferred half: the ring copy if there is one
+    const nrg_put* keep = (src && !write_ring) ? src : nullptr;
+    if (d_prev && resp_lo < lo + n && resp_hi > lo) {
+        u32 *sk = nullptr, *sv = nullptr;
+        timer_begin(c, "hm_prev", c->stream);
+        // slot ids < 2^31; the side-slot (0xFFFFFFFF) and full (0xFFFFFFFE) markers sort last
+        e = sort_pairs(c->sort, c->d_put_slot[epoch & 1], nullptr, n, 32, c->stream, &sk, &sv);
+        if (e != hipSuccess) return e;
+        hm_prev_kernel<<<(unsigned)((n + TPB - 1) / TPB), TPB, 0, c->stream>>>(
+            sk, sv, n, ring_src(c, keep, lo), c->d_table, c->d_ctl, epoch, resp_lo, resp_hi, d_prev, d_prev_found);
+        timer_end(c, "hm_prev", c->stream);
     }
-    hipError_t e;
-    if (n > 0) {
-        // values of this round may only be stored once the previous round's reads (possibly
-        // still running on the side stream) are done with the old ones
-        if ((e = side_join(c)) != hipSuccess) return e;
-        timer_begin(c, "hm_apply", st);
-        hm_apply_kernel<<<grid_for(n, 1024), TPB, 0, st>>>(src, ring, ring_mask, lo, n, c->d_put_slot, c->d_table,
-                                                           c->d_ctl, epoch);
-        timer_end(c, "hm_apply", st);
-    }
-    if (R > 0) {
-        // Reads of this round run on the side stream when pipelining, so that they overlap the
-        // next round's hm_index (which only claims slots and raises stamps, see hm_get_kernel).
-        hipStream_t gs = st;
-        if (c->pipeline) {
-            if ((e = hipEventRecord(c->ev_applied, st)) != hipSuccess) return e;
-            if ((e = hipStreamWaitEvent(c->side_stream, c->ev_applied, 0)) != hipSuccess) return e;
-            gs = c->side_stream;
-        }
-        const u32 G = c->gets_per_thread >= 4 ? 4 : (c->gets_per_thread == 2 ? 2 : 1);
-        const unsigned gb = (unsigned)((R + TPB * G - 1) / (TPB * G));
-        timer_begin(c, "hm_get", gs);
-        if (G == 4)
-            hm_get_kernel<4><<<gb, TPB, 0, gs>>>(c->d_table, c->slot_shift, tmask, c->d_ctl, epoch, d_get_keys, R,
-                                                d_get_vals, d_get_found);
-        else if (G == 2)
-            hm_get_kernel<2><<<gb, TPB, 0, gs>>>(c->d_table, c->slot_shift, tmask, c->d_ctl, epoch, d_get_keys, R,
-                                                d_get_vals, d_get_found);
-        else
-            hm_get_kernel<1><<<gb, TPB, 0, gs>>>(c->d_table, c->slot_shift, tmask, c->d_ctl, epoch, d_get_keys, R,
-                                                d_get_vals, d_get_found);
-        timer_end(c, "hm_get", gs);
-        if (c->pipeline) {
-            if ((e = hipEventRecord(c->ev_reads_done, gs)) != hipSuccess) return e;
-            c->side_pending = true;
-        }
-    }
+    HmDeferred& p = c->pend;
+    p.valid = true;
+    p.epoch = epoch;
+    p.src = keep;
+    p.lo = lo;
+    p.n = n;
+    p.keys = d_get_keys;
+    p.R = R;
+    p.vals = d_get_vals;
+    p.found = d_get_found;
+    if (!c->pipeline || keep) return hm_flush(c);
     return hipGetLastError();
 }
 
-hipError_t side_join(nrg_ctx* c) {
-    if (!c->side_pending) return hipSuccess;
-    c->side_pending = false;
-    return hipStreamWaitEvent(c->stream, c->ev_reads_done, 0);
-}
-
 hipError_t hm_get_only(nrg_ctx* c, const u64* d_keys, u64 n, u64* d_vals, uint8_t* d_found) {
-    if (n == 0) return hipSuccess;
-    return hm_replay_chunk(c, nullptr, 0, 0, false, d_keys, n, d_vals, d_found, 0, 0, nullptr, nullptr, false);
+    return hm_reads(c, d_keys, n, d_vals, d_found);
 }
 
 hipError_t hm_prefill_range(nrg_ctx* c, u64 n, u64 off) {
-    hipError_t e = side_join(c);
+    hipError_t e = hm_flush(c);
     if (e != hipSuccess) return e;
+    // a fresh epoch: later reads see these values in the slots, not an older round's record
+    const u32 epoch = ++c->epoch;
     hm_prefill_range_kernel<<<grid_for(n, 8192), TPB, 0, c->stream>>>(c->d_table, n, off, c->slot_shift,
-                                                                      c->slots - 1, c->d_ctl, c->epoch);
+                                                                      c->slots - 1, c->d_ctl, epoch);
     return hipGetLastError();
 }
 
 hipError_t hm_dump(nrg_ctx* c, u64* d_keys, u64* d_vals) {
-    hipError_t e = hipMemsetAsync(&c->d_ctl->counter, 0, sizeof(u64), c->stream);
+    hipError_t e = hm_flush(c);
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(&c->d_ctl->counter, 0, sizeof(u64), c->stream);
     if (e != hipSuccess) return e;
     hm_dump_kernel<<<grid_for(c->slots, 8192), TPB, 0, c->stream>>>(c->d_table, c->slots, c->d_ctl, d_keys, d_vals);
     return hipGetLastError();
 }
 
 hipError_t hm_digest(nrg_ctx* c, u64* d_out3) {
-    hipError_t e = hipMemsetAsync(d_out3, 0, 3 * sizeof(u64), c->stream);
+    hipError_t e = hm_flush(c);
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(d_out3, 0, 3 * sizeof(u64), c->stream);
     if (e != hipSuccess) return e;
     hm_digest_kernel<<<grid_for(c->slots, 8192), TPB, 0, c->stream>>>(c->d_table, c->slots, c->d_ctl, d_out3);
     return hipGetLastError();

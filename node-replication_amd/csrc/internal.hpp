@@ -1,6 +1,7 @@
 // internal.hpp — host-side structures shared by the runtime and the kernel launchers.
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -35,11 +36,24 @@ struct KTimer {
     u64 pending = 0;             // recorded pairs not yet harvested
     u64 launches = 0;
     double total_ms = 0.0;
+    u64 seen = 0;                // launches of this kernel since timing was enabled
 };
 
 struct Staging {  // growable device scratch for the host-pointer entry points
     void* p = nullptr;
     uint64_t bytes = 0;
+};
+
+// The apply + read half of a replayed hashmap round, kept for the next launch.
+struct HmDeferred {
+    bool valid = false;
+    u32 epoch = 0;
+    const nrg_put* src = nullptr;  // records of the round: src[i] if set, else ring[(lo + i) & mask]
+    u64 lo = 0, n = 0;
+    const u64* keys = nullptr;  // the round's reads (R may be 0)
+    u64 R = 0;
+    u64* vals = nullptr;
+    uint8_t* found = nullptr;
 };
 
 struct HostRun {  // origin tags of appended log ranges (the Entry::replica field)
@@ -68,17 +82,15 @@ struct nrg_ctx {
     uint32_t slot_shift = 0;  // 64 - log2_slots
     uint64_t slots = 0;
     nrg::Slot* d_table = nullptr;
-    uint32_t* d_put_slot = nullptr;  // per Put of the round: its table slot
+    uint32_t* d_put_slot[2] = {nullptr, nullptr};  // per Put of a round: its slot (by epoch parity)
     uint32_t epoch = 0;              // replay rounds so far (stamps carry the round's epoch)
-    uint32_t k1_items = 1;           // Puts per thread in hm_index (tuning knob NRG_K1_ITEMS)
-    uint32_t gets_per_thread = 1;    // Gets per thread in hm_get (tuning knob NRG_GETS)
-    // round pipelining: a round's reads run on side_stream, overlapping the next round's index
+    uint32_t k1_items = 1;           // Puts per thread in the index role (tuning knob NRG_K1_ITEMS)
+    uint32_t gets_per_thread = 1;    // Gets per thread in the read role (tuning knob NRG_GETS)
+    // Deferred second half of the last replayed round (apply its values, answer its reads):
+    // launched together with the next round's index pass, or by nrg_join / nrg_sync / any call
+    // that reads the table. With pipeline == false it is flushed at the end of every call.
     bool pipeline = false;
-    hipStream_t side_stream = nullptr;
-    hipEvent_t ev_applied = nullptr;     // main stream: round's values stored
-    hipEvent_t ev_reads_done = nullptr;  // side stream: round's reads finished
-    bool side_pending = false;           // ev_reads_done not yet joined into the main stream
-
+    nrg::HmDeferred pend;
     // ---- Stack ----
     uint32_t* d_stack = nullptr;
     uint32_t stack_key_bits = 0;
@@ -99,6 +111,7 @@ struct nrg_ctx {
 
     // ---- timing ----
     bool timing = false;
+    uint32_t timing_every = 1;  // event-stamp every n-th launch (nrg_kernel_timing(ctx, n))
     std::string timing_only;  // if non-empty, only this kernel is timed
     std::map<std::string, nrg::KTimer> timers;
 };
@@ -107,8 +120,22 @@ namespace nrg {
 // timing helpers (runtime.cpp)
 void timer_begin(nrg_ctx* c, const char* name, hipStream_t s = nullptr);
 void timer_end(nrg_ctx* c, const char* name, hipStream_t s = nullptr);
-// make the main stream wait for reads still running on the side stream
-hipError_t side_join(nrg_ctx* c);
+// Event pair for one launch of kernel `name` when it is being timed (false otherwise). The
+// pair is passed to hipExtLaunchKernelGGL, which stamps it from the kernel's own dispatch:
+// no marker packets between kernels, so timing does not perturb the timed stream.
+bool timer_events(nrg_ctx* c, const char* name, hipEvent_t* start, hipEvent_t* stop);
+
+#define NRG_LAUNCH(CTX, NAME, KERNEL, GRID, BLOCK, SHMEM, STREAM, ...)                                  \
+    do {                                                                                                \
+        hipEvent_t nrg_e0_, nrg_e1_;                                                                    \
+        if (timer_events((CTX), (NAME), &nrg_e0_, &nrg_e1_))                                            \
+            hipExtLaunchKernelGGL((KERNEL), dim3(GRID), dim3(BLOCK), (SHMEM), (STREAM), nrg_e0_, nrg_e1_, 0, \
+                                  __VA_ARGS__);                                                         \
+        else                                                                                            \
+            KERNEL<<<(GRID), (BLOCK), (SHMEM), (STREAM)>>>(__VA_ARGS__);                                \
+    } while (0)
+// launch the deferred apply + reads of the last hashmap round, if any (hashmap.hip)
+hipError_t hm_flush(nrg_ctx* c);
 
 // hashmap.hip
 hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool write_ring,

@@ -68,9 +68,19 @@ int use_device(nrg_ctx* c) {
     return NRG_OK;
 }
 
-// wait for everything queued on this replica, including reads on the side stream
+// the deferred half of the last hashmap round (hashmap.hip), launched now if there is one
+hipError_t hm_flush_if(nrg_ctx* c) { return c->cfg.ds_kind == NRG_DS_HASHMAP ? hm_flush(c) : hipSuccess; }
+
+// Log GC boundary: the slowest replica's tail (this replica's ltail), held back to the first
+// record of a deferred hashmap round, whose apply still reads its records from the ring.
+uint64_t gc_head(const nrg_ctx* c) {
+    if (c->pend.valid && !c->pend.src && c->pend.lo < c->ltail) return c->pend.lo;
+    return c->ltail;
+}
+
+// wait for everything queued on this replica, including a deferred hashmap round
 hipError_t sync_all(nrg_ctx* c) {
-    hipError_t e = side_join(c);
+    hipError_t e = hm_flush_if(c);
     if (e != hipSuccess) return e;
     return hipStreamSynchronize(c->stream);
 }
@@ -84,7 +94,6 @@ int check_err(nrg_ctx* c) {
         HIPCHK(hipMemcpyAsync(&c->d_ctl->err, &z, sizeof(z), hipMemcpyHostToDevice, c->stream));
         HIPCHK(sync_all(c));
         if (err & ERR_TABLE_FULL) return NRG_E_TABLE_FULL;
-        if (err & ERR_BLT_FULL) return NRG_E_CAPACITY;
         if (err & ERR_CAPACITY) return NRG_E_CAPACITY;
         return NRG_E_HIP;
     }
@@ -123,11 +132,12 @@ int exec_range(nrg_ctx* c, uint64_t resp_lo, uint64_t resp_hi, void* d_resp, uin
 int reserve(nrg_ctx* c, uint64_t n) {
     if (n > c->log_size - GC_FROM_HEAD) return NRG_E_RING_FULL;
     if (c->tail + n > c->head + c->log_size - GC_FROM_HEAD) {
-        c->head = c->ltail;
+        c->head = gc_head(c);
         if (c->tail + n > c->head + c->log_size - GC_FROM_HEAD) {
             int r = exec_range(c, 0, 0, nullptr, nullptr);
             if (r != NRG_OK) return r;
-            c->head = c->ltail;
+            HIPCHK(hm_flush_if(c));
+            c->head = gc_head(c);
         }
     }
     return NRG_OK;
@@ -186,6 +196,22 @@ void timer_begin(nrg_ctx* c, const char* name, hipStream_t s) {
         t.ev.push_back(e);
     }
     (void)hipEventRecord(t.ev[idx], s ? s : c->stream);
+}
+bool timer_events(nrg_ctx* c, const char* name, hipEvent_t* start, hipEvent_t* stop) {
+    if (!c->timing || (!c->timing_only.empty() && c->timing_only != name)) return false;
+    KTimer& t = c->timers[name];
+    // sampled: launches every-1, 2*every-1, ... (skips a stream's first launch when every > 1)
+    if (++t.seen % c->timing_every != 0) return false;
+    const size_t idx = t.pending * 2;
+    while (t.ev.size() < idx + 2) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return false;
+        t.ev.push_back(e);
+    }
+    *start = t.ev[idx];
+    *stop = t.ev[idx + 1];
+    t.pending++;
+    return true;
 }
 void timer_end(nrg_ctx* c, const char* name, hipStream_t s) {
     if (!c->timing || (!c->timing_only.empty() && c->timing_only != name)) return;
@@ -292,16 +318,12 @@ int nrg_open(int dev, const nrg_config* cfg_in, nrg_ctx** out) {
         c->slot_shift = 64 - cf.log2_slots;
         OPEN_CHK(hipMalloc(&c->d_table, c->slots * sizeof(Slot)));
         OPEN_CHK(hm_init(c));
-        OPEN_CHK(hipMalloc(&c->d_put_slot, mb * sizeof(uint32_t)));
+        OPEN_CHK(hipMalloc(&c->d_put_slot[0], mb * sizeof(uint32_t)));
+        OPEN_CHK(hipMalloc(&c->d_put_slot[1], mb * sizeof(uint32_t)));
         if (const char* e = std::getenv("NRG_K1_ITEMS")) c->k1_items = (uint32_t)std::atoi(e);
         if (const char* e = std::getenv("NRG_GETS")) c->gets_per_thread = (uint32_t)std::atoi(e);
         c->pipeline = cf.pipeline != 0;
         if (const char* e = std::getenv("NRG_PIPELINE")) c->pipeline = std::atoi(e) != 0;
-        if (c->pipeline) {
-            OPEN_CHK(hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking));
-            OPEN_CHK(hipEventCreateWithFlags(&c->ev_applied, hipEventDisableTiming));
-            OPEN_CHK(hipEventCreateWithFlags(&c->ev_reads_done, hipEventDisableTiming));
-        }
         c->epoch = 1;  // epoch 1 = the state built by prefill; replay rounds start at 2
         if (sort_alloc(c->sort, mb) != NRG_OK) { nrg_close(c); return NRG_E_NOMEM; }
     } else if (cf.ds_kind == NRG_DS_STACK) {
@@ -342,14 +364,8 @@ int nrg_close(nrg_ctx* c) {
     g_dev_set = c->device;
     if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
     if (c->stream && c->stream != c->own_stream) (void)hipStreamSynchronize(c->stream);
-    if (c->side_stream) {
-        (void)hipStreamSynchronize(c->side_stream);
-        (void)hipStreamDestroy(c->side_stream);
-    }
-    if (c->ev_applied) (void)hipEventDestroy(c->ev_applied);
-    if (c->ev_reads_done) (void)hipEventDestroy(c->ev_reads_done);
-    void* ptrs[] = {c->d_ring,  c->d_ctl,      c->d_table,   c->d_put_slot, c->d_stack,
-                    c->d_words, c->d_sort_aux, c->d_tmp_u64, c->d_scan_desc};
+    void* ptrs[] = {c->d_ring,    c->d_ctl,      c->d_table,   c->d_put_slot[0], c->d_put_slot[1],
+                    c->d_stack,   c->d_words,    c->d_sort_aux, c->d_tmp_u64,    c->d_scan_desc};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     sort_free(c->sort);
@@ -365,8 +381,11 @@ int nrg_close(nrg_ctx* c) {
 
 int nrg_set_stream(nrg_ctx* c, void* s) {
     if (!c) return NRG_E_INVAL;
+    // deferred hashmap work belongs to the old stream: launch it there first
+    hipError_t e = hm_flush_if(c);
+    if (e != hipSuccess) return hip_fail(e);
     c->stream = s ? (hipStream_t)s : c->own_stream;
-    return hip_fail(side_join(c));  // the new stream inherits reads still in flight
+    return NRG_OK;
 }
 
 void* nrg_get_stream(nrg_ctx* c) { return c ? (void*)c->stream : nullptr; }
@@ -383,7 +402,7 @@ int nrg_join(nrg_ctx* c) {
     if (!c) return NRG_E_INVAL;
     int r = use_device(c);
     if (r) return r;
-    HIPCHK(side_join(c));
+    HIPCHK(hm_flush_if(c));
     return NRG_OK;
 }
 
@@ -520,7 +539,6 @@ int nrg_hashmap_get(nrg_ctx* c, const uint64_t* keys, uint64_t n, uint64_t* vals
     if ((r = staging(c, s[0], n * 8)) || (r = staging(c, s[1], n * 8)) || (r = staging(c, s[2], n))) return r;
     HIPCHK(hipMemcpyAsync(s[0].p, keys, n * 8, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hm_get_only(c, (u64*)s[0].p, n, (u64*)s[1].p, (uint8_t*)s[2].p));
-    HIPCHK(side_join(c));  // the reads may have run on the side stream (config.pipeline)
     HIPCHK(hipMemcpyAsync(vals, s[1].p, n * 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipMemcpyAsync(found, s[2].p, n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(sync_all(c));
@@ -810,8 +828,10 @@ int nrg_gen_puts_async(nrg_ctx* c, nrg_put* d, const uint64_t* k, const uint64_t
 
 // ---- kernel timing -------------------------------------------------------------------------------
 int nrg_kernel_timing(nrg_ctx* c, int enable) {
-    if (!c) return NRG_E_INVAL;
+    if (!c || enable < 0) return NRG_E_INVAL;
     c->timing = enable != 0;
+    c->timing_every = enable > 1 ? (uint32_t)enable : 1;
+    for (auto& kv : c->timers) kv.second.seen = 0;
     return NRG_OK;
 }
 

@@ -244,9 +244,10 @@ class DeviceReplica:
     def gen_puts_device(self, d_out, d_keys, d_vals, n):
         L.check(self._lib.nrg_gen_puts_async(self._h, _dptr(d_out), _dptr(d_keys), _dptr(d_vals), n))
 
-    def kernel_timing(self, enable: bool = True, only: Optional[str] = None):
+    def kernel_timing(self, enable: bool = True, only: Optional[str] = None, every: int = 1):
+        """HIP-event timing of kernel `only` (all if None), on every `every`-th launch."""
         L.check(self._lib.nrg_kernel_timing_only(self._h, (only or "").encode()))
-        L.check(self._lib.nrg_kernel_timing(self._h, int(enable)))
+        L.check(self._lib.nrg_kernel_timing(self._h, max(1, int(every)) if enable else 0))
 
     def kernel_time(self, name: str):
         n = C.c_uint64()

@@ -70,6 +70,27 @@ def main():
             lines.append("%-28s %8s %11.3f %11.3f %14s %14s" % (
                 k[:28], r["Calls"], float(r["AverageNs"]) / 1e3, float(r["MinNs"]) / 1e3,
                 "%.1f" % (2 * fe[1]) if fe else "-", "%.1f" % wr[1] if wr else "-"))
+    # HBM traffic per launch of the round kernel, for bench.py's roofline.traffic
+    tk = None
+    try:
+        tk = json.loads(txt[-1])["roofline"].get("traffic_key")
+    except (NameError, ValueError, KeyError, IndexError):
+        pass
+    fe = next((v for k, v in fetch.items() if "hm_round_kernel" in k), None)
+    wr = next((v for k, v in write.items() if "hm_round_kernel" in k), None)
+    if tk and fe and wr:
+        tpath = os.path.join(os.path.dirname(os.path.abspath(out)), "traffic_hm_round.json")
+        try:
+            with open(tpath) as f:
+                tj = json.load(f)
+        except (OSError, ValueError):
+            tj = {}
+        tj[tk] = {"bytes_per_launch": int((2 * fe[1] + wr[1]) * 1024), "fetch_x2_bytes": int(2 * fe[1] * 1024),
+                  "write_bytes": int(wr[1] * 1024), "launches": fe[0], "source": os.path.basename(out)}
+        with open(tpath, "w") as f:
+            json.dump(tj, f, indent=1, sort_keys=True)
+        lines.append("traffic per hm_round launch: %.1f MB (FETCH_SIZE x2 %.1f MB + WRITE_SIZE %.1f MB) -> %s" % (
+            (2 * fe[1] + wr[1]) * 1024 / 1e6, 2 * fe[1] * 1024 / 1e6, wr[1] * 1024 / 1e6, tpath))
     text = "\n".join(lines) + "\n"
     with open(out, "w") as f:
         f.write(text)
