@@ -142,6 +142,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-prev-variant", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true", help="diagnostic: no HIP events in the timed region")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo: CPU rehearsal)")
+    ap.add_argument("--share-gpu", action="store_true", help="all ranks on cuda:0 (gloo rehearsal on a 1-GPU box)")
     ap.add_argument("--timing-every", type=int, default=8, help="event-stamp every n-th hm_round launch")
     ap.add_argument("--pipeline", type=int, default=1,
                     help="1: a round's apply+reads ride in the next round's launch (nrg_config.pipeline); "
@@ -156,10 +159,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
+    if args.share_gpu:
+        local = 0  # rehearsal of the N > 1 path with every rank on the box's one GPU (gloo only)
     torch.cuda.set_device(local)
     dev_t = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev_t)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev_t)  # RCCL over xGMI
+        else:
+            dist.init_process_group("gloo")
 
     import nrgpu
     from nrgpu import _lib as L
@@ -218,17 +226,22 @@ def main():
             if rc:
                 L.check(rc, "nrg_hashmap_round_async")
         else:
-            pv = pvals if prev else None
-            pf = pfound if prev else None
-            group.round(puts[p, :W], gkeys[p, :R], gvals, gfound, pv, pf, stride=W)
+            # the all-gather of round i+1 is in flight while round i replays
+            g = gathered.pop(i) if i in gathered else group.gather_async(puts[p, :W], stride=W)
+            if i + 1 < n_steps[0]:
+                gathered[i + 1] = group.gather_async(puts[(i + 1) % P, :W], stride=W)
+            group.replay(g, gkeys[p, :R], gvals, gfound, pvals if prev else None, pfound if prev else None)
 
     host_s = [0.0]
+    gathered = {}
+    n_steps = [0]
 
     def timed(n, prev=False):
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t = time.perf_counter()
+        n_steps[0] = n
         for i in range(n):
             step(i, prev)
         rep.join()  # launches the last round's deferred apply + reads: inside the timed region
@@ -243,6 +256,7 @@ def main():
             el = float(x.item())
         return el
 
+    n_steps[0] = args.warmup
     for i in range(args.warmup):
         step(i)
     rep.sync()

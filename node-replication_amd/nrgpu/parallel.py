@@ -20,8 +20,31 @@ import torch
 import torch.distributed as dist
 
 
+class Gathered:
+    """One round's all-gathered write log (in flight until wait())."""
+
+    __slots__ = ("buf", "work", "stride", "lens")
+
+    def __init__(self, buf, work, stride, lens):
+        self.buf, self.work, self.stride, self.lens = buf, work, stride, lens
+
+    def wait(self):
+        if self.work is not None:
+            self.work.wait()  # nccl: the current stream waits for the collective (host does not block)
+            self.work = None
+
+
 class ReplicatedHashMap:
-    """Drives one NrHashMap replica per rank through rounds of (write segment, reads)."""
+    """Drives one NrHashMap replica per rank through rounds of (write segment, reads).
+
+    round() = gather_async() + replay(). Callers that know the next round's writes early call
+    gather_async(next) before replay(current): the all-gather of round e+1 then runs on the
+    collective stream while round e replays (the replica's kernels copy the gathered records
+    into their own log ring, so a gathered buffer is free once its replay was enqueued; torch's
+    ProcessGroupNCCL orders each collective after the work already on the current stream).
+    """
+
+    NBUF = 3  # gathered-log buffers in rotation
 
     def __init__(self, replica, group: Optional[dist.ProcessGroup] = None, device: Optional[torch.device] = None):
         self.replica = replica
@@ -30,16 +53,17 @@ class ReplicatedHashMap:
         self.world = dist.get_world_size(group)
         self.device = device if device is not None else torch.device("cpu")
         self.backend = dist.get_backend(group)
-        self._buf = None
+        self._bufs = [None] * self.NBUF
+        self._next = 0
 
-    def _gather(self, seg: torch.Tensor, stride: int) -> torch.Tensor:
-        """All-gather fixed-stride segments ([stride, 2] int64 each) into [world*stride, 2]."""
-        need = self.world * stride * 2
-        if self._buf is None or self._buf.numel() < need or self._buf.device != seg.device:
-            self._buf = torch.empty(need, dtype=torch.int64, device=seg.device)
-        out = self._buf[:need]
-        dist.all_gather_into_tensor(out, seg.reshape(-1), group=self.group)
-        return out.view(self.world * stride, 2)
+    def _buf(self, need: int, device) -> torch.Tensor:
+        i = self._next
+        self._next = (i + 1) % self.NBUF
+        b = self._bufs[i]
+        if b is None or b.numel() < need or b.device != device:
+            b = torch.empty(need, dtype=torch.int64, device=device)
+            self._bufs[i] = b
+        return b[:need]
 
     def exchange_lengths(self, W: int):
         t = torch.tensor([W], dtype=torch.int64, device=self.device if self.backend == "nccl" else "cpu")
@@ -47,15 +71,9 @@ class ReplicatedHashMap:
         dist.all_gather(out, t, group=self.group)
         return [int(x.item()) for x in out]
 
-    def round(self, puts: torch.Tensor, get_keys: torch.Tensor, get_vals: torch.Tensor, get_found: torch.Tensor,
-              prev: Optional[torch.Tensor] = None, prev_found: Optional[torch.Tensor] = None,
-              stride: Optional[int] = None, lens=None):
-        """One NR round.
-
-        puts: [W, 2] int64 (key, value) on this rank's device, in this rank's issue order.
-        stride: segment capacity (fixed-size rounds skip the length exchange); lens: the
-        per-rank segment lengths if already known.
-        """
+    def gather_async(self, puts: torch.Tensor, stride: Optional[int] = None, lens=None) -> Gathered:
+        """Start the all-gather of this rank's write segment ([W, 2] int64 (key, value), in issue
+        order). Fixed-size rounds pass `stride` (segment capacity) and skip the length exchange."""
         W = puts.shape[0]
         if lens is None:
             lens = [W] * self.world if stride is not None else self.exchange_lengths(W)
@@ -65,11 +83,30 @@ class ReplicatedHashMap:
         if W < stride:
             seg = torch.zeros((stride, 2), dtype=torch.int64, device=puts.device)
             seg[:W] = puts
+        seg = seg.reshape(-1)
+        need = self.world * stride * 2
         if self.backend == "gloo" and seg.device.type != "cpu":
-            gathered = self._gather(seg.cpu(), stride).to(seg.device)
-        else:
-            gathered = self._gather(seg.contiguous(), stride)
+            out = self._buf(need, torch.device("cpu"))
+            dist.all_gather_into_tensor(out, seg.cpu(), group=self.group)
+            return Gathered(out.to(seg.device), None, stride, lens)
+        out = self._buf(need, seg.device)
+        work = dist.all_gather_into_tensor(out, seg.contiguous(), group=self.group, async_op=True)
+        return Gathered(out, work, stride, lens)
+
+    def replay(self, g: Gathered, get_keys: torch.Tensor, get_vals: torch.Tensor, get_found: torch.Tensor,
+               prev: Optional[torch.Tensor] = None, prev_found: Optional[torch.Tensor] = None):
+        """Append the gathered segments in rank order (the round's global log order), replay them,
+        answer this rank's reads against the post-round state; Put responses (prev) only for this
+        rank's own segment (nr/src/replica.rs:576-578)."""
+        g.wait()
         origins = [r + 1 for r in range(self.world)]  # replica ids start at 1 (nr/src/log.rs:272-292)
-        self.replica.hm_round_segments_device(gathered, stride, lens, origins, self.rank, get_keys,
+        self.replica.hm_round_segments_device(g.buf, g.stride, g.lens, origins, self.rank, get_keys,
                                               get_keys.shape[0], get_vals, get_found, prev, prev_found)
-        return gathered
+
+    def round(self, puts: torch.Tensor, get_keys: torch.Tensor, get_vals: torch.Tensor, get_found: torch.Tensor,
+              prev: Optional[torch.Tensor] = None, prev_found: Optional[torch.Tensor] = None,
+              stride: Optional[int] = None, lens=None):
+        """One NR round: puts [W, 2] int64 (key, value) on this rank's device, in issue order."""
+        g = self.gather_async(puts, stride, lens)
+        self.replay(g, get_keys, get_vals, get_found, prev, prev_found)
+        return g.buf.view(-1, 2)

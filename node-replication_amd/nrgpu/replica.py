@@ -114,9 +114,12 @@ class DeviceReplica:
         return first.value
 
     def log_append_segments(self, d_base, seg_stride: int, lens: Sequence[int], origins: Sequence[int]):
-        nseg = len(lens)
-        la = (C.c_uint64 * nseg)(*lens)
-        oa = (C.c_uint32 * nseg)(*origins)
+        key = (tuple(lens), tuple(origins))
+        if getattr(self, "_seg_key", None) != key:  # marshalled once per distinct round shape
+            nseg = len(lens)
+            self._seg_key = key
+            self._seg_arrays = ((C.c_uint64 * nseg)(*lens), (C.c_uint32 * nseg)(*origins), nseg)
+        la, oa, nseg = self._seg_arrays
         fa = (C.c_uint64 * nseg)()
         L.check(self._lib.nrg_log_append_segments_async(self._h, _dptr(d_base), nseg, seg_stride, la, oa, fa),
                 "append_segments")
@@ -161,9 +164,12 @@ class DeviceReplica:
 
     def hm_round_segments_device(self, d_base, seg_stride, lens, origins, resp_seg, d_get_keys, R, d_get_vals,
                                  d_get_found, d_prev=None, d_prev_found=None):
-        nseg = len(lens)
-        la = (C.c_uint64 * nseg)(*lens)
-        oa = (C.c_uint32 * nseg)(*origins)
+        key = (tuple(lens), tuple(origins))
+        if getattr(self, "_seg_key", None) != key:  # marshalled once per distinct round shape
+            nseg = len(lens)
+            self._seg_key = key
+            self._seg_arrays = ((C.c_uint64 * nseg)(*lens), (C.c_uint32 * nseg)(*origins), nseg)
+        la, oa, nseg = self._seg_arrays
         L.check(self._lib.nrg_hashmap_round_segments_async(
             self._h, _dptr(d_base), nseg, seg_stride, la, oa, resp_seg, _dptr(d_get_keys), R, _dptr(d_get_vals),
             _dptr(d_get_found), _dptr(d_prev), _dptr(d_prev_found)), "round_segments")
