@@ -19,12 +19,18 @@
 namespace nrg {
 
 constexpr int RS_TPB = 256;
-constexpr int RS_ITEMS = 8;
-constexpr int RS_TILE = RS_TPB * RS_ITEMS;
+constexpr int RS_TILE_MIN = RS_TPB * 2;  // smallest tile (RS_ITEMS = 2): sizes the descriptor array
+// Keys per thread. Measured on MI355X (100k keys): 2048-key tiles 10.3 us/pass, 512-key tiles
+// slower (the look-back is bound by agent-scope atomic latency, not by per-tile work).
+static inline int rs_items_for(u64 n) {
+    (void)n;
+    return 8;
+}
 constexpr u32 ST_AGG = 1u << 30;
 constexpr u32 ST_INC = 2u << 30;
 constexpr u32 ST_MASK = 3u << 30;
 constexpr u32 CNT_MASK = (1u << 30) - 1;
+constexpr int LB_WIN = 16;  // look-back window (descriptors loaded per step)
 constexpr u64 RS_HIST_WORDS = 4 * 256;
 constexpr u64 RS_TICKET_WORDS = 64;
 
@@ -68,10 +74,12 @@ __global__ __launch_bounds__(256) void rs_hist_kernel(const u32* __restrict__ ke
     }
 }
 
+template <int RS_ITEMS>
 __global__ __launch_bounds__(256) void rs_pass_kernel(const u32* __restrict__ kin, const u32* __restrict__ vin,
                                                       u32* __restrict__ kout, u32* __restrict__ vout, u64 n,
                                                       int shift, const u32* __restrict__ hist_p, u32* ticket,
                                                       u32* desc) {
+    constexpr int RS_TILE = RS_TPB * RS_ITEMS;
     __shared__ u32 s_k[RS_TILE];
     __shared__ u32 s_v[RS_TILE];
     __shared__ u32 s_wh[4 * 256];
@@ -139,17 +147,31 @@ __global__ __launch_bounds__(256) void rs_pass_kernel(const u32* __restrict__ ki
 
     u32 excl = 0;
     if (tile > 0) {
+        // Windowed look-back: LB_WIN predecessor descriptors are loaded together (independent
+        // loads in flight), then consumed newest-first until an inclusive one. A serial walk
+        // costs one memory round trip per predecessor tile; this costs one per LB_WIN.
         int tt = (int)tile - 1;
-        while (tt >= 0) {
-            const u32 v = __hip_atomic_load(desc + (u64)tt * 256 + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const u32 st = v & ST_MASK;
-            if (st == 0) {
-                __builtin_amdgcn_s_sleep(1);
-                continue;
+        for (;;) {
+            u32 v[LB_WIN];
+#pragma unroll
+            for (int q = 0; q < LB_WIN; q++)
+                v[q] = tt - q >= 0 ? __hip_atomic_load(desc + (u64)(tt - q) * 256 + d, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT)
+                                   : ST_INC;  // before tile 0: an inclusive zero
+            int used = 0;
+            bool done = false;
+#pragma unroll
+            for (int q = 0; q < LB_WIN; q++) {
+                if (done || used < q) continue;  // stopped earlier in the window
+                const u32 st = v[q] & ST_MASK;
+                if (st == 0) continue;  // not published yet: retry from here
+                excl += v[q] & CNT_MASK;
+                used = q + 1;
+                if (st == ST_INC) done = true;
             }
-            excl += v & CNT_MASK;
-            if (st == ST_INC) break;
-            tt--;
+            if (done) break;
+            tt -= used;
+            if (used < LB_WIN) __builtin_amdgcn_s_sleep(1);
         }
         __hip_atomic_store(my, ST_INC | (excl + tcnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -181,7 +203,7 @@ __global__ __launch_bounds__(256) void rs_pass_kernel(const u32* __restrict__ ki
 int sort_alloc(SortScratch& s, u64 cap) {
     if (cap == 0) cap = 1;
     s.cap = cap;
-    s.max_tiles = (cap + RS_TILE - 1) / RS_TILE;
+    s.max_tiles = (cap + RS_TILE_MIN - 1) / RS_TILE_MIN;
     s.ctl_words = RS_HIST_WORDS + RS_TICKET_WORDS + 4 * s.max_tiles * 256;
     for (int i = 0; i < 2; i++) {
         if (hipMalloc(&s.k[i], cap * 4) != hipSuccess) return NRG_E_NOMEM;
@@ -212,7 +234,9 @@ hipError_t sort_pairs(SortScratch& s, const u32* keys_in, const u32* vals_in, u6
     int passes = (key_bits + 7) / 8;
     if (passes < 1) passes = 1;
     if (passes > 4) passes = 4;
-    const u64 tiles = (n + RS_TILE - 1) / RS_TILE;
+    const int items = rs_items_for(n);
+    const u64 tile_keys = (u64)RS_TPB * items;
+    const u64 tiles = (n + tile_keys - 1) / tile_keys;
     const u64 words = RS_HIST_WORDS + RS_TICKET_WORDS + (u64)passes * tiles * 256;
     hipError_t e = hipMemsetAsync(s.ctlmem, 0, words * 4, st);
     if (e != hipSuccess) return e;
@@ -229,8 +253,16 @@ hipError_t sort_pairs(SortScratch& s, const u32* keys_in, const u32* vals_in, u6
     for (int p = 0; p < passes; p++) {
         u32* ko = s.k[p & 1];
         u32* vo = s.v[p & 1];
-        rs_pass_kernel<<<(unsigned)tiles, RS_TPB, 0, st>>>(kin, vin, ko, vo, n, 8 * p, hist + 256 * p,
-                                                          tickets + p, desc + (u64)p * tiles * 256);
+        u32* dsc = desc + (u64)p * tiles * 256;
+        if (items == 2)
+            rs_pass_kernel<2><<<(unsigned)tiles, RS_TPB, 0, st>>>(kin, vin, ko, vo, n, 8 * p, hist + 256 * p,
+                                                                 tickets + p, dsc);
+        else if (items == 4)
+            rs_pass_kernel<4><<<(unsigned)tiles, RS_TPB, 0, st>>>(kin, vin, ko, vo, n, 8 * p, hist + 256 * p,
+                                                                 tickets + p, dsc);
+        else
+            rs_pass_kernel<8><<<(unsigned)tiles, RS_TPB, 0, st>>>(kin, vin, ko, vo, n, 8 * p, hist + 256 * p,
+                                                                 tickets + p, dsc);
         kin = ko;
         vin = vo;
     }

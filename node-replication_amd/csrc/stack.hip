@@ -39,6 +39,7 @@ __device__ __forceinline__ long long fn_apply(Fn f, long long x) {
 constexpr u64 D_AGG = 1ull << 62;
 constexpr u64 D_INC = 2ull << 62;
 constexpr u64 D_MASK = 3ull << 62;
+constexpr int LB_WIN = 16;  // look-back window
 
 __device__ __forceinline__ u64 pack_agg(Fn f) {
     return D_AGG | ((u64)(f.b + (1ll << 30)) << 31) | (u64)f.a;
@@ -112,21 +113,33 @@ __global__ __launch_bounds__(ST_TPB) void st_scan_kernel(const nrg_stack_op* __r
                                __HIP_MEMORY_SCOPE_AGENT);
         } else {
             __hip_atomic_store(&desc[tile], pack_agg(tagg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // windowed look-back: LB_WIN predecessor descriptors per memory round trip,
+            // consumed newest-first (tile 0 always publishes an inclusive value)
             Fn acc = {0, 0};
             int tt = (int)tile - 1;
-            for (;;) {
-                const u64 v = __hip_atomic_load(&desc[tt], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const u64 st = v & D_MASK;
-                if (st == 0) {
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
+            bool done = false;
+            while (!done) {
+                u64 v[LB_WIN];
+#pragma unroll
+                for (int q = 0; q < LB_WIN; q++)
+                    v[q] = tt - q >= 0 ? __hip_atomic_load(&desc[tt - q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                       : 0ull;
+                int used = 0;
+#pragma unroll
+                for (int q = 0; q < LB_WIN; q++) {
+                    if (done || used < q) continue;
+                    const u64 st = v[q] & D_MASK;
+                    if (st == 0) continue;
+                    used = q + 1;
+                    if (st == D_INC) {
+                        dbase = fn_apply(acc, (long long)(v[q] & ~D_MASK));
+                        done = true;
+                    } else {
+                        acc = fn_then(unpack_agg(v[q]), acc);
+                    }
                 }
-                if (st == D_INC) {
-                    dbase = fn_apply(acc, (long long)(v & ~D_MASK));
-                    break;
-                }
-                acc = fn_then(unpack_agg(v), acc);
-                tt--;
+                tt -= used;
+                if (!done && used < LB_WIN) __builtin_amdgcn_s_sleep(1);
             }
             __hip_atomic_store(&desc[tile], D_INC | (u64)fn_apply(tagg, dbase), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);

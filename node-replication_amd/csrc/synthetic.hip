@@ -21,6 +21,7 @@ constexpr u32 SETBIT = 0x80000000u;
 constexpr int MS_TPB = 256;
 constexpr int MS_ITEMS = 8;
 constexpr int MS_TILE = MS_TPB * MS_ITEMS;
+constexpr int LB_WIN = 16;  // look-back window
 
 __global__ void sy_init_kernel(u64* words, u64 n) {
     for (u64 i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (u64)gridDim.x * 256ull) words[i] = i;
@@ -104,18 +105,28 @@ __global__ __launch_bounds__(MS_TPB) void sy_maxscan_kernel(const u32* __restric
             __hip_atomic_store(&desc[0], M_INC | tagg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
             __hip_atomic_store(&desc[tile], M_AGG | tagg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // windowed look-back: LB_WIN predecessor descriptors per memory round trip
             int tt = (int)tile - 1;
-            for (;;) {
-                const u64 v = __hip_atomic_load(&desc[tt], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const u64 st = v & M_MASK;
-                if (st == 0) {
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
+            bool done = false;
+            while (!done) {
+                u64 v[LB_WIN];
+#pragma unroll
+                for (int q = 0; q < LB_WIN; q++)
+                    v[q] = tt - q >= 0 ? __hip_atomic_load(&desc[tt - q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                       : 0ull;
+                int used = 0;
+#pragma unroll
+                for (int q = 0; q < LB_WIN; q++) {
+                    if (done || used < q) continue;
+                    const u64 st = v[q] & M_MASK;
+                    if (st == 0) continue;
+                    used = q + 1;
+                    const u32 x = (u32)v[q];
+                    pre = pre > x ? pre : x;
+                    if (st == M_INC) done = true;
                 }
-                const u32 x = (u32)v;
-                pre = pre > x ? pre : x;
-                if (st == M_INC) break;
-                tt--;
+                tt -= used;
+                if (!done && used < LB_WIN) __builtin_amdgcn_s_sleep(1);
             }
             const u32 ti = pre > tagg ? pre : tagg;
             __hip_atomic_store(&desc[tile], M_INC | ti, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
