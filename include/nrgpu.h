@@ -258,6 +258,14 @@ int nrg_gen_raw_async(nrg_ctx* ctx, uint64_t* d_out, uint64_t n, uint64_t seed);
 /* interleave: puts[i] = {keys[i], vals[i]} */
 int nrg_gen_puts_async(nrg_ctx* ctx, nrg_put* d_out, const uint64_t* d_keys, const uint64_t* d_vals,
                        uint64_t n);
+/* Zipf(theta) keys over [0, N) (Gray et al. SIGMOD'94 inverse CDF, ranks 1..N; scramble = 0:
+ * key = rank-1 so hot keys are adjacent, 1: key = mix64(rank) % N). Statistically identical to
+ * oracle/ orc_gen_zipf (device pow may differ from glibc's in the last ulp). theta != 1. */
+int nrg_gen_zipf_async(nrg_ctx* ctx, uint64_t* d_out, uint64_t n, uint64_t seed, uint64_t N, double theta,
+                       int scramble);
+/* Stack ops as benches/stack.rs:87-102 with a seeded stream: r = splitmix64_at(seed, i),
+ * op = r & 1 (1 = Push), val = r >> 32 (oracle/ orc_gen_stack_ops). */
+int nrg_gen_stack_ops_async(nrg_ctx* ctx, nrg_stack_op* d_out, uint64_t n, uint64_t seed);
 
 /* ---- timing: HIP events recorded around the dominant replay kernel -------------------- */
 /* enable = 0: off; 1: every launch; n > 1: every n-th launch (sampling keeps the timed stream

@@ -399,22 +399,6 @@ __global__ __launch_bounds__(TPB) void hm_digest_kernel(const Slot* __restrict__
     }
 }
 
-__global__ void gen_uniform_kernel(u64* out, u64 n, u64 seed, u64 span) {
-    for (u64 i = blockIdx.x * (u64)TPB + threadIdx.x; i < n; i += (u64)gridDim.x * TPB)
-        out[i] = mulhi64(sm64_at(seed, i), span);
-}
-__global__ void gen_raw_kernel(u64* out, u64 n, u64 seed) {
-    for (u64 i = blockIdx.x * (u64)TPB + threadIdx.x; i < n; i += (u64)gridDim.x * TPB) out[i] = sm64_at(seed, i);
-}
-__global__ void gen_puts_kernel(nrg_put* out, const u64* k, const u64* v, u64 n) {
-    for (u64 i = blockIdx.x * (u64)TPB + threadIdx.x; i < n; i += (u64)gridDim.x * TPB) {
-        nrg_put p;
-        p.key = k[i];
-        p.val = v[i];
-        out[i] = p;
-    }
-}
-
 struct SegArgs {
     u64 start[64];  // exclusive prefix of lens (in records)
     u64 total;
@@ -604,19 +588,6 @@ hipError_t hm_digest(nrg_ctx* c, u64* d_out3) {
     e = hipMemsetAsync(d_out3, 0, 3 * sizeof(u64), c->stream);
     if (e != hipSuccess) return e;
     hm_digest_kernel<<<grid_for(c->slots, 8192), TPB, 0, c->stream>>>(c->d_table, c->slots, c->d_ctl, d_out3);
-    return hipGetLastError();
-}
-
-hipError_t gen_uniform(nrg_ctx* c, u64* d, u64 n, u64 seed, u64 span) {
-    gen_uniform_kernel<<<grid_for(n, 8192), TPB, 0, c->stream>>>(d, n, seed, span);
-    return hipGetLastError();
-}
-hipError_t gen_raw(nrg_ctx* c, u64* d, u64 n, u64 seed) {
-    gen_raw_kernel<<<grid_for(n, 8192), TPB, 0, c->stream>>>(d, n, seed);
-    return hipGetLastError();
-}
-hipError_t gen_puts(nrg_ctx* c, nrg_put* d, const u64* k, const u64* v, u64 n) {
-    gen_puts_kernel<<<grid_for(n, 8192), TPB, 0, c->stream>>>(d, k, v, n);
     return hipGetLastError();
 }
 

@@ -91,6 +91,9 @@ struct nrg_ctx {
     // that reads the table. With pipeline == false it is flushed at the end of every call.
     bool pipeline = false;
     nrg::HmDeferred pend;
+    // Zipf generator cache: zeta(zipf_n, zipf_theta)
+    uint64_t zipf_n = 0;
+    double zipf_theta = 0.0, zipf_zetan = 0.0;
     // ---- Stack ----
     uint32_t* d_stack = nullptr;
     uint32_t stack_key_bits = 0;
@@ -150,6 +153,9 @@ hipError_t hm_digest(nrg_ctx* c, u64* d_out3);
 hipError_t gen_uniform(nrg_ctx* c, u64* d, u64 n, u64 seed, u64 span);
 hipError_t gen_raw(nrg_ctx* c, u64* d, u64 n, u64 seed);
 hipError_t gen_puts(nrg_ctx* c, nrg_put* d, const u64* k, const u64* v, u64 n);
+// workload.hip (also holds the three generators above)
+hipError_t gen_stack_ops(nrg_ctx* c, nrg_stack_op* d, u64 n, u64 seed);
+hipError_t gen_zipf(nrg_ctx* c, u64* d, u64 n, u64 seed, u64 N, double theta, int scramble);
 hipError_t copy_segments(nrg_ctx* c, const void* d_base, u32 nseg, u64 seg_stride, const u64* lens,
                          u64 dst_lo);
 

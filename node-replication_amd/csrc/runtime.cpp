@@ -826,6 +826,22 @@ int nrg_gen_puts_async(nrg_ctx* c, nrg_put* d, const uint64_t* k, const uint64_t
     return hip_fail(gen_puts(c, d, k, v, n));
 }
 
+int nrg_gen_zipf_async(nrg_ctx* c, uint64_t* d, uint64_t n, uint64_t seed, uint64_t N, double theta,
+                       int scramble) {
+    if (!c || (n && !d)) return NRG_E_INVAL;
+    int r = use_device(c);
+    if (r) return r;
+    if (N == 0 || !(theta > 0.0) || theta == 1.0) return NRG_E_INVAL;
+    return hip_fail(gen_zipf(c, d, n, seed, N, theta, scramble));
+}
+
+int nrg_gen_stack_ops_async(nrg_ctx* c, nrg_stack_op* d, uint64_t n, uint64_t seed) {
+    if (!c || (n && !d)) return NRG_E_INVAL;
+    int r = use_device(c);
+    if (r) return r;
+    return hip_fail(gen_stack_ops(c, d, n, seed));
+}
+
 // ---- kernel timing -------------------------------------------------------------------------------
 int nrg_kernel_timing(nrg_ctx* c, int enable) {
     if (!c || enable < 0) return NRG_E_INVAL;

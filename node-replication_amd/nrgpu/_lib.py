@@ -125,6 +125,8 @@ SIGNATURES = {
     "nrg_gen_uniform_async": (C.c_int, [vp, vp, u64, u64, u64]),
     "nrg_gen_raw_async": (C.c_int, [vp, vp, u64, u64]),
     "nrg_gen_puts_async": (C.c_int, [vp, vp, vp, vp, u64]),
+    "nrg_gen_zipf_async": (C.c_int, [vp, vp, u64, u64, u64, C.c_double, C.c_int]),
+    "nrg_gen_stack_ops_async": (C.c_int, [vp, vp, u64, u64]),
     "nrg_kernel_timing": (C.c_int, [vp, C.c_int]),
     "nrg_kernel_timing_only": (C.c_int, [vp, C.c_char_p]),
     "nrg_kernel_time": (C.c_int, [vp, C.c_char_p, u64p, C.POINTER(C.c_double)]),

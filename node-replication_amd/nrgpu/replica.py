@@ -247,6 +247,12 @@ class DeviceReplica:
     def gen_raw_device(self, d_out, n, seed):
         L.check(self._lib.nrg_gen_raw_async(self._h, _dptr(d_out), n, seed))
 
+    def gen_zipf_device(self, d_out, n, seed, N, theta=0.99, scramble=False):
+        L.check(self._lib.nrg_gen_zipf_async(self._h, _dptr(d_out), n, seed, N, float(theta), int(scramble)), "zipf")
+
+    def gen_stack_ops_device(self, d_out, n, seed):
+        L.check(self._lib.nrg_gen_stack_ops_async(self._h, _dptr(d_out), n, seed), "stack ops")
+
     def gen_puts_device(self, d_out, d_keys, d_vals, n):
         L.check(self._lib.nrg_gen_puts_async(self._h, _dptr(d_out), _dptr(d_keys), _dptr(d_vals), n))
 

@@ -77,3 +77,28 @@ def test_maxscan(nrg, orc, n, span, setfrac):
     torch.cuda.synchronize()
     nrg._lib.check(nrg.load().nrg_test_maxscan(dev.handle, dk.data_ptr(), dv.data_ptr(), n, out.data_ptr()))
     np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), want)
+
+
+def test_device_stack_and_zipf_generators(nrg, orc):
+    """Device generators used by bench.py: stack ops bit-exact with the oracle; Zipf keys equal
+    to the oracle's except where device pow and glibc pow round differently (rare, +-1 rank)."""
+    import torch
+
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_STACK, 0, max_batch=1024)
+    dev.use_torch_stream()
+    n = 200_000
+    d = torch.empty(n, dtype=torch.int64, device="cuda")
+    dev.gen_stack_ops_device(d, n, 77)
+    torch.cuda.synchronize()
+    ops = d.cpu().numpy().view("u8")
+    vals, opc = orc.gen_stack_ops(n, 77)
+    assert ((ops & 0xFFFFFFFF).astype("u4") == vals).all()
+    assert ((ops >> 32).astype("u4") == opc).all()
+    for scramble in (False, True):
+        dev.gen_zipf_device(d, n, 91, 1_000_000, 0.99, scramble)
+        torch.cuda.synchronize()
+        got = d.cpu().numpy().view("u8")
+        want = orc.gen_zipf(n, 91, 1_000_000, 0.99, scramble)
+        assert (got < 1_000_000).all()
+        assert (got != want).mean() < 1e-3
+    dev.close()
