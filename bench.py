@@ -107,13 +107,22 @@ def cpu_baseline(seconds: float, write_ratio: int, key_space: int, prefill: int)
 
 
 def traffic_key(args):
-    return "w%d_ops%d_ks%d_pf%d_s%d_n%d" % (args.write_ratio, args.ops_per_gpu, args.key_space, args.prefill,
-                                           args.log2_slots, int(os.environ.get("WORLD_SIZE", "1")))
+    if args.workload == "stack":
+        return "stack_ops%d_init%d_n%d" % (args.ops_per_gpu, args.stack_init, int(os.environ.get("WORLD_SIZE", "1")))
+    return "w%d_ops%d_ks%d_pf%d_s%d_%s_n%d" % (args.write_ratio, args.ops_per_gpu, args.key_space, args.prefill,
+                                              args.log2_slots, key_dist_name(args),
+                                              int(os.environ.get("WORLD_SIZE", "1")))
+
+
+def key_dist_name(args):
+    if args.dist == "uniform":
+        return "uniform"
+    return "zipf%g%s" % (args.theta, "s" if args.scramble else "")
 
 
 def measured_traffic(args):
-    """HBM bytes per hm_round launch from the PMC passes of tools/profile.sh (FETCH_SIZE x2 +
-    WRITE_SIZE, gfx950 correction per MI355X_MICROARCH.md), as committed by
+    """HBM bytes per launch of the dominant kernel from the PMC passes of tools/profile.sh
+    (FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction per MI355X_MICROARCH.md), as committed by
     tools/prof_summary.py for this exact workload; None when no matching profile exists."""
     path = os.path.join(ROOT, "profiles", "traffic_hm_round.json")
     try:
@@ -127,60 +136,110 @@ def measured_traffic(args):
     return {"bytes_per_launch": e["bytes_per_launch"], "source": e["source"]}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=400)
-    ap.add_argument("--warmup", type=int, default=40)
-    ap.add_argument("--write-ratio", type=int, default=10)
-    ap.add_argument("--ops-per-gpu", type=int, default=1_000_000)
-    ap.add_argument("--key-space", type=int, default=10_000_000)
-    ap.add_argument("--prefill", type=int, default=1 << 23)
-    ap.add_argument("--log2-slots", type=int, default=26)
-    ap.add_argument("--pool", type=int, default=64, help="distinct pre-generated input batches")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-prev-variant", action="store_true")
-    ap.add_argument("--no-kernel-timing", action="store_true", help="diagnostic: no HIP events in the timed region")
-    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
-                    help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo: CPU rehearsal)")
-    ap.add_argument("--share-gpu", action="store_true", help="all ranks on cuda:0 (gloo rehearsal on a 1-GPU box)")
-    ap.add_argument("--timing-every", type=int, default=8, help="event-stamp every n-th hm_round launch")
-    ap.add_argument("--pipeline", type=int, default=1,
-                    help="1: a round's apply+reads ride in the next round's launch (nrg_config.pipeline); "
-                         "0: every round call completes its own reads")
-    args = ap.parse_args()
+class Env:
+    """Process/distributed context of one bench run (one process per GPU)."""
 
-    import torch
-    import torch.distributed as dist
+    def __init__(self, args):
+        import torch
+        import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log(f"WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
-    if args.share_gpu:
-        local = 0  # rehearsal of the N > 1 path with every rank on the box's one GPU (gloo only)
-    torch.cuda.set_device(local)
-    dev_t = torch.device("cuda", local)
-    if world > 1:
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev_t)  # RCCL over xGMI
-        else:
-            dist.init_process_group("gloo")
+        self.torch, self.dist = torch, dist
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        if self.world != args.gpus:
+            log(f"WORLD_SIZE={self.world} but --gpus={args.gpus}; using WORLD_SIZE")
+        if args.share_gpu:
+            local = 0  # rehearsal of the N > 1 path with every rank on the box's one GPU (gloo only)
+        self.local = local
+        torch.cuda.set_device(local)
+        self.dev = torch.device("cuda", local)
+        if self.world > 1:
+            if args.backend == "nccl":
+                dist.init_process_group("nccl", device_id=self.dev)  # RCCL over xGMI
+            else:
+                dist.init_process_group("gloo")
 
+    def timed(self, n, step, rep, host_s=None):
+        """Barrier + sync, K steps, the replica's deferred work launched, sync + barrier; max over
+        ranks of the wall time."""
+        torch, dist = self.torch, self.dist
+        if self.world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for i in range(n):
+            step(i)
+        rep.join()  # launches the last round's deferred apply + reads: inside the timed region
+        if host_s is not None:
+            host_s[0] = time.perf_counter() - t
+        torch.cuda.synchronize()
+        if self.world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t
+        if self.world > 1:
+            x = torch.tensor([el], dtype=torch.float64, device=self.dev)
+            dist.all_reduce(x, op=dist.ReduceOp.MAX)
+            el = float(x.item())
+        return el
+
+    def close(self):
+        if self.world > 1:
+            self.dist.destroy_process_group()
+
+
+def common_fields(args, env, value, ms_per_step, metric, dtype, config):
+    return {
+        "metric": metric,
+        "value": round(value, 3),
+        "unit": "Mops/s",
+        "n_gpus": env.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": dtype,
+        "data": "synthetic",
+        "config": config,
+    }
+
+
+def roofline(kernel, k_bytes, k_n, k_ms, args, traffic):
+    k_avg_s = (k_ms / 1e3 / k_n) if k_n else float("nan")
+    achieved = k_bytes / k_avg_s / 1e9 if k_n else None
+    return {
+        "bound": "hbm",
+        "kernel": kernel,
+        "achieved": round(achieved, 1) if achieved else None,
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+        "traffic": traffic.get("bytes_per_launch") if traffic else None,
+        "traffic_source": traffic.get("source") if traffic else None,
+        "bytes_per_launch": int(k_bytes),
+        "sampled_every": args.timing_every,
+        "traffic_key": traffic_key(args),
+        "avg_launch_us": round(k_avg_s * 1e6, 3) if k_n else None,
+        "launches": k_n,
+    }
+
+
+# ---------------------------------------------------------------------------------------------
+def run_hashmap(args, env):
+    torch = env.torch
     import nrgpu
     from nrgpu import _lib as L
 
+    world, rank, dev_t = env.world, env.rank, env.dev
     W = args.ops_per_gpu * args.write_ratio // 100
     R = args.ops_per_gpu - W
     Wg = W * world
-    rep = nrgpu.DeviceReplica(L.NRG_DS_HASHMAP, local, log2_slots=args.log2_slots, max_batch=max(Wg, 1),
+    rep = nrgpu.DeviceReplica(L.NRG_DS_HASHMAP, env.local, log2_slots=args.log2_slots, max_batch=max(Wg, 1),
                               log_bytes=64 * 4 * max(Wg, 8192), replica_id=rank + 1, pipeline=args.pipeline)
     rep.use_torch_stream()
-    t0 = time.time()
     rep.hm_prefill_range(args.prefill, 1)
-    log(f"rank {rank}: prefill {args.prefill} keys in {time.time() - t0:.2f}s")
 
     # ---- inputs: a pool of distinct batches generated on device (seeds per rank/batch) ----
     P = max(1, min(args.pool, args.steps + args.warmup))
@@ -189,13 +248,20 @@ def main():
     tmp_k = torch.empty(max(W, 1), dtype=torch.int64, device=dev_t)
     tmp_v = torch.empty(max(W, 1), dtype=torch.int64, device=dev_t)
     seed0 = 0x4E52475055310001 + rank * 0x1000193
+
+    def keys_into(out, n, seed):
+        if args.dist == "uniform":
+            rep.gen_uniform_device(out, n, seed, args.key_space)
+        else:
+            rep.gen_zipf_device(out, n, seed, args.key_space, args.theta, args.scramble)
+
     for p in range(P):
         if W:
-            rep.gen_uniform_device(tmp_k, W, seed0 + 3 * p, args.key_space)
+            keys_into(tmp_k, W, seed0 + 3 * p)
             rep.gen_raw_device(tmp_v, W, seed0 + 3 * p + 1)
             rep.gen_puts_device(puts[p], tmp_k, tmp_v, W)
         if R:
-            rep.gen_uniform_device(gkeys[p], R, seed0 + 3 * p + 2, args.key_space)
+            keys_into(gkeys[p], R, seed0 + 3 * p + 2)
     gvals = torch.empty(max(R, 1), dtype=torch.int64, device=dev_t)
     gfound = torch.empty(max(R, 1), dtype=torch.uint8, device=dev_t)
     pvals = torch.empty(max(W, 1), dtype=torch.int64, device=dev_t)
@@ -203,8 +269,15 @@ def main():
     torch.cuda.synchronize()
 
     # distinct keys per batch (for the algorithmic byte count), outside the timed region
-    u_r = sum(int(torch.unique(gkeys[p, :R]).numel()) for p in range(min(P, 8))) / min(P, 8) if R else 0
-    u_w_local = sum(int(torch.unique(puts[p, :W, 0]).numel()) for p in range(min(P, 8))) / min(P, 8) if W else 0
+    nb = min(P, 8)
+    u_r = sum(int(torch.unique(gkeys[p, :R]).numel()) for p in range(nb)) / nb if R else 0
+    u_w_local = sum(int(torch.unique(puts[p, :W, 0]).numel()) for p in range(nb)) / nb if W else 0
+    if world > 1:  # distinct keys of the whole round's log (all ranks' segments)
+        x = torch.tensor([u_w_local], dtype=torch.float64, device=dev_t if args.backend == "nccl" else "cpu")
+        env.dist.all_reduce(x)
+        u_w = float(x.item())
+    else:
+        u_w = u_w_local
 
     group = None
     if world > 1:
@@ -217,9 +290,12 @@ def main():
     round_fn, h = rep._lib.nrg_hashmap_round_async, rep._h
     ptrs = [(puts[p].data_ptr(), gkeys[p].data_ptr()) for p in range(P)]
     gv_p, gf_p, pv_p, pf_p = gvals.data_ptr(), gfound.data_ptr(), pvals.data_ptr(), pfound.data_ptr()
+    gathered = {}
+    mode = {"prev": False, "n": 0}
 
-    def step(i, prev=False):
+    def step(i):
         p = i % P
+        prev = mode["prev"]
         if group is None:
             pp, gp = ptrs[p]
             rc = round_fn(h, pp, W, rank + 1, gp, R, gv_p, gf_p, pv_p if prev else None, pf_p if prev else None)
@@ -228,35 +304,15 @@ def main():
         else:
             # the all-gather of round i+1 is in flight while round i replays
             g = gathered.pop(i) if i in gathered else group.gather_async(puts[p, :W], stride=W)
-            if i + 1 < n_steps[0]:
+            if i + 1 < mode["n"]:
                 gathered[i + 1] = group.gather_async(puts[(i + 1) % P, :W], stride=W)
             group.replay(g, gkeys[p, :R], gvals, gfound, pvals if prev else None, pfound if prev else None)
 
-    host_s = [0.0]
-    gathered = {}
-    n_steps = [0]
+    def run(n, prev=False, host_s=None):
+        mode["prev"], mode["n"] = prev, n
+        return env.timed(n, step, rep, host_s)
 
-    def timed(n, prev=False):
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t = time.perf_counter()
-        n_steps[0] = n
-        for i in range(n):
-            step(i, prev)
-        rep.join()  # launches the last round's deferred apply + reads: inside the timed region
-        host_s[0] = time.perf_counter() - t
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        el = time.perf_counter() - t
-        if world > 1:
-            x = torch.tensor([el], dtype=torch.float64, device=dev_t)
-            dist.all_reduce(x, op=dist.ReduceOp.MAX)
-            el = float(x.item())
-        return el
-
-    n_steps[0] = args.warmup
+    mode["n"] = args.warmup
     for i in range(args.warmup):
         step(i)
     rep.sync()
@@ -267,97 +323,208 @@ def main():
     # stream it runs on). An event-stamped dispatch costs ~5 us of command-processor time, so
     # only every TIMING_EVERY-th launch is stamped (steady-state launches: round e's index plus
     # round e-1's apply and reads, i.e. one round of work each).
+    host_s = [0.0]
     rep.kernel_timing(not args.no_kernel_timing, only="hm_round", every=args.timing_every)
-    elapsed = timed(args.steps)
-    host_enqueue_us = host_s[0] * 1e6 / args.steps
+    elapsed = run(args.steps, host_s=host_s)
     k_n, k_ms = rep.kernel_time("hm_round")
     rep.kernel_timing(False)
     rep.sync()
-    ms_per_step = elapsed * 1e3 / args.steps
-    total_ops = world * args.ops_per_gpu * args.steps
-    value = total_ops / elapsed / 1e6
+    value = world * args.ops_per_gpu * args.steps / elapsed / 1e6
 
     prev_value = None
-    if not args.no_prev_variant and world == 1:
+    if not args.no_prev_variant:
         n2 = max(args.steps // 4, 10)
-        e2 = timed(n2, prev=True)
+        e2 = run(n2, prev=True)
         prev_value = world * args.ops_per_gpu * n2 / e2 / 1e6
     rep.sync()
-
     if rank != 0:
-        if world > 1:
-            dist.destroy_process_group()
-        return
+        return None
 
     # ---- roofline of the dominant kernel (hm_round: index of round e + apply/reads of e-1) ----
     # Algorithmic bytes per round: B = 16 R + 16 W_glob + 64 U_r + 128 U_w
     # (8-B key in + 8-B value out per Get, the 16-B records replayed, one 64-B sector per
     # distinct key read, read + write-back per distinct key written; Put responses are
     # Ok(None) here, so no 8 W_own term). Every sampled launch carries one round of work.
-    u_w = u_w_local * world
     round_bytes = 16 * R + 16 * Wg + 64 * u_r + 128 * u_w
-    k_bytes = round_bytes
-    k_avg_s = (k_ms / 1e3 / k_n) if k_n else float("nan")
-    achieved = k_bytes / k_avg_s / 1e9 if k_n else None
-    traffic = measured_traffic(args)
-    res = {
-        "metric": METRIC,
-        "value": round(value, 3),
-        "unit": "Mops/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(ms_per_step, 5),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u64",
-        "data": "synthetic",
-        "config": {
-            "workload": ("B1 NrHashMap replica per GPU: 2^%d-slot table, uniform keys over %d, prefill [0,%d)->k+1, "
-                         "rounds of %d ops/GPU = %d Put + %d Get%s" % (
-                             args.log2_slots, args.key_space, args.prefill, args.ops_per_gpu, W, R,
-                             "; write segments all-gathered over RCCL, every replica replays all %d Puts" % Wg
-                             if world > 1 else "")),
-            "write_ratio_pct": args.write_ratio,
-            "ops_per_gpu_per_round": args.ops_per_gpu,
-            "put_responses": "Ok(None) as benches/hashmap.rs:114-119",
-            "parallelism": "replicas%d" % world,
-        },
-        "roofline": {
-            "bound": "hbm",
-            "kernel": "hm_round",
-            "achieved": round(achieved, 1) if achieved else None,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-            "traffic": traffic.get("bytes_per_launch") if traffic else None,
-            "traffic_source": traffic.get("source") if traffic else None,
-            "bytes_per_launch": int(k_bytes),
-            "sampled_every": args.timing_every,
-            "traffic_key": traffic_key(args),
-            "avg_launch_us": round(k_avg_s * 1e6, 3) if k_n else None,
-            "launches": k_n,
-        },
-        "round": {
-            "algorithmic_bytes": int(round_bytes),
-            "achieved_GBps": round(round_bytes / (elapsed / args.steps) / 1e9, 1),
-            "host_enqueue_us": round(host_enqueue_us, 2),
-            "distinct_get_keys": int(u_r),
-            "distinct_put_keys": int(u_w),
-        },
+    dist_txt = ("uniform keys over %d" % args.key_space if args.dist == "uniform" else
+                "Zipf(theta=%g%s) keys over %d" % (args.theta, ", scrambled" if args.scramble else ", hot keys adjacent",
+                                                   args.key_space))
+    res = common_fields(args, env, value, elapsed * 1e3 / args.steps, METRIC, "u64", {
+        "workload": ("NrHashMap replica per GPU: 2^%d-slot table, %s, prefill [0,%d)->k+1, rounds of %d ops/GPU "
+                     "= %d Put + %d Get%s" % (
+                         args.log2_slots, dist_txt, args.prefill, args.ops_per_gpu, W, R,
+                         "; write segments all-gathered (%s), every replica replays all %d Puts" % (
+                             "RCCL over xGMI" if args.backend == "nccl" else "gloo rehearsal", Wg)
+                         if world > 1 else "")),
+        "baseline_config": "configs[1] (B1)" if (world == 1 and args.write_ratio == 10 and args.dist == "uniform")
+        else ("configs[2] (B8 weak scaling)" if args.dist == "uniform" else "configs[3] (Z)"),
+        "write_ratio_pct": args.write_ratio,
+        "ops_per_gpu_per_round": args.ops_per_gpu,
+        "put_responses": "Ok(None) as benches/hashmap.rs:114-119",
+        "parallelism": "replicas%d" % world,
+    })
+    res["roofline"] = roofline("hm_round", round_bytes, k_n, k_ms, args, measured_traffic(args))
+    res["round"] = {
+        "algorithmic_bytes": int(round_bytes),
+        "achieved_GBps": round(round_bytes / (elapsed / args.steps) / 1e9, 1),
+        "host_enqueue_us": round(host_s[0] * 1e6 / args.steps, 2),
+        "distinct_get_keys": int(u_r),
+        "distinct_put_keys": int(u_w),
     }
     if prev_value is not None:
         res["variants"] = {"prev_value_responses_Mops": round(prev_value, 3)}
-    if not args.no_cpu_baseline and world == 1:
+    if not args.no_cpu_baseline and world == 1 and args.dist == "uniform":
         log(f"cpu baseline: {args.cpu_seconds}s ...")
         try:
             res["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.write_ratio, args.key_space, args.prefill)
         except Exception as e:  # noqa: BLE001
             res["cpu_baseline"] = {"error": str(e)}
-    print(json.dumps(res), flush=True)
+    return res
+
+
+# ---------------------------------------------------------------------------------------------
+def stack_cpu_baseline(seconds, n_ops, init):
+    """The sequential oracle Stack (Vec::push/pop, benches/stack.rs:36-84) on one host core over
+    a bounded sample of the same op stream."""
+    import numpy as np
+    import oracle
+
+    st = oracle.Stack(np.arange(init, dtype=np.uint32))
+    vals, ops = oracle.gen_stack_ops(n_ops, 0x5AC)
+    t0 = time.perf_counter()
+    done = 0
+    while time.perf_counter() - t0 < seconds:
+        st.replay(vals, ops)
+        done += n_ops
+    el = time.perf_counter() - t0
+    return {"value": round(done / el / 1e6, 3), "unit": "Mops/s", "cores": 1, "kind": "port",
+            "sample": "%.1f s of %d-op push/pop batches (50/50, seeded) replayed by the sequential oracle Stack" % (
+                el, n_ops)}
+
+
+def run_stack(args, env):
+    torch = env.torch
+    import nrgpu
+    from nrgpu import _lib as L
+
+    world, rank, dev_t = env.world, env.rank, env.dev
+    N = args.ops_per_gpu
+    Ng = N * world
+    cap = args.stack_init + 4 * Ng + (1 << 16)
+    rep = nrgpu.DeviceReplica(L.NRG_DS_STACK, env.local, max_batch=Ng, stack_capacity=cap,
+                              log_bytes=64 * 4 * max(Ng, 8192), replica_id=rank + 1)
+    rep.use_torch_stream()
+    rep.st_init(list(range(args.stack_init)))  # benches/stack.rs:50-63: 0..50000
+    P = max(1, min(args.pool, args.steps + args.warmup))
+    ops = torch.empty((P, N), dtype=torch.int64, device=dev_t)
+    seed0 = 0x5354434B00000001 + rank * 0x1000193
+    for p in range(P):
+        rep.gen_stack_ops_device(ops[p], N, seed0 + p)
+    resp = torch.empty(N, dtype=torch.int32, device=dev_t)
+    some = torch.empty(N, dtype=torch.uint8, device=dev_t)
+    torch.cuda.synchronize()
+    # distinct slots written per round (S of SURVEY.md §8d): pushes at distinct depths; the
+    # depth walk is shift-invariant while it stays above 0 (it starts at 50k)
+    S = 0
+    for p in range(min(P, 4)):
+        o = ops[p]
+        push = (o >> 32) & 1
+        step_d = push * 2 - 1
+        d_before = torch.cumsum(step_d, 0) - step_d
+        S += int(torch.unique(d_before[push == 1]).numel())
+    S = S / min(P, 4) * world
+
+    group = None
     if world > 1:
-        dist.destroy_process_group()
+        from nrgpu.parallel import ReplicatedLog
+
+        group = ReplicatedLog(rep, device=dev_t)
+    append_fn, exec_fn, h = rep._lib.nrg_log_append_async, rep._lib.nrg_log_exec_async, rep._h
+    first = L.C.c_uint64()
+    ptrs = [ops[p].data_ptr() for p in range(P)]
+    r_p, s_p = resp.data_ptr(), some.data_ptr()
+    gathered = {}
+    mode = {"n": 0}
+
+    def step(i):
+        p = i % P
+        if group is None:
+            rc = append_fn(h, ptrs[p], N, rank + 1, L.C.byref(first))
+            if rc == 0:
+                rc = exec_fn(h, first.value, first.value + N, r_p, s_p)
+            if rc:
+                L.check(rc, "stack round")
+        else:
+            g = gathered.pop(i) if i in gathered else group.gather_async(ops[p], stride=N)
+            if i + 1 < mode["n"]:
+                gathered[i + 1] = group.gather_async(ops[(i + 1) % P], stride=N)
+            group.replay(g, resp, some)
+
+    mode["n"] = args.warmup
+    for i in range(args.warmup):
+        step(i)
+    rep.sync()
+    rep.kernel_timing(not args.no_kernel_timing, only="st_replay", every=args.timing_every)
+    mode["n"] = args.steps
+    elapsed = env.timed(args.steps, step, rep)
+    k_n, k_ms = rep.kernel_time("st_replay")
+    rep.kernel_timing(False)
+    rep.sync()
+    value = world * N * args.steps / elapsed / 1e6
+    if rank != 0:
+        return None
+    # SURVEY.md §8d: B = 8 N + 4 N + 4 S per replica per round (records, responses, slots written)
+    round_bytes = 8 * Ng + 4 * N + 4 * S
+    res = common_fields(args, env, value, elapsed * 1e3 / args.steps,
+                        "Mops/s whole node, Stack push/pop log replay (benches/stack.rs)", "u32", {
+                            "workload": ("Stack replica per GPU: initial %d elements, rounds of %d ops/GPU (50/50 "
+                                         "push/pop, seeded), pop responses for own ops%s" % (
+                                             args.stack_init, N, "; op segments all-gathered, every replica "
+                                             "replays all %d ops" % Ng if world > 1 else "")),
+                            "baseline_config": "configs[4] (S1/S8)",
+                            "ops_per_gpu_per_round": N,
+                            "parallelism": "replicas%d" % world,
+                        })
+    res["roofline"] = roofline("st_replay", round_bytes, k_n, k_ms, args, None)
+    res["round"] = {"algorithmic_bytes": int(round_bytes), "distinct_slots_written": int(S)}
+    if not args.no_cpu_baseline and world == 1:
+        res["cpu_baseline"] = stack_cpu_baseline(min(args.cpu_seconds, 10.0), N, args.stack_init)
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--warmup", type=int, default=40)
+    ap.add_argument("--workload", default="hashmap", choices=["hashmap", "stack"])
+    ap.add_argument("--write-ratio", type=int, default=10)
+    ap.add_argument("--ops-per-gpu", type=int, default=1_000_000)
+    ap.add_argument("--key-space", type=int, default=10_000_000)
+    ap.add_argument("--dist", default="uniform", choices=["uniform", "zipf"])
+    ap.add_argument("--theta", type=float, default=0.99)
+    ap.add_argument("--scramble", action="store_true", help="Zipf: key = mix64(rank) %% N (hot keys spread)")
+    ap.add_argument("--prefill", type=int, default=1 << 23)
+    ap.add_argument("--log2-slots", type=int, default=26)
+    ap.add_argument("--stack-init", type=int, default=50_000)
+    ap.add_argument("--pool", type=int, default=64, help="distinct pre-generated input batches")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-prev-variant", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true", help="diagnostic: no HIP events in the timed region")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo: CPU rehearsal)")
+    ap.add_argument("--share-gpu", action="store_true", help="all ranks on cuda:0 (gloo rehearsal on a 1-GPU box)")
+    ap.add_argument("--timing-every", type=int, default=8, help="event-stamp every n-th launch of the timed kernel")
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="1: a round's apply+reads ride in the next round's launch (nrg_config.pipeline); "
+                         "0: every round call completes its own reads")
+    args = ap.parse_args()
+    env = Env(args)
+    res = run_stack(args, env) if args.workload == "stack" else run_hashmap(args, env)
+    if res is not None:
+        print(json.dumps(res), flush=True)
+    env.close()
 
 
 if __name__ == "__main__":

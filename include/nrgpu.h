@@ -270,8 +270,8 @@ int nrg_gen_stack_ops_async(nrg_ctx* ctx, nrg_stack_op* d_out, uint64_t n, uint6
 /* ---- timing: HIP events recorded around the dominant replay kernel -------------------- */
 /* enable = 0: off; 1: every launch; n > 1: every n-th launch (sampling keeps the timed stream
  * unperturbed). The main replay kernel ("hm_round") is timed with start/stop events stamped
- * from its own dispatch (hipExtLaunchKernelGGL); other kernels ("hm_prev", "st_scan",
- * "st_sort", "sy_replay") with event records around them. nrg_kernel_time reads (timed
+ * from its own dispatch (hipExtLaunchKernelGGL); multi-kernel pipelines ("hm_prev",
+ * "st_replay", "sy_replay") with event records around them. nrg_kernel_time reads (timed
  * launches, their total milliseconds) after synchronising. */
 int nrg_kernel_timing(nrg_ctx* ctx, int enable);
 /* Restrict timing to one kernel name (NULL or "" = all). */

@@ -37,6 +37,7 @@ struct KTimer {
     u64 launches = 0;
     double total_ms = 0.0;
     u64 seen = 0;                // launches of this kernel since timing was enabled
+    bool open = false;           // timer_begin recorded a start event not yet closed
 };
 
 struct Staging {  // growable device scratch for the host-pointer entry points

@@ -189,6 +189,8 @@ namespace nrg {
 void timer_begin(nrg_ctx* c, const char* name, hipStream_t s) {
     if (!c->timing || (!c->timing_only.empty() && c->timing_only != name)) return;
     KTimer& t = c->timers[name];
+    t.open = false;
+    if (++t.seen % c->timing_every != 0) return;  // sampled, as timer_events
     const size_t idx = t.pending * 2;
     while (t.ev.size() < idx + 2) {
         hipEvent_t e;
@@ -196,6 +198,7 @@ void timer_begin(nrg_ctx* c, const char* name, hipStream_t s) {
         t.ev.push_back(e);
     }
     (void)hipEventRecord(t.ev[idx], s ? s : c->stream);
+    t.open = true;
 }
 bool timer_events(nrg_ctx* c, const char* name, hipEvent_t* start, hipEvent_t* stop) {
     if (!c->timing || (!c->timing_only.empty() && c->timing_only != name)) return false;
@@ -216,10 +219,10 @@ bool timer_events(nrg_ctx* c, const char* name, hipEvent_t* start, hipEvent_t* s
 void timer_end(nrg_ctx* c, const char* name, hipStream_t s) {
     if (!c->timing || (!c->timing_only.empty() && c->timing_only != name)) return;
     KTimer& t = c->timers[name];
-    const size_t idx = t.pending * 2;
-    if (t.ev.size() < idx + 2) return;
-    (void)hipEventRecord(t.ev[idx + 1], s ? s : c->stream);
+    if (!t.open) return;
+    (void)hipEventRecord(t.ev[t.pending * 2 + 1], s ? s : c->stream);
     t.pending++;
+    t.open = false;
 }
 }  // namespace nrg
 

@@ -228,20 +228,18 @@ hipError_t st_replay_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 resp_hi, 
     u32* keys = (u32*)c->d_tmp_u64;           // n u32
     u32* vals = keys + c->cfg.max_batch;      // n u32
     const bool want = d_resp != nullptr && resp_lo < lo + n && resp_hi > lo;
-    timer_begin(c, "st_scan");
+    timer_begin(c, "st_replay");
     st_scan_kernel<<<(unsigned)tiles, ST_TPB, 0, st>>>(ring, ring_mask, lo, n, c->d_ctl, desc, ticket, keys, vals,
                                                       sentinel, c->cfg.stack_capacity, want ? resp_lo : 0,
                                                       want ? resp_hi : 0, (int)c->cfg.stack_push_resp, d_resp, d_some);
-    timer_end(c, "st_scan");
     u32 *sk = nullptr, *sv = nullptr;
-    timer_begin(c, "st_sort");
     e = sort_pairs(c->sort, keys, vals, n, (int)c->stack_key_bits, st, &sk, &sv);
-    timer_end(c, "st_sort");
     if (e != hipSuccess) return e;
     const unsigned g = (unsigned)((n + 255) / 256);
     if (want) st_resolve_kernel<<<g, 256, 0, st>>>(sk, sv, n, ring, ring_mask, lo, c->d_stack, sentinel, resp_lo,
                                                   resp_hi, d_resp, d_some);
     st_commit_kernel<<<g, 256, 0, st>>>(sk, sv, n, ring, ring_mask, lo, c->d_stack, sentinel);
+    timer_end(c, "st_replay");
     return hipGetLastError();
 }
 
