@@ -50,6 +50,8 @@ struct IndexJob {
     u32* put_slot;
     u32 epoch;
     u32 nblocks;
+    u32 exp;  // diagnostic knobs (NRG_EXP; results are wrong when set): 1 no stamp atomics,
+              // 2 no LDS combining (one atomic per Put), 4 no apply role, 8 no index role
 };
 struct ApplyJob {
     RecSrc rec;
@@ -175,6 +177,10 @@ __device__ __forceinline__ void index_role(IndexJob j, u32 blk, Slot* table, u32
             continue;
         }
         j.put_slot[i] = (u32)s;
+        if (j.exp & 2) {
+            if (!(j.exp & 1)) atomicMax(slot_stamp(&table[s], par), stamp_of(j.epoch, i));
+            continue;
+        }
         // combine in LDS: max (i+1) per slot within the block
         u32 h = (u32)(mix64((u64)s) & (K1_LDS - 1));
         for (;;) {
@@ -190,7 +196,8 @@ __device__ __forceinline__ void index_role(IndexJob j, u32 blk, Slot* table, u32
     __syncthreads();
     for (int q = threadIdx.x; q < K1_LDS; q += TPB) {
         const u32 s = s_slot[q];
-        if (s != 0xFFFFFFFFu) atomicMax(slot_stamp(&table[s], par), ((u64)j.epoch << 32) | s_max[q]);
+        if (s != 0xFFFFFFFFu && !(j.exp & 1))
+            atomicMax(slot_stamp(&table[s], par), ((u64)j.epoch << 32) | s_max[q]);
     }
     if (threadIdx.x == 0 && s_created) atomicAdd(&ctl->nkeys, (u64)s_created);
 }
@@ -445,6 +452,9 @@ static void launch_round(nrg_ctx* c, const IndexJob& ij, const ApplyJob& aj, con
 static hipError_t launch(nrg_ctx* c, IndexJob& ij, ApplyJob& aj, ReadJob& rj) {
     const u32 K1 = c->k1_items >= 4 ? 4 : (c->k1_items == 2 ? 2 : 1);
     const u32 G = c->gets_per_thread >= 4 ? 4 : (c->gets_per_thread == 2 ? 2 : 1);
+    ij.exp = c->exp;
+    if (c->exp & 4) aj.n = 0;
+    if (c->exp & 8) ij.n = 0;
     ij.nblocks = (u32)((ij.n + TPB * K1 - 1) / (TPB * K1));
     aj.nblocks = (u32)((aj.n + TPB - 1) / TPB);
     rj.nblocks = (u32)((rj.R + TPB * G - 1) / (TPB * G));

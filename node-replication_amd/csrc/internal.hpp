@@ -87,6 +87,7 @@ struct nrg_ctx {
     uint32_t epoch = 0;              // replay rounds so far (stamps carry the round's epoch)
     uint32_t k1_items = 1;           // Puts per thread in the index role (tuning knob NRG_K1_ITEMS)
     uint32_t gets_per_thread = 1;    // Gets per thread in the read role (tuning knob NRG_GETS)
+    uint32_t exp = 0;                // diagnostic knobs (NRG_EXP), see hashmap.hip IndexJob::exp
     // Deferred second half of the last replayed round (apply its values, answer its reads):
     // launched together with the next round's index pass, or by nrg_join / nrg_sync / any call
     // that reads the table. With pipeline == false it is flushed at the end of every call.

@@ -325,6 +325,7 @@ int nrg_open(int dev, const nrg_config* cfg_in, nrg_ctx** out) {
         OPEN_CHK(hipMalloc(&c->d_put_slot[1], mb * sizeof(uint32_t)));
         if (const char* e = std::getenv("NRG_K1_ITEMS")) c->k1_items = (uint32_t)std::atoi(e);
         if (const char* e = std::getenv("NRG_GETS")) c->gets_per_thread = (uint32_t)std::atoi(e);
+        if (const char* e = std::getenv("NRG_EXP")) c->exp = (uint32_t)std::atoi(e);
         c->pipeline = cf.pipeline != 0;
         if (const char* e = std::getenv("NRG_PIPELINE")) c->pipeline = std::atoi(e) != 0;
         c->epoch = 1;  // epoch 1 = the state built by prefill; replay rounds start at 2

@@ -217,3 +217,49 @@ def test_ring_wrap_and_gc(nrg, orc):
     st = dev.log_state()
     assert st["tail"] == total and st["ltail"] == total and st["ctail"] == total
     _check_state(dev, om)
+
+
+@pytest.mark.parametrize("pipeline", [0, 1])
+def test_dense_segment_rounds(nrg, orc, pipeline):
+    """nrg_hashmap_round_segments_async on equal-length segments (the all-gathered round of the
+    multi-GPU bench): replayed in place in segment order, Put responses for one segment only,
+    reads against the post-round state; with pipeline=1 the reads complete at the next call."""
+    import torch
+
+    G, W, R = 4, 3000, 5000
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=17, max_batch=G * W, pipeline=pipeline)
+    dev.use_torch_stream()
+    om = orc.HashMap()
+    dev.hm_prefill_range(2000, 1)
+    om.prefill_range(2000, 1)
+    outs, want = [], []
+    for r in range(4):
+        segs = [(orc.gen_uniform(W, 500 + 10 * r + g, 9000), orc.gen_raw(W, 600 + 10 * r + g)) for g in range(G)]
+        segs[1][0][::37] = EMPTY
+        base = np.concatenate([_puts(k, v) for k, v in segs])
+        gk = orc.gen_uniform(R, 700 + r, 9500)
+        d_base = torch.from_numpy(base.view(np.int64).copy()).cuda()
+        d_gk = torch.from_numpy(gk.view(np.int64)).cuda()
+        d_gv = torch.empty(R, dtype=torch.int64, device="cuda")
+        d_gf = torch.empty(R, dtype=torch.uint8, device="cuda")
+        d_pv = torch.empty(W, dtype=torch.int64, device="cuda")
+        d_pf = torch.empty(W, dtype=torch.uint8, device="cuda")
+        own = r % G
+        dev.hm_round_segments_device(d_base, W, [W] * G, [g + 1 for g in range(G)], own, d_gk, R, d_gv, d_gf,
+                                     d_pv, d_pf)
+        outs.append((d_base, d_gk, d_gv, d_gf, d_pv, d_pf))
+        exp_prev = None
+        for g, (k, v) in enumerate(segs):
+            p, f = om.replay(k, v)
+            if g == own:
+                exp_prev = (p, f)
+        want.append((om.get_batch(gk), exp_prev))
+    dev.join()
+    torch.cuda.synchronize()
+    for (_, _, gv, gf, pv, pf), ((ov, of), (op, opf)) in zip(outs, want):
+        np.testing.assert_array_equal(gf.cpu().numpy(), of)
+        np.testing.assert_array_equal(gv.cpu().numpy().view(np.uint64), ov)
+        np.testing.assert_array_equal(pf.cpu().numpy(), opf)
+        np.testing.assert_array_equal(pv.cpu().numpy().view(np.uint64), op)
+    dev.sync()
+    _check_state(dev, om)
