@@ -18,6 +18,9 @@ constexpr u64 EMPTY_KEY = ~0ull;
 constexpr u32 ERR_TABLE_FULL = 1u;
 constexpr u32 ERR_CAPACITY = 4u;
 
+// Counters of keys created by replay rounds (index blocks add to slot blk % HM_CREATED_SLOTS).
+constexpr u64 HM_CREATED_SLOTS = 8192;
+
 // splitmix64 finaliser — identical constants to oracle/nr_oracle.c (orc_mix64) so that
 // device-generated workloads are reproducible by the CPU oracle.
 __host__ __device__ __forceinline__ u64 mix64(u64 z) {
@@ -61,10 +64,11 @@ __host__ __device__ __forceinline__ const u64* slot_stamp(const Slot* s, u32 par
 struct __attribute__((aligned(64))) DevCtl {
     u32 err;          // latched ERR_* bits
     u32 pad0;
-    u64 nkeys;        // hashmap: number of keys (including the side-slot key)
+    u64 nkeys;        // hashmap: keys inserted directly (prefill)
     long long depth;  // stack: current length
     u64 counter;      // scratch counter (dump compaction)
-    u64 pad1[4];
+    u64 nkeys_total;  // hashmap: nkeys + keys created by replay rounds (hm_count)
+    u64 pad1[3];
     Slot sp;          // side slot for key == EMPTY_KEY (present iff sp.created != 0)
 };
 

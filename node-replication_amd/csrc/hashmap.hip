@@ -50,6 +50,7 @@ struct IndexJob {
     u32* put_slot;
     u32 epoch;
     u32 nblocks;
+    u64* created_acc;  // [HM_CREATED_SLOTS] keys created by index blocks
     u32 exp;  // diagnostic knobs (NRG_EXP; results are wrong when set): 1 no stamp atomics,
               // 2 no LDS combining (one atomic per Put), 4 no apply role, 8 no index role
 };
@@ -199,7 +200,9 @@ __device__ __forceinline__ void index_role(IndexJob j, u32 blk, Slot* table, u32
         if (s != 0xFFFFFFFFu && !(j.exp & 1))
             atomicMax(slot_stamp(&table[s], par), ((u64)j.epoch << 32) | s_max[q]);
     }
-    if (threadIdx.x == 0 && s_created) atomicAdd(&ctl->nkeys, (u64)s_created);
+    // keys created by this block: spread over HM_CREATED_SLOTS counters (summed by hm_count);
+    // one same-address atomic per block would serialise at the memory side (~88 per us)
+    if (threadIdx.x == 0 && s_created) atomicAdd(&j.created_acc[blk % HM_CREATED_SLOTS], (u64)s_created);
 }
 
 // ---- role: apply(e) -------------------------------------------------------------------------
@@ -346,6 +349,17 @@ __global__ __launch_bounds__(TPB) void hm_prefill_range_kernel(Slot* table, u64 
     if (threadIdx.x == 0 && s_ins) atomicAdd(&ctl->nkeys, (u64)s_ins);
 }
 
+// number of keys = direct inserts (ctl->nkeys) + keys created by replay rounds
+__global__ __launch_bounds__(TPB) void hm_count_kernel(const u64* __restrict__ acc, u64 n, DevCtl* ctl) {
+    __shared__ u64 s_w[4];
+    u64 x = 0;
+    for (u64 q = threadIdx.x; q < n; q += TPB) x += acc[q];
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) ctl->nkeys_total = ctl->nkeys + s_w[0] + s_w[1] + s_w[2] + s_w[3];
+}
+
 __global__ __launch_bounds__(TPB) void hm_dump_kernel(const Slot* __restrict__ table, u64 slots, DevCtl* ctl,
                                                       u64* __restrict__ ok, u64* __restrict__ ov) {
     const u64 gid = blockIdx.x * (u64)TPB + threadIdx.x;
@@ -450,9 +464,14 @@ static void launch_round(nrg_ctx* c, const IndexJob& ij, const ApplyJob& aj, con
 }
 
 static hipError_t launch(nrg_ctx* c, IndexJob& ij, ApplyJob& aj, ReadJob& rj) {
-    const u32 K1 = c->k1_items >= 4 ? 4 : (c->k1_items == 2 ? 2 : 1);
+    // Puts per index thread: 4 for large rounds (a hot Zipf key then costs one global atomic per
+    // 1024 Puts instead of per 256: same-address atomics serialise; 50 % Zipf writes 99 -> 80 us),
+    // 1 for small rounds (more blocks in flight). NRG_K1_ITEMS overrides.
+    const u32 k1 = c->k1_items ? c->k1_items : (ij.n >= (1u << 18) ? 4 : 1);
+    const u32 K1 = k1 >= 4 ? 4 : (k1 == 2 ? 2 : 1);
     const u32 G = c->gets_per_thread >= 4 ? 4 : (c->gets_per_thread == 2 ? 2 : 1);
     ij.exp = c->exp;
+    ij.created_acc = c->d_created;
     if (c->exp & 4) aj.n = 0;
     if (c->exp & 8) ij.n = 0;
     ij.nblocks = (u32)((ij.n + TPB * K1 - 1) / (TPB * K1));
@@ -580,6 +599,13 @@ hipError_t hm_prefill_range(nrg_ctx* c, u64 n, u64 off) {
     const u32 epoch = ++c->epoch;
     hm_prefill_range_kernel<<<grid_for(n, 8192), TPB, 0, c->stream>>>(c->d_table, n, off, c->slot_shift,
                                                                       c->slots - 1, c->d_ctl, epoch);
+    return hipGetLastError();
+}
+
+hipError_t hm_count(nrg_ctx* c) {
+    hipError_t e = hm_flush(c);
+    if (e != hipSuccess) return e;
+    hm_count_kernel<<<1, TPB, 0, c->stream>>>(c->d_created, HM_CREATED_SLOTS, c->d_ctl);
     return hipGetLastError();
 }
 

@@ -85,7 +85,7 @@ struct nrg_ctx {
     nrg::Slot* d_table = nullptr;
     uint32_t* d_put_slot[2] = {nullptr, nullptr};  // per Put of a round: its slot (by epoch parity)
     uint32_t epoch = 0;              // replay rounds so far (stamps carry the round's epoch)
-    uint32_t k1_items = 1;           // Puts per thread in the index role (tuning knob NRG_K1_ITEMS)
+    uint32_t k1_items = 0;           // Puts per thread in the index role (0: by round size; NRG_K1_ITEMS)
     uint32_t gets_per_thread = 1;    // Gets per thread in the read role (tuning knob NRG_GETS)
     uint32_t exp = 0;                // diagnostic knobs (NRG_EXP), see hashmap.hip IndexJob::exp
     // Deferred second half of the last replayed round (apply its values, answer its reads):
@@ -93,6 +93,7 @@ struct nrg_ctx {
     // that reads the table. With pipeline == false it is flushed at the end of every call.
     bool pipeline = false;
     nrg::HmDeferred pend;
+    uint64_t* d_created = nullptr;  // [HM_CREATED_SLOTS] keys created by replay rounds
     // Zipf generator cache: zeta(zipf_n, zipf_theta)
     uint64_t zipf_n = 0;
     double zipf_theta = 0.0, zipf_zetan = 0.0;
@@ -151,6 +152,7 @@ hipError_t hm_get_only(nrg_ctx* c, const u64* d_keys, u64 n, u64* d_vals, uint8_
 hipError_t hm_init(nrg_ctx* c);
 hipError_t hm_prefill_range(nrg_ctx* c, u64 n, u64 off);
 hipError_t hm_dump(nrg_ctx* c, u64* d_keys, u64* d_vals);
+hipError_t hm_count(nrg_ctx* c);  // DevCtl::nkeys_total = number of keys
 hipError_t hm_digest(nrg_ctx* c, u64* d_out3);
 hipError_t gen_uniform(nrg_ctx* c, u64* d, u64 n, u64 seed, u64 span);
 hipError_t gen_raw(nrg_ctx* c, u64* d, u64 n, u64 seed);

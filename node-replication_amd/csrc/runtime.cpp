@@ -323,6 +323,8 @@ int nrg_open(int dev, const nrg_config* cfg_in, nrg_ctx** out) {
         OPEN_CHK(hm_init(c));
         OPEN_CHK(hipMalloc(&c->d_put_slot[0], mb * sizeof(uint32_t)));
         OPEN_CHK(hipMalloc(&c->d_put_slot[1], mb * sizeof(uint32_t)));
+        OPEN_CHK(hipMalloc(&c->d_created, HM_CREATED_SLOTS * sizeof(uint64_t)));
+        OPEN_CHK(hipMemsetAsync(c->d_created, 0, HM_CREATED_SLOTS * sizeof(uint64_t), c->stream));
         if (const char* e = std::getenv("NRG_K1_ITEMS")) c->k1_items = (uint32_t)std::atoi(e);
         if (const char* e = std::getenv("NRG_GETS")) c->gets_per_thread = (uint32_t)std::atoi(e);
         if (const char* e = std::getenv("NRG_EXP")) c->exp = (uint32_t)std::atoi(e);
@@ -369,7 +371,8 @@ int nrg_close(nrg_ctx* c) {
     if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
     if (c->stream && c->stream != c->own_stream) (void)hipStreamSynchronize(c->stream);
     void* ptrs[] = {c->d_ring,    c->d_ctl,      c->d_table,   c->d_put_slot[0], c->d_put_slot[1],
-                    c->d_stack,   c->d_words,    c->d_sort_aux, c->d_tmp_u64,    c->d_scan_desc};
+                    c->d_stack,   c->d_words,    c->d_sort_aux, c->d_tmp_u64,    c->d_scan_desc,
+                    c->d_created};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     sort_free(c->sort);
@@ -667,7 +670,8 @@ int nrg_hashmap_prefill_range(nrg_ctx* c, uint64_t n, uint64_t off) {
 int nrg_hashmap_size(nrg_ctx* c, uint64_t* n) {
     int r = need(c, NRG_DS_HASHMAP);
     if (r) return r;
-    HIPCHK(hipMemcpyAsync(n, &c->d_ctl->nkeys, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hm_count(c));
+    HIPCHK(hipMemcpyAsync(n, &c->d_ctl->nkeys_total, 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(sync_all(c));
     return check_err(c);
 }
