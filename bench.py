@@ -492,6 +492,27 @@ def run_stack(args, env):
     return res
 
 
+def write_scaleout_csv(path, name, world, ops_per_rank_per_round, steps, elapsed):
+    """Append rows in the reference harness's scaleout_benchmarks.csv format
+    (benches/mkbench.rs:498-552: name, rs, tm, batch_size, threads, duration, thread_id, core_id,
+    exp_time_in_sec, iterations), so CPU and GPU results plot with the reference's tooling
+    (benches/hashbench_plot.r). One row per GPU replica: rs = "GPU" (one replica per GPU, the
+    analogue of ReplicaStrategy::Socket per NUMA node), thread_id = core_id = rank, and the
+    per-second counter `iterations` = that replica's ops per second over the timed region (the
+    region is far shorter than the reference's 1-s sampling interval)."""
+    import csv
+
+    new = not os.path.exists(path)
+    with open(path, "a", newline="") as f:
+        w = csv.writer(f)
+        if new:
+            w.writerow(["name", "rs", "tm", "batch_size", "threads", "duration", "thread_id", "core_id",
+                        "exp_time_in_sec", "iterations"])
+        for r in range(world):
+            w.writerow([name, "GPU", "Sequential", ops_per_rank_per_round, world, round(elapsed, 6), r, r, 1,
+                        int(ops_per_rank_per_round * steps / elapsed)])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -515,6 +536,7 @@ def main():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo: CPU rehearsal)")
     ap.add_argument("--share-gpu", action="store_true", help="all ranks on cuda:0 (gloo rehearsal on a 1-GPU box)")
+    ap.add_argument("--csv", default=None, help="append scaleout_benchmarks.csv rows (reference format)")
     ap.add_argument("--timing-every", type=int, default=8, help="event-stamp every n-th launch of the timed kernel")
     ap.add_argument("--pipeline", type=int, default=1,
                     help="1: a round's apply+reads ride in the next round's launch (nrg_config.pipeline); "
@@ -523,6 +545,11 @@ def main():
     env = Env(args)
     res = run_stack(args, env) if args.workload == "stack" else run_hashmap(args, env)
     if res is not None:
+        if args.csv:
+            name = "nrstack-gpu" if args.workload == "stack" else "nrhashmap-gpu-wr%d-%s" % (
+                args.write_ratio, key_dist_name(args))
+            write_scaleout_csv(args.csv, name, env.world, args.ops_per_gpu, args.steps,
+                               res["ms_per_step"] * args.steps / 1e3)
         print(json.dumps(res), flush=True)
     env.close()
 

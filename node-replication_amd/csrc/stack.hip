@@ -39,7 +39,26 @@ __device__ __forceinline__ long long fn_apply(Fn f, long long x) {
 constexpr u64 D_AGG = 1ull << 62;
 constexpr u64 D_INC = 2ull << 62;
 constexpr u64 D_MASK = 3ull << 62;
-constexpr int LB_WIN = 16;  // look-back window
+
+// identity of fn_then (a = -infinity for max(a, x + b))
+constexpr Fn FN_ID = {0, -(1ll << 50)};
+
+// Compose the 64 lanes' functions in tile order, oldest (highest lane) applied first:
+// result = f_63 then f_62 ... then f_0, broadcast to every lane.
+__device__ __forceinline__ Fn wave_compose(Fn f) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int s = 1; s < 64; s <<= 1) {
+        Fn o;
+        o.b = __shfl_down(f.b, s, 64);
+        o.a = __shfl_down(f.a, s, 64);
+        if ((lane & (2 * s - 1)) == 0 && lane + s < 64) f = fn_then(o, f);
+    }
+    Fn r;
+    r.b = __shfl(f.b, 0, 64);
+    r.a = __shfl(f.a, 0, 64);
+    return r;
+}
 
 __device__ __forceinline__ u64 pack_agg(Fn f) {
     return D_AGG | ((u64)(f.b + (1ll << 30)) << 31) | (u64)f.a;
@@ -103,50 +122,51 @@ __global__ __launch_bounds__(ST_TPB) void st_scan_kernel(const nrg_stack_op* __r
     Fn wpre = {0, 0};
     for (int i = 0; i < w; i++) wpre = fn_then(wpre, Fn{s_wb[i], s_wa[i]});
     const Fn tpre = fn_then(wpre, ex);
-    if (t == 0) {
+    if (w == 0) {
+        // Wave 0 publishes the tile's aggregate and does the look-back with all 64 lanes:
+        // lane l reads tile (tt - l)'s descriptor, so one memory round trip covers 64
+        // predecessors (a one-lane walk costs a round trip per predecessor tile, and all tiles
+        // are in flight together, so each walks back to tile 0: 42 us for 1M ops).
         Fn tagg = {0, 0};
         for (int i = 0; i < 4; i++) tagg = fn_then(tagg, Fn{s_wb[i], s_wa[i]});
-        long long dbase;
+        long long dbase = 0;
         if (tile == 0) {
             dbase = ctl->depth;
-            __hip_atomic_store(&desc[0], D_INC | (u64)fn_apply(tagg, dbase), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0)
+                __hip_atomic_store(&desc[0], D_INC | (u64)fn_apply(tagg, dbase), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
         } else {
-            __hip_atomic_store(&desc[tile], pack_agg(tagg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            // windowed look-back: LB_WIN predecessor descriptors per memory round trip,
-            // consumed newest-first (tile 0 always publishes an inclusive value)
-            Fn acc = {0, 0};
+            if (lane == 0) __hip_atomic_store(&desc[tile], pack_agg(tagg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            Fn acc = FN_ID;  // composition of the predecessors consumed so far (older ones apply first)
             int tt = (int)tile - 1;
-            bool done = false;
-            while (!done) {
-                u64 v[LB_WIN];
-#pragma unroll
-                for (int q = 0; q < LB_WIN; q++)
-                    v[q] = tt - q >= 0 ? __hip_atomic_load(&desc[tt - q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                       : 0ull;
-                int used = 0;
-#pragma unroll
-                for (int q = 0; q < LB_WIN; q++) {
-                    if (done || used < q) continue;
-                    const u64 st = v[q] & D_MASK;
-                    if (st == 0) continue;
-                    used = q + 1;
-                    if (st == D_INC) {
-                        dbase = fn_apply(acc, (long long)(v[q] & ~D_MASK));
-                        done = true;
-                    } else {
-                        acc = fn_then(unpack_agg(v[q]), acc);
-                    }
+            for (;;) {
+                const int idx = tt - lane;
+                const u64 v = idx >= 0 ? __hip_atomic_load(&desc[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+                const u64 st = v & D_MASK;
+                const u64 nr = __ballot(st == 0);
+                const u64 ic = __ballot(st == D_INC);
+                const int first_nr = nr ? __ffsll((unsigned long long)nr) - 1 : 64;
+                const int first_ic = ic ? __ffsll((unsigned long long)ic) - 1 : 64;
+                const int use = first_ic < first_nr ? first_ic : first_nr;  // aggregates usable now
+                const Fn f = lane < use ? unpack_agg(v) : FN_ID;
+                acc = fn_then(wave_compose(f), acc);
+                if (first_ic < first_nr) {
+                    const long long incv = (long long)(__shfl(v, first_ic, 64) & ~D_MASK);
+                    dbase = fn_apply(acc, incv);
+                    break;
                 }
-                tt -= used;
-                if (!done && used < LB_WIN) __builtin_amdgcn_s_sleep(1);
+                tt -= use;
+                if (use < 64) __builtin_amdgcn_s_sleep(1);
             }
-            __hip_atomic_store(&desc[tile], D_INC | (u64)fn_apply(tagg, dbase), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0)
+                __hip_atomic_store(&desc[tile], D_INC | (u64)fn_apply(tagg, dbase), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
         }
-        const u64 ntiles = (n + ST_TILE - 1) / ST_TILE;
-        if ((u64)tile == ntiles - 1) ctl->depth = fn_apply(tagg, dbase);
-        s_dbase = dbase;
+        if (lane == 0) {
+            const u64 ntiles = (n + ST_TILE - 1) / ST_TILE;
+            if ((u64)tile == ntiles - 1) ctl->depth = fn_apply(tagg, dbase);
+            s_dbase = dbase;
+        }
     }
     __syncthreads();
     long long d = fn_apply(tpre, s_dbase);

@@ -21,7 +21,6 @@ constexpr u32 SETBIT = 0x80000000u;
 constexpr int MS_TPB = 256;
 constexpr int MS_ITEMS = 8;
 constexpr int MS_TILE = MS_TPB * MS_ITEMS;
-constexpr int LB_WIN = 16;  // look-back window
 
 __global__ void sy_init_kernel(u64* words, u64 n) {
     for (u64 i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (u64)gridDim.x * 256ull) words[i] = i;
@@ -99,39 +98,40 @@ __global__ __launch_bounds__(MS_TPB) void sy_maxscan_kernel(const u32* __restric
         if (i < w) wpre = wpre > s_w[i] ? wpre : s_w[i];
         tagg = tagg > s_w[i] ? tagg : s_w[i];
     }
-    if (t == 0) {
+    if (w == 0) {
+        // wave 0: lane l reads tile (tt - l)'s descriptor (64 predecessors per round trip)
         u32 pre = 0;
         if (tile == 0) {
-            __hip_atomic_store(&desc[0], M_INC | tagg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0) __hip_atomic_store(&desc[0], M_INC | tagg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
-            __hip_atomic_store(&desc[tile], M_AGG | tagg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            // windowed look-back: LB_WIN predecessor descriptors per memory round trip
+            if (lane == 0) __hip_atomic_store(&desc[tile], M_AGG | tagg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             int tt = (int)tile - 1;
-            bool done = false;
-            while (!done) {
-                u64 v[LB_WIN];
-#pragma unroll
-                for (int q = 0; q < LB_WIN; q++)
-                    v[q] = tt - q >= 0 ? __hip_atomic_load(&desc[tt - q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                       : 0ull;
-                int used = 0;
-#pragma unroll
-                for (int q = 0; q < LB_WIN; q++) {
-                    if (done || used < q) continue;
-                    const u64 st = v[q] & M_MASK;
-                    if (st == 0) continue;
-                    used = q + 1;
-                    const u32 x = (u32)v[q];
-                    pre = pre > x ? pre : x;
-                    if (st == M_INC) done = true;
+            for (;;) {
+                const int idx = tt - lane;
+                const u64 v = idx >= 0 ? __hip_atomic_load(&desc[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+                const u64 st = v & M_MASK;
+                const u64 nr = __ballot(st == 0);
+                const u64 ic = __ballot(st == M_INC);
+                const int first_nr = nr ? __ffsll((unsigned long long)nr) - 1 : 64;
+                const int first_ic = ic ? __ffsll((unsigned long long)ic) - 1 : 64;
+                const bool found = first_ic < first_nr;
+                const int use = found ? first_ic + 1 : first_nr;
+                u32 x = lane < use ? (u32)v : 0u;
+                for (int off = 32; off > 0; off >>= 1) {
+                    const u32 y = __shfl_xor(x, off, 64);
+                    x = x > y ? x : y;
                 }
-                tt -= used;
-                if (!done && used < LB_WIN) __builtin_amdgcn_s_sleep(1);
+                pre = pre > x ? pre : x;
+                if (found) break;
+                tt -= use;
+                if (use < 64) __builtin_amdgcn_s_sleep(1);
             }
-            const u32 ti = pre > tagg ? pre : tagg;
-            __hip_atomic_store(&desc[tile], M_INC | ti, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0) {
+                const u32 ti = pre > tagg ? pre : tagg;
+                __hip_atomic_store(&desc[tile], M_INC | ti, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
-        s_base = pre;
+        if (lane == 0) s_base = pre;
     }
     __syncthreads();
     u32 pre = s_base > wpre ? s_base : wpre;

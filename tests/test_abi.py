@@ -76,3 +76,22 @@ def test_null_and_bad_arguments_are_errors_not_crashes(lib):
     rc = lib.nrg_open(0, C.byref(cfg), C.byref(out))
     assert rc in (L.NRG_E_INVAL, L.NRG_E_NODEV)
     assert lib.nrg_sync(None) == L.NRG_E_INVAL
+
+
+def test_scaleout_csv_format(tmp_path):
+    """bench.py --csv writes the reference harness's scaleout_benchmarks.csv columns
+    (benches/mkbench.rs:518-545), header once, one row per replica."""
+    import csv
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    p = tmp_path / "scaleout_benchmarks.csv"
+    bench.write_scaleout_csv(str(p), "nrhashmap-gpu", 2, 1_000_000, 10, 0.005)
+    bench.write_scaleout_csv(str(p), "nrhashmap-gpu", 2, 1_000_000, 10, 0.005)
+    rows = list(csv.reader(open(p)))
+    assert rows[0] == ["name", "rs", "tm", "batch_size", "threads", "duration", "thread_id", "core_id",
+                       "exp_time_in_sec", "iterations"]
+    assert len(rows) == 5 and rows[1][6] == "0" and rows[2][6] == "1"
+    assert int(rows[1][9]) == 2_000_000_000
