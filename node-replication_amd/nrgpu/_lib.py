@@ -10,7 +10,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libnrgpu.so")
+LIB_PATH = os.environ.get("NRGPU_LIB") or os.path.join(PKG_ROOT, "lib", "libnrgpu.so")  # env: A/B builds
 
 # import torch first (when present) so that the process has ONE HIP runtime: torch ships
 # its own libamdhip64.so.7 and the loader then reuses it for libnrgpu.so by SONAME.
