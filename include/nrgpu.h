@@ -98,11 +98,12 @@ typedef struct {
 /* ---- configuration ------------------------------------------------------------------ */
 typedef struct {
     uint32_t ds_kind;         /* NRG_DS_*                                                  */
-    uint32_t log2_slots;      /* hashmap: table has 2^log2_slots 32-B slots (default 26)    */
+    uint32_t log2_slots;      /* hashmap: table has 2^log2_slots 64-B slots (default 26)    */
     uint64_t log_bytes;       /* Log::new(bytes): ring entries = bytes/64 rounded as in the
                                  reference (min 2*GC_FROM_HEAD, power of two). 0 = 32 MiB   */
     uint64_t max_batch;       /* largest number of log records replayed per kernel pass;
-                                 larger exec ranges are replayed in order, in chunks        */
+                                 larger exec ranges are replayed in order, in chunks
+                                 (< 2^30; stack: <= 2^24)                                   */
     uint64_t max_reads;       /* largest read batch per call                               */
     uint64_t stack_capacity;  /* stack: maximum number of elements                          */
     uint64_t synth_n;         /* synthetic: number of words (default 200000)               */

@@ -68,7 +68,9 @@ struct __attribute__((aligned(64))) DevCtl {
     long long depth;  // stack: current length
     u64 counter;      // scratch counter (dump compaction)
     u64 nkeys_total;  // hashmap: nkeys + keys created by replay rounds (hm_count)
-    u64 pad1[3];
+    long long depth0;      // stack: length before the chunk being replayed
+    long long depth_next;  // stack: length after it (st_commit_kernel moves it to depth)
+    u64 pad1;
     Slot sp;          // side slot for key == EMPTY_KEY (present iff sp.created != 0)
 };
 

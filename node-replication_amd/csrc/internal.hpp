@@ -99,7 +99,7 @@ struct nrg_ctx {
     double zipf_theta = 0.0, zipf_zetan = 0.0;
     // ---- Stack ----
     uint32_t* d_stack = nullptr;
-    uint32_t stack_key_bits = 0;
+    void* d_st_aux = nullptr;  // per-tile minima, last-Push tables and cross-tile Pops (stack.hip)
 
     // ---- Synthetic ----
     uint64_t* d_words = nullptr;
@@ -166,6 +166,7 @@ hipError_t copy_segments(nrg_ctx* c, const void* d_base, u32 nseg, u64 seg_strid
 // stack.hip
 hipError_t st_replay_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 resp_hi, uint32_t* d_resp,
                            uint8_t* d_some);
+u64 st_aux_bytes(u64 max_batch);  // size of nrg_ctx::d_st_aux
 
 // synthetic.hip
 hipError_t sy_init(nrg_ctx* c);

@@ -333,14 +333,19 @@ int nrg_open(int dev, const nrg_config* cfg_in, nrg_ctx** out) {
         c->epoch = 1;  // epoch 1 = the state built by prefill; replay rounds start at 2
         if (sort_alloc(c->sort, mb) != NRG_OK) { nrg_close(c); return NRG_E_NOMEM; }
     } else if (cf.ds_kind == NRG_DS_STACK) {
-        if (!cf.stack_capacity || cf.stack_capacity >= (1ull << 31)) { nrg_close(c); return NRG_E_INVAL; }
+        // max_batch <= 2^24: st_cross_kernel stages one minimum per 2048-op tile in LDS
+        if (!cf.stack_capacity || cf.stack_capacity >= (1ull << 31) || mb > (1ull << 24)) {
+            nrg_close(c);
+            return NRG_E_INVAL;
+        }
         OPEN_CHK(hipMalloc(&c->d_stack, cf.stack_capacity * sizeof(uint32_t)));
-        c->stack_key_bits = bits_for(cf.stack_capacity);  // sentinel = 2^bits - 1 >= capacity
-        OPEN_CHK(hipMalloc(&c->d_tmp_u64, mb * sizeof(uint64_t)));
+        OPEN_CHK(hipMalloc(&c->d_tmp_u64, mb * sizeof(uint64_t)));  // last-Push window: 2 * mb u32
+        OPEN_CHK(hipMemsetAsync(c->d_tmp_u64, 0, mb * sizeof(uint64_t), c->stream));
         c->tmp_words = mb;
         c->scan_desc_words = 2 * (32 + (mb + 2047) / 2048);
         OPEN_CHK(hipMalloc(&c->d_scan_desc, c->scan_desc_words * 4));
-        if (sort_alloc(c->sort, mb) != NRG_OK) { nrg_close(c); return NRG_E_NOMEM; }
+        OPEN_CHK(hipMalloc(&c->d_st_aux, st_aux_bytes(mb)));
+        if (const char* e = std::getenv("NRG_EXP")) c->exp = (uint32_t)std::atoi(e);
     } else {
         const uint64_t T = cf.synth_hot_writes + cf.synth_cold_writes;
         if (!cf.synth_n || cf.synth_hot_reads == 0 || cf.synth_n <= cf.synth_hot_reads || T == 0 || T > 64 ||
@@ -372,7 +377,7 @@ int nrg_close(nrg_ctx* c) {
     if (c->stream && c->stream != c->own_stream) (void)hipStreamSynchronize(c->stream);
     void* ptrs[] = {c->d_ring,    c->d_ctl,      c->d_table,   c->d_put_slot[0], c->d_put_slot[1],
                     c->d_stack,   c->d_words,    c->d_sort_aux, c->d_tmp_u64,    c->d_scan_desc,
-                    c->d_created};
+                    c->d_created, c->d_st_aux};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     sort_free(c->sort);
