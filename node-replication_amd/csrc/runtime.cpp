@@ -344,6 +344,7 @@ int nrg_open(int dev, const nrg_config* cfg_in, nrg_ctx** out) {
         c->tmp_words = mb;
         c->scan_desc_words = 2 * (32 + (mb + 2047) / 2048);
         OPEN_CHK(hipMalloc(&c->d_scan_desc, c->scan_desc_words * 4));
+        OPEN_CHK(hipMemsetAsync(c->d_scan_desc, 0, c->scan_desc_words * 4, c->stream));
         OPEN_CHK(hipMalloc(&c->d_st_aux, st_aux_bytes(mb)));
         if (const char* e = std::getenv("NRG_EXP")) c->exp = (uint32_t)std::atoi(e);
     } else {

@@ -21,9 +21,8 @@
 // only. The chunk's final content of a slot is its last Push, picked with one atomicMax per
 // (tile, pushed slot) in a window of 2n slots around the chunk's starting depth.
 //
-// Kernels: st_tile_kernel (scan + LDS bitonic sort + in-tile pairing + tables),
-// st_cross_kernel (cross-tile Pops; launched only when responses are wanted),
-// st_commit_kernel (last Pushes -> stack, depth update).
+// Kernels: st_tile_kernel (scan + in-tile pairing + tables), st_finish_kernel (cross-tile
+// Pops, last Pushes -> stack, depth update).
 #include "internal.hpp"
 
 namespace nrg {
@@ -86,9 +85,11 @@ __device__ __forceinline__ Fn unpack_agg(u64 v) {
 // Per-tile results of st_tile_kernel, read by st_cross_kernel.
 struct StTiles {
     long long* tmin;   // [tiles] minimum depth reached in the tile (start and end included)
-    uint16_t* table;   // [tiles][ST_TILE] position of the tile's last Push to slot tmin + r
+    u32* table;        // [tiles][ST_TILE] value of the tile's last Push to slot tmin + r, for the
+                       // slots below the tile's end depth (the only ones ever looked up)
     u32* ucnt;         // [tiles] Pops whose Push is outside the tile
     u32* upop;         // [tiles][ST_TILE] those Pops: (slot - tmin) << 11 | position
+    u32* uval;         // [tiles][ST_TILE] their slot's content before the chunk (if below it)
 };
 
 __device__ __forceinline__ long long block_min4(long long x, long long* s_w, int w, int lane) {
@@ -108,11 +109,11 @@ constexpr u32 ST_INF = 0xFFFFu;
 
 __global__ __launch_bounds__(ST_TPB) void st_tile_kernel(const nrg_stack_op* __restrict__ ring, u64 ring_mask, u64 lo,
                                                          u64 n, DevCtl* ctl, u64* desc, u32* ticket, StTiles tl,
-                                                         u32* __restrict__ last, u64 cap, u64 resp_lo, u64 resp_hi,
-                                                         int push_resp, u32* __restrict__ resp,
-                                                         uint8_t* __restrict__ some) {
+                                                         u32* __restrict__ last, const u32* __restrict__ stack,
+                                                         u64 cap, u64 resp_lo, u64 resp_hi, int push_resp,
+                                                         u32* __restrict__ resp, uint8_t* __restrict__ some) {
     __shared__ long long s_wb[4], s_wa[4], s_wmin[4];
-    __shared__ u32 s_tile, s_ucnt;
+    __shared__ u32 s_tile, s_ucnt, s_aend;
     __shared__ long long s_dbase;
     __shared__ u32 s_val[ST_TILE];             // op values by position
     __shared__ uint16_t s_A[ST_TILE + 1];      // depth after op i (- tmin) at [i + 1]; [0] = start
@@ -331,8 +332,12 @@ __global__ __launch_bounds__(ST_TPB) void st_tile_kernel(const nrg_stack_op* __r
                 }
             }
             if (r == -2) {  // the Push is in an earlier tile or before the chunk
+                // No tile writes the stack before st_finish_kernel, so read the pre-chunk
+                // content now; it is the answer when no earlier tile of the chunk pushed s.
                 const u32 k = atomicAdd(&s_ucnt, 1u);
+                const long long slot = tmin + s;
                 tl.upop[(u64)tile * ST_TILE + k] = (s << 11) | pos;
+                tl.uval[(u64)tile * ST_TILE + k] = slot < d0 && (u64)slot < cap ? stack[slot] : 0u;
             } else if (inwin) {
                 resp[g - resp_lo] = s_val[r + 1];
                 some[g - resp_lo] = 1;
@@ -340,13 +345,14 @@ __global__ __launch_bounds__(ST_TPB) void st_tile_kernel(const nrg_stack_op* __r
         }
         prv = a[q];
     }
+    if (t == ST_TPB - 1) s_aend = a[ST_ITEMS - 1];
     __syncthreads();
-    uint16_t* tab = tl.table + (u64)tile * ST_TILE;
-    for (int r = t; r < ST_TILE; r += ST_TPB) {
+    // Levels [tmin, end depth) each have a last Push (suffix records); no other level has one.
+    u32* tab = tl.table + (u64)tile * ST_TILE;
+    for (u32 r = t; r < s_aend; r += ST_TPB) {
         const uint16_t p = s_tab[r];
-        tab[r] = p;
-        if (p != ST_NO_PUSH)
-            atomicMax(&last[(u64)(tmin + r - d0 + (long long)n)], ((tile << 11) | p) + 1u);
+        tab[r] = s_val[p];
+        atomicMax(&last[(u64)(tmin + r - d0 + (long long)n)], ((tile << 11) | p) + 1u);
     }
     if (t == 0) {
         tl.tmin[tile] = tmin;
@@ -354,34 +360,83 @@ __global__ __launch_bounds__(ST_TPB) void st_tile_kernel(const nrg_stack_op* __r
     }
 }
 
-// Pops whose Push lies in an earlier tile (or before the chunk). The block stages the minima
-// of tiles [0, tile) in LDS with the minimum of every 64-tile group, so a walk back skips a
-// group whose minimum is above the slot in one step.
-__global__ __launch_bounds__(256) void st_cross_kernel(const nrg_stack_op* __restrict__ ring, u64 ring_mask, u64 lo,
-                                                       StTiles tl, const u32* __restrict__ stack, u64 cap,
-                                                       u64 resp_lo, u64 resp_hi, u32* __restrict__ resp,
-                                                       uint8_t* __restrict__ some) {
-    extern __shared__ long long s_tm[];  // [tiles] minima, then [tiles / 64 + 1] group minima
+// One block per tile after st_tile_kernel. Every block stages all tile minima in LDS (with the
+// minimum of every 64-tile group) and then
+//   * commits: for the slots any tile pushed — [min tmin, max tmin + 2048) of the window
+//     [depth0 - n, depth0 + n) — writes the chunk's last Push and clears the window entry;
+//   * resolves the tile's Pops whose Push lies in an earlier tile: the nearest earlier tile
+//     whose minimum is <= the slot (a walk that skips 8- and 64-tile groups whose minimum is
+//     above the slot), or the pre-chunk content st_tile_kernel read.
+// Block 0 publishes the new depth.
+__global__ __launch_bounds__(256) void st_finish_kernel(const nrg_stack_op* __restrict__ ring, u64 ring_mask, u64 lo,
+                                                        u64 n, DevCtl* ctl, StTiles tl, u32* __restrict__ last,
+                                                        u32* __restrict__ stack, u64 cap, u64 resp_lo, u64 resp_hi,
+                                                        u32* __restrict__ resp, uint8_t* __restrict__ some,
+                                                        u64* desc, u32* ticket) {
+    extern __shared__ long long s_tm[];  // [tiles] tile minima, [tiles/8 + 1] and [tiles/64 + 1] group minima
+    __shared__ long long s_lo[4], s_hi[4];
+    const u32 tiles = gridDim.x;
     const u32 tile = blockIdx.x;
-    const u32 cnt = tl.ucnt[tile];
-    if (cnt == 0) return;
-    const int t = threadIdx.x, lane = t & 63;
-    const u32 ngr = (tile + 63) / 64;
-    long long* s_gm = s_tm + gridDim.x;
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    // independent loads first: they overlap the staging below
+    const long long d0 = ctl->depth0;
+    const u32 cnt = resp ? tl.ucnt[tile] : 0u;
+    const u32 v0 = tl.upop[(u64)tile * ST_TILE + t];
+    const u32 uv0 = tl.uval[(u64)tile * ST_TILE + t];
+    if (t == 0) desc[tile] = 0;  // ready for the next chunk (the tile kernel is done)
+    if (tile == 0 && t == 0) *ticket = 0;
+    const u32 ngr = (tiles + 63) / 64;
+    long long* s_g8 = s_tm + tiles;
+    long long* s_gm = s_g8 + tiles / 8 + 1;
+    long long mn = 1ll << 62, mx = -(1ll << 62);
     for (u32 k = t; k < ngr * 64; k += 256) {
-        long long m = k < tile ? tl.tmin[k] : (1ll << 62);
-        if (k < tile) s_tm[k] = m;
+        const long long v = k < tiles ? tl.tmin[k] : (1ll << 62);
+        if (k < tiles) {
+            s_tm[k] = v;
+            mx = v > mx ? v : mx;
+        }
+        long long m = v;
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
+        for (int off = 1; off < 64; off <<= 1) {
             const long long x = __shfl_xor(m, off, 64);
             m = x < m ? x : m;
+            if (off == 4 && (lane & 7) == 0 && (k >> 3) <= tiles / 8) s_g8[k >> 3] = m;
         }
         if (lane == 0) s_gm[k >> 6] = m;
+        mn = m < mn ? m : mn;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const long long x = __shfl_xor(mx, off, 64);
+        mx = x > mx ? x : mx;
+    }
+    if (lane == 0) {
+        s_lo[w] = mn;
+        s_hi[w] = mx;
     }
     __syncthreads();
-    const long long tmin = tl.tmin[tile];
+    if (tile == 0 && t == 0) ctl->depth = ctl->depth_next;
+    {
+        long long smin = s_lo[0], smax = s_hi[0];
+        for (int i = 1; i < 4; i++) {
+            smin = s_lo[i] < smin ? s_lo[i] : smin;
+            smax = s_hi[i] > smax ? s_hi[i] : smax;
+        }
+        long long ilo = smin - d0 + (long long)n, ihi = smax + ST_TILE - d0 + (long long)n;
+        ilo = ilo < 0 ? 0 : ilo;
+        ihi = ihi > 2 * (long long)n ? 2 * (long long)n : ihi;
+        for (long long i = ilo + tile * 256ll + t; i < ihi; i += (long long)tiles * 256) {
+            const u32 x = last[i];
+            if (!x) continue;
+            last[i] = 0;
+            const long long slot = i + d0 - (long long)n;
+            if ((u64)slot < cap)
+                stack[slot] = ring[(lo + (u64)((x - 1) >> 11) * ST_TILE + ((x - 1) & 2047u)) & ring_mask].val;
+        }
+    }
+    const long long tmin = s_tm[tile];
     for (u32 j = t; j < cnt; j += 256) {
-        const u32 v = tl.upop[(u64)tile * ST_TILE + j];
+        const u32 v = j == (u32)t ? v0 : tl.upop[(u64)tile * ST_TILE + j];
         const u64 g = lo + (u64)tile * ST_TILE + (v & 2047u);
         if (g < resp_lo || g >= resp_hi) continue;
         const long long s = tmin + (v >> 11);
@@ -391,34 +446,20 @@ __global__ __launch_bounds__(256) void st_cross_kernel(const nrg_stack_op* __res
                 k -= 64;
                 continue;
             }
+            if ((k & 7) == 7 && s_g8[k >> 3] > s) {
+                k -= 8;
+                continue;
+            }
             if (s_tm[k] <= s) break;
             k--;
         }
         u32 val;
-        if (k >= 0) {
-            const u32 pos = tl.table[(u64)k * ST_TILE + (u64)(s - s_tm[k])];
-            val = ring[(lo + (u64)k * ST_TILE + pos) & ring_mask].val;
-        } else {
-            val = (u64)s < cap ? stack[s] : 0u;
-        }
+        if (k >= 0)
+            val = tl.table[(u64)k * ST_TILE + (u64)(s - s_tm[k])];
+        else
+            val = j == (u32)t ? uv0 : tl.uval[(u64)tile * ST_TILE + j];
         resp[g - resp_lo] = val;
         some[g - resp_lo] = 1;
-    }
-}
-
-// Slot window [depth0 - n, depth0 + n): write each slot's last Push of the chunk, clear the
-// window for the next chunk, and publish the new depth.
-__global__ __launch_bounds__(256) void st_commit_kernel(const nrg_stack_op* __restrict__ ring, u64 ring_mask, u64 lo,
-                                                        u64 n, DevCtl* ctl, u32* __restrict__ last,
-                                                        u32* __restrict__ stack, u64 cap) {
-    const long long d0 = ctl->depth0;
-    if (blockIdx.x == 0 && threadIdx.x == 0) ctl->depth = ctl->depth_next;
-    for (u64 i = blockIdx.x * 256ull + threadIdx.x; i < 2 * n; i += (u64)gridDim.x * 256) {
-        const u32 x = last[i];
-        if (!x) continue;
-        last[i] = 0;
-        const long long slot = (long long)i + d0 - (long long)n;
-        if ((u64)slot < cap) stack[slot] = ring[(lo + (u64)((x - 1) >> 11) * ST_TILE + ((x - 1) & 2047u)) & ring_mask].val;
     }
 }
 
@@ -428,37 +469,34 @@ hipError_t st_replay_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 resp_hi, 
     const u64 ring_mask = c->log_size - 1;
     const nrg_stack_op* ring = (const nrg_stack_op*)c->d_ring;
     const u64 tiles = (n + ST_TILE - 1) / ST_TILE;
-    // descriptors: [ticket (64 words of u32 = 32 u64)] [tiles u64]
+    // descriptors: [ticket (64 words of u32 = 32 u64)] [tiles u64]; zero at open, and
+    // st_finish_kernel clears what st_tile_kernel used (no memset launch per chunk)
     u64* desc = (u64*)c->d_scan_desc + 32;
     u32* ticket = c->d_scan_desc;
-    hipError_t e = hipMemsetAsync(c->d_scan_desc, 0, (32 + tiles) * sizeof(u64), st);
-    if (e != hipSuccess) return e;
     const u64 mt = (c->cfg.max_batch + ST_TILE - 1) / ST_TILE;
     StTiles tl;
     tl.tmin = (long long*)c->d_st_aux;
     tl.ucnt = (u32*)(tl.tmin + mt);
     tl.upop = tl.ucnt + mt;
-    tl.table = (uint16_t*)(tl.upop + mt * ST_TILE);
+    tl.uval = tl.upop + mt * ST_TILE;
+    tl.table = tl.uval + mt * ST_TILE;
     u32* last = (u32*)c->d_tmp_u64;  // 2 * max_batch u32, zero between chunks
     const bool want = d_resp != nullptr && resp_lo < lo + n && resp_hi > lo;
     const u64 rlo = want ? resp_lo : 0, rhi = want ? resp_hi : 0;
     timer_begin(c, "st_replay");
     st_tile_kernel<<<(unsigned)tiles, ST_TPB, 0, st>>>(ring, ring_mask, lo, n, c->d_ctl, desc, ticket, tl, last,
-                                                      c->cfg.stack_capacity, rlo, rhi,
+                                                      c->d_stack, c->cfg.stack_capacity, rlo, rhi,
                                                       (int)c->cfg.stack_push_resp, d_resp, d_some);
-    if (want)
-        st_cross_kernel<<<(unsigned)tiles, 256, (tiles + tiles / 64 + 1) * 8, st>>>(ring, ring_mask, lo, tl, c->d_stack, c->cfg.stack_capacity,
-                                                        rlo, rhi, d_resp, d_some);
-    const u64 cg = (2 * n + 255) / 256;
-    st_commit_kernel<<<(unsigned)(cg < 2048 ? cg : 2048), 256, 0, st>>>(ring, ring_mask, lo, n, c->d_ctl, last,
-                                                                        c->d_stack, c->cfg.stack_capacity);
+    st_finish_kernel<<<(unsigned)tiles, 256, (tiles + tiles / 8 + tiles / 64 + 2) * 8, st>>>(
+        ring, ring_mask, lo, n, c->d_ctl, tl, last, c->d_stack, c->cfg.stack_capacity, rlo, rhi,
+        want ? d_resp : nullptr, d_some, desc, ticket);
     timer_end(c, "st_replay");
     return hipGetLastError();
 }
 
 u64 st_aux_bytes(u64 max_batch) {
     const u64 mt = (max_batch + ST_TILE - 1) / ST_TILE;
-    return mt * (8 + 4) + mt * ST_TILE * (4 + 2);
+    return mt * (8 + 4) + mt * ST_TILE * (4 + 4 + 4);
 }
 
 }  // namespace nrg
