@@ -121,6 +121,7 @@ __global__ __launch_bounds__(ST_TPB) void st_tile_kernel(const nrg_stack_op* __r
     __shared__ uint16_t s_sp[9][ST_TPB];
     __shared__ uint16_t s_sw[4];               // per wave: minimum of its threads
     __shared__ uint16_t s_tab[ST_TILE];        // last Push position per relative slot
+    __shared__ u32 s_q[4][ST_ITEMS * 64];      // per wave: Pops answered beyond their thread
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     if (t == 0) {
         s_tile = atomicAdd(ticket, 1u);
@@ -293,8 +294,10 @@ __global__ __launch_bounds__(ST_TPB) void st_tile_kernel(const nrg_stack_op* __r
     }
 
     // Each Pop returns the Push right after the last earlier position whose depth is <= the
-    // depth the Pop leaves (a previous-smaller-or-equal query over the tile).
+    // depth the Pop leaves (a previous-smaller-or-equal query over the tile). Pops that the
+    // thread cannot answer from its own ops are queued per wave and answered with all lanes.
     u32 prv = astart;
+    u32 qn = 0;  // wave-uniform queue length
 #pragma unroll
     for (int q = 0; q < ST_ITEMS; q++) {
         const u32 pos = (u32)(t * ST_ITEMS + q);
@@ -308,42 +311,59 @@ __global__ __launch_bounds__(ST_TPB) void st_tile_kernel(const nrg_stack_op* __r
             resp[g - resp_lo] = push_resp ? ops[q].val : 0u;
             some[g - resp_lo] = push_resp ? 1 : 0;
         }
+        bool need = false;
         if (pop) {
             const u32 s = a[q];
-            int r = -2;
+            int r = astart <= s ? t * ST_ITEMS - 1 : -2;
 #pragma unroll
             for (int qq = 0; qq < ST_ITEMS; qq++)
                 if (qq < q && a[qq] <= s) r = t * ST_ITEMS + qq;
-            if (r == -2) {
-                // nearest earlier thread whose minimum is <= s: binary lifting, 9 steps
-                int k = t - 1;
-#pragma unroll
-                for (int j = 8; j >= 0; j--)
-                    if (k >= 0 && s_sp[j][k] > s) k -= 1 << j;
-                if (k >= 0) {
-                    u32 v[ST_ITEMS];
-#pragma unroll
-                    for (int qq = 0; qq < ST_ITEMS; qq++) v[qq] = s_A[k * ST_ITEMS + qq + 1];
-#pragma unroll
-                    for (int qq = 0; qq < ST_ITEMS; qq++)
-                        if (v[qq] <= s) r = k * ST_ITEMS + qq;
-                } else if (s_A[0] <= s) {
-                    r = -1;
+            if (r != -2) {
+                if (inwin) {
+                    resp[g - resp_lo] = s_val[r + 1];
+                    some[g - resp_lo] = 1;
                 }
-            }
-            if (r == -2) {  // the Push is in an earlier tile or before the chunk
-                // No tile writes the stack before st_finish_kernel, so read the pre-chunk
-                // content now; it is the answer when no earlier tile of the chunk pushed s.
-                const u32 k = atomicAdd(&s_ucnt, 1u);
-                const long long slot = tmin + s;
-                tl.upop[(u64)tile * ST_TILE + k] = (s << 11) | pos;
-                tl.uval[(u64)tile * ST_TILE + k] = slot < d0 && (u64)slot < cap ? stack[slot] : 0u;
-            } else if (inwin) {
-                resp[g - resp_lo] = s_val[r + 1];
-                some[g - resp_lo] = 1;
+            } else {
+                need = true;
             }
         }
+        const u64 m = __ballot(need);
+        if (need) s_q[w][qn + __popcll(m & ((1ull << lane) - 1))] = (a[q] << 11) | pos;
+        qn += (u32)__popcll(m);
         prv = a[q];
+    }
+    __syncthreads();
+    for (u32 i = lane; i < qn; i += 64) {
+        const u32 e = s_q[w][i];
+        const u32 s = e >> 11, pos = e & 2047u;
+        // nearest earlier thread whose minimum is <= s: binary lifting, 9 steps
+        int k = (int)(pos / ST_ITEMS) - 1;
+        int r = -2;
+#pragma unroll
+        for (int j = 8; j >= 0; j--)
+            if (k >= 0 && s_sp[j][k] > s) k -= 1 << j;
+        if (k >= 0) {
+            u32 v[ST_ITEMS];
+#pragma unroll
+            for (int qq = 0; qq < ST_ITEMS; qq++) v[qq] = s_A[k * ST_ITEMS + qq + 1];
+#pragma unroll
+            for (int qq = 0; qq < ST_ITEMS; qq++)
+                if (v[qq] <= s) r = k * ST_ITEMS + qq;
+        } else if (s_A[0] <= s) {
+            r = -1;
+        }
+        const u64 g = lo + tbase + pos;
+        if (r == -2) {  // the Push is in an earlier tile or before the chunk
+            // No tile writes the stack before st_finish_kernel, so read the pre-chunk
+            // content now; it is the answer when no earlier tile of the chunk pushed s.
+            const u32 h = atomicAdd(&s_ucnt, 1u);
+            const long long slot = tmin + s;
+            tl.upop[(u64)tile * ST_TILE + h] = e;
+            tl.uval[(u64)tile * ST_TILE + h] = slot < d0 && (u64)slot < cap ? stack[slot] : 0u;
+        } else if (g >= resp_lo && g < resp_hi) {
+            resp[g - resp_lo] = s_val[r + 1];
+            some[g - resp_lo] = 1;
+        }
     }
     if (t == ST_TPB - 1) s_aend = a[ST_ITEMS - 1];
     __syncthreads();
