@@ -900,9 +900,14 @@ int nrg_kernel_time(nrg_ctx* c, const char* which, uint64_t* launches, double* t
 // ---- test hooks (include/nrgpu_testing.h) -----------------------------------------------------
 extern "C" int nrg_test_sort_pairs(nrg_ctx* c, const uint32_t* d_keys, const uint32_t* d_vals, uint64_t n,
                                    int key_bits, uint32_t* d_ok, uint32_t* d_ov) {
-    if (!c || n > c->sort.cap) return NRG_E_INVAL;
+    if (!c) return NRG_E_INVAL;
     int r = use_device(c);
     if (r) return r;
+    if (n > c->sort.cap) {  // stack contexts replay without sorting: scratch on demand
+        HIPCHK(sync_all(c));
+        sort_free(c->sort);
+        if (sort_alloc(c->sort, n) != NRG_OK) return NRG_E_NOMEM;
+    }
     u32 *sk = nullptr, *sv = nullptr;
     HIPCHK(sort_pairs(c->sort, d_keys, d_vals, n, key_bits, c->stream, &sk, &sv));
     if (n) {
@@ -919,6 +924,9 @@ extern "C" int nrg_test_maxscan(nrg_ctx* c, const uint32_t* d_keys, const uint32
     int r = use_device(c);
     if (r) return r;
     HIPCHK(sy_maxscan(c, d_keys, d_vals, n, d_out));
+    // stack contexts keep their look-back descriptors zero between chunks
+    if (c->cfg.ds_kind == NRG_DS_STACK)
+        HIPCHK(hipMemsetAsync(c->d_scan_desc, 0, c->scan_desc_words * 4, c->stream));
     HIPCHK(sync_all(c));
     return NRG_OK;
 }

@@ -76,8 +76,16 @@ def main():
         tk = json.loads(txt[-1])["roofline"].get("traffic_key")
     except (NameError, ValueError, KeyError, IndexError):
         pass
-    fe = next((v for k, v in fetch.items() if "hm_round_kernel" in k), None)
-    wr = next((v for k, v in write.items() if "hm_round_kernel" in k), None)
+    # the timed unit: one hm_round launch, or one stack chunk (st_tile + st_finish kernels)
+    parts = ["st_tile_kernel", "st_finish_kernel"] if tk and tk.startswith("stack") else ["hm_round_kernel"]
+
+    def per_unit(tab):
+        got = [next((v for k, v in tab.items() if p in k), None) for p in parts]
+        if any(g is None for g in got):
+            return None
+        return (got[0][0], sum(g[1] for g in got))
+
+    fe, wr = per_unit(fetch), per_unit(write)
     if tk and fe and wr:
         tpath = os.path.join(os.path.dirname(os.path.abspath(out)), "traffic_hm_round.json")
         try:
@@ -89,7 +97,7 @@ def main():
                   "write_bytes": int(wr[1] * 1024), "launches": fe[0], "source": os.path.basename(out)}
         with open(tpath, "w") as f:
             json.dump(tj, f, indent=1, sort_keys=True)
-        lines.append("traffic per hm_round launch: %.1f MB (FETCH_SIZE x2 %.1f MB + WRITE_SIZE %.1f MB) -> %s" % (
+        lines.append("traffic per " + "+".join(parts) + " launch: %.1f MB (FETCH_SIZE x2 %.1f MB + WRITE_SIZE %.1f MB) -> %s" % (
             (2 * fe[1] + wr[1]) * 1024 / 1e6, 2 * fe[1] * 1024 / 1e6, wr[1] * 1024 / 1e6, tpath))
     text = "\n".join(lines) + "\n"
     with open(out, "w") as f:
