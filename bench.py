@@ -154,6 +154,10 @@ class Env:
         self.local = local
         torch.cuda.set_device(local)
         self.dev = torch.device("cuda", local)
+        # one non-blocking stream for the replica and this process's torch work (the null
+        # stream would order against every blocking stream, RCCL's included)
+        self.stream = torch.cuda.Stream(self.dev)
+        torch.cuda.set_stream(self.stream)
         if self.world > 1:
             if args.backend == "nccl":
                 dist.init_process_group("nccl", device_id=self.dev)  # RCCL over xGMI

@@ -131,10 +131,13 @@ typedef struct nrg_ctx nrg_ctx;
 int nrg_open(int hip_device, const nrg_config* cfg, nrg_ctx** out);
 int nrg_close(nrg_ctx* ctx);
 
-/* Use `hip_stream` (a hipStream_t, or NULL for the context's own stream) for all further
- * work on this context. */
+/* Use `hip_stream` (a hipStream_t; NULL is the device's null stream, as in HIP) for all
+ * further work on this context. A new context works on a non-blocking stream of its own,
+ * returned by nrg_own_stream. Work on a caller's stream is ordered with the caller's other
+ * work on it; the own stream is NOT ordered with the null stream. */
 int nrg_set_stream(nrg_ctx* ctx, void* hip_stream);
 void* nrg_get_stream(nrg_ctx* ctx);
+void* nrg_own_stream(nrg_ctx* ctx);
 
 /* Replica::sync analogue: wait for all queued work; report latched device errors. */
 int nrg_sync(nrg_ctx* ctx);

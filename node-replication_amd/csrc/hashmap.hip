@@ -448,6 +448,274 @@ static inline unsigned grid_for(u64 n, u64 cap = 4096) {
     return (unsigned)g;
 }
 
+// ---- owner path: partitioned replay of large rounds (no election atomics, no apply pass) -----
+//
+// A round's Puts are split by the top 8 bits of mix64(key) (the home slot's top bits) into
+// 256 buckets; every key belongs to exactly one bucket, and one block of hm_own_kernel owns
+// each (bucket, sub-bucket). That block picks every key's last writer in LDS and stores the
+// value into the slot itself, so no global atomicMax elects writers and no apply pass runs:
+//
+//   hm_part_kernel  tiles of 1024 Puts in ticket order: dedup by key in LDS (the tile's last
+//                   writer and its value), count per bucket, decoupled look-back over the
+//                   tiles' per-bucket counts (the rs_pass scheme), scatter (key, value) into
+//                   fixed-capacity bucket regions. Look-back offsets keep tile order inside a
+//                   region, so a key's last writer is its LAST entry in the region. Entries past
+//                   a region's capacity go to an overflow list with their would-be position.
+//   hm_own_kernel   per (bucket, sub-bucket): the max region position per key in LDS, then
+//                   find-or-claim the slot and store the value; the side-slot key rides the
+//                   usual stamp (one atomicMax per Put of key u64::MAX, applied by block 0).
+//
+// Reads of the round run after hm_own_kernel (next launch) and see the values in the slots.
+//
+// Status: opt-in (NRG_OWNER_MIN), parity-green, SLOWER than the stamp path on MI355X
+// (profiles/r01_variants/owner_path.txt): at 800k Puts + 900k Gets per round 135 us vs 110 us
+// (part 40 us, own 65 us); at B1 65 us vs 37 us. The part pass alone has a ~10 us latency
+// floor (load, LDS count, look-back, scatter) plus 7 us of LDS dedup at 100k Puts, so the
+// global atomics it removes (45 us at 800k) are not recovered. Kept for the next round's work
+// on the write path.
+constexpr int PT_KP = 8;
+constexpr int PT_TILE = TPB * PT_KP;  // 2048 Puts per part tile
+constexpr int PT_LDS = 2 * PT_TILE;   // dedup table entries
+constexpr int NBKT = 256;             // buckets (one look-back digit per thread)
+constexpr int OW_LDS = 2048;          // per-block key table of hm_own_kernel
+constexpr u32 OW_CLASS = 1024;        // region entries per class (table load <= 1/2)
+constexpr int OW_K = OW_LDS / TPB;    // elected keys per thread, loads issued together
+constexpr u32 PT_AGG = 1u << 30, PT_INC = 2u << 30, PT_MASK = 3u << 30, PT_CNT = (1u << 30) - 1;
+constexpr int PT_WIN = 32;
+
+__device__ __forceinline__ u32 bucket_of(u64 x) { return (u32)(x >> 56); }  // x = mix64(key)
+
+struct PartBufs {
+    u32* ticket;   // [1]
+    u32* ovf_cnt;  // [1]
+    u32* desc;     // [tiles][NBKT] look-back granules {status:2, count:30}
+    u64* bkey;     // [NBKT][cap]
+    u64* bval;     // [NBKT][cap]
+    u64* okey;     // overflow entries
+    u64* oval;
+    u32* opos;     // would-be region position
+    u32* obkt;     // bucket
+    u64 cap;
+};
+
+__global__ __launch_bounds__(TPB) void hm_part_kernel(RecSrc rec, nrg_put* ring_out, u64 n, u32 epoch, PartBufs pb,
+                                                      DevCtl* ctl) {
+    __shared__ u64 s_key[PT_LDS];
+    __shared__ u32 s_max[PT_LDS];  // 1 + the tile offset of the key's last writer
+    __shared__ u32 s_cnt[NBKT];
+    __shared__ u32 s_excl[NBKT];
+    __shared__ u32 s_tile;
+    const int t = threadIdx.x;
+    if (t == 0) s_tile = atomicAdd(pb.ticket, 1u);
+    for (int q = t; q < PT_LDS; q += TPB) {
+        s_key[q] = EMPTY_KEY;
+        s_max[q] = 0;
+    }
+    s_cnt[t] = 0;
+    __syncthreads();
+    const u32 tile = s_tile;
+    const u64 base = (u64)tile * PT_TILE;
+    const u32 par = epoch & 1;
+    nrg_put r[PT_KP];
+#pragma unroll
+    for (int q = 0; q < PT_KP; q++) {
+        const u64 i = base + (u64)q * TPB + t;
+        r[q] = i < n ? rec.at(i) : nrg_put{EMPTY_KEY, 0};
+    }
+    u32 hh[PT_KP];
+#pragma unroll
+    for (int q = 0; q < PT_KP; q++) {
+        const u64 i = base + (u64)q * TPB + t;
+        hh[q] = 0xFFFFFFFFu;
+        if (i >= n) continue;
+        if (ring_out) ring_out[(rec.lo + i) & rec.mask] = r[q];
+        const u64 k = r[q].key;
+        if (k == EMPTY_KEY) {  // the side-slot key keeps the stamp election (hm_own_kernel applies it)
+            atomicMax(slot_stamp(&ctl->sp, par), stamp_of(epoch, i));
+            continue;
+        }
+        u32 h = (u32)(mix64(k) >> 20) & (PT_LDS - 1);
+        for (;;) {
+            const u64 old = atomicCAS(&s_key[h], EMPTY_KEY, k);
+            if (old == EMPTY_KEY || old == k) break;
+            h = (h + 1) & (PT_LDS - 1);
+        }
+        atomicMax(&s_max[h], (u32)(i - base) + 1u);
+        hh[q] = h;
+    }
+    __syncthreads();
+    // per-bucket counts (the order inside a tile's run does not matter: one entry per key)
+    u32 rk[PT_LDS / TPB];
+#pragma unroll
+    for (int e = 0; e < PT_LDS / TPB; e++) {
+        const u64 k = s_key[e * TPB + t];
+        rk[e] = k != EMPTY_KEY ? atomicAdd(&s_cnt[bucket_of(mix64(k))], 1u) : 0u;
+    }
+    __syncthreads();
+    // thread t owns bucket t: publish the count, look back over earlier tiles
+    const u32 tcnt = s_cnt[t];
+    u32* my = pb.desc + (u64)tile * NBKT + t;
+    __hip_atomic_store(my, (tile == 0 ? PT_INC : PT_AGG) | tcnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    u32 excl = 0;
+    if (tile > 0) {
+        int tt = (int)tile - 1;
+        for (;;) {
+            u32 v[PT_WIN];
+#pragma unroll
+            for (int q = 0; q < PT_WIN; q++)
+                v[q] = tt - q >= 0 ? __hip_atomic_load(pb.desc + (u64)(tt - q) * NBKT + t, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT)
+                                   : PT_INC;
+            int used = 0;
+            bool done = false;
+#pragma unroll
+            for (int q = 0; q < PT_WIN; q++) {
+                if (done || used < q) continue;
+                const u32 st = v[q] & PT_MASK;
+                if (st == 0) continue;
+                excl += v[q] & PT_CNT;
+                used = q + 1;
+                if (st == PT_INC) done = true;
+            }
+            if (done) break;
+            tt -= used;
+            if (used < PT_WIN) __builtin_amdgcn_s_sleep(1);
+        }
+        __hip_atomic_store(my, PT_INC | (excl + tcnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    s_excl[t] = excl;
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < PT_LDS / TPB; e++) {
+        const u64 k = s_key[e * TPB + t];
+        if (k == EMPTY_KEY) continue;
+        const u32 b = bucket_of(mix64(k));
+        const u32 pos = s_excl[b] + rk[e];
+        const u64 v = rec.at(base + s_max[e * TPB + t] - 1).val;  // the tile's records are still cached
+        if (pos < pb.cap) {
+            pb.bkey[(u64)b * pb.cap + pos] = k;
+            pb.bval[(u64)b * pb.cap + pos] = v;
+        } else {
+            const u32 o = atomicAdd(pb.ovf_cnt, 1u);
+            pb.okey[o] = k;
+            pb.oval[o] = v;
+            pb.opos[o] = pos;
+            pb.obkt[o] = b;
+        }
+    }
+}
+
+__global__ __launch_bounds__(TPB) void hm_own_kernel(RecSrc rec, u32 epoch, u32 ntiles, PartBufs pb, u32 split,
+                                                     Slot* table, u32 shift, u64 tmask, DevCtl* ctl,
+                                                     u64* created_acc, u32* clear_desc, u64 clear_words,
+                                                     u32* clear_ctl) {
+    __shared__ u64 s_k[OW_LDS];
+    __shared__ u64 s_w[OW_LDS];  // max of ((region position + 1) << 32 | overflow index)
+    __shared__ uint16_t s_list[OW_LDS];
+    __shared__ u32 s_created, s_full, s_n;
+    const int t = threadIdx.x;
+    const u32 o = blockIdx.x;
+    const u32 b = o / split, sub = o % split;
+    // the other parity's buffers (used two owner rounds ago) are cleared for the next round
+    for (u64 q = (u64)o * TPB + t; q < clear_words; q += (u64)gridDim.x * TPB) clear_desc[q] = 0;
+    if (o == 0 && t < 2) clear_ctl[t] = 0;
+    const u32 total = pb.desc[(u64)(ntiles - 1) * NBKT + b] & PT_CNT;  // last tile's inclusive count
+    const u32 nin = total < pb.cap ? total : (u32)pb.cap;
+    const u32 novf = total > pb.cap ? *pb.ovf_cnt : 0u;
+    const u32 mine = (total + split - 1) / split;  // region entries of this sub-bucket, about
+    const u32 classes = mine > OW_CLASS ? (mine + OW_CLASS - 1) / OW_CLASS : 1u;
+    if (t == 0) {
+        s_created = 0;
+        s_full = 0;
+    }
+    u32 created = 0;
+    for (u32 c = 0; c < classes; c++) {
+        for (int q = t; q < OW_LDS; q += TPB) {
+            s_k[q] = EMPTY_KEY;
+            s_w[q] = 0;
+        }
+        __syncthreads();
+        for (u32 p = t; p < nin + novf; p += TPB) {
+            u64 k, w;
+            if (p < nin) {
+                k = pb.bkey[(u64)b * pb.cap + p];
+                w = ((u64)(p + 1) << 32);
+            } else {
+                const u32 q = p - nin;
+                if (pb.obkt[q] != b) continue;
+                k = pb.okey[q];
+                w = ((u64)(pb.opos[q] + 1) << 32) | q;
+            }
+            const u64 x = mix64(k);
+            if (((x >> 40) & (split - 1)) != sub) continue;
+            if (classes > 1 && (u32)((x >> 8) % classes) != c) continue;
+            u32 h = (u32)(x >> 20) & (OW_LDS - 1);
+            u32 tries = 0;
+            for (;;) {
+                const u64 old = atomicCAS(&s_k[h], EMPTY_KEY, k);
+                if (old == EMPTY_KEY || old == k) break;
+                h = (h + 1) & (OW_LDS - 1);
+                if (++tries == OW_LDS) {
+                    s_full = 1;
+                    break;
+                }
+            }
+            if (tries < OW_LDS) atomicMax(&s_w[h], w);
+        }
+        __syncthreads();
+        // compact the elected keys, then give each thread up to OW_K of them with every value
+        // load and first probe in flight together
+        if (t == 0) s_n = 0;
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < OW_K; e++) {
+            const int q = e * TPB + t;
+            if (s_k[q] != EMPTY_KEY) s_list[atomicAdd(&s_n, 1u)] = (uint16_t)q;
+        }
+        __syncthreads();
+        const u32 nl = s_n;
+        u64 kk[OW_K], vv[OW_K], k0[OW_K], hs[OW_K];
+#pragma unroll
+        for (int e = 0; e < OW_K; e++) {
+            const u32 li = (u32)e * TPB + t;
+            kk[e] = EMPTY_KEY;
+            if (li >= nl) continue;
+            const u32 q = s_list[li];
+            kk[e] = s_k[q];
+            const u64 w = s_w[q];
+            const u32 pos = (u32)(w >> 32) - 1;
+            vv[e] = pos < pb.cap ? pb.bval[(u64)b * pb.cap + pos] : pb.oval[(u32)w];
+            hs[e] = table_home(kk[e], shift);
+            k0[e] = table[hs[e]].key;
+        }
+#pragma unroll
+        for (int e = 0; e < OW_K; e++) {
+            if (kk[e] == EMPTY_KEY) continue;
+            const long long sl = find_or_claim(table, kk[e], hs[e], tmask, k0[e], epoch, &created);
+            if (sl < 0) {
+                atomicOr(&ctl->err, ERR_TABLE_FULL);
+                continue;
+            }
+            table[sl].val = vv[e];
+        }
+        __syncthreads();
+    }
+    if (s_full) atomicOr(&ctl->err, ERR_TABLE_FULL);  // LDS table overflow (hash skew): reported, not hidden
+    if (o == 0 && t == 0) {  // the side slot
+        const u64 st = *slot_stamp(&ctl->sp, epoch & 1);
+        if ((u32)(st >> 32) == epoch) {
+            if (ctl->sp.created == 0) {
+                ctl->sp.created = epoch;
+                created++;
+            }
+            ctl->sp.val = rec.at((u64)(u32)st - 1).val;
+        }
+    }
+    if (created) atomicAdd(&s_created, created);
+    __syncthreads();
+    if (t == 0 && s_created) atomicAdd(&created_acc[o % HM_CREATED_SLOTS], (u64)s_created);
+}
+
 // ---- host side ----------------------------------------------------------------------------
 static RecSrc ring_src(nrg_ctx* c, const nrg_put* src, u64 lo) {
     RecSrc r;
@@ -539,6 +807,65 @@ static hipError_t hm_reads(nrg_ctx* c, const u64* keys, u64 R, u64* vals, uint8_
     return launch(c, ij, aj, rj);
 }
 
+hipError_t hm_owner_alloc(nrg_ctx* c, u64 mb) {
+    OwnerBufs& ob = c->own;
+    ob.cap = 2 * ((mb + NBKT - 1) / NBKT) + 4096;
+    const u64 tiles = (mb + PT_TILE - 1) / PT_TILE;
+    hipError_t e;
+#define OB_ALLOC(P, BYTES)                     \
+    if ((e = hipMalloc(&(P), (BYTES))) != hipSuccess) return e;
+    OB_ALLOC(ob.ctl, 4 * sizeof(u32));
+    OB_ALLOC(ob.desc[0], tiles * NBKT * sizeof(u32));
+    OB_ALLOC(ob.desc[1], tiles * NBKT * sizeof(u32));
+    OB_ALLOC(ob.bkey, NBKT * ob.cap * sizeof(u64));
+    OB_ALLOC(ob.bval, NBKT * ob.cap * sizeof(u64));
+    OB_ALLOC(ob.okey, mb * sizeof(u64));
+    OB_ALLOC(ob.oval, mb * sizeof(u64));
+    OB_ALLOC(ob.opos, mb * sizeof(u32));
+    OB_ALLOC(ob.obkt, mb * sizeof(u32));
+#undef OB_ALLOC
+    if ((e = hipMemsetAsync(ob.ctl, 0, 4 * sizeof(u32), c->stream)) != hipSuccess) return e;
+    for (int i = 0; i < 2; i++)
+        if ((e = hipMemsetAsync(ob.desc[i], 0, tiles * NBKT * sizeof(u32), c->stream)) != hipSuccess) return e;
+    return hipSuccess;
+}
+
+void hm_owner_free(nrg_ctx* c) {
+    OwnerBufs& ob = c->own;
+    void* ptrs[] = {ob.ctl, ob.desc[0], ob.desc[1], ob.bkey, ob.bval, ob.okey, ob.oval, ob.opos, ob.obkt};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    ob = OwnerBufs{};
+}
+
+// One owner-path round (see hm_part_kernel): partition, then elect + store per bucket.
+static hipError_t owner_round(nrg_ctx* c, const nrg_put* src, nrg_put* ring_out, u64 lo, u64 n, u32 epoch) {
+    OwnerBufs& ob = c->own;
+    const u32 set = c->owner_rounds++ & 1;
+    PartBufs pb;
+    pb.ticket = ob.ctl + 2 * set;
+    pb.ovf_cnt = ob.ctl + 2 * set + 1;
+    pb.desc = ob.desc[set];
+    pb.bkey = ob.bkey;
+    pb.bval = ob.bval;
+    pb.okey = ob.okey;
+    pb.oval = ob.oval;
+    pb.opos = ob.opos;
+    pb.obkt = ob.obkt;
+    pb.cap = ob.cap;
+    const u64 tiles = (n + PT_TILE - 1) / PT_TILE;
+    const RecSrc rs = ring_src(c, src, lo);
+    NRG_LAUNCH(c, "hm_part", hm_part_kernel, (unsigned)tiles, TPB, 0, c->stream, rs, ring_out, n, epoch, pb, c->d_ctl);
+    u32 split = 1;  // sub-buckets per bucket: about <= 768 region entries per owner block
+    while ((u64)split * NBKT * 768 < n && split < 64) split <<= 1;
+    NRG_LAUNCH(c, "hm_own", hm_own_kernel, NBKT * split, TPB, 0, c->stream, rs, epoch, (u32)tiles, pb, split,
+               c->d_table, c->slot_shift, (u64)(c->slots - 1), c->d_ctl, c->d_created, ob.desc[set ^ 1],
+               ob.tiles[set ^ 1] * NBKT, ob.ctl + 2 * (set ^ 1));
+    ob.tiles[set] = tiles;
+    ob.tiles[set ^ 1] = 0;  // cleared by this launch
+    return hipGetLastError();
+}
+
 hipError_t hm_init(nrg_ctx* c) {
     hm_init_table_kernel<<<grid_for(c->slots, 16384), TPB, 0, c->stream>>>(c->d_table, c->slots);
     return hipGetLastError();
@@ -552,6 +879,28 @@ hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool
     (void)touch_log;
     if (n == 0) return hm_reads(c, d_get_keys, R, d_get_vals, d_get_found);
     const nrg_put* src = (const nrg_put*)src_recs;
+    const bool want_prev = d_prev && resp_lo < lo + n && resp_hi > lo;
+    if (c->owner_min && n >= c->owner_min && !want_prev) {
+        // the previous round's apply + reads see the table before this round's stores
+        hipError_t e = hm_flush(c);
+        if (e != hipSuccess) return e;
+        const u32 epoch = ++c->epoch;
+        e = owner_round(c, src, write_ring ? (nrg_put*)c->d_ring : nullptr, lo, n, epoch);
+        if (e != hipSuccess) return e;
+        const nrg_put* keep = (src && !write_ring) ? src : nullptr;
+        HmDeferred& p = c->pend;  // reads only: the values are already in the slots
+        p.valid = true;
+        p.epoch = epoch;
+        p.src = keep;
+        p.lo = lo;
+        p.n = 0;
+        p.keys = d_get_keys;
+        p.R = R;
+        p.vals = d_get_vals;
+        p.found = d_get_found;
+        if (!c->pipeline || keep) return hm_flush(c);
+        return hipGetLastError();
+    }
     const u32 epoch = ++c->epoch;
     IndexJob ij{};
     ij.rec = ring_src(c, src, lo);

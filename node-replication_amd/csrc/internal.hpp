@@ -57,6 +57,22 @@ struct HmDeferred {
     uint8_t* found = nullptr;
 };
 
+// Buffers of the partitioned (owner) replay of large hashmap rounds (hashmap.hip). Look-back
+// descriptors, ticket and overflow counter come in two sets used by alternate owner rounds:
+// hm_own_kernel clears the set the next owner round will use.
+struct OwnerBufs {
+    u32* ctl = nullptr;                 // [2][2]: ticket, overflow count per set
+    u32* desc[2] = {nullptr, nullptr};  // [tiles][256] per set
+    u64* bkey = nullptr;                // [256][cap] bucket regions
+    u64* bval = nullptr;
+    u64* okey = nullptr;                // [max_batch] overflow entries
+    u64* oval = nullptr;
+    u32* opos = nullptr;
+    u32* obkt = nullptr;
+    u64 cap = 0;
+    u64 tiles[2] = {0, 0};              // tiles the last round of each set used
+};
+
 struct HostRun {  // origin tags of appended log ranges (the Entry::replica field)
     u64 first, count;
     u32 origin;
@@ -94,6 +110,10 @@ struct nrg_ctx {
     bool pipeline = false;
     nrg::HmDeferred pend;
     uint64_t* d_created = nullptr;  // [HM_CREATED_SLOTS] keys created by replay rounds
+    // Rounds of >= owner_min Puts take the partitioned path (0: never; NRG_OWNER_MIN).
+    uint64_t owner_min = 0;
+    uint32_t owner_rounds = 0;
+    nrg::OwnerBufs own;
     // Zipf generator cache: zeta(zipf_n, zipf_theta)
     uint64_t zipf_n = 0;
     double zipf_theta = 0.0, zipf_zetan = 0.0;
@@ -150,6 +170,8 @@ hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool
                            bool touch_log);
 hipError_t hm_get_only(nrg_ctx* c, const u64* d_keys, u64 n, u64* d_vals, uint8_t* d_found);
 hipError_t hm_init(nrg_ctx* c);
+hipError_t hm_owner_alloc(nrg_ctx* c, u64 max_batch);
+void hm_owner_free(nrg_ctx* c);
 hipError_t hm_prefill_range(nrg_ctx* c, u64 n, u64 off);
 hipError_t hm_dump(nrg_ctx* c, u64* d_keys, u64* d_vals);
 hipError_t hm_count(nrg_ctx* c);  // DevCtl::nkeys_total = number of keys

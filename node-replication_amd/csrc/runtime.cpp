@@ -328,6 +328,8 @@ int nrg_open(int dev, const nrg_config* cfg_in, nrg_ctx** out) {
         if (const char* e = std::getenv("NRG_K1_ITEMS")) c->k1_items = (uint32_t)std::atoi(e);
         if (const char* e = std::getenv("NRG_GETS")) c->gets_per_thread = (uint32_t)std::atoi(e);
         if (const char* e = std::getenv("NRG_EXP")) c->exp = (uint32_t)std::atoi(e);
+        if (const char* e = std::getenv("NRG_OWNER_MIN")) c->owner_min = (uint64_t)std::atoll(e);
+        if (c->owner_min) OPEN_CHK(hm_owner_alloc(c, mb));  // buffers only when the path is enabled
         c->pipeline = cf.pipeline != 0;
         if (const char* e = std::getenv("NRG_PIPELINE")) c->pipeline = std::atoi(e) != 0;
         c->epoch = 1;  // epoch 1 = the state built by prefill; replay rounds start at 2
@@ -382,6 +384,7 @@ int nrg_close(nrg_ctx* c) {
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     sort_free(c->sort);
+    hm_owner_free(c);
     Staging* s = stg(c);
     for (int i = 0; i < 4; i++)
         if (s[i].p) (void)hipFree(s[i].p);
@@ -397,11 +400,13 @@ int nrg_set_stream(nrg_ctx* c, void* s) {
     // deferred hashmap work belongs to the old stream: launch it there first
     hipError_t e = hm_flush_if(c);
     if (e != hipSuccess) return hip_fail(e);
-    c->stream = s ? (hipStream_t)s : c->own_stream;
+    c->stream = (hipStream_t)s;  // NULL: the device's null stream, as in HIP
     return NRG_OK;
 }
 
 void* nrg_get_stream(nrg_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+void* nrg_own_stream(nrg_ctx* c) { return c ? (void*)c->own_stream : nullptr; }
 
 int nrg_sync(nrg_ctx* c) {
     if (!c) return NRG_E_INVAL;

@@ -89,6 +89,7 @@ SIGNATURES = {
     "nrg_close": (C.c_int, [vp]),
     "nrg_set_stream": (C.c_int, [vp, vp]),
     "nrg_get_stream": (vp, [vp]),
+    "nrg_own_stream": (vp, [vp]),
     "nrg_sync": (C.c_int, [vp]),
     "nrg_join": (C.c_int, [vp]),
     "nrg_strerror": (C.c_char_p, [C.c_int]),

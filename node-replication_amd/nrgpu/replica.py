@@ -85,9 +85,14 @@ class DeviceReplica:
         L.check(self._lib.nrg_set_stream(self._h, C.c_void_p(stream_ptr)), "nrg_set_stream")
 
     def use_torch_stream(self):
+        """Order this replica's work with torch's current stream on its device (the null
+        stream when torch is on its default stream)."""
         import torch
 
         self.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def use_own_stream(self):
+        self.set_stream(self._lib.nrg_own_stream(self._h) or 0)
 
     def sync(self):
         L.check(self._lib.nrg_sync(self._h), "nrg_sync")

@@ -263,3 +263,54 @@ def test_dense_segment_rounds(nrg, orc, pipeline):
         np.testing.assert_array_equal(pv.cpu().numpy().view(np.uint64), op)
     dev.sync()
     _check_state(dev, om)
+
+
+def _mix64(x):
+    x = x.astype(np.uint64)
+    with np.errstate(over="ignore"):
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return x ^ (x >> np.uint64(31))
+
+
+def test_owner_path_rounds(nrg, orc, monkeypatch):
+    """The opt-in partitioned replay (NRG_OWNER_MIN): pipelined rounds with side-slot keys, a
+    Zipf round, and a round whose keys all fall in ONE bucket (region overflow list and the
+    multi-class LDS election), each against the sequential oracle."""
+    import torch
+
+    monkeypatch.setenv("NRG_OWNER_MIN", "1")
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=17, max_batch=8192, pipeline=1)
+    dev.use_torch_stream()
+    om = orc.HashMap()
+    dev.hm_prefill_range(3000, 1)
+    om.prefill_range(3000, 1)
+    cand = np.arange(1, 4_000_000, dtype=np.uint64)
+    one_bucket = cand[(_mix64(cand) >> np.uint64(56)) == 0][:6000]  # 6000 > region capacity 4160
+    assert len(one_bucket) == 6000
+    rounds = [orc.gen_uniform(6000, 240 + r, 9000) for r in range(3)]
+    rounds.append(orc.gen_zipf(8000, 250, 20000, 0.99))
+    rounds.append(np.concatenate([one_bucket, one_bucket[:1500]]))  # duplicates across tiles
+    outs, want = [], []
+    for r, keys in enumerate(rounds):
+        keys = keys.copy()
+        if r < 3:
+            keys[::97] = EMPTY
+        W = len(keys)
+        vals = orc.gen_raw(W, 260 + r)
+        R = 7000
+        gk = np.concatenate([orc.gen_uniform(R - 100, 270 + r, 9500), one_bucket[:100]])
+        d_puts = torch.from_numpy(_puts(keys, vals).view(np.int64).copy()).cuda()
+        d_gk = torch.from_numpy(gk.view(np.int64)).cuda()
+        d_gv = torch.full((R,), -1, dtype=torch.int64, device="cuda")
+        d_gf = torch.full((R,), 7, dtype=torch.uint8, device="cuda")
+        dev.hm_round_device(d_puts, W, 1, d_gk, R, d_gv, d_gf, None, None)
+        outs.append((d_puts, d_gk, d_gv, d_gf))
+        om.replay(keys, vals)
+        want.append(om.get_batch(gk))
+    dev.join()
+    for r, (_, _, gv, gf) in enumerate(outs):
+        np.testing.assert_array_equal(gf.cpu().numpy(), want[r][1], err_msg=f"round {r} found")
+        np.testing.assert_array_equal(gv.cpu().numpy().view(np.uint64), want[r][0], err_msg=f"round {r} vals")
+    dev.sync()
+    _check_state(dev, om)
