@@ -109,6 +109,8 @@ def cpu_baseline(seconds: float, write_ratio: int, key_space: int, prefill: int)
 def traffic_key(args):
     if args.workload == "stack":
         return "stack_ops%d_init%d_n%d" % (args.ops_per_gpu, args.stack_init, int(os.environ.get("WORLD_SIZE", "1")))
+    if args.workload == "synthetic":
+        return "synthetic_ops%d_n%d" % (args.ops_per_gpu, int(os.environ.get("WORLD_SIZE", "1")))
     return "w%d_ops%d_ks%d_pf%d_s%d_%s_n%d" % (args.write_ratio, args.ops_per_gpu, args.key_space, args.prefill,
                                               args.log2_slots, key_dist_name(args),
                                               int(os.environ.get("WORLD_SIZE", "1")))
@@ -406,6 +408,113 @@ def stack_cpu_baseline(seconds, n_ops, init):
                 el, n_ops)}
 
 
+def synth_cpu_baseline(seconds, n_ops):
+    """The sequential oracle AbstractDataStructure (benches/synthetic.rs:112-195) on one host
+    core over a bounded sample of the same kind of ReadWrite stream."""
+    import numpy as np
+    import oracle
+
+    sy = oracle.Synthetic()
+    raw = oracle.gen_raw(3 * n_ops, 0x5E7)
+    ops = np.stack([raw[0::3] % 64, raw[1::3], raw[2::3], np.ones(n_ops, np.uint64)], axis=1)
+    t0 = time.perf_counter()
+    done = 0
+    while time.perf_counter() - t0 < seconds:
+        sy.replay(ops)
+        done += n_ops
+    el = time.perf_counter() - t0
+    return {"value": round(done / el / 1e6, 3), "unit": "Mops/s", "cores": 1, "kind": "port",
+            "sample": "%.1f s of %d-op ReadWrite batches (tid < 64, seeded) replayed by the sequential oracle "
+                      "AbstractDataStructure (200,000 words)" % (el, n_ops)}
+
+
+def run_synthetic(args, env):
+    """AbstractDataStructure log replay (benches/synthetic.rs:60-195, ReadWrite only as the
+    bench issues, :302,316): rounds of N ops per GPU, each ReadWrite = 1 hot + 5 cold touches
+    of a 200,000-word storage."""
+    torch = env.torch
+    import nrgpu
+    from nrgpu import _lib as L
+
+    world, rank, dev_t = env.world, env.rank, env.dev
+    N = args.ops_per_gpu
+    Ng = N * world
+    rep = nrgpu.DeviceReplica(L.NRG_DS_SYNTHETIC, env.local, max_batch=Ng, log_bytes=64 * 4 * max(Ng, 8192),
+                              replica_id=rank + 1)
+    rep.use_torch_stream()
+    P = max(1, min(args.pool, 8, args.steps + args.warmup))
+    gen = torch.Generator(device=dev_t)
+    gen.manual_seed(0x53594E54 + rank)
+    lo, hi = -(1 << 63), (1 << 63) - 1
+    ops = torch.empty((P, N, 4), dtype=torch.int64, device=dev_t)
+    for p in range(P):  # {tid, r1, r2, op}: tid = a core id < 64, op = ReadWrite
+        ops[p, :, 0] = torch.randint(0, 64, (N,), generator=gen, device=dev_t)
+        ops[p, :, 1] = torch.randint(lo, hi, (N,), generator=gen, device=dev_t)
+        ops[p, :, 2] = torch.randint(lo, hi, (N,), generator=gen, device=dev_t)
+        ops[p, :, 3] = 1
+    resp = torch.empty(N, dtype=torch.int64, device=dev_t)
+    some = torch.empty(N, dtype=torch.uint8, device=dev_t)
+    torch.cuda.synchronize()
+    group = None
+    if world > 1:
+        from nrgpu.parallel import ReplicatedLog
+
+        group = ReplicatedLog(rep, device=dev_t)
+    append_fn, exec_fn, h = rep._lib.nrg_log_append_async, rep._lib.nrg_log_exec_async, rep._h
+    first = L.C.c_uint64()
+    ptrs = [ops[p].data_ptr() for p in range(P)]
+    r_p, s_p = resp.data_ptr(), some.data_ptr()
+    gathered = {}
+    mode = {"n": 0}
+
+    def step(i):
+        p = i % P
+        if group is None:
+            rc = append_fn(h, ptrs[p], N, rank + 1, L.C.byref(first))
+            if rc == 0:
+                rc = exec_fn(h, first.value, first.value + N, r_p, s_p)
+            if rc:
+                L.check(rc, "synthetic round")
+        else:
+            g = gathered.pop(i) if i in gathered else group.gather_async(ops[p], stride=N)
+            if i + 1 < mode["n"]:
+                gathered[i + 1] = group.gather_async(ops[(i + 1) % P], stride=N)
+            group.replay(g, resp, some)
+
+    mode["n"] = args.warmup
+    for i in range(args.warmup):
+        step(i)
+    rep.sync()
+    rep.kernel_timing(not args.no_kernel_timing, only="sy_replay", every=args.timing_every)
+    mode["n"] = args.steps
+    elapsed = env.timed(args.steps, step, rep)
+    k_n, k_ms = rep.kernel_time("sy_replay")
+    rep.kernel_timing(False)
+    rep.sync()
+    value = world * N * args.steps / elapsed / 1e6
+    if rank != 0:
+        return None
+    # SURVEY.md §8d: B = 32 N + 2 * 8 * 200,000 per replica per batch (records; storage read and
+    # written once, L2-resident); touches are reported beside it
+    round_bytes = 32 * Ng + 2 * 8 * 200_000
+    res = common_fields(args, env, value, elapsed * 1e3 / args.steps,
+                        "Mops/s whole node, synthetic AbstractDataStructure log replay (benches/synthetic.rs)",
+                        "u64", {
+                            "workload": ("AbstractDataStructure replica per GPU: 200,000 words, rounds of %d ReadWrite "
+                                         "ops/GPU (tid < 64, random r1/r2), sums for own ops%s" % (
+                                             N, "; op segments all-gathered, every replica replays all %d ops" % Ng
+                                             if world > 1 else "")),
+                            "ops_per_gpu_per_round": N,
+                            "parallelism": "replicas%d" % world,
+                        })
+    res["roofline"] = roofline("sy_replay", round_bytes, k_n, k_ms, args, None)
+    res["round"] = {"algorithmic_bytes": int(round_bytes),
+                    "touches_per_s": round(6 * Ng * args.steps / elapsed, 1)}
+    if not args.no_cpu_baseline and world == 1:
+        res["cpu_baseline"] = synth_cpu_baseline(min(args.cpu_seconds, 10.0), min(N, 1 << 20))
+    return res
+
+
 def run_stack(args, env):
     torch = env.torch
     import nrgpu
@@ -522,7 +631,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=40)
-    ap.add_argument("--workload", default="hashmap", choices=["hashmap", "stack"])
+    ap.add_argument("--workload", default="hashmap", choices=["hashmap", "stack", "synthetic"])
     ap.add_argument("--write-ratio", type=int, default=10)
     ap.add_argument("--ops-per-gpu", type=int, default=1_000_000)
     ap.add_argument("--key-space", type=int, default=10_000_000)
@@ -547,11 +656,12 @@ def main():
                          "0: every round call completes its own reads")
     args = ap.parse_args()
     env = Env(args)
-    res = run_stack(args, env) if args.workload == "stack" else run_hashmap(args, env)
+    runner = {"stack": run_stack, "synthetic": run_synthetic}.get(args.workload, run_hashmap)
+    res = runner(args, env)
     if res is not None:
         if args.csv:
-            name = "nrstack-gpu" if args.workload == "stack" else "nrhashmap-gpu-wr%d-%s" % (
-                args.write_ratio, key_dist_name(args))
+            name = {"stack": "nrstack-gpu", "synthetic": "nrsynthetic-gpu"}.get(
+                args.workload, "nrhashmap-gpu-wr%d-%s" % (args.write_ratio, key_dist_name(args)))
             write_scaleout_csv(args.csv, name, env.world, args.ops_per_gpu, args.steps,
                                res["ms_per_step"] * args.steps / 1e3)
         print(json.dumps(res), flush=True)
