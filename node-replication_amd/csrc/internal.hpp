@@ -125,6 +125,7 @@ struct nrg_ctx {
     uint64_t* d_words = nullptr;
     uint64_t* d_sort_aux = nullptr;  // per-touch max-scan output
     uint32_t synth_key_bits = 0;
+    void* d_sy_aux = nullptr;  // bucket replay scratch (synthetic.hip); nullptr: sort path
 
     // ---- shared scratch ----
     nrg::SortScratch sort;
@@ -195,5 +196,7 @@ hipError_t sy_init(nrg_ctx* c);
 hipError_t sy_replay_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 resp_hi, u64* d_resp,
                            uint8_t* d_some);
 hipError_t sy_read(nrg_ctx* c, const nrg_synth_rd* d_ops, u64 n, u64* d_sums);
+bool sy_bucket_eligible(const nrg_config& cf);  // configs the sort-free bucket replay handles
+u64 sy_bucket_aux_bytes(const nrg_config& cf);  // size of nrg_ctx::d_sy_aux
 hipError_t sy_maxscan(nrg_ctx* c, const u32* sk, const u32* sv, u64 n, u32* M);
 }  // namespace nrg

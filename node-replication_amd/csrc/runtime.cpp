@@ -364,6 +364,10 @@ int nrg_open(int dev, const nrg_config* cfg_in, nrg_ctx** out) {
         c->scan_desc_words = 2 * (32 + (mb * T + 2047) / 2048);
         OPEN_CHK(hipMalloc(&c->d_scan_desc, c->scan_desc_words * 4));
         if (sort_alloc(c->sort, mb * T) != NRG_OK) { nrg_close(c); return NRG_E_NOMEM; }
+        // sort-free bucket replay where the config allows it; NRG_SY_SORT=1 keeps the sort path
+        const char* force_sort = std::getenv("NRG_SY_SORT");
+        if (sy_bucket_eligible(cf) && !(force_sort && std::atoi(force_sort)))
+            OPEN_CHK(hipMalloc(&c->d_sy_aux, sy_bucket_aux_bytes(cf)));
         OPEN_CHK(sy_init(c));
     }
     OPEN_CHK(hipStreamSynchronize(c->stream));
@@ -380,7 +384,7 @@ int nrg_close(nrg_ctx* c) {
     if (c->stream && c->stream != c->own_stream) (void)hipStreamSynchronize(c->stream);
     void* ptrs[] = {c->d_ring,    c->d_ctl,      c->d_table,   c->d_put_slot[0], c->d_put_slot[1],
                     c->d_stack,   c->d_words,    c->d_sort_aux, c->d_tmp_u64,    c->d_scan_desc,
-                    c->d_created, c->d_st_aux};
+                    c->d_created, c->d_st_aux,   c->d_sy_aux};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     sort_free(c->sort);

@@ -207,6 +207,449 @@ __global__ __launch_bounds__(256) void sy_read_kernel(const nrg_synth_rd* __rest
     sums[i] = sum;
 }
 
+// ---- bucket replay: no global sort ------------------------------------------------------
+// The default path for the reference's configurations (1 <= cold_writes <= 8, hot_reads <= 16,
+// <= 1024 buckets of 512 cold words, rounds <= 8M ops). Hot and cold words are disjoint, so:
+//   hot   words: each 2048-op tile folds its hot touches into a summary per hot word
+//               {has SET, tid of the last SET, touches after it}; the summaries compose
+//               associatively in log order (sy_sum_kernel's block 0 folds them).
+//   cold  words: sy_part_kernel writes each tile's cold touches grouped by bucket
+//               (word >> 9), in log order within a bucket (wave ballot ranking), plus a
+//               [bucket][tile] count table; sy_bucket_kernel (one workgroup per bucket)
+//               gathers the bucket's touches tile by tile — log order — and replays them
+//               against the bucket's 512 words held in LDS, 1024 touches at a time (a
+//               per-wave, per-word count table orders same-word touches across waves);
+//               every touch's seen value goes back to its slot in the tile layout;
+//               sy_sum_kernel adds them per op with LDS atomics (coalesced responses).
+// Replaces expand + 3 radix passes + max-scan + scattered u64 atomics (620 us per 1M ops).
+constexpr u32 SYB_SHIFT = 9;
+constexpr u32 SYB_WORDS = 1u << SYB_SHIFT;
+constexpr int SYA_TPB = 512, SYA_WAVES = SYA_TPB / 64, SYA_OROUNDS = 4;
+constexpr u32 SYA_OPS = SYA_WAVES * SYA_OROUNDS * 64;  // ops per tile
+constexpr u32 SY_MAX_NB = 1024, SY_MAX_HOT = 16, SY_MAX_TILES = 4096, SY_MAX_CW = 8;
+constexpr int SYB_TPB = 1024, SYB_WAVES = SYB_TPB / 64, SYB_PER = 16;
+constexpr int SYC_TPB = 512;
+constexpr u32 NOTOUCH = 0xFFFFFFFFu;
+
+// Hot word summary of a run of touches: has ? value = base + cnt : value = before + cnt.
+struct SyHot {
+    u32 cnt;
+    u32 has;
+    u64 base;
+};
+__device__ __forceinline__ SyHot hot_compose(SyHot a, SyHot b) {
+    if (b.has) return b;
+    a.cnt += b.cnt;
+    return a;
+}
+
+__device__ __forceinline__ u64 shfl_u64(u64 v, int src) {
+    const u32 lo = (u32)__shfl((int)(u32)v, src, 64);
+    const u32 hi = (u32)__shfl((int)(u32)(v >> 32), src, 64);
+    return ((u64)hi << 32) | lo;
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// lanes of the wave whose key equals this lane's (key < 2^nbits), among `cand`
+__device__ __forceinline__ u64 match_lanes(u32 key, u32 nbits, u64 cand) {
+    for (u32 q = 0; q < nbits; q++) {
+        const bool bit = (key >> q) & 1u;
+        const u64 bm = __ballot(bit);
+        cand &= bit ? bm : ~bm;
+    }
+    return cand;
+}
+
+template <int CW>
+__global__ __launch_bounds__(SYA_TPB) void sy_part_kernel(const nrg_synth_op* __restrict__ ring, u64 ring_mask, u64 lo,
+                                                          u64 n, u64 span, u32 HR, u32 HW, u32 T, u32 NB, u32 nbits,
+                                                          u32 ntiles, uint2* __restrict__ E, u32* __restrict__ cnt_bt,
+                                                          SyHot* __restrict__ hot) {
+    __shared__ u32 s_wcnt[SYA_WAVES][SY_MAX_NB];
+    __shared__ u32 s_words[SYA_WAVES][64 * CW];
+    __shared__ SyHot s_hot[SYA_WAVES][SY_MAX_HOT];
+    __shared__ u32 s_part[SYA_WAVES];
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const u32 tile = blockIdx.x;
+    const u64 op0 = (u64)tile * SYA_OPS;
+    for (u32 i = tid; i < SYA_WAVES * SY_MAX_NB; i += SYA_TPB) (&s_wcnt[0][0])[i] = 0;
+    if (lane < SY_MAX_HOT) s_hot[w][lane] = SyHot{0, 0, 0};
+    __syncthreads();
+    const u64 lt = (1ull << lane) - 1;
+    u32 xs[SYA_OROUNDS * CW];
+    u32 pk[SYA_OROUNDS * CW];
+#pragma unroll
+    for (int orr = 0; orr < SYA_OROUNDS; orr++) {
+        // 64 consecutive ops per wave round; lane = op
+        const u64 i = op0 + (u64)(w * SYA_OROUNDS + orr) * 64 + lane;
+        const bool valid = i < n;
+        nrg_synth_op o{0, 0, 0, 0};
+        if (valid) o = ring[(lo + i) & ring_mask];
+        const bool set = valid && o.op == NRG_SYNTH_WRITE_ONLY;
+        // hot touches (r2 + j) % HR, j < HW, skipped when r2 + HW wraps; ordered (lane, j)
+        const bool hot_ok = valid && (o.r2 + HW >= o.r2);
+        const u32 h0 = hot_ok ? (u32)(o.r2 % HR) : 0u;
+        for (u32 h = 0; h < HR; h++) {
+            int ls = -1;
+            u32 js = 0, tot = 0;
+            for (u32 j = 0; j < HW; j++) {
+                const bool on = hot_ok && (h0 + j) % HR == h;
+                const u64 m = __ballot(on);
+                const u64 sm = __ballot(on && set);
+                tot += (u32)__popcll(m);
+                if (sm) {
+                    const int l = 63 - __clzll(sm);
+                    if (l >= ls) {
+                        ls = l;
+                        js = j;
+                    }
+                }
+            }
+            if (tot == 0) continue;
+            u32 after = tot;
+            u64 base = 0;
+            if (ls >= 0) {
+                after = 0;
+                const u64 gt = ls == 63 ? 0ull : (~0ull << (ls + 1));
+                for (u32 j = 0; j < HW; j++) {
+                    const u64 m = __ballot(hot_ok && (h0 + j) % HR == h);
+                    after += (u32)__popcll(m & gt) + ((j > js && ((m >> ls) & 1ull)) ? 1u : 0u);
+                }
+                base = shfl_u64(o.tid, ls);
+            }
+            if (lane == 0) {
+                SyHot cur = s_hot[w][h];
+                s_hot[w][h] = ls >= 0 ? SyHot{after, 1u, base} : SyHot{cur.cnt + tot, cur.has, cur.base};
+            }
+        }
+        // cold touches: this lane's CW words, then rank them in log order (op-major) per bucket
+        u64 begin = o.r1 * o.tid;
+#pragma unroll
+        for (int k = 0; k < CW; k++) {
+            const u32 x = (u32)(begin % span + HR);
+            begin += o.r2;
+            s_words[w][lane * CW + k] = valid ? (x | (set ? SETBIT : 0u)) : NOTOUCH;
+        }
+        wave_lds_sync();
+#pragma unroll
+        for (int r = 0; r < CW; r++) {
+            const u32 v = s_words[w][r * 64 + lane];
+            const bool tv = v != NOTOUCH;
+            const u32 b = tv ? (((v & ~SETBIT) - HR) >> SYB_SHIFT) : 0u;
+            const u64 peers = match_lanes(b, nbits, __ballot(tv));
+            u32 rank = 0;
+            if (tv) {
+                const u32 c0 = s_wcnt[w][b];
+                rank = c0 + (u32)__popcll(peers & lt);
+                if (63 - __clzll(peers) == lane) s_wcnt[w][b] = c0 + (u32)__popcll(peers);
+            }
+            xs[orr * CW + r] = v;
+            pk[orr * CW + r] = (b << 16) | rank;
+        }
+        wave_lds_sync();
+    }
+    __syncthreads();
+    // bucket totals over the waves; wave prefixes; thread t owns buckets 2t, 2t+1
+    u32 tot2[2];
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        const u32 b = 2 * tid + q;
+        u32 acc = 0;
+        if (b < NB)
+            for (int ww = 0; ww < SYA_WAVES; ww++) {
+                const u32 c = s_wcnt[ww][b];
+                s_wcnt[ww][b] = acc;
+                acc += c;
+            }
+        tot2[q] = acc;
+    }
+    const u32 v2 = tot2[0] + tot2[1];
+    u32 inc = v2;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const u32 y = __shfl_up(inc, off, 64);
+        if (lane >= off) inc += y;
+    }
+    if (lane == 63) s_part[w] = inc;
+    __syncthreads();
+    u32 excl = inc - v2;
+    for (int ww = 0; ww < w; ww++) excl += s_part[ww];
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        const u32 b = 2 * tid + q;
+        if (b < NB) {
+            const u32 toff = excl + (q ? tot2[0] : 0u);
+            for (int ww = 0; ww < SYA_WAVES; ww++) s_wcnt[ww][b] += toff;
+            cnt_bt[(u64)b * ntiles + tile] = (toff << 16) | tot2[q];
+        }
+    }
+    if ((u32)tid < HR) {
+        SyHot a{0, 0, 0};
+        for (int ww = 0; ww < SYA_WAVES; ww++) a = hot_compose(a, s_hot[ww][tid]);
+        hot[(u64)tile * HR + tid] = a;
+    }
+    __syncthreads();
+    uint2* Et = E + (u64)tile * (SYA_OPS * CW);
+#pragma unroll
+    for (int orr = 0; orr < SYA_OROUNDS; orr++) {
+#pragma unroll
+        for (int r = 0; r < CW; r++) {
+            const u32 v = xs[orr * CW + r];
+            if (v == NOTOUCH) continue;
+            const u32 p = pk[orr * CW + r];
+            const u32 pos = s_wcnt[w][p >> 16] + (p & 0xFFFFu);
+            const u32 t = r * 64 + lane;
+            const u32 opl = (u32)(op0 + (u64)(w * SYA_OROUNDS + orr) * 64) + t / CW;
+            const u32 order = opl * T + HW + t % CW;
+            Et[pos] = make_uint2(order | (v & SETBIT), v & ~SETBIT);
+        }
+    }
+}
+
+__global__ __launch_bounds__(SYB_TPB) void sy_bucket_kernel(const uint2* __restrict__ E, const u32* __restrict__ cnt_bt,
+                                                            u32 ntiles, u32 tile_entries, u64* __restrict__ V,
+                                                            u64* __restrict__ words, u64 N, u32 HR,
+                                                            const nrg_synth_op* __restrict__ ring, u64 ring_mask, u64 lo,
+                                                            u32 T) {
+    __shared__ u32 s_pre[SY_MAX_TILES + 1];
+    __shared__ unsigned short s_off[SY_MAX_TILES];
+    __shared__ u64 s_cur[SYB_WORDS];
+    __shared__ u32 s_T[SYB_WAVES][SYB_WORDS];
+    __shared__ u32 s_part[SYB_WAVES];
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const u32 b = blockIdx.x;
+    const u64 w0 = (u64)HR + (u64)b * SYB_WORDS;
+    for (u32 t = tid; t < ntiles; t += SYB_TPB) {
+        const u32 p = cnt_bt[(u64)b * ntiles + t];
+        s_off[t] = (unsigned short)(p >> 16);
+        s_pre[t] = p & 0xFFFFu;
+    }
+    if (tid < (int)SYB_WORDS) s_cur[tid] = w0 + tid < N ? words[w0 + tid] : 0ull;
+    for (u32 i = tid; i < SYB_WAVES * SYB_WORDS; i += SYB_TPB) (&s_T[0][0])[i] = 0;
+    __syncthreads();
+    // exclusive scan of the per-tile counts: thread owns tiles [tid*K, tid*K + K)
+    const u32 K = (ntiles + SYB_TPB - 1) / SYB_TPB;
+    u32 loc = 0;
+    for (u32 q = 0; q < K; q++) {
+        const u32 t = tid * K + q;
+        if (t < ntiles) loc += s_pre[t];
+    }
+    u32 inc = loc;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const u32 y = __shfl_up(inc, off, 64);
+        if (lane >= off) inc += y;
+    }
+    if (lane == 63) s_part[w] = inc;
+    __syncthreads();
+    u32 run = inc - loc;
+    for (int ww = 0; ww < w; ww++) run += s_part[ww];
+    u32 total = 0;
+    for (int ww = 0; ww < SYB_WAVES; ww++) total += s_part[ww];
+    for (u32 q = 0; q < K; q++) {
+        const u32 t = tid * K + q;
+        if (t < ntiles) {
+            const u32 c = s_pre[t];
+            s_pre[t] = run;
+            run += c;
+        }
+    }
+    if (tid == 0) s_pre[ntiles] = total;
+    __syncthreads();
+    const u64 lt = (1ull << lane) - 1;
+    u32 tag = 0;
+    for (u32 base = 0; base < total; base += SYB_TPB * SYB_PER) {
+        uint2 ent[SYB_PER];
+        u32 gpos[SYB_PER];
+#pragma unroll
+        for (int q = 0; q < SYB_PER; q++) {
+            const u32 i = base + q * SYB_TPB + tid;
+            gpos[q] = 0;
+            ent[q] = make_uint2(0, 0);
+            if (i < total) {
+                u32 a = 0, z = ntiles;  // last tile with s_pre <= i
+                while (a < z) {
+                    const u32 m = (a + z) >> 1;
+                    if (s_pre[m] <= i) a = m + 1;
+                    else z = m;
+                }
+                const u32 t = a - 1;
+                gpos[q] = t * tile_entries + s_off[t] + (i - s_pre[t]);
+                ent[q] = E[gpos[q]];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < SYB_PER; q++) {
+            if (base + q * SYB_TPB >= total) break;
+            const u32 i = base + q * SYB_TPB + tid;
+            const bool valid = i < total;
+            const u32 xl = valid ? (u32)(ent[q].y - w0) : 0u;
+            const bool isset = valid && (ent[q].x & SETBIT);
+            const u64 peers = match_lanes(xl, SYB_SHIFT, __ballot(valid));
+            if (++tag == 0x10000u) {  // tags are 16 bits: clear the table and restart
+                __syncthreads();
+                for (u32 k = tid; k < SYB_WAVES * SYB_WORDS; k += SYB_TPB) (&s_T[0][0])[k] = 0;
+                __syncthreads();
+                tag = 1;
+            }
+            const bool wlast = valid && 63 - __clzll(peers) == lane;
+            if (wlast) s_T[w][xl] = (tag << 16) | (u32)__popcll(peers);
+            const int anyset = __syncthreads_or(isset);
+            u64 seen = 0;
+            if (!anyset) {
+                u32 before = 0;
+                bool later = false;
+                if (valid) {
+                    for (int ww = 0; ww < SYB_WAVES; ww++) {
+                        const u32 e = s_T[ww][xl];
+                        if (ww != w && (e >> 16) == tag) {
+                            if (ww < w) before += e & 0xFFFFu;
+                            else later = true;
+                        }
+                    }
+                    seen = s_cur[xl] + before + (u64)__popcll(peers & lt);
+                }
+                __syncthreads();
+                if (wlast && !later) s_cur[xl] = seen + 1;
+            } else {
+                // a WriteOnly in this chunk: waves apply their touches in order
+                const u64 mytid = isset ? ring[(lo + (ent[q].x & ~SETBIT) / T) & ring_mask].tid : 0ull;
+                const u64 S = __ballot(isset) & peers & lt;
+                const int s = S ? 63 - __clzll(S) : lane;
+                const u64 stid = shfl_u64(mytid, s);
+                for (int ww = 0; ww < SYB_WAVES; ww++) {
+                    if (ww == w && valid) {
+                        const u64 P = peers & lt;
+                        if (S) seen = stid + (u64)__popcll(P & ~((2ull << s) - 1));
+                        else seen = s_cur[xl] + (u64)__popcll(P);
+                        if (wlast) s_cur[xl] = isset ? mytid : seen + 1;
+                    }
+                    __syncthreads();
+                }
+            }
+            if (valid) V[gpos[q]] = isset ? 0ull : seen;
+        }
+    }
+    __syncthreads();
+    if (tid < (int)SYB_WORDS && w0 + tid < N) words[w0 + tid] = s_cur[tid];
+}
+
+__global__ __launch_bounds__(SYC_TPB) void sy_sum_kernel(const uint2* __restrict__ E, const u64* __restrict__ V, u32 CW,
+                                                         u64 n, u32 T, u64 lo, u64 resp_lo, u64 resp_hi,
+                                                         u64* __restrict__ resp, uint8_t* __restrict__ some, u32 tile0,
+                                                         u32 want, const SyHot* __restrict__ hot, u32 ntiles, u32 HR,
+                                                         u64* __restrict__ words) {
+    __shared__ u64 s_sum[SYA_OPS];
+    const int tid = threadIdx.x;
+    if (want) {
+        const u64 tile = tile0 + blockIdx.x;
+        const u64 op0 = tile * SYA_OPS;
+        const u32 nops = (u32)(n - op0 < SYA_OPS ? n - op0 : SYA_OPS);
+        for (u32 i = tid; i < SYA_OPS; i += SYC_TPB) s_sum[i] = 0;
+        __syncthreads();
+        const uint2* Et = E + tile * SYA_OPS * CW;
+        const u64* Vt = V + tile * SYA_OPS * CW;
+        const u32 ne = nops * CW;
+        for (u32 e = tid; e < ne; e += SYC_TPB) {
+            const u32 opl = (Et[e].x & ~SETBIT) / T - (u32)op0;
+            atomicAdd((unsigned long long*)&s_sum[opl], (unsigned long long)Vt[e]);
+        }
+        __syncthreads();
+        for (u32 i = tid; i < nops; i += SYC_TPB) {
+            const u64 g = lo + op0 + i;
+            if (g >= resp_lo && g < resp_hi) {
+                resp[g - resp_lo] = s_sum[i];
+                if (some) some[g - resp_lo] = 1;
+            }
+        }
+    }
+    if (blockIdx.x != 0) return;
+    // hot words: ordered fold of the tiles' summaries
+    __syncthreads();
+    SyHot* s_h = (SyHot*)s_sum;  // SYC_TPB entries
+    const u32 K = (ntiles + SYC_TPB - 1) / SYC_TPB;
+    for (u32 h = 0; h < HR; h++) {
+        SyHot a{0, 0, 0};
+        for (u32 q = 0; q < K; q++) {
+            const u32 t = tid * K + q;
+            if (t < ntiles) a = hot_compose(a, hot[(u64)t * HR + h]);
+        }
+        s_h[tid] = a;
+        for (int st = 1; st < SYC_TPB; st <<= 1) {
+            __syncthreads();
+            if ((tid & (2 * st - 1)) == 0) s_h[tid] = hot_compose(s_h[tid], s_h[tid + st]);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            const SyHot r = s_h[0];
+            words[h] = r.has ? r.base + r.cnt : words[h] + r.cnt;
+        }
+        __syncthreads();
+    }
+}
+
+bool sy_bucket_eligible(const nrg_config& cf) {
+    const u64 span = cf.synth_n - cf.synth_hot_reads;
+    return cf.synth_cold_writes >= 1 && cf.synth_cold_writes <= SY_MAX_CW && cf.synth_hot_reads <= SY_MAX_HOT &&
+           (span + SYB_WORDS - 1) / SYB_WORDS <= SY_MAX_NB && cf.max_batch <= (u64)SY_MAX_TILES * SYA_OPS;
+}
+
+u64 sy_bucket_aux_bytes(const nrg_config& cf) {
+    const u64 span = cf.synth_n - cf.synth_hot_reads;
+    const u64 NB = (span + SYB_WORDS - 1) / SYB_WORDS;
+    const u64 tiles = (cf.max_batch + SYA_OPS - 1) / SYA_OPS;
+    return tiles * SYA_OPS * cf.synth_cold_writes * 8 + NB * tiles * 4 + tiles * cf.synth_hot_reads * sizeof(SyHot) + 256;
+}
+
+static hipError_t sy_bucket_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 resp_hi, u64* d_resp, uint8_t* d_some) {
+    hipStream_t st = c->stream;
+    const nrg_config& cf = c->cfg;
+    const u32 HW = cf.synth_hot_writes, CW = cf.synth_cold_writes, HR = cf.synth_hot_reads;
+    const u32 T = HW + CW;
+    const u64 span = cf.synth_n - HR;
+    const u32 NB = (u32)((span + SYB_WORDS - 1) / SYB_WORDS);
+    u32 nbits = 0;
+    while ((1u << nbits) < NB) nbits++;
+    const u32 ntiles = (u32)((n + SYA_OPS - 1) / SYA_OPS);
+    const u64 max_tiles = (cf.max_batch + SYA_OPS - 1) / SYA_OPS;
+    const u64 ring_mask = c->log_size - 1;
+    const nrg_synth_op* ring = (const nrg_synth_op*)c->d_ring;
+    uint2* E = (uint2*)c->d_tmp_u64;
+    u64* V = (u64*)c->d_sy_aux;
+    u32* cnt = (u32*)(V + max_tiles * SYA_OPS * CW);
+    SyHot* hot = (SyHot*)(((uintptr_t)(cnt + (u64)NB * max_tiles) + 15) & ~(uintptr_t)15);
+    timer_begin(c, "sy_replay");
+#define SY_PART(CWV)                                                                                              \
+    case CWV:                                                                                                     \
+        sy_part_kernel<CWV><<<ntiles, SYA_TPB, 0, st>>>(ring, ring_mask, lo, n, span, HR, HW, T, NB, nbits, ntiles, \
+                                                        E, cnt, hot);                                             \
+        break
+    switch (CW) {
+        SY_PART(1); SY_PART(2); SY_PART(3); SY_PART(4); SY_PART(5); SY_PART(6); SY_PART(7); SY_PART(8);
+        default: return hipErrorInvalidValue;
+    }
+#undef SY_PART
+    sy_bucket_kernel<<<NB, SYB_TPB, 0, st>>>(E, cnt, ntiles, SYA_OPS * CW, V, c->d_words, cf.synth_n, HR, ring,
+                                             ring_mask, lo, T);
+    const bool want = d_resp != nullptr && resp_lo < lo + n && resp_hi > lo;
+    u32 t0 = 0, t1 = 1;
+    if (want) {
+        const u64 a = resp_lo > lo ? resp_lo - lo : 0;
+        const u64 z = resp_hi < lo + n ? resp_hi - lo : n;
+        t0 = (u32)(a / SYA_OPS);
+        t1 = (u32)((z + SYA_OPS - 1) / SYA_OPS);
+    }
+    sy_sum_kernel<<<t1 - t0, SYC_TPB, 0, st>>>(E, V, CW, n, T, lo, resp_lo, resp_hi, d_resp, d_some, t0, want ? 1u : 0u,
+                                               hot, ntiles, HR, c->d_words);
+    timer_end(c, "sy_replay");
+    return hipGetLastError();
+}
+
 hipError_t sy_init(nrg_ctx* c) {
     sy_init_kernel<<<1024, 256, 0, c->stream>>>(c->d_words, c->cfg.synth_n);
     return hipGetLastError();
@@ -214,6 +657,7 @@ hipError_t sy_init(nrg_ctx* c) {
 
 hipError_t sy_replay_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 resp_hi, u64* d_resp, uint8_t* d_some) {
     if (n == 0) return hipSuccess;
+    if (c->d_sy_aux) return sy_bucket_chunk(c, lo, n, resp_lo, resp_hi, d_resp, d_some);
     hipStream_t st = c->stream;
     const nrg_config& cf = c->cfg;
     const u32 HW = cf.synth_hot_writes, CW = cf.synth_cold_writes, HR = cf.synth_hot_reads;

@@ -1,4 +1,7 @@
-"""AbstractDataStructure parity (benches/synthetic.rs): HIP sort-based replay vs oracle.
+"""AbstractDataStructure parity (benches/synthetic.rs): HIP replay vs oracle.
+
+Both replay paths are covered: the default sort-free bucket replay and the sort-based one
+(NRG_SY_SORT=1, kept for configurations the bucket path does not take).
 
 The bench uses ReadWrite only with tid = core id (:296-335); WriteOnly and ReadOnly are
 part of the data structure's Dispatch (:177-195) and are covered too, including the
@@ -22,9 +25,31 @@ def _ops(orc, n, seed, tids, wo_frac):
     return r
 
 
+@pytest.fixture(params=["bucket", "sort"])
+def path(request, monkeypatch):
+    if request.param == "sort":
+        monkeypatch.setenv("NRG_SY_SORT", "1")
+    else:
+        monkeypatch.delenv("NRG_SY_SORT", raising=False)
+    return request.param
+
+
+def _check_rounds(nrg, orc, dev, os_, rounds, n, seed, tids, wo, tweak=None):
+    for r in range(rounds):
+        ops = _ops(orc, n, seed + r, tids, wo)
+        if tweak:
+            tweak(ops)
+        first = dev.log_append(ops, 1)
+        resp, some = dev.log_exec(first, first + n)
+        oresp = os_.replay(np.stack([ops["tid"], ops["r1"], ops["r2"], ops["op"]], axis=1))
+        np.testing.assert_array_equal(resp, oresp)
+        assert np.all(some == 1)
+    np.testing.assert_array_equal(dev.sy_dump(), os_.dump())
+
+
 @pytest.mark.parametrize("n,wo,tids", [(1000, 0, [0]), (20000, 0, [0, 1, 5, 63]), (20000, 30, [3, 7]),
                                        (5000, 100, [1, 2])])
-def test_synth_rounds(nrg, orc, n, wo, tids):
+def test_synth_rounds(nrg, orc, path, n, wo, tids):
     dev = nrg.DeviceReplica(nrg._lib.NRG_DS_SYNTHETIC, 0, max_batch=1 << 15)
     os_ = orc.Synthetic()
     for r in range(3):
@@ -43,3 +68,36 @@ def test_synth_rounds(nrg, orc, n, wo, tids):
         np.testing.assert_array_equal(dev.sy_read(rd),
                                       os_.read(np.stack([rd["tid"], rd["r1"], rd["r2"]], axis=1)))
     np.testing.assert_array_equal(dev.sy_dump(), os_.dump())
+
+
+def test_synth_large_rounds(nrg, orc, path):
+    """Many 2048-op tiles and all 391 buckets: the bench's op kind (ReadWrite, tid < 64)."""
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_SYNTHETIC, 0, max_batch=1 << 19)
+    _check_rounds(nrg, orc, dev, orc.Synthetic(), 3, 300_000, 4242, list(range(64)), 0)
+    dev.close()
+
+
+@pytest.mark.parametrize("wo", [0, 10])
+def test_synth_one_word(nrg, orc, path, wo):
+    """tid = 0 and r2 = 0: every cold touch of every op lands on word hot_reads (one bucket
+    with 5n touches, several 16K-touch passes) and every hot touch on word 0."""
+    def tweak(ops):
+        ops["r2"][:] = 0
+        ops["tid"][::7] = 0
+
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_SYNTHETIC, 0, max_batch=1 << 16)
+    _check_rounds(nrg, orc, dev, orc.Synthetic(), 2, 40_000, 77, [0], wo, tweak)
+    dev.close()
+
+
+def test_synth_partial_tiles_mixed(nrg, orc, path):
+    """Round sizes that end mid-tile and mid-wave, WriteOnly runs, wrapped hot ranges."""
+    def tweak(ops):
+        ops["op"][1000:1300] = 0
+        ops["r2"][::37] = 0xFFFFFFFFFFFFFFFF
+
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_SYNTHETIC, 0, max_batch=1 << 15)
+    os_ = orc.Synthetic()
+    for n, seed in ((1, 5), (63, 6), (2049, 7), (4095, 8), (12345, 9)):
+        _check_rounds(nrg, orc, dev, os_, 1, n, seed, [0, 2, 9, 31, 63], 5, tweak if n > 1300 else None)
+    dev.close()
