@@ -365,6 +365,7 @@ int nrg_open(int dev, const nrg_config* cfg_in, nrg_ctx** out) {
         OPEN_CHK(hipMalloc(&c->d_scan_desc, c->scan_desc_words * 4));
         if (sort_alloc(c->sort, mb * T) != NRG_OK) { nrg_close(c); return NRG_E_NOMEM; }
         // sort-free bucket replay where the config allows it; NRG_SY_SORT=1 keeps the sort path
+        if (const char* e = std::getenv("NRG_EXP")) c->exp = (uint32_t)std::atoi(e);
         const char* force_sort = std::getenv("NRG_SY_SORT");
         if (sy_bucket_eligible(cf) && !(force_sort && std::atoi(force_sort)))
             OPEN_CHK(hipMalloc(&c->d_sy_aux, sy_bucket_aux_bytes(cf)));

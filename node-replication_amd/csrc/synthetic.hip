@@ -225,11 +225,30 @@ __global__ __launch_bounds__(256) void sy_read_kernel(const nrg_synth_rd* __rest
 constexpr u32 SYB_SHIFT = 9;
 constexpr u32 SYB_WORDS = 1u << SYB_SHIFT;
 constexpr int SYA_TPB = 512, SYA_WAVES = SYA_TPB / 64, SYA_OROUNDS = 4;
-constexpr u32 SYA_OPS = SYA_WAVES * SYA_OROUNDS * 64;  // ops per tile
-constexpr u32 SY_MAX_NB = 1024, SY_MAX_HOT = 16, SY_MAX_TILES = 4096, SY_MAX_CW = 8;
-constexpr int SYB_TPB = 1024, SYB_WAVES = SYB_TPB / 64, SYB_PER = 16;
+constexpr u32 SYA_OPS = SYA_WAVES * SYA_OROUNDS * 64;  // ops per tile (11 bits)
+constexpr u32 SY_MAX_NB = 512, SY_MAX_HOT = 16, SY_MAX_TILES = 4096, SY_MAX_CW = 8;
+constexpr int SYB_TPB = 512, SYB_WAVES = SYB_TPB / 64, SYB_PER = 8;
+constexpr u32 SYB_PASS = SYB_TPB * SYB_PER;  // touches per pass of a bucket workgroup
 constexpr int SYC_TPB = 512;
 constexpr u32 NOTOUCH = 0xFFFFFFFFu;
+
+// A cold touch in the tile layout, 4 bytes: word within its bucket (9 bits), SET (1), cold
+// index k (3), op within its tile (11). The bucket and tile are implied by the position.
+__device__ __forceinline__ u32 ent_make(u32 xl, bool set, u32 k, u32 opl) {
+    return xl | (set ? 1u << 9 : 0u) | (k << 10) | (opl << 13);
+}
+__device__ __forceinline__ u32 ent_word(u32 e) { return e & (SYB_WORDS - 1); }
+__device__ __forceinline__ bool ent_set(u32 e) { return (e >> 9) & 1u; }
+__device__ __forceinline__ u32 ent_op(u32 e) { return e >> 13; }
+
+// x mod d for d < 2^32 with m = floor((2^64 - 1) / d): the quotient estimate is at most two low
+// (a software 64-bit division costs ~10x more: 10 us of a 1M-op partition pass)
+__device__ __forceinline__ u64 mod_recip(u64 x, u64 d, u64 m) {
+    u64 r = x - __umul64hi(x, m) * d;
+    if (r >= d) r -= d;
+    if (r >= d) r -= d;
+    return r;
+}
 
 // Hot word summary of a run of touches: has ? value = base + cnt : value = before + cnt.
 struct SyHot {
@@ -249,51 +268,77 @@ __device__ __forceinline__ u64 shfl_u64(u64 v, int src) {
     return ((u64)hi << 32) | lo;
 }
 
+// orders a wave's own LDS accesses across lanes (the hardware keeps one wave's LDS
+// instructions in order; this stops the compiler from moving them)
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// lanes of the wave whose key equals this lane's (key < 2^nbits), among `cand`
-__device__ __forceinline__ u64 match_lanes(u32 key, u32 nbits, u64 cand) {
-    for (u32 q = 0; q < nbits; q++) {
-        const bool bit = (key >> q) & 1u;
-        const u64 bm = __ballot(bit);
-        cand &= bit ? bm : ~bm;
+// Stable ranking of one wave round in a wave-private (mask, count) table: every lane with a
+// key ORs its bit into mask[key]; the mask read back is the set of lanes with that key
+// (cheaper than matching the key bit by bit with ballots). Returns count[key] + the number
+// of lower lanes with the same key; the highest such lane advances count and clears mask.
+template <typename CNT>
+__device__ __forceinline__ u32 wave_rank(bool on, u32 key, int lane, u64* mask, CNT* count, u64* peers_out) {
+    if (on) atomicOr((unsigned long long*)&mask[key], 1ull << lane);
+    wave_lds_sync();
+    u64 peers = 0;
+    u32 c0 = 0;
+    if (on) {
+        peers = mask[key];
+        c0 = count[key];
     }
-    return cand;
+    wave_lds_sync();
+    if (on && 63 - __clzll(peers) == lane) {
+        mask[key] = 0;
+        count[key] = (CNT)(c0 + (u32)__popcll(peers));
+    }
+    wave_lds_sync();
+    *peers_out = peers;
+    return c0 + (u32)__popcll(peers & ((1ull << lane) - 1));
 }
 
 template <int CW>
 __global__ __launch_bounds__(SYA_TPB) void sy_part_kernel(const nrg_synth_op* __restrict__ ring, u64 ring_mask, u64 lo,
-                                                          u64 n, u64 span, u32 HR, u32 HW, u32 T, u32 NB, u32 nbits,
-                                                          u32 ntiles, uint2* __restrict__ E, u32* __restrict__ cnt_bt,
+                                                          u64 n, u64 span, u64 span_m, u32 HR, u64 hr_m, u32 HW, u32 NB,
+                                                          u32 ntiles, u32* __restrict__ E, u32* __restrict__ cnt_bt,
                                                           SyHot* __restrict__ hot) {
-    __shared__ u32 s_wcnt[SYA_WAVES][SY_MAX_NB];
-    __shared__ u32 s_words[SYA_WAVES][64 * CW];
+    __shared__ unsigned short s_wcnt[SYA_WAVES][SY_MAX_NB];
+    // ranking tables and staged words, then (same bytes) the tile's touches grouped by bucket
+    __shared__ union {
+        struct {
+            u64 mask[SYA_WAVES][SY_MAX_NB];
+            u32 words[SYA_WAVES][64 * CW];
+        } r;
+        u32 stage[SYA_OPS * CW];
+    } s_u;
     __shared__ SyHot s_hot[SYA_WAVES][SY_MAX_HOT];
     __shared__ u32 s_part[SYA_WAVES];
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const u32 tile = blockIdx.x;
     const u64 op0 = (u64)tile * SYA_OPS;
-    for (u32 i = tid; i < SYA_WAVES * SY_MAX_NB; i += SYA_TPB) (&s_wcnt[0][0])[i] = 0;
+    for (u32 i = tid; i < SYA_WAVES * SY_MAX_NB / 2; i += SYA_TPB) ((u32*)&s_wcnt[0][0])[i] = 0;
+    for (u32 i = tid; i < SYA_WAVES * SY_MAX_NB; i += SYA_TPB) (&s_u.r.mask[0][0])[i] = 0;
     if (lane < SY_MAX_HOT) s_hot[w][lane] = SyHot{0, 0, 0};
     __syncthreads();
-    const u64 lt = (1ull << lane) - 1;
     u32 xs[SYA_OROUNDS * CW];
     u32 pk[SYA_OROUNDS * CW];
+    const u32 opw = (u32)(w * SYA_OROUNDS) * 64 + lane;  // this lane's op in round 0, within the tile
+    nrg_synth_op nx{0, 0, 0, 0};
+    if (op0 + opw < n) nx = ring[(lo + op0 + opw) & ring_mask];
 #pragma unroll
     for (int orr = 0; orr < SYA_OROUNDS; orr++) {
-        // 64 consecutive ops per wave round; lane = op
-        const u64 i = op0 + (u64)(w * SYA_OROUNDS + orr) * 64 + lane;
-        const bool valid = i < n;
-        nrg_synth_op o{0, 0, 0, 0};
-        if (valid) o = ring[(lo + i) & ring_mask];
+        // 64 consecutive ops per wave round; lane = op; the next round's record is in flight
+        const bool valid = op0 + opw + orr * 64 < n;
+        const nrg_synth_op o = nx;
+        if (orr + 1 < SYA_OROUNDS && op0 + opw + (orr + 1) * 64 < n)
+            nx = ring[(lo + op0 + opw + (orr + 1) * 64) & ring_mask];
         const bool set = valid && o.op == NRG_SYNTH_WRITE_ONLY;
         // hot touches (r2 + j) % HR, j < HW, skipped when r2 + HW wraps; ordered (lane, j)
         const bool hot_ok = valid && (o.r2 + HW >= o.r2);
-        const u32 h0 = hot_ok ? (u32)(o.r2 % HR) : 0u;
+        const u32 h0 = hot_ok ? (u32)mod_recip(o.r2, HR, hr_m) : 0u;
         for (u32 h = 0; h < HR; h++) {
             int ls = -1;
             u32 js = 0, tot = 0;
@@ -331,45 +376,33 @@ __global__ __launch_bounds__(SYA_TPB) void sy_part_kernel(const nrg_synth_op* __
         u64 begin = o.r1 * o.tid;
 #pragma unroll
         for (int k = 0; k < CW; k++) {
-            const u32 x = (u32)(begin % span + HR);
+            const u32 x = (u32)mod_recip(begin, span, span_m) + HR;
             begin += o.r2;
-            s_words[w][lane * CW + k] = valid ? (x | (set ? SETBIT : 0u)) : NOTOUCH;
+            s_u.r.words[w][lane * CW + k] = valid ? (x | (set ? SETBIT : 0u)) : NOTOUCH;
         }
         wave_lds_sync();
 #pragma unroll
         for (int r = 0; r < CW; r++) {
-            const u32 v = s_words[w][r * 64 + lane];
+            const u32 v = s_u.r.words[w][r * 64 + lane];
             const bool tv = v != NOTOUCH;
             const u32 b = tv ? (((v & ~SETBIT) - HR) >> SYB_SHIFT) : 0u;
-            const u64 peers = match_lanes(b, nbits, __ballot(tv));
-            u32 rank = 0;
-            if (tv) {
-                const u32 c0 = s_wcnt[w][b];
-                rank = c0 + (u32)__popcll(peers & lt);
-                if (63 - __clzll(peers) == lane) s_wcnt[w][b] = c0 + (u32)__popcll(peers);
-            }
+            u64 peers;
+            const u32 rank = wave_rank(tv, b, lane, s_u.r.mask[w], s_wcnt[w], &peers);
             xs[orr * CW + r] = v;
             pk[orr * CW + r] = (b << 16) | rank;
         }
-        wave_lds_sync();
     }
     __syncthreads();
-    // bucket totals over the waves; wave prefixes; thread t owns buckets 2t, 2t+1
-    u32 tot2[2];
-#pragma unroll
-    for (int q = 0; q < 2; q++) {
-        const u32 b = 2 * tid + q;
-        u32 acc = 0;
-        if (b < NB)
-            for (int ww = 0; ww < SYA_WAVES; ww++) {
-                const u32 c = s_wcnt[ww][b];
-                s_wcnt[ww][b] = acc;
-                acc += c;
-            }
-        tot2[q] = acc;
-    }
-    const u32 v2 = tot2[0] + tot2[1];
-    u32 inc = v2;
+    // bucket totals over the waves; wave prefixes; thread t owns bucket t
+    const u32 bt = tid;
+    u32 tot = 0;
+    if (bt < NB)
+        for (int ww = 0; ww < SYA_WAVES; ww++) {
+            const u32 c = s_wcnt[ww][bt];
+            s_wcnt[ww][bt] = (unsigned short)tot;
+            tot += c;
+        }
+    u32 inc = tot;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
         const u32 y = __shfl_up(inc, off, 64);
@@ -377,16 +410,11 @@ __global__ __launch_bounds__(SYA_TPB) void sy_part_kernel(const nrg_synth_op* __
     }
     if (lane == 63) s_part[w] = inc;
     __syncthreads();
-    u32 excl = inc - v2;
-    for (int ww = 0; ww < w; ww++) excl += s_part[ww];
-#pragma unroll
-    for (int q = 0; q < 2; q++) {
-        const u32 b = 2 * tid + q;
-        if (b < NB) {
-            const u32 toff = excl + (q ? tot2[0] : 0u);
-            for (int ww = 0; ww < SYA_WAVES; ww++) s_wcnt[ww][b] += toff;
-            cnt_bt[(u64)b * ntiles + tile] = (toff << 16) | tot2[q];
-        }
+    u32 toff = inc - tot;
+    for (int ww = 0; ww < w; ww++) toff += s_part[ww];
+    if (bt < NB) {
+        for (int ww = 0; ww < SYA_WAVES; ww++) s_wcnt[ww][bt] = (unsigned short)(s_wcnt[ww][bt] + toff);
+        cnt_bt[(u64)bt * ntiles + tile] = (toff << 16) | tot;
     }
     if ((u32)tid < HR) {
         SyHot a{0, 0, 0};
@@ -394,7 +422,6 @@ __global__ __launch_bounds__(SYA_TPB) void sy_part_kernel(const nrg_synth_op* __
         hot[(u64)tile * HR + tid] = a;
     }
     __syncthreads();
-    uint2* Et = E + (u64)tile * (SYA_OPS * CW);
 #pragma unroll
     for (int orr = 0; orr < SYA_OROUNDS; orr++) {
 #pragma unroll
@@ -402,25 +429,34 @@ __global__ __launch_bounds__(SYA_TPB) void sy_part_kernel(const nrg_synth_op* __
             const u32 v = xs[orr * CW + r];
             if (v == NOTOUCH) continue;
             const u32 p = pk[orr * CW + r];
-            const u32 pos = s_wcnt[w][p >> 16] + (p & 0xFFFFu);
             const u32 t = r * 64 + lane;
-            const u32 opl = (u32)(op0 + (u64)(w * SYA_OROUNDS + orr) * 64) + t / CW;
-            const u32 order = opl * T + HW + t % CW;
-            Et[pos] = make_uint2(order | (v & SETBIT), v & ~SETBIT);
+            const u32 opl = (u32)(w * SYA_OROUNDS + orr) * 64 + t / CW;
+            const u32 xl = ((v & ~SETBIT) - HR) & (SYB_WORDS - 1);
+            s_u.stage[s_wcnt[w][p >> 16] + (p & 0xFFFFu)] = ent_make(xl, (v & SETBIT) != 0, t % CW, opl);
         }
     }
+    __syncthreads();
+    const u32 nops = (u32)(n - op0 < SYA_OPS ? n - op0 : SYA_OPS);
+    u32* Et = E + (u64)tile * (SYA_OPS * CW);
+    for (u32 i = tid; i < nops * CW; i += SYA_TPB) Et[i] = s_u.stage[i];
 }
 
-__global__ __launch_bounds__(SYB_TPB) void sy_bucket_kernel(const uint2* __restrict__ E, const u32* __restrict__ cnt_bt,
+// One workgroup per bucket. Passes of SYB_PASS touches in log order; wave w takes the pass's
+// w-th contiguous SYB_PER rounds of 64: wave-private per-word counts rank the wave's
+// touches without barriers, then per-word prefixes over the waves place them. A pass with a
+// WriteOnly in it is applied wave by wave instead (values depend on the last SET).
+__global__ __launch_bounds__(SYB_TPB) void sy_bucket_kernel(const u32* __restrict__ E, const u32* __restrict__ cnt_bt,
                                                             u32 ntiles, u32 tile_entries, u64* __restrict__ V,
                                                             u64* __restrict__ words, u64 N, u32 HR,
-                                                            const nrg_synth_op* __restrict__ ring, u64 ring_mask, u64 lo,
-                                                            u32 T) {
-    __shared__ u32 s_pre[SY_MAX_TILES + 1];
-    __shared__ unsigned short s_off[SY_MAX_TILES];
+                                                            const nrg_synth_op* __restrict__ ring, u64 ring_mask, u64 lo) {
+    extern __shared__ u32 s_dyn[];  // s_pre[ntiles + 1], s_off[ntiles] (u16)
     __shared__ u64 s_cur[SYB_WORDS];
-    __shared__ u32 s_T[SYB_WAVES][SYB_WORDS];
+    __shared__ u32 s_wc[SYB_WAVES][SYB_WORDS];
+    __shared__ u64 s_mk[SYB_WAVES][SYB_WORDS];
+    __shared__ unsigned short s_tile[SYB_PASS];
     __shared__ u32 s_part[SYB_WAVES];
+    u32* s_pre = s_dyn;
+    unsigned short* s_off = (unsigned short*)(s_dyn + ntiles + 1);
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const u32 b = blockIdx.x;
     const u64 w0 = (u64)HR + (u64)b * SYB_WORDS;
@@ -429,8 +465,11 @@ __global__ __launch_bounds__(SYB_TPB) void sy_bucket_kernel(const uint2* __restr
         s_off[t] = (unsigned short)(p >> 16);
         s_pre[t] = p & 0xFFFFu;
     }
-    if (tid < (int)SYB_WORDS) s_cur[tid] = w0 + tid < N ? words[w0 + tid] : 0ull;
-    for (u32 i = tid; i < SYB_WAVES * SYB_WORDS; i += SYB_TPB) (&s_T[0][0])[i] = 0;
+    for (u32 i = tid; i < SYB_WORDS; i += SYB_TPB) s_cur[i] = w0 + i < N ? words[w0 + i] : 0ull;
+    for (u32 i = tid; i < SYB_WAVES * SYB_WORDS; i += SYB_TPB) {
+        (&s_wc[0][0])[i] = 0;
+        (&s_mk[0][0])[i] = 0;
+    }
     __syncthreads();
     // exclusive scan of the per-tile counts: thread owns tiles [tid*K, tid*K + K)
     const u32 K = (ntiles + SYB_TPB - 1) / SYB_TPB;
@@ -461,86 +500,106 @@ __global__ __launch_bounds__(SYB_TPB) void sy_bucket_kernel(const uint2* __restr
     }
     if (tid == 0) s_pre[ntiles] = total;
     __syncthreads();
-    const u64 lt = (1ull << lane) - 1;
-    u32 tag = 0;
-    for (u32 base = 0; base < total; base += SYB_TPB * SYB_PER) {
-        uint2 ent[SYB_PER];
-        u32 gpos[SYB_PER];
+    for (u32 base = 0; base < total; base += SYB_PASS) {
+        // tile of every touch of the pass
+        for (u32 t = tid; t < ntiles; t += SYB_TPB) {
+            const u32 a = s_pre[t] > base ? s_pre[t] : base;
+            const u32 z = s_pre[t + 1] < base + SYB_PASS ? s_pre[t + 1] : base + SYB_PASS;
+            for (u32 j = a; j < z; j++) s_tile[j - base] = (unsigned short)t;
+        }
+        __syncthreads();
+        u32 ent[SYB_PER], gpos[SYB_PER];
+        u64 sv[SYB_PER];
+        bool myset = false;
 #pragma unroll
         for (int q = 0; q < SYB_PER; q++) {
-            const u32 i = base + q * SYB_TPB + tid;
+            const u32 i = base + (u32)w * (SYB_PER * 64) + q * 64 + lane;
             gpos[q] = 0;
-            ent[q] = make_uint2(0, 0);
+            ent[q] = 0;
             if (i < total) {
-                u32 a = 0, z = ntiles;  // last tile with s_pre <= i
-                while (a < z) {
-                    const u32 m = (a + z) >> 1;
-                    if (s_pre[m] <= i) a = m + 1;
-                    else z = m;
-                }
-                const u32 t = a - 1;
+                const u32 t = s_tile[i - base];
                 gpos[q] = t * tile_entries + s_off[t] + (i - s_pre[t]);
                 ent[q] = E[gpos[q]];
+                myset |= ent_set(ent[q]);
+            }
+        }
+        const int anyset = __syncthreads_or(myset);
+        if (!anyset) {
+#pragma unroll
+            for (int q = 0; q < SYB_PER; q++) {
+                const u32 i = base + (u32)w * (SYB_PER * 64) + q * 64 + lane;
+                u64 peers;
+                sv[q] = wave_rank(i < total, ent_word(ent[q]), lane, s_mk[w], s_wc[w], &peers);
+            }
+            __syncthreads();
+            u64 totw = 0;
+            if (tid < (int)SYB_WORDS) {
+                u32 acc = 0;
+                for (int ww = 0; ww < SYB_WAVES; ww++) {
+                    const u32 c = s_wc[ww][tid];
+                    s_wc[ww][tid] = acc;
+                    acc += c;
+                }
+                totw = acc;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < SYB_PER; q++) {
+                const u32 xl = ent_word(ent[q]);
+                sv[q] += s_cur[xl] + s_wc[w][xl];
+            }
+            __syncthreads();
+            if (tid < (int)SYB_WORDS) {
+                s_cur[tid] += totw;
+                for (int ww = 0; ww < SYB_WAVES; ww++) s_wc[ww][tid] = 0;
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < SYB_PER; q++) {
+                const bool isset = ent_set(ent[q]);  // 0 for touches past the end
+                const u64 op = (u64)(gpos[q] / tile_entries) * SYA_OPS + ent_op(ent[q]);
+                sv[q] = isset ? ring[(lo + op) & ring_mask].tid : 0ull;
+            }
+            for (int ww = 0; ww < SYB_WAVES; ww++) {
+                if (ww == w) {
+#pragma unroll
+                    for (int q = 0; q < SYB_PER; q++) {
+                        const u32 i = base + (u32)w * (SYB_PER * 64) + q * 64 + lane;
+                        const bool valid = i < total;
+                        const u32 xl = ent_word(ent[q]);
+                        const bool isset = valid && ent_set(ent[q]);
+                        u64 peers;
+                        (void)wave_rank(valid, xl, lane, s_mk[w], s_wc[w], &peers);
+                        const u64 P = peers & ((1ull << lane) - 1);
+                        const u64 S = __ballot(isset) & P;
+                        const int sl = S ? 63 - __clzll(S) : lane;
+                        const u64 stid = shfl_u64(sv[q], sl);
+                        u64 seen = 0;
+                        if (valid) {
+                            if (S) seen = stid + (u64)__popcll(P & ~((2ull << sl) - 1));
+                            else seen = s_cur[xl] + (u64)__popcll(P);
+                        }
+                        wave_lds_sync();
+                        if (valid && 63 - __clzll(peers) == lane) s_cur[xl] = isset ? sv[q] : seen + 1;
+                        wave_lds_sync();
+                        sv[q] = isset ? 0ull : seen;
+                    }
+                    for (u32 k = lane; k < SYB_WORDS; k += 64) s_wc[w][k] = 0;
+                }
+                __syncthreads();
             }
         }
 #pragma unroll
-        for (int q = 0; q < SYB_PER; q++) {
-            if (base + q * SYB_TPB >= total) break;
-            const u32 i = base + q * SYB_TPB + tid;
-            const bool valid = i < total;
-            const u32 xl = valid ? (u32)(ent[q].y - w0) : 0u;
-            const bool isset = valid && (ent[q].x & SETBIT);
-            const u64 peers = match_lanes(xl, SYB_SHIFT, __ballot(valid));
-            if (++tag == 0x10000u) {  // tags are 16 bits: clear the table and restart
-                __syncthreads();
-                for (u32 k = tid; k < SYB_WAVES * SYB_WORDS; k += SYB_TPB) (&s_T[0][0])[k] = 0;
-                __syncthreads();
-                tag = 1;
-            }
-            const bool wlast = valid && 63 - __clzll(peers) == lane;
-            if (wlast) s_T[w][xl] = (tag << 16) | (u32)__popcll(peers);
-            const int anyset = __syncthreads_or(isset);
-            u64 seen = 0;
-            if (!anyset) {
-                u32 before = 0;
-                bool later = false;
-                if (valid) {
-                    for (int ww = 0; ww < SYB_WAVES; ww++) {
-                        const u32 e = s_T[ww][xl];
-                        if (ww != w && (e >> 16) == tag) {
-                            if (ww < w) before += e & 0xFFFFu;
-                            else later = true;
-                        }
-                    }
-                    seen = s_cur[xl] + before + (u64)__popcll(peers & lt);
-                }
-                __syncthreads();
-                if (wlast && !later) s_cur[xl] = seen + 1;
-            } else {
-                // a WriteOnly in this chunk: waves apply their touches in order
-                const u64 mytid = isset ? ring[(lo + (ent[q].x & ~SETBIT) / T) & ring_mask].tid : 0ull;
-                const u64 S = __ballot(isset) & peers & lt;
-                const int s = S ? 63 - __clzll(S) : lane;
-                const u64 stid = shfl_u64(mytid, s);
-                for (int ww = 0; ww < SYB_WAVES; ww++) {
-                    if (ww == w && valid) {
-                        const u64 P = peers & lt;
-                        if (S) seen = stid + (u64)__popcll(P & ~((2ull << s) - 1));
-                        else seen = s_cur[xl] + (u64)__popcll(P);
-                        if (wlast) s_cur[xl] = isset ? mytid : seen + 1;
-                    }
-                    __syncthreads();
-                }
-            }
-            if (valid) V[gpos[q]] = isset ? 0ull : seen;
-        }
+        for (int q = 0; q < SYB_PER; q++)
+            if (base + (u32)w * (SYB_PER * 64) + q * 64 + lane < total) V[gpos[q]] = sv[q];
     }
     __syncthreads();
-    if (tid < (int)SYB_WORDS && w0 + tid < N) words[w0 + tid] = s_cur[tid];
+    for (u32 i = tid; i < SYB_WORDS; i += SYB_TPB)
+        if (w0 + i < N) words[w0 + i] = s_cur[i];
 }
 
-__global__ __launch_bounds__(SYC_TPB) void sy_sum_kernel(const uint2* __restrict__ E, const u64* __restrict__ V, u32 CW,
-                                                         u64 n, u32 T, u64 lo, u64 resp_lo, u64 resp_hi,
+__global__ __launch_bounds__(SYC_TPB) void sy_sum_kernel(const u32* __restrict__ E, const u64* __restrict__ V, u32 CW,
+                                                         u64 n, u64 lo, u64 resp_lo, u64 resp_hi,
                                                          u64* __restrict__ resp, uint8_t* __restrict__ some, u32 tile0,
                                                          u32 want, const SyHot* __restrict__ hot, u32 ntiles, u32 HR,
                                                          u64* __restrict__ words) {
@@ -552,13 +611,11 @@ __global__ __launch_bounds__(SYC_TPB) void sy_sum_kernel(const uint2* __restrict
         const u32 nops = (u32)(n - op0 < SYA_OPS ? n - op0 : SYA_OPS);
         for (u32 i = tid; i < SYA_OPS; i += SYC_TPB) s_sum[i] = 0;
         __syncthreads();
-        const uint2* Et = E + tile * SYA_OPS * CW;
+        const u32* Et = E + tile * SYA_OPS * CW;
         const u64* Vt = V + tile * SYA_OPS * CW;
         const u32 ne = nops * CW;
-        for (u32 e = tid; e < ne; e += SYC_TPB) {
-            const u32 opl = (Et[e].x & ~SETBIT) / T - (u32)op0;
-            atomicAdd((unsigned long long*)&s_sum[opl], (unsigned long long)Vt[e]);
-        }
+        for (u32 e = tid; e < ne; e += SYC_TPB)
+            atomicAdd((unsigned long long*)&s_sum[ent_op(Et[e])], (unsigned long long)Vt[e]);
         __syncthreads();
         for (u32 i = tid; i < nops; i += SYC_TPB) {
             const u64 g = lo + op0 + i;
@@ -603,39 +660,39 @@ u64 sy_bucket_aux_bytes(const nrg_config& cf) {
     const u64 span = cf.synth_n - cf.synth_hot_reads;
     const u64 NB = (span + SYB_WORDS - 1) / SYB_WORDS;
     const u64 tiles = (cf.max_batch + SYA_OPS - 1) / SYA_OPS;
-    return tiles * SYA_OPS * cf.synth_cold_writes * 8 + NB * tiles * 4 + tiles * cf.synth_hot_reads * sizeof(SyHot) + 256;
+    return tiles * SYA_OPS * cf.synth_cold_writes * 12 + NB * tiles * 4 + tiles * cf.synth_hot_reads * sizeof(SyHot) +
+           256;
 }
 
 static hipError_t sy_bucket_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 resp_hi, u64* d_resp, uint8_t* d_some) {
     hipStream_t st = c->stream;
     const nrg_config& cf = c->cfg;
     const u32 HW = cf.synth_hot_writes, CW = cf.synth_cold_writes, HR = cf.synth_hot_reads;
-    const u32 T = HW + CW;
     const u64 span = cf.synth_n - HR;
     const u32 NB = (u32)((span + SYB_WORDS - 1) / SYB_WORDS);
-    u32 nbits = 0;
-    while ((1u << nbits) < NB) nbits++;
+    const u64 span_m = ~0ull / span, hr_m = ~0ull / HR;
     const u32 ntiles = (u32)((n + SYA_OPS - 1) / SYA_OPS);
     const u64 max_tiles = (cf.max_batch + SYA_OPS - 1) / SYA_OPS;
     const u64 ring_mask = c->log_size - 1;
     const nrg_synth_op* ring = (const nrg_synth_op*)c->d_ring;
-    uint2* E = (uint2*)c->d_tmp_u64;
     u64* V = (u64*)c->d_sy_aux;
-    u32* cnt = (u32*)(V + max_tiles * SYA_OPS * CW);
+    u32* E = (u32*)(V + max_tiles * SYA_OPS * CW);
+    u32* cnt = E + max_tiles * SYA_OPS * CW;
     SyHot* hot = (SyHot*)(((uintptr_t)(cnt + (u64)NB * max_tiles) + 15) & ~(uintptr_t)15);
     timer_begin(c, "sy_replay");
-#define SY_PART(CWV)                                                                                              \
-    case CWV:                                                                                                     \
-        sy_part_kernel<CWV><<<ntiles, SYA_TPB, 0, st>>>(ring, ring_mask, lo, n, span, HR, HW, T, NB, nbits, ntiles, \
-                                                        E, cnt, hot);                                             \
+#define SY_PART(CWV)                                                                                               \
+    case CWV:                                                                                                      \
+        sy_part_kernel<CWV><<<ntiles, SYA_TPB, 0, st>>>(ring, ring_mask, lo, n, span, span_m, HR, hr_m, HW, NB, ntiles, \
+                                                        E, cnt, hot);                                              \
         break
     switch (CW) {
         SY_PART(1); SY_PART(2); SY_PART(3); SY_PART(4); SY_PART(5); SY_PART(6); SY_PART(7); SY_PART(8);
         default: return hipErrorInvalidValue;
     }
 #undef SY_PART
-    sy_bucket_kernel<<<NB, SYB_TPB, 0, st>>>(E, cnt, ntiles, SYA_OPS * CW, V, c->d_words, cf.synth_n, HR, ring,
-                                             ring_mask, lo, T);
+    const size_t dyn = (size_t)(ntiles + 1) * 4 + (size_t)ntiles * 2;
+    sy_bucket_kernel<<<NB, SYB_TPB, dyn, st>>>(E, cnt, ntiles, SYA_OPS * CW, V, c->d_words, cf.synth_n, HR, ring,
+                                               ring_mask, lo);
     const bool want = d_resp != nullptr && resp_lo < lo + n && resp_hi > lo;
     u32 t0 = 0, t1 = 1;
     if (want) {
@@ -644,7 +701,7 @@ static hipError_t sy_bucket_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 re
         t0 = (u32)(a / SYA_OPS);
         t1 = (u32)((z + SYA_OPS - 1) / SYA_OPS);
     }
-    sy_sum_kernel<<<t1 - t0, SYC_TPB, 0, st>>>(E, V, CW, n, T, lo, resp_lo, resp_hi, d_resp, d_some, t0, want ? 1u : 0u,
+    sy_sum_kernel<<<t1 - t0, SYC_TPB, 0, st>>>(E, V, CW, n, lo, resp_lo, resp_hi, d_resp, d_some, t0, want ? 1u : 0u,
                                                hot, ntiles, HR, c->d_words);
     timer_end(c, "sy_replay");
     return hipGetLastError();
