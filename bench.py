@@ -507,7 +507,7 @@ def run_synthetic(args, env):
                             "ops_per_gpu_per_round": N,
                             "parallelism": "replicas%d" % world,
                         })
-    res["roofline"] = roofline("sy_replay", round_bytes, k_n, k_ms, args, None)
+    res["roofline"] = roofline("sy_replay", round_bytes, k_n, k_ms, args, measured_traffic(args))
     res["round"] = {"algorithmic_bytes": int(round_bytes),
                     "touches_per_s": round(6 * Ng * args.steps / elapsed, 1)}
     if not args.no_cpu_baseline and world == 1:
@@ -598,7 +598,7 @@ def run_stack(args, env):
                             "ops_per_gpu_per_round": N,
                             "parallelism": "replicas%d" % world,
                         })
-    res["roofline"] = roofline("st_replay", round_bytes, k_n, k_ms, args, None)
+    res["roofline"] = roofline("st_replay", round_bytes, k_n, k_ms, args, measured_traffic(args))
     res["round"] = {"algorithmic_bytes": int(round_bytes), "distinct_slots_written": int(S)}
     if not args.no_cpu_baseline and world == 1:
         res["cpu_baseline"] = stack_cpu_baseline(min(args.cpu_seconds, 10.0), N, args.stack_init)

@@ -52,7 +52,8 @@ struct IndexJob {
     u32 nblocks;
     u64* created_acc;  // [HM_CREATED_SLOTS] keys created by index blocks
     u32 exp;  // diagnostic knobs (NRG_EXP; results are wrong when set): 1 no stamp atomics,
-              // 2 no LDS combining (one atomic per Put), 4 no apply role, 8 no index role
+              // 2 no LDS combining (one atomic per Put), 4 no apply role, 8 no index role,
+              // 16 workgroup-scope stamp atomics
 };
 struct ApplyJob {
     RecSrc rec;
@@ -199,8 +200,13 @@ __device__ __forceinline__ void index_role(IndexJob j, u32 blk, Slot* table, u32
     __syncthreads();
     for (int q = threadIdx.x; q < K1_LDS; q += TPB) {
         const u32 s = s_slot[q];
-        if (s != 0xFFFFFFFFu && !(j.exp & 1))
-            atomicMax(slot_stamp(&table[s], par), ((u64)j.epoch << 32) | s_max[q]);
+        if (s != 0xFFFFFFFFu && !(j.exp & 1)) {
+            if (j.exp & 16)  // timing knob: workgroup-scope (XCD-L2-executed) atomic; wrong across XCDs
+                __hip_atomic_fetch_max(slot_stamp(&table[s], par), ((u64)j.epoch << 32) | s_max[q], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+            else
+                atomicMax(slot_stamp(&table[s], par), ((u64)j.epoch << 32) | s_max[q]);
+        }
     }
     // keys created by this block: spread over HM_CREATED_SLOTS counters (summed by hm_count);
     // one same-address atomic per block would serialise at the memory side (~88 per us)

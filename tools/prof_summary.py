@@ -77,7 +77,13 @@ def main():
     except (NameError, ValueError, KeyError, IndexError):
         pass
     # the timed unit: one hm_round launch, or one stack chunk (st_tile + st_finish kernels)
-    parts = ["st_tile_kernel", "st_finish_kernel"] if tk and tk.startswith("stack") else ["hm_round_kernel"]
+    # (stack: st_tile + st_finish kernels; synthetic: sy_part + sy_bucket + sy_sum kernels)
+    if tk and tk.startswith("stack"):
+        parts = ["st_tile_kernel", "st_finish_kernel"]
+    elif tk and tk.startswith("synthetic"):
+        parts = ["sy_part_kernel", "sy_bucket_kernel", "sy_sum_kernel"]
+    else:
+        parts = ["hm_round_kernel"]
 
     def per_unit(tab):
         got = [next((v for k, v in tab.items() if p in k), None) for p in parts]
