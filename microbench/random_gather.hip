@@ -134,6 +134,66 @@ float time_it(F f, int reps) {
     return ms / reps;
 }
 
+
+// NrHashMap Get-shaped variants over 64-B slots (the replica's layout): the key comes from a
+// streamed key array (dependent load), one or two 16-B loads of the slot's line, value and
+// found byte stored. Separates the cost of each piece of hm_round's read role.
+struct __attribute__((aligned(16))) Slot64 {
+    u64 k, v, s1, c, s0, p0, p1, p2;
+};
+__global__ void init_keys(u64* keys, u64 n) {
+    const u64 i = blockIdx.x * 256ull + threadIdx.x;
+    if (i < n) keys[i] = mix64(i + 12345);
+}
+template <int KEYLOAD, int TWO, int STORE>
+__global__ __launch_bounds__(256) void gget(const Slot64* __restrict__ t, const u64* __restrict__ keys, u64 mask,
+                                            u64 n, u64* __restrict__ vals, unsigned char* __restrict__ found,
+                                            u64* out) {
+    const u64 i = blockIdx.x * 256ull + threadIdx.x;
+    if (i >= n) return;
+    const u64 key = KEYLOAD ? keys[i] : mix64(i * 0x9E3779B97F4A7C15ull);
+    const Slot64* p = &t[mix64(key) & mask];
+    const uint4 a = *(const uint4*)&p->k;
+    uint4 b = {0, 0, 0, 0};
+    if (TWO) b = *(const uint4*)&p->s1;
+    const u64 k = ((u64)a.y << 32) | a.x;
+    const u64 v = (((u64)a.w << 32) | a.z) + b.x + b.z;
+    if (STORE) {
+        vals[i] = k == key ? v : 0;
+        found[i] = k == key;
+    } else if ((k ^ v) == 0x12345) {
+        out[0] = k;
+    }
+}
+
+// lane pairs: lane 2j loads {key, val}, lane 2j+1 the {stamp, created} 16 B of the same slot
+// (one 32-B access per Get in one wave instruction), exchanged with a lane shuffle
+template <int STORE>
+__global__ __launch_bounds__(256) void gpair(const Slot64* __restrict__ t, const u64* __restrict__ keys, u64 mask,
+                                             u64 n, u64* __restrict__ vals, unsigned char* __restrict__ found,
+                                             u64* out) {
+    const u64 i = (blockIdx.x * 256ull + threadIdx.x) >> 1;
+    const int half = threadIdx.x & 1;
+    const u64 key = i < n ? keys[i] : 0;
+    const Slot64* p = &t[mix64(key) & mask];
+    const uint4 a = i < n ? *((const uint4*)&p->k + half) : uint4{0, 0, 0, 0};
+    uint4 o;
+    o.x = __shfl_xor((int)a.x, 1);
+    o.y = __shfl_xor((int)a.y, 1);
+    o.z = __shfl_xor((int)a.z, 1);
+    o.w = __shfl_xor((int)a.w, 1);
+    const uint4 kv = half ? o : a, sc = half ? a : o;
+    const u64 k = ((u64)kv.y << 32) | kv.x;
+    const u64 v = (((u64)kv.w << 32) | kv.z) + sc.x + sc.z;
+    if (i >= n) return;
+    if (STORE) {
+        if (!half) vals[i] = k == key ? v : 0;
+        else found[i] = k == key;
+    } else if ((k ^ v) == 0x12345) {
+        out[0] = k;
+    }
+}
+
 int main(int argc, char** argv) {
     const int log2 = argc > 1 ? atoi(argv[1]) : 26;
     const u64 slots = 1ull << log2, mask = slots - 1;
@@ -144,6 +204,37 @@ int main(int argc, char** argv) {
     CHK(hipMalloc(&t, slots * sizeof(Slot)));
     CHK(hipMemset(t, 1, slots * sizeof(Slot)));
     CHK(hipMalloc(&out, 64));
+    if (argc > 3) {  // Get-shaped variants over 2^log2 64-B slots
+        CHK(hipFree(t));
+        Slot64* t64;
+        u64 *keys, *vals;
+        unsigned char* fnd;
+        CHK(hipMalloc(&t64, slots * sizeof(Slot64)));
+        CHK(hipMemset(t64, 1, slots * sizeof(Slot64)));
+        CHK(hipMalloc(&keys, 16 * n * 8));
+        CHK(hipMalloc(&vals, n * 8));
+        CHK(hipMalloc(&fnd, n));
+        printf("64-B slot table %llu slots (%.2f GiB), %llu Gets per launch\n", slots, slots * 64.0 / (1 << 30), n);
+        const unsigned g = (unsigned)((n + 255) / 256);
+        init_keys<<<16 * g, 256>>>(keys, 16 * n);
+        int rot = 0;  // 16 distinct key batches in rotation: no MALL reuse between launches
+#define RUNG(A, B, C)                                                                                      \
+    {                                                                                                      \
+        float ms = time_it([&] { gget<A, B, C><<<g, 256>>>(t64, keys + (rot++ % 16) * n, mask, n, vals, fnd, out); }, reps); \
+        printf("get key%d two%d store%d  %8.2f us  %7.2f Glookups/s\n", A, B, C, ms * 1e3, n / (ms / 1e3) / 1e9); \
+    }
+        for (int st = 0; st < 2; st++) {
+            const unsigned g2 = (unsigned)((2 * n + 255) / 256);
+            float ms = time_it([&] {
+                const u64* kb = keys + (rot++ % 16) * n;
+                if (st) gpair<1><<<g2, 256>>>(t64, kb, mask, n, vals, fnd, out);
+                else gpair<0><<<g2, 256>>>(t64, kb, mask, n, vals, fnd, out);
+            }, reps);
+            printf("get pair  key1 store%d  %8.2f us  %7.2f Glookups/s\n", st, ms * 1e3, n / (ms / 1e3) / 1e9);
+        }
+        RUNG(0, 0, 0) RUNG(0, 1, 0) RUNG(0, 0, 1) RUNG(0, 1, 1) RUNG(1, 0, 0) RUNG(1, 1, 0) RUNG(1, 0, 1) RUNG(1, 1, 1)
+        return 0;
+    }
     printf("table %llu slots (%.2f GiB), %llu lookups per launch\n", slots, slots * 16.0 / (1 << 30), n);
     auto report = [&](const char* name, float ms, double useful_bytes) {
         double s = ms / 1e3;
