@@ -12,6 +12,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #define CHK(x)                                                                          \
@@ -209,7 +210,11 @@ int main(int argc, char** argv) {
         Slot64* t64;
         u64 *keys, *vals;
         unsigned char* fnd;
-        CHK(hipMalloc(&t64, slots * sizeof(Slot64)));
+        // argv[3]: get = hipMalloc; getuc = uncached (MTYPE UC); getfg = fine-grained
+        if (!strcmp(argv[3], "getuc")) CHK(hipExtMallocWithFlags((void**)&t64, slots * sizeof(Slot64), hipDeviceMallocUncached));
+        else if (!strcmp(argv[3], "getfg")) CHK(hipExtMallocWithFlags((void**)&t64, slots * sizeof(Slot64), hipDeviceMallocFinegrained));
+        else CHK(hipMalloc(&t64, slots * sizeof(Slot64)));
+        printf("table allocation: %s\n", argv[3]);
         CHK(hipMemset(t64, 1, slots * sizeof(Slot64)));
         CHK(hipMalloc(&keys, 16 * n * 8));
         CHK(hipMalloc(&vals, n * 8));
