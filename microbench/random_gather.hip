@@ -195,6 +195,22 @@ __global__ __launch_bounds__(256) void gpair(const Slot64* __restrict__ t, const
     }
 }
 
+// scattered stamp atomics into 64-B slots of the replica-sized table: 64-bit vs 32-bit max
+template <typename T>
+__global__ __launch_bounds__(256) void a_slot(Slot64* t, u64 mask, u64 n, u64 seed, int off) {
+    const u64 i = blockIdx.x * 256ull + threadIdx.x;
+    if (i >= n) return;
+    T* p = (T*)((char*)&t[mix64(seed + i) & mask] + off);
+    atomicMax(p, (T)(i + 1));
+}
+
+// scattered plain 8-B stores into 64-B slots of the replica-sized table
+__global__ __launch_bounds__(256) void st_slot(Slot64* t, u64 mask, u64 n, u64 seed) {
+    const u64 i = blockIdx.x * 256ull + threadIdx.x;
+    if (i >= n) return;
+    t[mix64(seed + i) & mask].s1 = i + 1;
+}
+
 int main(int argc, char** argv) {
     const int log2 = argc > 1 ? atoi(argv[1]) : 26;
     const u64 slots = 1ull << log2, mask = slots - 1;
@@ -236,6 +252,15 @@ int main(int argc, char** argv) {
                 else gpair<0><<<g2, 256>>>(t64, kb, mask, n, vals, fnd, out);
             }, reps);
             printf("get pair  key1 store%d  %8.2f us  %7.2f Glookups/s\n", st, ms * 1e3, n / (ms / 1e3) / 1e9);
+        }
+        {
+            int seed = 0;
+            float ms = time_it([&] { a_slot<unsigned long long><<<g, 256>>>(t64, mask, n, 1000 + seed++, 16); }, reps);
+            printf("atomicMax u64 into slots  %8.2f us  %7.2f Gops/s\n", ms * 1e3, n / (ms / 1e3) / 1e9);
+            ms = time_it([&] { a_slot<unsigned int><<<g, 256>>>(t64, mask, n, 2000 + seed++, 16); }, reps);
+            printf("atomicMax u32 into slots  %8.2f us  %7.2f Gops/s\n", ms * 1e3, n / (ms / 1e3) / 1e9);
+            ms = time_it([&] { st_slot<<<g, 256>>>(t64, mask, n, 3000 + seed++); }, reps);
+            printf("plain u64 store into slots %7.2f us  %7.2f Gops/s\n", ms * 1e3, n / (ms / 1e3) / 1e9);
         }
         RUNG(0, 0, 0) RUNG(0, 1, 0) RUNG(0, 0, 1) RUNG(0, 1, 1) RUNG(1, 0, 0) RUNG(1, 1, 0) RUNG(1, 0, 1) RUNG(1, 1, 1)
         return 0;

@@ -20,6 +20,8 @@ constexpr u32 ERR_CAPACITY = 4u;
 
 // Counters of keys created by replay rounds (index blocks add to slot blk % HM_CREATED_SLOTS).
 constexpr u64 HM_CREATED_SLOTS = 8192;
+// Slot buckets of the bucket election (hashmap.hip hm_elect_kernel): at most this many.
+constexpr u32 HM_BK_MAX = 1024;
 
 // splitmix64 finaliser — identical constants to oracle/nr_oracle.c (orc_mix64) so that
 // device-generated workloads are reproducible by the CPU oracle.

@@ -29,6 +29,8 @@
 
 namespace nrg {
 
+typedef u64 u64x2 __attribute__((ext_vector_type(2)));
+
 constexpr int TPB = 256;
 constexpr u32 SIDE_SLOT = 0xFFFFFFFFu;   // put_slot value of the EMPTY_KEY key (side slot)
 constexpr u32 FULL_SLOT = 0xFFFFFFFEu;   // put_slot value of a Put that found no slot
@@ -51,9 +53,12 @@ struct IndexJob {
     u32 epoch;
     u32 nblocks;
     u64* created_acc;  // [HM_CREATED_SLOTS] keys created by index blocks
+    u64x2* bk_ent;  // bucket election (hm_elect_kernel): per index block, its distinct {slot, i+1; value}
+    u32* bk_cnt;  // entries grouped by slot bucket; [bucket][block] = offset << 16 | count
+    u32 bk_shift;  // bucket of slot s = s >> bk_shift
+    u32 bk_nb;     // buckets (power of two, <= HM_BK_MAX)
     u32 exp;  // diagnostic knobs (NRG_EXP; results are wrong when set): 1 no stamp atomics,
-              // 2 no LDS combining (one atomic per Put), 4 no apply role, 8 no index role,
-              // 16 workgroup-scope stamp atomics
+              // 2 no LDS combining (one atomic per Put), 4 no apply role, 8 no index role
 };
 struct ApplyJob {
     RecSrc rec;
@@ -108,6 +113,29 @@ __device__ __forceinline__ bool resolve(View w, u32 ep, RecSrc rec, bool use_rec
     return true;
 }
 
+// Block-wide exclusive prefix sum of one u32 per thread (TPB threads); *total gets the sum.
+__device__ __forceinline__ u32 block_scan_excl(u32 v, u32* total) {
+    __shared__ u32 s_w[TPB / 64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    u32 inc = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const u32 y = __shfl_up(inc, off, 64);
+        if (lane >= off) inc += y;
+    }
+    if (lane == 63) s_w[w] = inc;
+    __syncthreads();
+    u32 pre = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < TPB / 64; i++) {
+        pre += i < w ? s_w[i] : 0u;
+        tot += s_w[i];
+    }
+    __syncthreads();
+    if (total) *total = tot;
+    return pre + inc - v;
+}
+
 // find-or-claim k from slot s (its key already loaded as key0); returns slot or -1 if full
 __device__ __forceinline__ long long find_or_claim(Slot* table, u64 k, u64 s, u64 tmask, u64 key0, u32 epoch,
                                                    u32* created) {
@@ -130,7 +158,7 @@ __device__ __forceinline__ long long find_or_claim(Slot* table, u64 k, u64 s, u6
 }
 
 // ---- role: index(e) -------------------------------------------------------------------------
-template <int K1_ITEMS>
+template <int K1_ITEMS, bool BK>
 __device__ __forceinline__ void index_role(IndexJob j, u32 blk, Slot* table, u32 shift, u64 tmask,
                                            DevCtl* ctl) {
     constexpr int K1_TILE = TPB * K1_ITEMS;
@@ -138,10 +166,13 @@ __device__ __forceinline__ void index_role(IndexJob j, u32 blk, Slot* table, u32
     __shared__ u32 s_slot[K1_LDS];
     __shared__ u32 s_max[K1_LDS];
     __shared__ u32 s_created;
+    __shared__ u32 s_bk[BK ? HM_BK_MAX : 1];
     for (int q = threadIdx.x; q < K1_LDS; q += TPB) {
         s_slot[q] = 0xFFFFFFFFu;
         s_max[q] = 0;
     }
+    if constexpr (BK)
+        for (int q = threadIdx.x; q < (int)j.bk_nb; q += TPB) s_bk[q] = 0;
     if (threadIdx.x == 0) s_created = 0;
     __syncthreads();
     const u32 par = j.epoch & 1;
@@ -150,6 +181,9 @@ __device__ __forceinline__ void index_role(IndexJob j, u32 blk, Slot* table, u32
     u64 sl_idx[K1_ITEMS];
     u64 key0[K1_ITEMS];
     nrg_put rec[K1_ITEMS];
+    u32 hq[K1_ITEMS];  // LDS combine entry of each record (bucket election), ~0u: none
+#pragma unroll
+    for (int q = 0; q < K1_ITEMS; q++) hq[q] = ~0u;
     // issue every record load and every first probe before waiting on any of them
 #pragma unroll
     for (int q = 0; q < K1_ITEMS; q++) {
@@ -193,18 +227,62 @@ __device__ __forceinline__ void index_role(IndexJob j, u32 blk, Slot* table, u32
             h = (h + 1) & (K1_LDS - 1);
         }
         atomicMax(&s_max[h], (u32)(i + 1));
+        hq[q] = h;
+        sl_idx[q] = (u64)s;
     }
     // one key-count atomic per block: a same-address atomic per thread serialises at the
     // memory side (16k new keys cost ~16 us that way)
     if (created) atomicAdd(&s_created, created);
     __syncthreads();
-    for (int q = threadIdx.x; q < K1_LDS; q += TPB) {
-        const u32 s = s_slot[q];
-        if (s != 0xFFFFFFFFu && !(j.exp & 1)) {
-            if (j.exp & 16)  // timing knob: workgroup-scope (XCD-L2-executed) atomic; wrong across XCDs
-                __hip_atomic_fetch_max(slot_stamp(&table[s], par), ((u64)j.epoch << 32) | s_max[q], __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_WORKGROUP);
-            else
+    if constexpr (BK) {
+        // Bucket election: no stamp atomics. The block's distinct (slot, last i+1) pairs go to
+        // its tile of bk_ent grouped by slot bucket (order inside a bucket is irrelevant: the
+        // elector takes the maximum); bk_cnt[bucket][block] says where.
+        // the block's last record per slot is the one whose i+1 won the LDS combine; its
+        // thread holds the value, so entries carry it and the elector gathers no records
+        bool win[K1_ITEMS];
+#pragma unroll
+        for (int q = 0; q < K1_ITEMS; q++) {
+            const u64 i = base + (u64)q * TPB + threadIdx.x;
+            win[q] = hq[q] != ~0u && s_max[hq[q]] == (u32)(i + 1);
+            if (win[q]) atomicAdd(&s_bk[(u32)sl_idx[q] >> j.bk_shift], 1u);
+        }
+        __syncthreads();
+        constexpr int PER = HM_BK_MAX / TPB;  // buckets per thread (bk_nb <= HM_BK_MAX)
+        u32 c[PER], loc = 0;
+#pragma unroll
+        for (int r = 0; r < PER; r++) {
+            const u32 b = threadIdx.x * PER + r;
+            c[r] = b < j.bk_nb ? s_bk[b] : 0u;
+            loc += c[r];
+        }
+        const u32 run = block_scan_excl(loc, nullptr);
+        __syncthreads();
+        u32 off = run;
+#pragma unroll
+        for (int r = 0; r < PER; r++) {
+            const u32 b = threadIdx.x * PER + r;
+            if (b < j.bk_nb) {
+                j.bk_cnt[(u64)b * j.nblocks + blk] = (off << 16) | c[r];
+                s_bk[b] = off;
+            }
+            off += c[r];
+        }
+        __syncthreads();
+        u64x2* ent = j.bk_ent + (u64)blk * K1_TILE;
+#pragma unroll
+        for (int q = 0; q < K1_ITEMS; q++) {
+            if (!win[q]) continue;
+            const u64 i = base + (u64)q * TPB + threadIdx.x;
+            u64x2 e;
+            e.x = (sl_idx[q] << 32) | (u64)(i + 1);
+            e.y = rec[q].val;
+            ent[atomicAdd(&s_bk[(u32)sl_idx[q] >> j.bk_shift], 1u)] = e;
+        }
+    } else {
+        for (int q = threadIdx.x; q < K1_LDS; q += TPB) {
+            const u32 s = s_slot[q];
+            if (s != 0xFFFFFFFFu && !(j.exp & 1))
                 atomicMax(slot_stamp(&table[s], par), ((u64)j.epoch << 32) | s_max[q]);
         }
     }
@@ -273,12 +351,12 @@ __device__ __forceinline__ void read_role(ReadJob j, u32 blk, const Slot* table,
 
 // One launch = {index(e)} + {apply(p)} + {reads(p)} over disjoint block ranges (any may be
 // empty). Index blocks come first so the latency-bound pass is dispatched first.
-template <int K1_ITEMS, int G>
+template <int K1_ITEMS, int G, bool BK>
 __global__ __launch_bounds__(TPB) void hm_round_kernel(IndexJob ij, ApplyJob aj, ReadJob rj, Slot* table, u32 shift,
                                                        u64 tmask, DevCtl* ctl) {
     u32 b = blockIdx.x;
     if (b < ij.nblocks) {
-        index_role<K1_ITEMS>(ij, b, table, shift, tmask, ctl);
+        index_role<K1_ITEMS, BK>(ij, b, table, shift, tmask, ctl);
         return;
     }
     b -= ij.nblocks;
@@ -288,6 +366,128 @@ __global__ __launch_bounds__(TPB) void hm_round_kernel(IndexJob ij, ApplyJob aj,
     }
     b -= aj.nblocks;
     read_role<G>(rj, b, table, shift, tmask, ctl);
+}
+
+// Bucket election + apply of one round (the large-round alternative to the stamp atomics):
+// one block per slot bucket gathers the bucket's (slot, i+1) entries from every index block's
+// tile, keeps the maximum i+1 per slot in an LDS hash table (the last writer in log order) and
+// stores that record's value into the slot: one plain store per distinct key instead of a
+// scattered device atomic per Put (25.6 G/s) and a stamp re-read per Put in apply (plain
+// scattered 8-B stores run at 69 G/s, profiles/r01_get_floor.txt). A bucket whose distinct
+// slots overflow the table is redone in 2, 4, ... slot sub-ranges (the stores are idempotent).
+// The side slot (key u64::MAX) keeps its stamp; block 0 applies it.
+constexpr int HM_EL_HT = 2048;
+constexpr int HM_EL_CH = 2048;  // entries gathered per pass (one u16 tile id each in LDS)
+constexpr int HM_EL_PER = HM_EL_CH / TPB;
+__global__ __launch_bounds__(TPB) void hm_elect_kernel(const u64x2* __restrict__ ent, const u32* __restrict__ cnt,
+                                                       u32 nblocks, u32 bk_shift, RecSrc rec, Slot* table,
+                                                       DevCtl* ctl, u32 epoch) {
+    constexpr int K1_TILE = TPB * 8;  // bucket rounds index 8 Puts per thread
+    extern __shared__ u32 s_dyn[];    // s_pre[nblocks + 1] entry prefix, s_off[nblocks] (u16)
+    __shared__ u32 s_hk[HM_EL_HT];
+    __shared__ u32 s_hv[HM_EL_HT];
+    __shared__ uint16_t s_tile[HM_EL_CH];
+    u32* s_pre = s_dyn;
+    uint16_t* s_off = (uint16_t*)(s_dyn + nblocks + 1);
+    const u32 b = blockIdx.x;
+    // this bucket's (offset, count) in every index tile; thread owns tiles [tid*K, tid*K + K)
+    const u32 K = (nblocks + TPB - 1) / TPB;
+    u32 loc = 0;
+    for (u32 q = 0; q < K; q++) {
+        const u32 t = threadIdx.x * K + q;
+        if (t < nblocks) {
+            const u32 v = cnt[(u64)b * nblocks + t];
+            s_off[t] = (uint16_t)(v >> 16);
+            s_pre[t] = v & 0xFFFFu;
+            loc += v & 0xFFFFu;
+        }
+    }
+    u32 total;
+    u32 run = block_scan_excl(loc, &total);
+    for (u32 q = 0; q < K; q++) {
+        const u32 t = threadIdx.x * K + q;
+        if (t < nblocks) {
+            const u32 c = s_pre[t];
+            s_pre[t] = run;
+            run += c;
+        }
+    }
+    if (threadIdx.x == 0) s_pre[nblocks] = total;
+    u32 lp = 0;  // parts = 2^lp slot sub-ranges of the bucket, about <= HT/2 entries each
+    while ((total >> lp) > HM_EL_HT / 2 && lp < bk_shift) lp++;
+    __syncthreads();
+    u64x2 x[HM_EL_PER];
+    // the chunk [base, base + CH) of this bucket's entries into registers, all loads in flight
+    auto load_chunk = [&](u32 base) {
+        for (u32 q = 0; q < K; q++) {
+            const u32 t = threadIdx.x * K + q;
+            if (t >= nblocks) break;
+            const u32 lo_ = s_pre[t] > base ? s_pre[t] : base;
+            const u32 hi_ = s_pre[t + 1] < base + HM_EL_CH ? s_pre[t + 1] : base + HM_EL_CH;
+            for (u32 i = lo_; i < hi_; i++) s_tile[i - base] = (uint16_t)t;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < HM_EL_PER; r++) {
+            const u32 i = base + r * TPB + threadIdx.x;
+            x[r].x = ~0ull;
+            if (i < total) {
+                const u32 t = s_tile[i - base];
+                x[r] = ent[(u64)t * K1_TILE + s_off[t] + (i - s_pre[t])];
+            }
+        }
+        __syncthreads();  // s_tile is reused by the next chunk
+    };
+    auto in_part = [&](u32 sl, u32 p) { return !lp || ((sl >> (bk_shift - lp)) & ((1u << lp) - 1)) == p; };
+    const bool one_chunk = total <= (u32)HM_EL_CH;
+    for (u32 p = 0; p < (1u << lp);) {
+        for (int q = threadIdx.x; q < HM_EL_HT; q += TPB) {
+            s_hk[q] = 0xFFFFFFFFu;
+            s_hv[q] = 0;
+        }
+        bool ovf = false;
+        for (u32 base = 0; base < total; base += HM_EL_CH) {  // 1: latest i+1 per slot
+            load_chunk(base);
+#pragma unroll
+            for (int r = 0; r < HM_EL_PER; r++) {
+                if (x[r].x == ~0ull) continue;
+                const u32 sl = (u32)(x[r].x >> 32);
+                if (!in_part(sl, p)) continue;
+                u32 h = (u32)(mix64(sl) & (HM_EL_HT - 1));
+                int pr = 0;
+                for (; pr < HM_EL_HT; pr++) {
+                    const u32 old = atomicCAS(&s_hk[h], 0xFFFFFFFFu, sl);
+                    if (old == 0xFFFFFFFFu || old == sl) break;
+                    h = (h + 1) & (HM_EL_HT - 1);
+                }
+                if (pr == HM_EL_HT) ovf = true;
+                else atomicMax(&s_hv[h], (u32)x[r].x);
+            }
+        }
+        if (__syncthreads_or(ovf)) {  // more distinct slots than the table holds: finer parts
+            lp++;
+            p = 0;
+            continue;
+        }
+        for (u32 base = 0; base < total; base += HM_EL_CH) {  // 2: the winners store their values
+            if (!one_chunk) load_chunk(base);
+#pragma unroll
+            for (int r = 0; r < HM_EL_PER; r++) {
+                if (x[r].x == ~0ull) continue;
+                const u32 sl = (u32)(x[r].x >> 32);
+                if (!in_part(sl, p)) continue;
+                u32 h = (u32)(mix64(sl) & (HM_EL_HT - 1));
+                while (s_hk[h] != sl) h = (h + 1) & (HM_EL_HT - 1);
+                if (s_hv[h] == (u32)x[r].x) table[sl].val = x[r].y;
+            }
+        }
+        __syncthreads();
+        p++;
+    }
+    if (b == 0 && threadIdx.x == 0) {
+        const u64 st = *slot_stamp(&ctl->sp, epoch & 1);
+        if ((u32)(st >> 32) == epoch) ctl->sp.val = rec.at((u64)(u32)st - 1).val;
+    }
 }
 
 // Previous-value responses (HashMap::insert's return, nr/examples/hashmap.rs:46-50): with the
@@ -732,10 +932,10 @@ static RecSrc ring_src(nrg_ctx* c, const nrg_put* src, u64 lo) {
     return r;
 }
 
-template <int K1, int G>
+template <int K1, int G, bool BK = false>
 static void launch_round(nrg_ctx* c, const IndexJob& ij, const ApplyJob& aj, const ReadJob& rj) {
     const u32 blocks = ij.nblocks + aj.nblocks + rj.nblocks;
-    NRG_LAUNCH(c, "hm_round", (hm_round_kernel<K1, G>), blocks, TPB, 0, c->stream, ij, aj, rj, c->d_table,
+    NRG_LAUNCH(c, "hm_round", (hm_round_kernel<K1, G, BK>), blocks, TPB, 0, c->stream, ij, aj, rj, c->d_table,
                c->slot_shift, (u64)(c->slots - 1), c->d_ctl);
 }
 
@@ -744,7 +944,8 @@ static hipError_t launch(nrg_ctx* c, IndexJob& ij, ApplyJob& aj, ReadJob& rj) {
     // that holds it (same-address atomics serialise), so large (write-heavy) rounds use fewer,
     // bigger blocks (Zipf 0.99 at 50 % writes: 99 us with 1, 79 with 4, 65 with 8; uniform
     // unchanged); small rounds keep 1 (B1: 36.8 us vs 39.0 with 4). NRG_K1_ITEMS overrides.
-    const u32 k1 = c->k1_items ? c->k1_items : (ij.n >= (1u << 18) ? 8 : 1);
+    const bool bk = ij.bk_ent != nullptr;  // bucket election: 8 Puts per index thread
+    const u32 k1 = bk ? 8 : c->k1_items ? c->k1_items : (ij.n >= (1u << 18) ? 8 : 1);
     const u32 K1 = k1 >= 8 ? 8 : k1 >= 4 ? 4 : (k1 == 2 ? 2 : 1);
     const u32 G = c->gets_per_thread >= 4 ? 4 : (c->gets_per_thread == 2 ? 2 : 1);
     ij.exp = c->exp;
@@ -755,6 +956,12 @@ static hipError_t launch(nrg_ctx* c, IndexJob& ij, ApplyJob& aj, ReadJob& rj) {
     aj.nblocks = (u32)((aj.n + TPB - 1) / TPB);
     rj.nblocks = (u32)((rj.R + TPB * G - 1) / (TPB * G));
     if (ij.nblocks + aj.nblocks + rj.nblocks == 0) return hipSuccess;
+    if (bk) {
+        if (G == 1) launch_round<8, 1, true>(c, ij, aj, rj);
+        else if (G == 2) launch_round<8, 2, true>(c, ij, aj, rj);
+        else launch_round<8, 4, true>(c, ij, aj, rj);
+        return hipGetLastError();
+    }
 #define NRG_RK(A, B) \
     if (K1 == A && G == B) launch_round<A, B>(c, ij, aj, rj)
     NRG_RK(1, 1); else NRG_RK(1, 2); else NRG_RK(1, 4); else NRG_RK(2, 1); else NRG_RK(2, 2); else NRG_RK(2, 4);
@@ -914,6 +1121,16 @@ hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool
     ij.n = n;
     ij.put_slot = c->d_put_slot[epoch & 1];
     ij.epoch = epoch;
+    const bool bk = c->elect_min && n >= c->elect_min && !want_prev;
+    if (bk) {  // buckets of about 1024 entries (a power of two in [64, HM_BK_MAX])
+        u32 nb_log = 6;
+        while ((1ull << nb_log) * 1024 < n && (1u << nb_log) < HM_BK_MAX) nb_log++;
+        if (nb_log > 64 - c->slot_shift) nb_log = 64 - c->slot_shift;
+        ij.bk_ent = (u64x2*)c->d_bk_ent;
+        ij.bk_cnt = c->d_bk_cnt;
+        ij.bk_nb = 1u << nb_log;
+        ij.bk_shift = (64 - c->slot_shift) - nb_log;
+    }
     ApplyJob aj;
     ReadJob rj;
     deferred_jobs(c, aj, rj);  // the previous round's second half rides along
@@ -922,6 +1139,13 @@ hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool
     if (e != hipSuccess) return e;
     // records of this round for its deferred half: the ring copy if there is one
     const nrg_put* keep = (src && !write_ring) ? src : nullptr;
+    if (bk) {
+        const u32 nblocks = (u32)((n + TPB * 8 - 1) / (TPB * 8));
+        NRG_LAUNCH(c, "hm_elect", hm_elect_kernel, ij.bk_nb, TPB, (nblocks + 1) * 4 + nblocks * 2, c->stream, (const u64x2*)c->d_bk_ent,
+                   c->d_bk_cnt, nblocks, ij.bk_shift, ring_src(c, keep, lo), c->d_table, c->d_ctl, epoch);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
     if (d_prev && resp_lo < lo + n && resp_hi > lo) {
         u32 *sk = nullptr, *sv = nullptr;
         timer_begin(c, "hm_prev", c->stream);
@@ -937,7 +1161,7 @@ hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool
     p.epoch = epoch;
     p.src = keep;
     p.lo = lo;
-    p.n = n;
+    p.n = bk ? 0 : n;  // bucket rounds were applied by hm_elect_kernel: reads only
     p.keys = d_get_keys;
     p.R = R;
     p.vals = d_get_vals;

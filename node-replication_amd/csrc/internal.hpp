@@ -113,6 +113,11 @@ struct nrg_ctx {
     // Rounds of >= owner_min Puts take the partitioned path (0: never; NRG_OWNER_MIN).
     uint64_t owner_min = 0;
     uint32_t owner_rounds = 0;
+    // Rounds of >= elect_min Puts elect last writers per slot bucket in LDS (hm_elect_kernel)
+    // instead of stamp atomics (0: never; NRG_ELECT_MIN overrides the default).
+    uint64_t elect_min = 0;
+    void* d_bk_ent = nullptr;      // [tiles of 2048] 16-B {slot << 32 | i+1, value} per index block
+    uint32_t* d_bk_cnt = nullptr;  // [HM_BK_MAX][tiles] offset << 16 | count
     nrg::OwnerBufs own;
     // Zipf generator cache: zeta(zipf_n, zipf_theta)
     uint64_t zipf_n = 0;

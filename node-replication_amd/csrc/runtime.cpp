@@ -184,10 +184,20 @@ int staging(nrg_ctx* c, Staging& st, uint64_t bytes) {
 }  // namespace
 
 namespace nrg {
+// c->timing_only: empty (time every kernel) or a comma-separated list of kernel names
+static bool timer_match(const nrg_ctx* c, const char* name) {
+    if (c->timing_only.empty()) return true;
+    const std::string& w = c->timing_only;
+    const size_t n = std::strlen(name);
+    for (size_t p = 0; (p = w.find(name, p)) != std::string::npos; p++)
+        if ((p == 0 || w[p - 1] == ',') && (p + n == w.size() || w[p + n] == ',')) return true;
+    return false;
+}
 // HIP events around a kernel, recorded on the stream that kernel is launched on. When
-// c->timing_only is set, only that kernel is bracketed (keeps event packets off the others).
+// c->timing_only is set, only the kernels it names are bracketed (keeps event packets off
+// the others).
 void timer_begin(nrg_ctx* c, const char* name, hipStream_t s) {
-    if (!c->timing || (!c->timing_only.empty() && c->timing_only != name)) return;
+    if (!c->timing || !timer_match(c, name)) return;
     KTimer& t = c->timers[name];
     t.open = false;
     if (++t.seen % c->timing_every != 0) return;  // sampled, as timer_events
@@ -201,7 +211,7 @@ void timer_begin(nrg_ctx* c, const char* name, hipStream_t s) {
     t.open = true;
 }
 bool timer_events(nrg_ctx* c, const char* name, hipEvent_t* start, hipEvent_t* stop) {
-    if (!c->timing || (!c->timing_only.empty() && c->timing_only != name)) return false;
+    if (!c->timing || !timer_match(c, name)) return false;
     KTimer& t = c->timers[name];
     // sampled: launches every-1, 2*every-1, ... (skips a stream's first launch when every > 1)
     if (++t.seen % c->timing_every != 0) return false;
@@ -217,7 +227,7 @@ bool timer_events(nrg_ctx* c, const char* name, hipEvent_t* start, hipEvent_t* s
     return true;
 }
 void timer_end(nrg_ctx* c, const char* name, hipStream_t s) {
-    if (!c->timing || (!c->timing_only.empty() && c->timing_only != name)) return;
+    if (!c->timing || !timer_match(c, name)) return;
     KTimer& t = c->timers[name];
     if (!t.open) return;
     (void)hipEventRecord(t.ev[t.pending * 2 + 1], s ? s : c->stream);
@@ -330,6 +340,17 @@ int nrg_open(int dev, const nrg_config* cfg_in, nrg_ctx** out) {
         if (const char* e = std::getenv("NRG_EXP")) c->exp = (uint32_t)std::atoi(e);
         if (const char* e = std::getenv("NRG_OWNER_MIN")) c->owner_min = (uint64_t)std::atoll(e);
         if (c->owner_min) OPEN_CHK(hm_owner_alloc(c, mb));  // buffers only when the path is enabled
+        // Rounds of >= 350k Puts elect per slot bucket (hm_elect_kernel): measured faster from
+        // 400k Puts on (800k + 900k Gets, the per-GPU round at 8 GPUs: 112.8 -> 94.4 us; Zipf
+        // 0.99 at 50 % writes 64.8 -> 47.5), slower at 200k (45.7 -> 58.2) where the stamp
+        // atomics are cheaper than a second launch. profiles/r01_bucket_election.txt
+        c->elect_min = 350000;
+        if (const char* e = std::getenv("NRG_ELECT_MIN")) c->elect_min = (uint64_t)std::atoll(e);
+        if (c->elect_min && mb >= c->elect_min) {
+            const uint64_t tiles = (mb + 2047) / 2048;
+            OPEN_CHK(hipMalloc(&c->d_bk_ent, tiles * 2048 * 2 * sizeof(uint64_t)));
+            OPEN_CHK(hipMalloc(&c->d_bk_cnt, (uint64_t)HM_BK_MAX * tiles * sizeof(uint32_t)));
+        }
         c->pipeline = cf.pipeline != 0;
         if (const char* e = std::getenv("NRG_PIPELINE")) c->pipeline = std::atoi(e) != 0;
         c->epoch = 1;  // epoch 1 = the state built by prefill; replay rounds start at 2
@@ -385,7 +406,7 @@ int nrg_close(nrg_ctx* c) {
     if (c->stream && c->stream != c->own_stream) (void)hipStreamSynchronize(c->stream);
     void* ptrs[] = {c->d_ring,    c->d_ctl,      c->d_table,   c->d_put_slot[0], c->d_put_slot[1],
                     c->d_stack,   c->d_words,    c->d_sort_aux, c->d_tmp_u64,    c->d_scan_desc,
-                    c->d_created, c->d_st_aux,   c->d_sy_aux};
+                    c->d_created, c->d_st_aux,   c->d_sy_aux,   c->d_bk_ent,     c->d_bk_cnt};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     sort_free(c->sort);
