@@ -380,9 +380,9 @@ constexpr int HM_EL_HT = 2048;
 constexpr int HM_EL_CH = 2048;  // entries gathered per pass (one u16 tile id each in LDS)
 constexpr int HM_EL_PER = HM_EL_CH / TPB;
 __global__ __launch_bounds__(TPB) void hm_elect_kernel(const u64x2* __restrict__ ent, const u32* __restrict__ cnt,
-                                                       u32 nblocks, u32 bk_shift, RecSrc rec, Slot* table,
+                                                       u32 nblocks, u32 tile, u32 bk_shift, RecSrc rec, Slot* table,
                                                        DevCtl* ctl, u32 epoch) {
-    constexpr int K1_TILE = TPB * 8;  // bucket rounds index 8 Puts per thread
+    const u32 K1_TILE = tile;  // entries per index block (TPB x its Puts per thread)
     extern __shared__ u32 s_dyn[];    // s_pre[nblocks + 1] entry prefix, s_off[nblocks] (u16)
     __shared__ u32 s_hk[HM_EL_HT];
     __shared__ u32 s_hv[HM_EL_HT];
@@ -939,13 +939,17 @@ static void launch_round(nrg_ctx* c, const IndexJob& ij, const ApplyJob& aj, con
                c->slot_shift, (u64)(c->slots - 1), c->d_ctl);
 }
 
+// Puts per index thread in bucket rounds: 4 below 600k Puts, 8 above (400k + 900k Gets: 64.3
+// vs 68.4 us per round; 500k + 500k: 67.9 vs 71.9; 800k + 900k: 99.7 vs 95.7). NRG_BK_K1 overrides.
+static u32 bk_k1(const nrg_ctx* c, u64 n) { return c->bk_k1 ? c->bk_k1 : (n >= 600000 ? 8u : 4u); }
+
 static hipError_t launch(nrg_ctx* c, IndexJob& ij, ApplyJob& aj, ReadJob& rj) {
     // Puts per index thread: a hot key costs one same-address stamp atomic per index block
     // that holds it (same-address atomics serialise), so large (write-heavy) rounds use fewer,
     // bigger blocks (Zipf 0.99 at 50 % writes: 99 us with 1, 79 with 4, 65 with 8; uniform
     // unchanged); small rounds keep 1 (B1: 36.8 us vs 39.0 with 4). NRG_K1_ITEMS overrides.
     const bool bk = ij.bk_ent != nullptr;  // bucket election: 8 Puts per index thread
-    const u32 k1 = bk ? 8 : c->k1_items ? c->k1_items : (ij.n >= (1u << 18) ? 8 : 1);
+    const u32 k1 = bk ? bk_k1(c, ij.n) : c->k1_items ? c->k1_items : (ij.n >= (1u << 18) ? 8 : 1);
     const u32 K1 = k1 >= 8 ? 8 : k1 >= 4 ? 4 : (k1 == 2 ? 2 : 1);
     const u32 G = c->gets_per_thread >= 4 ? 4 : (c->gets_per_thread == 2 ? 2 : 1);
     ij.exp = c->exp;
@@ -957,9 +961,9 @@ static hipError_t launch(nrg_ctx* c, IndexJob& ij, ApplyJob& aj, ReadJob& rj) {
     rj.nblocks = (u32)((rj.R + TPB * G - 1) / (TPB * G));
     if (ij.nblocks + aj.nblocks + rj.nblocks == 0) return hipSuccess;
     if (bk) {
-        if (G == 1) launch_round<8, 1, true>(c, ij, aj, rj);
-        else if (G == 2) launch_round<8, 2, true>(c, ij, aj, rj);
-        else launch_round<8, 4, true>(c, ij, aj, rj);
+        if (K1 == 4) launch_round<4, 1, true>(c, ij, aj, rj);
+        else if (K1 == 2) launch_round<2, 1, true>(c, ij, aj, rj);
+        else launch_round<8, 1, true>(c, ij, aj, rj);
         return hipGetLastError();
     }
 #define NRG_RK(A, B) \
@@ -1140,9 +1144,9 @@ hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool
     // records of this round for its deferred half: the ring copy if there is one
     const nrg_put* keep = (src && !write_ring) ? src : nullptr;
     if (bk) {
-        const u32 nblocks = (u32)((n + TPB * 8 - 1) / (TPB * 8));
+        const u32 nblocks = ij.nblocks;  // index tiles of TPB * bk_k1 Puts
         NRG_LAUNCH(c, "hm_elect", hm_elect_kernel, ij.bk_nb, TPB, (nblocks + 1) * 4 + nblocks * 2, c->stream, (const u64x2*)c->d_bk_ent,
-                   c->d_bk_cnt, nblocks, ij.bk_shift, ring_src(c, keep, lo), c->d_table, c->d_ctl, epoch);
+                   c->d_bk_cnt, nblocks, TPB * bk_k1(c, n), ij.bk_shift, ring_src(c, keep, lo), c->d_table, c->d_ctl, epoch);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

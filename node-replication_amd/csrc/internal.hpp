@@ -116,6 +116,7 @@ struct nrg_ctx {
     // Rounds of >= elect_min Puts elect last writers per slot bucket in LDS (hm_elect_kernel)
     // instead of stamp atomics (0: never; NRG_ELECT_MIN overrides the default).
     uint64_t elect_min = 0;
+    uint32_t bk_k1 = 0;  // Puts per index thread in bucket rounds (0: by size; 2, 4, 8: NRG_BK_K1)
     void* d_bk_ent = nullptr;      // [tiles of 2048] 16-B {slot << 32 | i+1, value} per index block
     uint32_t* d_bk_cnt = nullptr;  // [HM_BK_MAX][tiles] offset << 16 | count
     nrg::OwnerBufs own;

@@ -346,9 +346,10 @@ int nrg_open(int dev, const nrg_config* cfg_in, nrg_ctx** out) {
         // atomics are cheaper than a second launch. profiles/r01_bucket_election.txt
         c->elect_min = 350000;
         if (const char* e = std::getenv("NRG_ELECT_MIN")) c->elect_min = (uint64_t)std::atoll(e);
+        if (const char* e = std::getenv("NRG_BK_K1")) c->bk_k1 = std::atoi(e) >= 8 ? 8 : std::atoi(e) >= 4 ? 4 : 2;
         if (c->elect_min && mb >= c->elect_min) {
-            const uint64_t tiles = (mb + 2047) / 2048;
-            OPEN_CHK(hipMalloc(&c->d_bk_ent, tiles * 2048 * 2 * sizeof(uint64_t)));
+            const uint64_t tiles = (mb + 511) / 512;  // index tiles of 256 x (2, 4 or 8) Puts
+            OPEN_CHK(hipMalloc(&c->d_bk_ent, tiles * 512 * 2 * sizeof(uint64_t)));
             OPEN_CHK(hipMalloc(&c->d_bk_cnt, (uint64_t)HM_BK_MAX * tiles * sizeof(uint32_t)));
         }
         c->pipeline = cf.pipeline != 0;
