@@ -340,11 +340,11 @@ int nrg_open(int dev, const nrg_config* cfg_in, nrg_ctx** out) {
         if (const char* e = std::getenv("NRG_EXP")) c->exp = (uint32_t)std::atoi(e);
         if (const char* e = std::getenv("NRG_OWNER_MIN")) c->owner_min = (uint64_t)std::atoll(e);
         if (c->owner_min) OPEN_CHK(hm_owner_alloc(c, mb));  // buffers only when the path is enabled
-        // Rounds of >= 350k Puts elect per slot bucket (hm_elect_kernel): measured faster from
-        // 400k Puts on (800k + 900k Gets, the per-GPU round at 8 GPUs: 112.8 -> 94.4 us; Zipf
-        // 0.99 at 50 % writes 64.8 -> 47.5), slower at 200k (45.7 -> 58.2) where the stamp
-        // atomics are cheaper than a second launch. profiles/r01_bucket_election.txt
-        c->elect_min = 350000;
+        // Rounds of >= 250k Puts elect per slot bucket (hm_elect_kernel) instead of stamp atomics:
+        // measured crossover between 200k Puts (+ 900k Gets: 45.7 us stamp vs 49.3 bucket) and
+        // 300k (61.3 vs 56.2); 800k: 112.5 vs 94.3; Zipf 0.99 at 50 % writes: 64.9 vs 47.4.
+        // profiles/r01_bucket_election.txt
+        c->elect_min = 250000;
         if (const char* e = std::getenv("NRG_ELECT_MIN")) c->elect_min = (uint64_t)std::atoll(e);
         if (const char* e = std::getenv("NRG_BK_K1")) c->bk_k1 = std::atoi(e) >= 8 ? 8 : std::atoi(e) >= 4 ? 4 : 2;
         if (c->elect_min && mb >= c->elect_min) {
