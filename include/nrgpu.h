@@ -237,6 +237,12 @@ int nrg_hashmap_digest(nrg_ctx* ctx, uint64_t out[3]);
 /* ---- Stack --------------------------------------------------------------------------- */
 /* Stack::default(): storage = vals[0..n) (bottom first). */
 int nrg_stack_init(nrg_ctx* ctx, const uint32_t* vals, uint64_t n);
+/* Replica::combine for one stack batch (nr/src/replica.rs:544-595): Log::append of the n ops
+ * in d_ops (device) with `origin`, then Log::exec, fused into one replay pass that writes the
+ * log copy itself. Pop responses for these ops (d_pop_vals[i], d_some_bits[i]; nullable) as
+ * nrg_log_exec_async gives them. Same result as nrg_log_append_async + nrg_log_exec_async. */
+int nrg_stack_round_async(nrg_ctx* ctx, const nrg_stack_op* d_ops, uint64_t n, uint32_t origin,
+                          uint32_t* d_pop_vals, uint8_t* d_some_bits);
 /* Dispatch::dispatch(Peek) after sync: top of stack. */
 int nrg_stack_peek(nrg_ctx* ctx, uint32_t* val, uint8_t* some);
 int nrg_stack_len(nrg_ctx* ctx, uint64_t* n);

@@ -740,6 +740,26 @@ int nrg_hashmap_digest(nrg_ctx* c, uint64_t out[3]) {
 }
 
 // ---- Stack ---------------------------------------------------------------------------------
+int nrg_stack_round_async(nrg_ctx* c, const nrg_stack_op* d_ops, uint64_t n, uint32_t origin, uint32_t* d_pop_vals,
+                          uint8_t* d_some_bits) {
+    int r = need(c, NRG_DS_STACK);
+    if (r) return r;
+    if (n > c->cfg.max_batch) return NRG_E_CAPACITY;
+    if (n && !d_ops) return NRG_E_INVAL;
+    if (!d_pop_vals || !d_some_bits) d_pop_vals = nullptr, d_some_bits = nullptr;
+    // catch up on anything appended by others first (Replica::combine execs the whole log)
+    if ((r = exec_range(c, 0, 0, nullptr, nullptr))) return r;
+    if ((r = reserve(c, n))) return r;
+    const uint64_t lo = c->tail;
+    // one replay pass that also writes the log copy (Log::append + Log::exec of this batch)
+    HIPCHK(st_replay_chunk(c, lo, n, lo, lo + n, d_pop_vals, d_some_bits, d_ops));
+    if (n) note_origin(c, lo, n, origin);
+    c->tail = lo + n;
+    c->ltail = c->tail;
+    if (c->ctail < c->tail) c->ctail = c->tail;
+    return NRG_OK;
+}
+
 int nrg_stack_init(nrg_ctx* c, const uint32_t* vals, uint64_t n) {
     int r = need(c, NRG_DS_STACK);
     if (r) return r;

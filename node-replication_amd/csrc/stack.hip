@@ -107,7 +107,10 @@ __device__ __forceinline__ long long block_min4(long long x, long long* s_w, int
 
 constexpr u32 ST_INF = 0xFFFFu;
 
-__global__ __launch_bounds__(ST_TPB) void st_tile_kernel(const nrg_stack_op* __restrict__ ring, u64 ring_mask, u64 lo,
+// src: the chunk's records in a caller buffer (nrg_stack_round_async); the kernel then writes
+// the log copy itself (Log::append fused into the replay). nullptr: records are in the ring.
+__global__ __launch_bounds__(ST_TPB) void st_tile_kernel(const nrg_stack_op* __restrict__ src, nrg_stack_op* ring,
+                                                         u64 ring_mask, u64 lo,
                                                          u64 n, DevCtl* ctl, u64* desc, u32* ticket, StTiles tl,
                                                          u32* __restrict__ last, const u32* __restrict__ stack,
                                                          u64 cap, u64 resp_lo, u64 resp_hi, int push_resp,
@@ -139,7 +142,7 @@ __global__ __launch_bounds__(ST_TPB) void st_tile_kernel(const nrg_stack_op* __r
     for (int q = 0; q < ST_ITEMS; q++) {
         const u64 i = base + q;
         if (i < n) {
-            ops[q] = ring[(lo + i) & ring_mask];
+            ops[q] = src ? src[i] : ring[(lo + i) & ring_mask];
             Fn f;
             f.b = ops[q].op ? 1 : -1;
             f.a = ops[q].op ? 1 : 0;
@@ -147,6 +150,12 @@ __global__ __launch_bounds__(ST_TPB) void st_tile_kernel(const nrg_stack_op* __r
         } else {
             ops[q].op = 2;  // padding
             ops[q].val = 0;
+        }
+    }
+    if (src) {  // the log copy, lane-contiguous (the loads above are 8 records per thread)
+        for (u32 k = t; k < ST_TILE; k += ST_TPB) {
+            const u64 i = tbase + k;
+            if (i < n) ring[(lo + i) & ring_mask] = src[i];
         }
     }
     // wave inclusive scan of thread aggregates (order matters)
@@ -483,11 +492,12 @@ __global__ __launch_bounds__(256) void st_finish_kernel(const nrg_stack_op* __re
     }
 }
 
-hipError_t st_replay_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 resp_hi, uint32_t* d_resp, uint8_t* d_some) {
+hipError_t st_replay_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 resp_hi, uint32_t* d_resp, uint8_t* d_some,
+                           const nrg_stack_op* src) {
     if (n == 0) return hipSuccess;
     hipStream_t st = c->stream;
     const u64 ring_mask = c->log_size - 1;
-    const nrg_stack_op* ring = (const nrg_stack_op*)c->d_ring;
+    nrg_stack_op* ring = (nrg_stack_op*)c->d_ring;
     const u64 tiles = (n + ST_TILE - 1) / ST_TILE;
     // descriptors: [ticket (64 words of u32 = 32 u64)] [tiles u64]; zero at open, and
     // st_finish_kernel clears what st_tile_kernel used (no memset launch per chunk)
@@ -504,7 +514,7 @@ hipError_t st_replay_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 resp_hi, 
     const bool want = d_resp != nullptr && resp_lo < lo + n && resp_hi > lo;
     const u64 rlo = want ? resp_lo : 0, rhi = want ? resp_hi : 0;
     timer_begin(c, "st_replay");
-    st_tile_kernel<<<(unsigned)tiles, ST_TPB, 0, st>>>(ring, ring_mask, lo, n, c->d_ctl, desc, ticket, tl, last,
+    st_tile_kernel<<<(unsigned)tiles, ST_TPB, 0, st>>>(src, ring, ring_mask, lo, n, c->d_ctl, desc, ticket, tl, last,
                                                       c->d_stack, c->cfg.stack_capacity, rlo, rhi,
                                                       (int)c->cfg.stack_push_resp, d_resp, d_some);
     st_finish_kernel<<<(unsigned)tiles, 256, (tiles + tiles / 8 + tiles / 64 + 2) * 8, st>>>(

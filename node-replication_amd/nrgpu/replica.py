@@ -146,6 +146,12 @@ class DeviceReplica:
     def log_exec_device(self, resp_lo=0, resp_hi=0, d_resp=None, d_some=None):
         L.check(self._lib.nrg_log_exec_async(self._h, resp_lo, resp_hi, _dptr(d_resp), _dptr(d_some)), "exec")
 
+    def st_round_device(self, d_ops, n: int, origin: int, d_resp=None, d_some=None):
+        """Replica::combine for one stack batch on device buffers: append + exec in one replay
+        pass (nrg_stack_round_async); Pop responses for these ops into d_resp / d_some."""
+        L.check(self._lib.nrg_stack_round_async(self._h, _dptr(d_ops), n, origin, _dptr(d_resp), _dptr(d_some)),
+                "stack_round")
+
     def log_reset(self):
         L.check(self._lib.nrg_log_reset(self._h))
 

@@ -41,6 +41,33 @@ def test_stack_rounds(nrg, orc, init_n, n, rounds, push_resp):
     np.testing.assert_array_equal(dev.st_dump(), os_.dump())
 
 
+@pytest.mark.parametrize("init_n,n,rounds,push_resp", [(1000, 5000, 4, 0), (50000, 200000, 3, 0), (3, 20000, 3, 1)])
+def test_stack_round_fused(nrg, orc, init_n, n, rounds, push_resp):
+    """nrg_stack_round_async (append fused into the replay pass) == append + exec == the oracle;
+    the log copy it writes is what a later exec of another replica replays."""
+    import torch
+
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_STACK, 0, max_batch=1 << 18, stack_capacity=1 << 20,
+                            stack_push_resp=push_resp)
+    init = np.arange(init_n, dtype=np.uint32)
+    dev.st_init(init)
+    os_ = orc.Stack(init)
+    resp = torch.zeros(n, dtype=torch.int32, device="cuda")
+    some = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    for r in range(rounds):
+        vals, ops = orc.gen_stack_ops(n, 91 + r)
+        if init_n == 3:
+            ops[: n // 2] = 0  # long runs of pops on an empty stack (saturating depth)
+        d_ops = torch.from_numpy(_ops(vals, ops).view(np.int64).copy()).cuda()
+        dev.st_round_device(d_ops, n, 1, resp, some)
+        torch.cuda.synchronize()
+        oresp, osome = os_.replay(vals, ops, push_resp=bool(push_resp))
+        np.testing.assert_array_equal(some.cpu().numpy(), osome)
+        np.testing.assert_array_equal(resp.cpu().numpy().view(np.uint32), oresp)
+        assert dev.st_len() == len(os_)
+    np.testing.assert_array_equal(dev.st_dump(), os_.dump())
+
+
 def test_stack_chunked_exec(nrg, orc):
     dev = nrg.DeviceReplica(nrg._lib.NRG_DS_STACK, 0, max_batch=3000, stack_capacity=1 << 16)
     init = np.arange(100, dtype=np.uint32)
