@@ -464,8 +464,7 @@ def run_synthetic(args, env):
         from nrgpu.parallel import ReplicatedLog
 
         group = ReplicatedLog(rep, device=dev_t)
-    append_fn, exec_fn, h = rep._lib.nrg_log_append_async, rep._lib.nrg_log_exec_async, rep._h
-    first = L.C.c_uint64()
+    round_fn, h = rep._lib.nrg_synth_round_async, rep._h
     ptrs = [ops[p].data_ptr() for p in range(P)]
     r_p, s_p = resp.data_ptr(), some.data_ptr()
     gathered = {}
@@ -474,9 +473,8 @@ def run_synthetic(args, env):
     def step(i):
         p = i % P
         if group is None:
-            rc = append_fn(h, ptrs[p], N, rank + 1, L.C.byref(first))
-            if rc == 0:
-                rc = exec_fn(h, first.value, first.value + N, r_p, s_p)
+            # Replica::combine of the batch: Log::append fused into the partition pass
+            rc = round_fn(h, ptrs[p], N, rank + 1, r_p, s_p)
             if rc:
                 L.check(rc, "synthetic round")
         else:

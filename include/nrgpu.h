@@ -250,6 +250,11 @@ int nrg_stack_dump(nrg_ctx* ctx, uint32_t* vals, uint64_t cap, uint64_t* n);
 
 /* ---- AbstractDataStructure (synthetic) ------------------------------------------------ */
 /* Dispatch::dispatch(ReadOnly(tid, r1, r2)) for a batch, after sync. */
+/* Replica::combine for one batch of AbstractDataStructure write ops (device buffer): Log::append
+ * fused into the replay's first pass, then Log::exec; sums (responses) for these ops as
+ * nrg_log_exec_async gives them (nullable). Same result as append + exec. */
+int nrg_synth_round_async(nrg_ctx* ctx, const nrg_synth_op* d_ops, uint64_t n, uint32_t origin,
+                          uint64_t* d_resp, uint8_t* d_some);
 int nrg_synth_read(nrg_ctx* ctx, const nrg_synth_rd* ops, uint64_t n, uint64_t* sums);
 int nrg_synth_read_async(nrg_ctx* ctx, const nrg_synth_rd* d_ops, uint64_t n, uint64_t* d_sums);
 int nrg_synth_dump(nrg_ctx* ctx, uint64_t* words, uint64_t cap, uint64_t* n);

@@ -200,7 +200,7 @@ u64 st_aux_bytes(u64 max_batch);  // size of nrg_ctx::d_st_aux
 // synthetic.hip
 hipError_t sy_init(nrg_ctx* c);
 hipError_t sy_replay_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 resp_hi, u64* d_resp,
-                           uint8_t* d_some);
+                           uint8_t* d_some, const nrg_synth_op* src = nullptr);
 hipError_t sy_read(nrg_ctx* c, const nrg_synth_rd* d_ops, u64 n, u64* d_sums);
 bool sy_bucket_eligible(const nrg_config& cf);  // configs the sort-free bucket replay handles
 u64 sy_bucket_aux_bytes(const nrg_config& cf);  // size of nrg_ctx::d_sy_aux

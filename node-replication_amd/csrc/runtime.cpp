@@ -760,6 +760,24 @@ int nrg_stack_round_async(nrg_ctx* c, const nrg_stack_op* d_ops, uint64_t n, uin
     return NRG_OK;
 }
 
+int nrg_synth_round_async(nrg_ctx* c, const nrg_synth_op* d_ops, uint64_t n, uint32_t origin, uint64_t* d_resp,
+                          uint8_t* d_some) {
+    int r = need(c, NRG_DS_SYNTHETIC);
+    if (r) return r;
+    if (n > c->cfg.max_batch) return NRG_E_CAPACITY;
+    if (n && !d_ops) return NRG_E_INVAL;
+    if (!d_resp || !d_some) d_resp = nullptr, d_some = nullptr;
+    if ((r = exec_range(c, 0, 0, nullptr, nullptr))) return r;
+    if ((r = reserve(c, n))) return r;
+    const uint64_t lo = c->tail;
+    HIPCHK(sy_replay_chunk(c, lo, n, lo, lo + n, d_resp, d_some, d_ops));
+    if (n) note_origin(c, lo, n, origin);
+    c->tail = lo + n;
+    c->ltail = c->tail;
+    if (c->ctail < c->tail) c->ctail = c->tail;
+    return NRG_OK;
+}
+
 int nrg_stack_init(nrg_ctx* c, const uint32_t* vals, uint64_t n) {
     int r = need(c, NRG_DS_STACK);
     if (r) return r;

@@ -301,7 +301,10 @@ __device__ __forceinline__ u32 wave_rank(bool on, u32 key, int lane, u64* mask, 
 }
 
 template <int CW>
-__global__ __launch_bounds__(SYA_TPB) void sy_part_kernel(const nrg_synth_op* __restrict__ ring, u64 ring_mask, u64 lo,
+// src: the chunk's ops in a caller buffer (nrg_synth_round_async); the kernel then writes the
+// log copy itself (lane-contiguous). nullptr: the ops are in the ring.
+__global__ __launch_bounds__(SYA_TPB) void sy_part_kernel(const nrg_synth_op* __restrict__ src, nrg_synth_op* ring,
+                                                          u64 ring_mask, u64 lo,
                                                           u64 n, u64 span, u64 span_m, u32 HR, u64 hr_m, u32 HW, u32 NB,
                                                           u32 ntiles, u32* __restrict__ E, u32* __restrict__ cnt_bt,
                                                           SyHot* __restrict__ hot) {
@@ -327,14 +330,15 @@ __global__ __launch_bounds__(SYA_TPB) void sy_part_kernel(const nrg_synth_op* __
     u32 pk[SYA_OROUNDS * CW];
     const u32 opw = (u32)(w * SYA_OROUNDS) * 64 + lane;  // this lane's op in round 0, within the tile
     nrg_synth_op nx{0, 0, 0, 0};
-    if (op0 + opw < n) nx = ring[(lo + op0 + opw) & ring_mask];
+    if (op0 + opw < n) nx = src ? src[op0 + opw] : ring[(lo + op0 + opw) & ring_mask];
 #pragma unroll
     for (int orr = 0; orr < SYA_OROUNDS; orr++) {
         // 64 consecutive ops per wave round; lane = op; the next round's record is in flight
         const bool valid = op0 + opw + orr * 64 < n;
         const nrg_synth_op o = nx;
         if (orr + 1 < SYA_OROUNDS && op0 + opw + (orr + 1) * 64 < n)
-            nx = ring[(lo + op0 + opw + (orr + 1) * 64) & ring_mask];
+            nx = src ? src[op0 + opw + (orr + 1) * 64] : ring[(lo + op0 + opw + (orr + 1) * 64) & ring_mask];
+        if (src && valid) ring[(lo + op0 + opw + orr * 64) & ring_mask] = o;
         const bool set = valid && o.op == NRG_SYNTH_WRITE_ONLY;
         // hot touches (r2 + j) % HR, j < HW, skipped when r2 + HW wraps; ordered (lane, j)
         const bool hot_ok = valid && (o.r2 + HW >= o.r2);
@@ -664,7 +668,8 @@ u64 sy_bucket_aux_bytes(const nrg_config& cf) {
            256;
 }
 
-static hipError_t sy_bucket_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 resp_hi, u64* d_resp, uint8_t* d_some) {
+static hipError_t sy_bucket_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 resp_hi, u64* d_resp, uint8_t* d_some,
+                                  const nrg_synth_op* src) {
     hipStream_t st = c->stream;
     const nrg_config& cf = c->cfg;
     const u32 HW = cf.synth_hot_writes, CW = cf.synth_cold_writes, HR = cf.synth_hot_reads;
@@ -674,7 +679,7 @@ static hipError_t sy_bucket_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 re
     const u32 ntiles = (u32)((n + SYA_OPS - 1) / SYA_OPS);
     const u64 max_tiles = (cf.max_batch + SYA_OPS - 1) / SYA_OPS;
     const u64 ring_mask = c->log_size - 1;
-    const nrg_synth_op* ring = (const nrg_synth_op*)c->d_ring;
+    nrg_synth_op* ring = (nrg_synth_op*)c->d_ring;
     u64* V = (u64*)c->d_sy_aux;
     u32* E = (u32*)(V + max_tiles * SYA_OPS * CW);
     u32* cnt = E + max_tiles * SYA_OPS * CW;
@@ -682,7 +687,7 @@ static hipError_t sy_bucket_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 re
     timer_begin(c, "sy_replay");
 #define SY_PART(CWV)                                                                                               \
     case CWV:                                                                                                      \
-        sy_part_kernel<CWV><<<ntiles, SYA_TPB, 0, st>>>(ring, ring_mask, lo, n, span, span_m, HR, hr_m, HW, NB, ntiles, \
+        sy_part_kernel<CWV><<<ntiles, SYA_TPB, 0, st>>>(src, ring, ring_mask, lo, n, span, span_m, HR, hr_m, HW, NB, ntiles, \
                                                         E, cnt, hot);                                              \
         break
     switch (CW) {
@@ -712,9 +717,20 @@ hipError_t sy_init(nrg_ctx* c) {
     return hipGetLastError();
 }
 
-hipError_t sy_replay_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 resp_hi, u64* d_resp, uint8_t* d_some) {
+hipError_t sy_replay_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 resp_hi, u64* d_resp, uint8_t* d_some,
+                           const nrg_synth_op* src) {
     if (n == 0) return hipSuccess;
-    if (c->d_sy_aux) return sy_bucket_chunk(c, lo, n, resp_lo, resp_hi, d_resp, d_some);
+    if (c->d_sy_aux) return sy_bucket_chunk(c, lo, n, resp_lo, resp_hi, d_resp, d_some, src);
+    if (src) {  // the sort path replays from the ring: append the ops first (wrapping)
+        const u64 mask = c->log_size - 1, first = std::min<u64>(n, c->log_size - (lo & mask));
+        nrg_synth_op* ring = (nrg_synth_op*)c->d_ring;
+        hipError_t e = hipMemcpyAsync(ring + (lo & mask), src, first * sizeof(nrg_synth_op), hipMemcpyDeviceToDevice,
+                                      c->stream);
+        if (e == hipSuccess && first < n)
+            e = hipMemcpyAsync(ring, src + first, (n - first) * sizeof(nrg_synth_op), hipMemcpyDeviceToDevice,
+                               c->stream);
+        if (e != hipSuccess) return e;
+    }
     hipStream_t st = c->stream;
     const nrg_config& cf = c->cfg;
     const u32 HW = cf.synth_hot_writes, CW = cf.synth_cold_writes, HR = cf.synth_hot_reads;

@@ -106,6 +106,7 @@ SIGNATURES = {
     "nrg_hashmap_get_async": (C.c_int, [vp, vp, u64, vp, vp]),
     "nrg_hashmap_round_async": (C.c_int, [vp, vp, u64, u32, vp, u64, vp, vp, vp, vp]),
     "nrg_stack_round_async": (C.c_int, [vp, vp, u64, u32, vp, vp]),
+    "nrg_synth_round_async": (C.c_int, [vp, vp, u64, u32, vp, vp]),
     "nrg_hashmap_round_segments_async": (C.c_int, [vp, vp, u32, u64, u64p, C.POINTER(u32), u32, vp, u64, vp, vp,
                                                    vp, vp]),
     "nrg_hashmap_prefill": (C.c_int, [vp, vp, vp, u64]),

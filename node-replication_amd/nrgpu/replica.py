@@ -152,6 +152,11 @@ class DeviceReplica:
         L.check(self._lib.nrg_stack_round_async(self._h, _dptr(d_ops), n, origin, _dptr(d_resp), _dptr(d_some)),
                 "stack_round")
 
+    def sy_round_device(self, d_ops, n: int, origin: int, d_resp=None, d_some=None):
+        """Replica::combine for one synthetic batch on device buffers (nrg_synth_round_async)."""
+        L.check(self._lib.nrg_synth_round_async(self._h, _dptr(d_ops), n, origin, _dptr(d_resp), _dptr(d_some)),
+                "synth_round")
+
     def log_reset(self):
         L.check(self._lib.nrg_log_reset(self._h))
 

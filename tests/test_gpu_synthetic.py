@@ -101,3 +101,24 @@ def test_synth_partial_tiles_mixed(nrg, orc, path):
     for n, seed in ((1, 5), (63, 6), (2049, 7), (4095, 8), (12345, 9)):
         _check_rounds(nrg, orc, dev, os_, 1, n, seed, [0, 2, 9, 31, 63], 5, tweak if n > 1300 else None)
     dev.close()
+
+
+@pytest.mark.parametrize("n,wo,tids", [(20000, 0, [0, 1, 5, 63]), (20000, 30, [3, 7])])
+def test_synth_round_fused(nrg, orc, path, n, wo, tids):
+    """nrg_synth_round_async (append fused into the first replay pass) == the oracle, over
+    several rounds whose ring positions wrap (small log)."""
+    import torch
+
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_SYNTHETIC, 0, max_batch=1 << 15, log_bytes=64 * 65536)
+    os_ = orc.Synthetic()
+    resp = torch.zeros(n, dtype=torch.int64, device="cuda")
+    some = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    for r in range(5):
+        ops = _ops(orc, n, 950 + r, tids, wo)
+        d_ops = torch.from_numpy(ops.view(np.int64).reshape(n, -1).copy()).cuda()
+        dev.sy_round_device(d_ops, n, 1, resp, some)
+        torch.cuda.synchronize()
+        oresp = os_.replay(np.stack([ops["tid"], ops["r1"], ops["r2"], ops["op"]], axis=1))
+        np.testing.assert_array_equal(resp.cpu().numpy().view(np.uint64), oresp)
+        assert np.all(some.cpu().numpy() == 1)
+    np.testing.assert_array_equal(dev.sy_dump(), os_.dump())
