@@ -314,3 +314,60 @@ def test_owner_path_rounds(nrg, orc, monkeypatch):
         np.testing.assert_array_equal(gv.cpu().numpy().view(np.uint64), want[r][0], err_msg=f"round {r} vals")
     dev.sync()
     _check_state(dev, om)
+
+
+def _bucket_rounds(nrg, orc, dev, om, rounds):
+    import torch
+
+    outs, want = [], []
+    for r, keys in enumerate(rounds):
+        W = len(keys)
+        vals = orc.gen_raw(W, 330 + r)
+        R = 5000
+        gk = np.concatenate([orc.gen_uniform(R - len(keys[:500]), 340 + r, 1 << 22), keys[:500]])
+        R = len(gk)
+        d_puts = torch.from_numpy(_puts(keys, vals).view(np.int64).copy()).cuda()
+        d_gk = torch.from_numpy(gk.view(np.int64)).cuda()
+        d_gv = torch.full((R,), -1, dtype=torch.int64, device="cuda")
+        d_gf = torch.full((R,), 7, dtype=torch.uint8, device="cuda")
+        dev.hm_round_device(d_puts, W, 1, d_gk, R, d_gv, d_gf, None, None)
+        outs.append((d_puts, d_gk, d_gv, d_gf))
+        om.replay(keys, vals)
+        want.append(om.get_batch(gk))
+    dev.join()
+    for r, (_, _, gv, gf) in enumerate(outs):
+        np.testing.assert_array_equal(gf.cpu().numpy(), want[r][1], err_msg=f"round {r} found")
+        np.testing.assert_array_equal(gv.cpu().numpy().view(np.uint64), want[r][0], err_msg=f"round {r} vals")
+    assert dev.hm_digest() == om.digest()
+
+
+def test_bucket_election_default_rounds(nrg, orc):
+    """Rounds of >= 250k Puts take the bucket election by default (hm_elect_kernel): pipelined
+    uniform and Zipf rounds with side-slot keys, a stamp round in between (mode switch both
+    ways), against the sequential oracle."""
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=22, max_batch=1 << 19, pipeline=1)
+    dev.use_torch_stream()
+    om = orc.HashMap()
+    dev.hm_prefill_range(1 << 20, 1)
+    om.prefill_range(1 << 20, 1)
+    rounds = [orc.gen_uniform(300_000, 300, 3_000_000), orc.gen_zipf(400_000, 301, 2_000_000, 0.99),
+              orc.gen_uniform(50_000, 302, 3_000_000), orc.gen_uniform(260_000, 303, 1 << 22)]
+    rounds[0] = rounds[0].copy()
+    rounds[0][::997] = EMPTY
+    _bucket_rounds(nrg, orc, dev, om, rounds)
+
+
+def test_bucket_election_part_overflow(nrg, orc, monkeypatch):
+    """2500 keys of a round home into the first 4096 slots of one bucket: the elector's first
+    split (4096-slot parts) overflows its 2048-entry LDS table, and the bucket is redone in
+    2048-slot parts."""
+    monkeypatch.setenv("NRG_ELECT_MIN", "1")
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=20, max_batch=1 << 14, pipeline=1)
+    dev.use_torch_stream()
+    om = orc.HashMap()
+    cand = np.arange(1, 4_000_000, dtype=np.uint64)
+    low = cand[(_mix64(cand) >> np.uint64(44)) < 4096][:2500]
+    assert len(low) == 2500
+    rounds = [np.concatenate([low, low[:600]]), orc.gen_uniform(9000, 310, 50_000),
+              np.concatenate([low[::-1], low[:300]])]
+    _bucket_rounds(nrg, orc, dev, om, rounds)
