@@ -947,9 +947,10 @@ static hipError_t launch(nrg_ctx* c, IndexJob& ij, ApplyJob& aj, ReadJob& rj) {
     // Puts per index thread: a hot key costs one same-address stamp atomic per index block
     // that holds it (same-address atomics serialise), so large (write-heavy) rounds use fewer,
     // bigger blocks (Zipf 0.99 at 50 % writes: 99 us with 1, 79 with 4, 65 with 8; uniform
-    // unchanged); small rounds keep 1 (B1: 36.8 us vs 39.0 with 4). NRG_K1_ITEMS overrides.
+    // unchanged); small rounds use 2 (B1: 36.4 us with 1 or 2, 39.0 with 4; Zipf 0.99 at 10 %
+    // writes: 54.2 with 1, 47.7 with 2, 39.2 with 4). NRG_K1_ITEMS overrides.
     const bool bk = ij.bk_ent != nullptr;  // bucket election: 8 Puts per index thread
-    const u32 k1 = bk ? bk_k1(c, ij.n) : c->k1_items ? c->k1_items : (ij.n >= (1u << 18) ? 8 : 1);
+    const u32 k1 = bk ? bk_k1(c, ij.n) : c->k1_items ? c->k1_items : (ij.n >= (1u << 18) ? 8 : 2);
     const u32 K1 = k1 >= 8 ? 8 : k1 >= 4 ? 4 : (k1 == 2 ? 2 : 1);
     const u32 G = c->gets_per_thread >= 4 ? 4 : (c->gets_per_thread == 2 ? 2 : 1);
     ij.exp = c->exp;
