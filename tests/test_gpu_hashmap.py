@@ -371,3 +371,36 @@ def test_bucket_election_part_overflow(nrg, orc, monkeypatch):
     rounds = [np.concatenate([low, low[:600]]), orc.gen_uniform(9000, 310, 50_000),
               np.concatenate([low[::-1], low[:300]])]
     _bucket_rounds(nrg, orc, dev, om, rounds)
+
+
+def test_b1_full_size_rounds(nrg, orc):
+    """BASELINE configs[1] at full size: 2^26-slot table, prefill [0, 2^23) -> k+1, uniform keys
+    over 10M, rounds of 100k Puts + 900k Gets (stamp election), then an 800k-Put round (the
+    per-GPU replay at 8 GPUs, bucket election) -- every Get response and the final replica
+    digest bit-exact against the sequential oracle."""
+    import torch
+
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=26, max_batch=1 << 20, pipeline=1,
+                            log_bytes=64 * 4 * (1 << 20))
+    dev.use_torch_stream()
+    om = orc.HashMap()
+    dev.hm_prefill_range(1 << 23, 1)
+    om.prefill_range(1 << 23, 1)
+    outs, want = [], []
+    for r, (W, R) in enumerate([(100_000, 900_000), (100_000, 900_000), (800_000, 900_000)]):
+        keys = orc.gen_uniform(W, 0x4E52 + 3 * r, 10_000_000)
+        vals = orc.gen_raw(W, 0x4E52 + 3 * r + 1)
+        gk = orc.gen_uniform(R, 0x4E52 + 3 * r + 2, 10_000_000)
+        d_puts = torch.from_numpy(_puts(keys, vals).view(np.int64).copy()).cuda()
+        d_gk = torch.from_numpy(gk.view(np.int64)).cuda()
+        d_gv = torch.full((R,), -1, dtype=torch.int64, device="cuda")
+        d_gf = torch.full((R,), 7, dtype=torch.uint8, device="cuda")
+        dev.hm_round_device(d_puts, W, 1, d_gk, R, d_gv, d_gf, None, None)
+        outs.append((d_puts, d_gk, d_gv, d_gf))
+        om.replay(keys, vals)
+        want.append(om.get_batch(gk))
+    dev.join()
+    for r, (_, _, gv, gf) in enumerate(outs):
+        np.testing.assert_array_equal(gf.cpu().numpy(), want[r][1], err_msg=f"round {r} found")
+        np.testing.assert_array_equal(gv.cpu().numpy().view(np.uint64), want[r][0], err_msg=f"round {r} vals")
+    assert dev.hm_digest() == om.digest()

@@ -89,3 +89,27 @@ def test_stack_capacity_error(nrg, orc):
     with pytest.raises(nrg.NrgError) as e:
         dev.log_exec()
     assert e.value.code == nrg._lib.NRG_E_CAPACITY
+
+
+def test_stack_bench_size_rounds(nrg, orc):
+    """BASELINE configs[4] at full size: initial 50,000 elements, rounds of 1M ops (50/50), pop
+    responses and final storage bit-exact against the sequential Vec oracle."""
+    import torch
+
+    n = 1_000_000
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_STACK, 0, max_batch=n, stack_capacity=1 << 22,
+                            log_bytes=64 * 4 * n)
+    init = np.arange(50_000, dtype=np.uint32)
+    dev.st_init(init)
+    os_ = orc.Stack(init)
+    resp = torch.zeros(n, dtype=torch.int32, device="cuda")
+    some = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    for r in range(3):
+        vals, ops = orc.gen_stack_ops(n, 0x5AC + r)
+        d_ops = torch.from_numpy(_ops(vals, ops).view(np.int64).copy()).cuda()
+        dev.st_round_device(d_ops, n, 1, resp, some)
+        torch.cuda.synchronize()
+        oresp, osome = os_.replay(vals, ops)
+        np.testing.assert_array_equal(some.cpu().numpy(), osome)
+        np.testing.assert_array_equal(resp.cpu().numpy().view(np.uint32), oresp)
+    np.testing.assert_array_equal(dev.st_dump(), os_.dump())

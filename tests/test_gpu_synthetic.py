@@ -122,3 +122,23 @@ def test_synth_round_fused(nrg, orc, path, n, wo, tids):
         np.testing.assert_array_equal(resp.cpu().numpy().view(np.uint64), oresp)
         assert np.all(some.cpu().numpy() == 1)
     np.testing.assert_array_equal(dev.sy_dump(), os_.dump())
+
+
+def test_synth_bench_size_rounds(nrg, orc):
+    """The bench's synthetic rounds at full size: 1M ReadWrite ops (tid < 64) against the
+    200,000-word storage, every sum and the final storage bit-exact against the oracle."""
+    import torch
+
+    n = 1_000_000
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_SYNTHETIC, 0, max_batch=n, log_bytes=64 * 4 * n)
+    os_ = orc.Synthetic()
+    resp = torch.zeros(n, dtype=torch.int64, device="cuda")
+    some = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    for r in range(2):
+        ops = _ops(orc, n, 970 + r, list(range(64)), 0)
+        d_ops = torch.from_numpy(ops.view(np.int64).reshape(n, -1).copy()).cuda()
+        dev.sy_round_device(d_ops, n, 1, resp, some)
+        torch.cuda.synchronize()
+        oresp = os_.replay(np.stack([ops["tid"], ops["r1"], ops["r2"], ops["op"]], axis=1))
+        np.testing.assert_array_equal(resp.cpu().numpy().view(np.uint64), oresp)
+    np.testing.assert_array_equal(dev.sy_dump(), os_.dump())
