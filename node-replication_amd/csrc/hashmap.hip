@@ -31,7 +31,7 @@ namespace nrg {
 
 typedef u64 u64x2 __attribute__((ext_vector_type(2)));
 
-constexpr int TPB = 256;
+constexpr int TPB = 256;  // B1: 36.6 us/round; 128: 36.4 (noise); 512: 37.6 (profiles/r01_variants/tpb_sweep.txt)
 constexpr u32 SIDE_SLOT = 0xFFFFFFFFu;   // put_slot value of the EMPTY_KEY key (side slot)
 constexpr u32 FULL_SLOT = 0xFFFFFFFEu;   // put_slot value of a Put that found no slot
 
@@ -559,13 +559,17 @@ __global__ __launch_bounds__(TPB) void hm_prefill_range_kernel(Slot* table, u64 
 
 // number of keys = direct inserts (ctl->nkeys) + keys created by replay rounds
 __global__ __launch_bounds__(TPB) void hm_count_kernel(const u64* __restrict__ acc, u64 n, DevCtl* ctl) {
-    __shared__ u64 s_w[4];
+    __shared__ u64 s_w[TPB / 64];
     u64 x = 0;
     for (u64 q = threadIdx.x; q < n; q += TPB) x += acc[q];
     for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
     if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = x;
     __syncthreads();
-    if (threadIdx.x == 0) ctl->nkeys_total = ctl->nkeys + s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    if (threadIdx.x == 0) {
+        u64 t = ctl->nkeys;
+        for (int w = 0; w < TPB / 64; w++) t += s_w[w];
+        ctl->nkeys_total = t;
+    }
 }
 
 __global__ __launch_bounds__(TPB) void hm_dump_kernel(const Slot* __restrict__ table, u64 slots, DevCtl* ctl,
@@ -588,7 +592,7 @@ __global__ __launch_bounds__(TPB) void hm_dump_kernel(const Slot* __restrict__ t
 
 __global__ __launch_bounds__(TPB) void hm_digest_kernel(const Slot* __restrict__ table, u64 slots,
                                                         const DevCtl* ctl, u64* out3) {
-    __shared__ u64 s_c[4], s_s[4], s_x[4];
+    __shared__ u64 s_c[TPB / 64], s_s[TPB / 64], s_x[TPB / 64];
     const u64 gid = blockIdx.x * (u64)TPB + threadIdx.x;
     u64 c = 0, sm = 0, x = 0;
     if (gid == 0 && ctl->sp.created) {
@@ -619,9 +623,12 @@ __global__ __launch_bounds__(TPB) void hm_digest_kernel(const Slot* __restrict__
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        c = s_c[0] + s_c[1] + s_c[2] + s_c[3];
-        sm = s_s[0] + s_s[1] + s_s[2] + s_s[3];
-        x = s_x[0] ^ s_x[1] ^ s_x[2] ^ s_x[3];
+        c = sm = x = 0;
+        for (int v = 0; v < TPB / 64; v++) {
+            c += s_c[v];
+            sm += s_s[v];
+            x ^= s_x[v];
+        }
         atomicAdd(&out3[0], c);
         atomicAdd(&out3[1], sm);
         atomicXor(&out3[2], x);
