@@ -226,8 +226,9 @@ int main(int argc, char** argv) {
         Slot64* t64;
         u64 *keys, *vals;
         unsigned char* fnd;
-        // argv[3]: get = hipMalloc; getuc = uncached (MTYPE UC); getfg = fine-grained
+        // argv[3]: get = hipMalloc; getuc = uncached (MTYPE UC); getfg = fine-grained; getct = contiguous
         if (!strcmp(argv[3], "getuc")) CHK(hipExtMallocWithFlags((void**)&t64, slots * sizeof(Slot64), hipDeviceMallocUncached));
+        else if (!strcmp(argv[3], "getct")) CHK(hipExtMallocWithFlags((void**)&t64, slots * sizeof(Slot64), hipDeviceMallocContiguous));
         else if (!strcmp(argv[3], "getfg")) CHK(hipExtMallocWithFlags((void**)&t64, slots * sizeof(Slot64), hipDeviceMallocFinegrained));
         else CHK(hipMalloc(&t64, slots * sizeof(Slot64)));
         printf("table allocation: %s\n", argv[3]);
