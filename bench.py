@@ -77,13 +77,45 @@ def cpu_budget(n_affinity: int) -> int:
     return max(1, n)
 
 
-def cpu_baseline(seconds: float, write_ratio: int, key_space: int, prefill: int):
-    """C++ restatement of nr (flat combining + shared log + per-replica RwLock) timed on this
-    host's cores, one Replica per NUMA node (oracle/nr_cpu.cpp)."""
+def host_topology():
+    """nproc, physical cores, SMT state and NUMA node count of this host (BASELINE.md §2;
+    the reference's harness records its topology the same way, benches/mkbench.rs:592-604)."""
+    cores = set()
+    base = "/sys/devices/system/cpu"
+    try:
+        for d in os.listdir(base):
+            if d.startswith("cpu") and d[3:].isdigit():
+                try:
+                    with open(os.path.join(base, d, "topology", "core_id")) as f:
+                        core = f.read().strip()
+                    with open(os.path.join(base, d, "topology", "physical_package_id")) as f:
+                        pkg = f.read().strip()
+                    cores.add((pkg, core))
+                except OSError:
+                    pass
+    except OSError:
+        pass
+    smt = None
+    try:
+        with open(os.path.join(base, "smt", "active")) as f:
+            smt = f.read().strip() == "1"
+    except OSError:
+        pass
+    try:
+        numa = len([d for d in os.listdir("/sys/devices/system/node") if d.startswith("node") and d[4:].isdigit()])
+    except OSError:
+        numa = None
+    return {"nproc": os.cpu_count(), "physical_cores": len(cores) or None, "smt": smt, "numa_nodes": numa,
+            "cpus_allowed": len(os.sched_getaffinity(0)), "cpu_budget": cpu_budget(len(os.sched_getaffinity(0)))}
+
+
+def _nr_cpu_run(seconds, write_ratio, key_space, prefill, threads=None):
+    """One run of the C++ restatement of nr (flat combining + shared log + per-replica RwLock),
+    one Replica per NUMA node over the threads used (oracle/nr_cpu.cpp)."""
     import oracle
 
     cpus = sorted(os.sched_getaffinity(0))
-    budget = cpu_budget(len(cpus))
+    budget = cpu_budget(len(cpus)) if threads is None else threads
     nodes = numa_groups(cpus)
     # spread the thread budget evenly over the NUMA nodes (lowest-numbered CPUs of each node are
     # physical cores; their SMT siblings come later), one Replica per node
@@ -94,7 +126,15 @@ def cpu_baseline(seconds: float, write_ratio: int, key_space: int, prefill: int)
         cpu_list += g
         rep += [r] * len(g)
     res = oracle.nr_hashmap_bench(cpu_list, rep, seconds, write_ratio, key_space, prefill, 2_500_000, 0xC0FFEE)
-    return {
+    return res, cpu_list, groups
+
+
+def cpu_baseline(seconds: float, write_ratio: int, key_space: int, prefill: int):
+    """The B1 stream through the C++ restatement of nr on this host's cores (the reported
+    baseline), plus BASELINE configs[0] as the reference defines it (5M keys, prefill 2^22,
+    5 s, benches/hashmap.rs:30-48) and a 1-thread point."""
+    res, cpu_list, groups = _nr_cpu_run(seconds, write_ratio, key_space, prefill)
+    out = {
         "value": round(res.ops / res.seconds / 1e6, 3),
         "unit": "Mops/s",
         "cores": len(cpu_list),
@@ -103,7 +143,17 @@ def cpu_baseline(seconds: float, write_ratio: int, key_space: int, prefill: int)
                    f"[0,{prefill}), {write_ratio}% writes, 2.5M-op per-thread shuffles, 128 ops per clock check) "
                    f"through the C++ restatement of nr on {len(cpu_list)} threads, {len(groups)} replica(s) "
                    f"(one per NUMA node); {res.ops} ops"),
+        "host": host_topology(),
     }
+    c0, c0_cpus, c0_groups = _nr_cpu_run(5.0, 10, 5_000_000, 1 << 22)
+    out["configs0"] = {"value": round(c0.ops / c0.seconds / 1e6, 3), "unit": "Mops/s", "cores": len(c0_cpus),
+                       "replicas": len(c0_groups),
+                       "sample": "BASELINE configs[0]: 5M keys, prefill [0,2^22), uniform, 10% writes, %.1f s" %
+                                 c0.seconds}
+    t1, _, _ = _nr_cpu_run(5.0, write_ratio, key_space, prefill, threads=1)
+    out["one_thread"] = {"value": round(t1.ops / t1.seconds / 1e6, 3), "unit": "Mops/s", "cores": 1,
+                         "sample": "the B1 stream on 1 thread, 1 replica, %.1f s" % t1.seconds}
+    return out
 
 
 def traffic_key(args):
@@ -285,8 +335,15 @@ def run_hashmap(args, env):
     else:
         u_w = u_w_local
 
-    group = None
-    if world > 1:
+    group = cgroup = None
+    if world > 1 and args.backend == "nccl":
+        # the C ABI's replica group: RCCL all-gather on a library-owned stream, replay on ours
+        from nrgpu.parallel import ReplicaGroup
+
+        cgroup = ReplicaGroup(rep, rank, world)
+        inputs = torch.cuda.Stream(dev_t)  # inputs exist before the timed region: gathers run ahead
+        cgroup.set_input_stream(inputs.cuda_stream)
+    elif world > 1:
         from nrgpu.parallel import ReplicatedHashMap
 
         group = ReplicatedHashMap(rep, device=dev_t)
@@ -302,7 +359,10 @@ def run_hashmap(args, env):
     def step(i):
         p = i % P
         prev = mode["prev"]
-        if group is None:
+        if cgroup is not None:
+            pp, gp = ptrs[p]
+            cgroup.round_async(pp, W, pv_p if prev else None, pf_p if prev else None, gp, R, gv_p, gf_p)
+        elif group is None:
             pp, gp = ptrs[p]
             rc = round_fn(h, pp, W, rank + 1, gp, R, gv_p, gf_p, pv_p if prev else None, pf_p if prev else None)
             if rc:
@@ -363,7 +423,8 @@ def run_hashmap(args, env):
                      "= %d Put + %d Get%s" % (
                          args.log2_slots, dist_txt, args.prefill, args.ops_per_gpu, W, R,
                          "; write segments all-gathered (%s), every replica replays all %d Puts" % (
-                             "RCCL over xGMI" if args.backend == "nccl" else "gloo rehearsal", Wg)
+                             "RCCL over xGMI from libnrgpu.so's replica group" if args.backend == "nccl"
+                             else "gloo rehearsal", Wg)
                          if world > 1 else "")),
         "baseline_config": "configs[1] (B1)" if (world == 1 and args.write_ratio == 10 and args.dist == "uniform")
         else ("configs[2] (B8 weak scaling)" if args.dist == "uniform" else "configs[3] (Z)"),
@@ -459,8 +520,14 @@ def run_synthetic(args, env):
     resp = torch.empty(N, dtype=torch.int64, device=dev_t)
     some = torch.empty(N, dtype=torch.uint8, device=dev_t)
     torch.cuda.synchronize()
-    group = None
-    if world > 1:
+    group = cgroup = None
+    if world > 1 and args.backend == "nccl":
+        from nrgpu.parallel import ReplicaGroup
+
+        cgroup = ReplicaGroup(rep, rank, world)
+        inputs = torch.cuda.Stream(dev_t)
+        cgroup.set_input_stream(inputs.cuda_stream)
+    elif world > 1:
         from nrgpu.parallel import ReplicatedLog
 
         group = ReplicatedLog(rep, device=dev_t)
@@ -472,7 +539,9 @@ def run_synthetic(args, env):
 
     def step(i):
         p = i % P
-        if group is None:
+        if cgroup is not None:
+            cgroup.round_async(ptrs[p], N, r_p, s_p)
+        elif group is None:
             # Replica::combine of the batch: Log::append fused into the partition pass
             rc = round_fn(h, ptrs[p], N, rank + 1, r_p, s_p)
             if rc:
@@ -549,8 +618,14 @@ def run_stack(args, env):
         S += int(torch.unique(d_before[push == 1]).numel())
     S = S / min(P, 4) * world
 
-    group = None
-    if world > 1:
+    group = cgroup = None
+    if world > 1 and args.backend == "nccl":
+        from nrgpu.parallel import ReplicaGroup
+
+        cgroup = ReplicaGroup(rep, rank, world)
+        inputs = torch.cuda.Stream(dev_t)
+        cgroup.set_input_stream(inputs.cuda_stream)
+    elif world > 1:
         from nrgpu.parallel import ReplicatedLog
 
         group = ReplicatedLog(rep, device=dev_t)
@@ -562,7 +637,9 @@ def run_stack(args, env):
 
     def step(i):
         p = i % P
-        if group is None:
+        if cgroup is not None:
+            cgroup.round_async(ptrs[p], N, r_p, s_p)
+        elif group is None:
             # Replica::combine of the batch: Log::append fused into the replay pass
             rc = round_fn(h, ptrs[p], N, rank + 1, r_p, s_p)
             if rc:
@@ -650,11 +727,15 @@ def main():
                     help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo: CPU rehearsal)")
     ap.add_argument("--share-gpu", action="store_true", help="all ranks on cuda:0 (gloo rehearsal on a 1-GPU box)")
     ap.add_argument("--csv", default=None, help="append scaleout_benchmarks.csv rows (reference format)")
-    ap.add_argument("--timing-every", type=int, default=8, help="event-stamp every n-th launch of the timed kernel")
+    ap.add_argument("--timing-every", type=int, default=0,
+                    help="event-stamp every n-th launch of the timed kernel (0: max(1, min(8, steps // 10)), "
+                         "so the roofline averages >= 10 launches)")
     ap.add_argument("--pipeline", type=int, default=1,
                     help="1: a round's apply+reads ride in the next round's launch (nrg_config.pipeline); "
                          "0: every round call completes its own reads")
     args = ap.parse_args()
+    if args.timing_every <= 0:
+        args.timing_every = max(1, min(8, args.steps // 10))
     env = Env(args)
     runner = {"stack": run_stack, "synthetic": run_synthetic}.get(args.workload, run_hashmap)
     res = runner(args, env)

@@ -20,6 +20,8 @@
  *   nrg_hashmap_dump / digest     Replica::verify(closure)           nr/src/replica.rs:443-467
  *   nrg_stack_*                   Stack Dispatch                     benches/stack.rs:36-84, nr/tests/stack.rs:31-96
  *   nrg_synth_*                   AbstractDataStructure Dispatch     benches/synthetic.rs:60-195
+ *   nrg_group_*                   the shared Log across NUMA nodes   nr/src/log.rs:494-511 (every replica
+ *                                 (RCCL all-gather of write segments) replays every entry), :473-524
  *
  * Conventions
  *   - Every function returns NRG_OK (0) or a negative NRG_E_* code. Nothing throws or aborts.
@@ -258,6 +260,60 @@ int nrg_synth_round_async(nrg_ctx* ctx, const nrg_synth_op* d_ops, uint64_t n, u
 int nrg_synth_read(nrg_ctx* ctx, const nrg_synth_rd* ops, uint64_t n, uint64_t* sums);
 int nrg_synth_read_async(nrg_ctx* ctx, const nrg_synth_rd* d_ops, uint64_t n, uint64_t* d_sums);
 int nrg_synth_dump(nrg_ctx* ctx, uint64_t* words, uint64_t cap, uint64_t* n);
+
+/* ---- multi-GPU replica groups (RCCL over xGMI) --------------------------------------------
+ * The reference shares ONE log between replicas through cache-coherent memory: every replica's
+ * Log::exec reads every entry (nr/src/log.rs:494-511, :473-524). Across GPUs the write segments
+ * of a round are all-gathered with RCCL (ncclAllGather, one communicator per GPU, over xGMI)
+ * and every replica replays the identical global log W_0 || W_1 || ... || W_{n-1} (rank order);
+ * reads stay on their GPU; write responses go to the origin replica only
+ * (nr/src/replica.rs:576-578). The all-gather runs on a library-owned stream per GPU and the
+ * gathered buffers rotate, so the all-gather of round e+1 overlaps the replay of round e.
+ * RCCL is loaded at the first group call (librccl.so.1, the process's own copy if one is
+ * already loaded); without it these calls return NRG_E_COMM. */
+#define NRG_E_COMM (-9)          /* RCCL unavailable or a collective failed               */
+#define NRG_GROUP_ID_BYTES 128   /* ncclUniqueId                                           */
+
+typedef struct nrg_group nrg_group;
+
+/* A group member's part of one round (all pointers are device pointers on its GPU). */
+typedef struct {
+    const void* recs;          /* this replica's write segment (log records, issue order)       */
+    uint64_t n;                /* records in it                                                  */
+    void* resp;                /* nullable: responses to its own writes (as nrg_log_exec_async)  */
+    uint8_t* some;
+    const uint64_t* get_keys;  /* hashmap: reads answered against the post-round state          */
+    uint64_t n_gets;
+    uint64_t* get_vals;
+    uint8_t* get_found;
+} nrg_round;
+
+/* ncclGetUniqueId: one process creates the id and ships it to the others (any side channel). */
+int nrg_group_unique_id(uint8_t id[NRG_GROUP_ID_BYTES]);
+/* One process per GPU: `replica` joins group `id` as rank `rank` of `nranks` (ncclCommInitRank
+ * on the replica's device). Replica ids should be rank + 1 (Log::register order). */
+int nrg_group_join(nrg_ctx* replica, const uint8_t id[NRG_GROUP_ID_BYTES], int nranks, int rank,
+                   nrg_group** out);
+/* One process driving n GPUs: opens one replica per device (cfg, replica_id = i + 1) and one
+ * communicator per device (ncclCommInitAll). The group owns these replicas. */
+int nrg_group_open(const int* devices, int n, const nrg_config* cfg, nrg_group** out);
+/* Closes the communicators and the group's buffers (and the replicas nrg_group_open opened). */
+int nrg_group_close(nrg_group* g);
+/* nranks: group size; nlocal: members driven by this process; rank0: rank of local member 0. */
+int nrg_group_info(const nrg_group* g, int* nranks, int* nlocal, int* rank0);
+nrg_ctx* nrg_group_replica(nrg_group* g, int member);
+/* The all-gather of a member's segment waits for work queued on `hip_stream` when the round is
+ * issued (default: the replica's own stream, which also orders it after the previous replay;
+ * give the stream the inputs are produced on to let all-gathers run ahead of replays). */
+int nrg_group_set_input_stream(nrg_group* g, int member, void* hip_stream);
+/* One NR round on every local member: all-gather of the members' write segments (RCCL), then on
+ * each replica Log::append of the gathered segments in rank order + Log::exec + its reads.
+ * `seg_lens[r]` = rank r's segment length (NULL: every rank has rounds[0].n records; a
+ * single-process group takes its members' n). Stream ordered; borrows buffers until the
+ * replica stream passes this round (config.pipeline = 1: until nrg_join / the next call). */
+int nrg_group_round_async(nrg_group* g, const nrg_round* rounds, const uint64_t* seg_lens);
+/* Wait for all queued group work and report latched device errors of every local replica. */
+int nrg_group_sync(nrg_group* g);
 
 /* ---- device memory helpers (for callers without their own allocator) ----------------- */
 int nrg_dev_alloc(nrg_ctx* ctx, uint64_t bytes, void** d_ptr);

@@ -18,10 +18,13 @@ constexpr u64 EMPTY_KEY = ~0ull;
 constexpr u32 ERR_TABLE_FULL = 1u;
 constexpr u32 ERR_CAPACITY = 4u;
 
-// Counters of keys created by replay rounds (index blocks add to slot blk % HM_CREATED_SLOTS).
+// Counters of keys created by replay rounds (elector blocks add to slot blk % HM_CREATED_SLOTS).
 constexpr u64 HM_CREATED_SLOTS = 8192;
-// Slot buckets of the bucket election (hashmap.hip hm_elect_kernel): at most this many.
+// Slot buckets of a replay round (hashmap.hip hm_elect_kernel): at most this many.
 constexpr u32 HM_BK_MAX = 1024;
+// Largest hashmap replay chunk: keeps the elector's per-tile LDS tables (one u32 + one u16
+// per index tile of >= 1024 Puts) and 16-bit tile offsets within bounds.
+constexpr u64 HM_MAX_BATCH = 1ull << 23;
 
 // splitmix64 finaliser — identical constants to oracle/nr_oracle.c (orc_mix64) so that
 // device-generated workloads are reproducible by the CPU oracle.
@@ -38,42 +41,36 @@ __device__ __forceinline__ u64 mulhi64(u64 a, u64 b) { return __umul64hi(a, b); 
 // Home slot of a key: top bits of the mixed key.
 __device__ __forceinline__ u64 table_home(u64 key, u32 shift) { return mix64(key) >> shift; }
 
-// 64-byte table slot, two per 128-B line. A random read costs one 128-B line at the memory
-// side whatever its width (TCC_EA0_RDREQ_128B = 1 per lookup, profiles/r01_rdreq_size.txt),
-// so the replay's bookkeeping rides in the same line as key and value:
-//   stamp of parity p  last writer of the key in the most recent round of epoch parity p:
-//             epoch << 32 | 1 + offset in that round (raised with atomicMax). Two words so a
-//             round's index pass (parity e&1) can run while the previous round's apply and
-//             reads (parity (e-1)&1) are still in flight.
-//   created   epoch of the round that inserted the key (0 while a claim is in progress).
-// Layout: a read needs {key, val} and {created, stamp of its parity}; `created` sits between
-// the two stamps so that both pairs are one 16-B load (bytes 16-31 or 24-39).
-struct __attribute__((aligned(64))) Slot {
-    u64 key;     // EMPTY_KEY when free
+// 16-byte table slot {key, value}, eight per 128-B line: 2^26 slots = 1 GiB. Nothing else lives
+// in the table: a replay round never writes a slot while the same launch reads it (hashmap.hip:
+// the index pass only reads, the elector launch claims keys and stores values), so no epochs,
+// stamps or creation marks are needed, and the footprint a random Get ranges over is 4x smaller
+// than with the 64-B slots of the first design (1 GiB vs 4 GiB: 23.8 vs 27.5 us per 1M Gets,
+// profiles/r01_get_footprint.txt).
+struct __attribute__((aligned(16))) Slot {
+    u64 key;  // EMPTY_KEY when free
     u64 val;
-    u64 stamp1;  // odd epochs
-    u32 created;
-    u32 pad;
-    u64 stamp0;  // even epochs
-    u64 pad2[3];
 };
-__host__ __device__ __forceinline__ u64* slot_stamp(Slot* s, u32 par) { return par ? &s->stamp1 : &s->stamp0; }
-__host__ __device__ __forceinline__ const u64* slot_stamp(const Slot* s, u32 par) {
-    return par ? &s->stamp1 : &s->stamp0;
-}
 
 // One replica-wide control block in HBM.
 struct __attribute__((aligned(64))) DevCtl {
     u32 err;          // latched ERR_* bits
-    u32 pad0;
+    u32 sp_present;   // hashmap: the key EMPTY_KEY is present (its value is sp_val)
     u64 nkeys;        // hashmap: keys inserted directly (prefill)
     long long depth;  // stack: current length
     u64 counter;      // scratch counter (dump compaction)
     u64 nkeys_total;  // hashmap: nkeys + keys created by replay rounds (hm_count)
     long long depth0;      // stack: length before the chunk being replayed
     long long depth_next;  // stack: length after it (st_commit_kernel moves it to depth)
-    u64 pad1;
-    Slot sp;          // side slot for key == EMPTY_KEY (present iff sp.created != 0)
+    u64 sp_val;       // hashmap: value of the key EMPTY_KEY (side slot)
+    u64 sp_st[3];     // hashmap overlay rounds: last writer (i+1) of EMPTY_KEY, per overlay
+};
+
+// Overlay slot (hashmap.hip overlay rounds): a key written by the round and the largest i+1
+// among its Puts (the round's last writer of the key, raised with atomicMax).
+struct __attribute__((aligned(16))) OvSlot {
+    u64 key;  // EMPTY_KEY when free
+    u64 st;   // i + 1 of the last writer
 };
 
 __device__ __forceinline__ u64 ld_relaxed(const u64* p) {

@@ -1,0 +1,355 @@
+// group.cpp — multi-GPU replica groups: the write segments of a round are all-gathered with RCCL
+// over xGMI and every replica replays the identical global log (include/nrgpu.h, nrg_group_*).
+//
+// Reference: the shared Log of nr/src/log.rs, read by every replica's exec loop
+// (nr/src/log.rs:494-511, :473-524) through cache-coherent memory. Here each GPU keeps its own
+// copy of the log; one ncclAllGather per round moves the new entries to every copy, in rank
+// order, which is the round's deterministic global log order.
+//
+// Per member and round e (b = e % NBUF):
+//   comm stream : wait(input ready) -> wait(freed[b]) -> [pad copy] -> ncclAllGather -> gathered[b]
+//   replica     : wait(gathered[b]) -> Log::append + Log::exec + reads (replay kernels) -> freed[b]
+// The comm stream never waits for a replay except through freed[b] (NBUF rounds back), so the
+// all-gather of round e+1 runs while round e replays.
+//
+// RCCL is resolved with dlopen at the first group call: the process's own librccl.so.1 when one
+// is already loaded (torch ships one), else the system's. libnrgpu.so itself does not link it.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "internal.hpp"
+
+namespace {
+
+struct Rccl {
+    decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+    decltype(&ncclCommInitRank) init_rank = nullptr;
+    decltype(&ncclCommInitAll) init_all = nullptr;
+    decltype(&ncclAllGather) all_gather = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclCommDestroy) destroy = nullptr;
+};
+
+std::mutex g_rccl_mu;
+bool g_rccl_tried = false;
+Rccl g_rccl;
+bool g_rccl_ok = false;
+
+const Rccl* rccl() {
+    std::lock_guard<std::mutex> lk(g_rccl_mu);
+    if (!g_rccl_tried) {
+        g_rccl_tried = true;
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+        if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (h) {
+            Rccl r;
+            r.get_unique_id = (decltype(r.get_unique_id))dlsym(h, "ncclGetUniqueId");
+            r.init_rank = (decltype(r.init_rank))dlsym(h, "ncclCommInitRank");
+            r.init_all = (decltype(r.init_all))dlsym(h, "ncclCommInitAll");
+            r.all_gather = (decltype(r.all_gather))dlsym(h, "ncclAllGather");
+            r.group_start = (decltype(r.group_start))dlsym(h, "ncclGroupStart");
+            r.group_end = (decltype(r.group_end))dlsym(h, "ncclGroupEnd");
+            r.destroy = (decltype(r.destroy))dlsym(h, "ncclCommDestroy");
+            g_rccl_ok = r.get_unique_id && r.init_rank && r.init_all && r.all_gather && r.group_start &&
+                        r.group_end && r.destroy;
+            if (g_rccl_ok) g_rccl = r;
+        }
+    }
+    return g_rccl_ok ? &g_rccl : nullptr;
+}
+
+constexpr int NBUF = 3;  // gathered-log buffers in rotation per member
+
+struct Member {
+    nrg_ctx* ctx = nullptr;
+    int rank = 0;
+    ncclComm_t comm = nullptr;
+    hipStream_t cstream = nullptr;  // library-owned: pad copies + all-gathers
+    hipStream_t in_stream = nullptr;
+    bool in_set = false;
+    hipEvent_t in_ev = nullptr;
+    void* gbuf[NBUF] = {};
+    uint64_t gbytes[NBUF] = {};
+    hipEvent_t gathered[NBUF] = {};
+    hipEvent_t freed[NBUF] = {};
+    bool used[NBUF] = {};
+    void* sbuf = nullptr;  // padded send copy when a segment is shorter than the stride
+    uint64_t sbytes = 0;
+};
+
+int hip_rc(hipError_t e) { return e == hipSuccess ? NRG_OK : (e == hipErrorOutOfMemory ? NRG_E_NOMEM : NRG_E_HIP); }
+
+#define GCHK(x)                          \
+    do {                                 \
+        hipError_t _e = (x);             \
+        if (_e != hipSuccess) return hip_rc(_e); \
+    } while (0)
+
+int member_init(Member& m) {
+    int r = nrg::ctx_use_device(m.ctx);
+    if (r) return r;
+    GCHK(hipStreamCreateWithFlags(&m.cstream, hipStreamNonBlocking));
+    GCHK(hipEventCreateWithFlags(&m.in_ev, hipEventDisableTiming));
+    for (int b = 0; b < NBUF; b++) {
+        GCHK(hipEventCreateWithFlags(&m.gathered[b], hipEventDisableTiming));
+        GCHK(hipEventCreateWithFlags(&m.freed[b], hipEventDisableTiming));
+    }
+    return NRG_OK;
+}
+
+void member_free(Member& m, const Rccl* R) {
+    if (!m.ctx) return;
+    (void)nrg::ctx_use_device(m.ctx);
+    if (m.cstream) (void)hipStreamSynchronize(m.cstream);
+    if (m.comm && R) R->destroy(m.comm);
+    for (int b = 0; b < NBUF; b++) {
+        if (m.gbuf[b]) (void)hipFree(m.gbuf[b]);
+        if (m.gathered[b]) (void)hipEventDestroy(m.gathered[b]);
+        if (m.freed[b]) (void)hipEventDestroy(m.freed[b]);
+    }
+    if (m.sbuf) (void)hipFree(m.sbuf);
+    if (m.in_ev) (void)hipEventDestroy(m.in_ev);
+    if (m.cstream) (void)hipStreamDestroy(m.cstream);
+    m = Member{};
+}
+
+}  // namespace
+
+struct nrg_group {
+    int nranks = 0;
+    int rank0 = 0;
+    bool owns = false;  // replicas opened by nrg_group_open
+    std::vector<Member> m;
+    uint64_t round = 0;
+};
+
+extern "C" {
+
+int nrg_group_unique_id(uint8_t id[NRG_GROUP_ID_BYTES]) {
+    if (!id) return NRG_E_INVAL;
+    const Rccl* R = rccl();
+    if (!R) return NRG_E_COMM;
+    ncclUniqueId u;
+    if (R->get_unique_id(&u) != ncclSuccess) return NRG_E_COMM;
+    static_assert(sizeof(u) == NRG_GROUP_ID_BYTES, "ncclUniqueId size");
+    std::memcpy(id, &u, NRG_GROUP_ID_BYTES);
+    return NRG_OK;
+}
+
+int nrg_group_join(nrg_ctx* replica, const uint8_t id[NRG_GROUP_ID_BYTES], int nranks, int rank, nrg_group** out) {
+    if (!replica || !id || !out || nranks < 1 || rank < 0 || rank >= nranks || nranks > 64) return NRG_E_INVAL;
+    *out = nullptr;
+    const Rccl* R = rccl();
+    if (!R) return NRG_E_COMM;
+    nrg_group* g = new (std::nothrow) nrg_group();
+    if (!g) return NRG_E_NOMEM;
+    g->nranks = nranks;
+    g->rank0 = rank;
+    g->m.resize(1);
+    Member& m = g->m[0];
+    m.ctx = replica;
+    m.rank = rank;
+    int r = member_init(m);
+    ncclUniqueId u;
+    std::memcpy(&u, id, NRG_GROUP_ID_BYTES);
+    if (r == NRG_OK && R->init_rank(&m.comm, nranks, u, rank) != ncclSuccess) r = NRG_E_COMM;
+    if (r != NRG_OK) {
+        member_free(m, R);
+        delete g;
+        return r;
+    }
+    *out = g;
+    return NRG_OK;
+}
+
+int nrg_group_open(const int* devices, int n, const nrg_config* cfg, nrg_group** out) {
+    if (!devices || n < 1 || n > 64 || !cfg || !out) return NRG_E_INVAL;
+    *out = nullptr;
+    const Rccl* R = rccl();
+    if (!R) return NRG_E_COMM;
+    nrg_group* g = new (std::nothrow) nrg_group();
+    if (!g) return NRG_E_NOMEM;
+    g->nranks = n;
+    g->rank0 = 0;
+    g->owns = true;
+    g->m.resize(n);
+    int r = NRG_OK;
+    for (int i = 0; i < n && r == NRG_OK; i++) {
+        nrg_config c = *cfg;
+        c.replica_id = (uint32_t)i + 1;  // Log::register hands out ids from 1 (nr/src/log.rs:272-292)
+        r = nrg_open(devices[i], &c, &g->m[i].ctx);
+        g->m[i].rank = i;
+        if (r == NRG_OK) r = member_init(g->m[i]);
+    }
+    if (r == NRG_OK) {
+        std::vector<ncclComm_t> comms(n);
+        if (R->init_all(comms.data(), n, devices) != ncclSuccess) r = NRG_E_COMM;
+        else
+            for (int i = 0; i < n; i++) g->m[i].comm = comms[i];
+    }
+    if (r != NRG_OK) {
+        nrg_group_close(g);
+        return r;
+    }
+    *out = g;
+    return NRG_OK;
+}
+
+int nrg_group_close(nrg_group* g) {
+    if (!g) return NRG_E_INVAL;
+    const Rccl* R = rccl();
+    for (Member& m : g->m) {
+        nrg_ctx* c = m.ctx;
+        member_free(m, R);
+        if (g->owns && c) nrg_close(c);
+    }
+    delete g;
+    return NRG_OK;
+}
+
+int nrg_group_info(const nrg_group* g, int* nranks, int* nlocal, int* rank0) {
+    if (!g) return NRG_E_INVAL;
+    if (nranks) *nranks = g->nranks;
+    if (nlocal) *nlocal = (int)g->m.size();
+    if (rank0) *rank0 = g->rank0;
+    return NRG_OK;
+}
+
+nrg_ctx* nrg_group_replica(nrg_group* g, int member) {
+    if (!g || member < 0 || member >= (int)g->m.size()) return nullptr;
+    return g->m[member].ctx;
+}
+
+int nrg_group_set_input_stream(nrg_group* g, int member, void* s) {
+    if (!g || member < 0 || member >= (int)g->m.size()) return NRG_E_INVAL;
+    g->m[member].in_stream = (hipStream_t)s;
+    g->m[member].in_set = true;
+    return NRG_OK;
+}
+
+int nrg_group_round_async(nrg_group* g, const nrg_round* rounds, const uint64_t* seg_lens) {
+    if (!g || !rounds) return NRG_E_INVAL;
+    const Rccl* R = rccl();
+    if (!R) return NRG_E_COMM;
+    const int nl = (int)g->m.size();
+    const uint32_t kind = g->m[0].ctx->cfg.ds_kind;
+    const uint64_t rb = g->m[0].ctx->rec_bytes;
+    // every rank's segment length, in rank order
+    std::vector<uint64_t> lens(g->nranks);
+    for (int r = 0; r < g->nranks; r++) {
+        if (seg_lens) lens[r] = seg_lens[r];
+        else if (nl == g->nranks) lens[r] = rounds[r].n;
+        else lens[r] = rounds[0].n;
+    }
+    uint64_t stride = 0;
+    for (uint64_t l : lens) stride = l > stride ? l : stride;
+    for (int i = 0; i < nl; i++) {
+        const nrg_round& x = rounds[i];
+        if (g->m[i].ctx->cfg.ds_kind != kind || x.n != lens[g->m[i].rank] || (x.n && !x.recs)) return NRG_E_INVAL;
+    }
+    std::vector<uint32_t> origins(g->nranks);
+    for (int r = 0; r < g->nranks; r++) origins[r] = (uint32_t)r + 1;
+    const int b = (int)(g->round % NBUF);
+    const uint64_t seg_bytes = stride * rb;
+    std::vector<const void*> send(nl);
+    if (stride) {
+        for (int i = 0; i < nl; i++) {
+            Member& m = g->m[i];
+            const nrg_round& x = rounds[i];
+            int r = nrg::ctx_use_device(m.ctx);
+            if (r) return r;
+            // the all-gather reads the caller's segment: ordered after its producer
+            GCHK(hipEventRecord(m.in_ev, m.in_set ? m.in_stream : m.ctx->stream));
+            GCHK(hipStreamWaitEvent(m.cstream, m.in_ev, 0));
+            // and it overwrites gathered buffer b: ordered after the replay that read it
+            if (m.used[b]) GCHK(hipStreamWaitEvent(m.cstream, m.freed[b], 0));
+            const uint64_t need = (uint64_t)g->nranks * seg_bytes;
+            if (m.gbytes[b] < need) {
+                GCHK(hipStreamSynchronize(m.cstream));
+                if (m.gbuf[b]) GCHK(hipFree(m.gbuf[b]));
+                m.gbuf[b] = nullptr;
+                m.gbytes[b] = 0;
+                GCHK(hipMalloc(&m.gbuf[b], need));
+                m.gbytes[b] = need;
+            }
+            if (x.n == stride) {
+                send[i] = x.recs;
+            } else {  // pad a short segment to the common stride
+                if (m.sbytes < seg_bytes) {
+                    GCHK(hipStreamSynchronize(m.cstream));
+                    if (m.sbuf) GCHK(hipFree(m.sbuf));
+                    m.sbuf = nullptr;
+                    m.sbytes = 0;
+                    GCHK(hipMalloc(&m.sbuf, seg_bytes));
+                    m.sbytes = seg_bytes;
+                }
+                if (x.n) GCHK(hipMemcpyAsync(m.sbuf, x.recs, x.n * rb, hipMemcpyDeviceToDevice, m.cstream));
+                GCHK(hipMemsetAsync((char*)m.sbuf + x.n * rb, 0, seg_bytes - x.n * rb, m.cstream));
+                send[i] = m.sbuf;
+            }
+        }
+        if (R->group_start() != ncclSuccess) return NRG_E_COMM;
+        ncclResult_t res = ncclSuccess;
+        for (int i = 0; i < nl && res == ncclSuccess; i++) {
+            Member& m = g->m[i];
+            res = R->all_gather(send[i], m.gbuf[b], seg_bytes / 8, ncclUint64, m.comm, m.cstream);
+        }
+        if (R->group_end() != ncclSuccess || res != ncclSuccess) return NRG_E_COMM;
+    }
+    for (int i = 0; i < nl; i++) {
+        Member& m = g->m[i];
+        const nrg_round& x = rounds[i];
+        nrg_ctx* c = m.ctx;
+        int r = nrg::ctx_use_device(c);
+        if (r) return r;
+        if (stride) {
+            GCHK(hipEventRecord(m.gathered[b], m.cstream));
+            GCHK(hipStreamWaitEvent(c->stream, m.gathered[b], 0));
+        }
+        if (kind == NRG_DS_HASHMAP) {
+            if (stride)
+                r = nrg_hashmap_round_segments_async(c, (const nrg_put*)m.gbuf[b], (uint32_t)g->nranks, stride,
+                                                     lens.data(), origins.data(), (uint32_t)m.rank, x.get_keys,
+                                                     x.n_gets, x.get_vals, x.get_found, (uint64_t*)x.resp, x.some);
+            else
+                r = nrg_hashmap_round_async(c, nullptr, 0, origins[m.rank], x.get_keys, x.n_gets, x.get_vals,
+                                            x.get_found, nullptr, nullptr);
+        } else if (stride) {
+            std::vector<uint64_t> firsts(g->nranks);
+            r = nrg_log_append_segments_async(c, m.gbuf[b], (uint32_t)g->nranks, stride, lens.data(), origins.data(),
+                                              firsts.data());
+            if (r == NRG_OK)
+                r = nrg_log_exec_async(c, firsts[m.rank], firsts[m.rank] + lens[m.rank], x.resp, x.some);
+        }
+        if (r) return r;
+        if (stride) {
+            GCHK(hipEventRecord(m.freed[b], c->stream));
+            m.used[b] = true;
+        }
+    }
+    g->round++;
+    return NRG_OK;
+}
+
+int nrg_group_sync(nrg_group* g) {
+    if (!g) return NRG_E_INVAL;
+    int rc = NRG_OK;
+    for (Member& m : g->m) {
+        int r = nrg::ctx_use_device(m.ctx);
+        if (r) return r;
+        GCHK(hipStreamSynchronize(m.cstream));
+        r = nrg_sync(m.ctx);
+        if (r && rc == NRG_OK) rc = r;
+    }
+    return rc;
+}
+
+}  // extern "C"

@@ -4,38 +4,42 @@
 // benches/hashmap.rs:114-119, nr/examples/hashmap.rs:46-50) and the read path
 // Replica::read_only -> dispatch (nr/src/replica.rs:483-497, benches/hashmap.rs:107-111).
 //
-// Table: 2^k open-addressing slots of 64 B (common.hpp), linear probing from
-// mix64(key) >> (64 - k). A replay round covers the log records [lo, lo+n) and gets a fresh
-// epoch e (never reused). Its work splits into two halves:
+// Table: 2^k open-addressing slots of 16 B {key, value} (common.hpp), linear probing from
+// mix64(key) >> (64 - k); the one key equal to the empty marker lives in DevCtl (side slot).
+// A replay round covers the log records [lo, lo+n) and takes two launches:
 //
-//   index(e)   per Put: find the key's slot, or claim an empty one with a 64-bit CAS
-//              (created = e); elect the round's last writer of every key with
-//              atomicMax(slot.stamp[e&1], e<<32 | i+1), pre-combined per block in LDS so a
-//              hot key costs one global atomic per block (Zipf streams). Writes put_slot[i]
-//              and, when the round is appended here, the log copy.
-//   apply(e)   per Put: the elected writer (stamp[e&1] == (e, i+1)) stores its value.
-//   reads(e)   per Get, against the state after round e: a key counts iff 0 < created <= e;
-//              its value is the round's elected record when stamp[e&1] carries epoch e
-//              (apply(e) may still be storing it), else the slot's value.
+//   hm_round_kernel  index(e) on its first blocks, reads(e-1) on the rest. index(e) only READS
+//                    the table: per Put it finds the key's slot, or notes that the key is new
+//                    (id = its home slot), drops Puts that a later Put of the same key in the
+//                    same block overwrites, and writes one 24-B entry {id, i+1, value; key} per
+//                    surviving Put into its tile, grouped by slot bucket and in log order inside
+//                    each bucket. reads(e-1) answer the previous round's Gets from the slots.
+//   hm_elect_kernel  one block per slot bucket gathers the bucket's entries from every tile in
+//                    log order, keeps one LDS hash entry per key (the largest i+1 = the round's
+//                    last writer), claims a slot for every new key (64-bit CAS) and stores each
+//                    key's final value: one plain scattered store per distinct key. With
+//                    previous-value responses wanted (HashMap::insert's return) every Put keeps
+//                    its entry and one wave walks the bucket in log order: a Put's previous
+//                    value is its predecessor's in the bucket walk, or the slot's value before
+//                    the round, or None for a key the round created.
 //
-// All three roles live in ONE kernel (hm_round_kernel, disjoint block ranges), launched as
-// {index(e) | apply(e-1) + reads(e-1)}: the latency-bound index pass of a round overlaps the
-// bandwidth-bound reads of the previous one. This is race-free because index(e) only claims
-// empty slots (invisible to reads(e-1): created is 0 or e) and raises stamp[e&1], while
-// apply(e-1)/reads(e-1) only look at stamp[(e-1)&1] and at values that index never writes.
-// The result equals the sequential replay: last-writer-wins per key in log order, and reads
-// after the round's writes (SURVEY.md §8a round semantics).
+// Why this is the sequential replay: every key lives in exactly one bucket (found keys by
+// slot, new keys by home slot; within one round all Puts of a key agree, since nothing claims
+// slots while index(e) runs), log order is preserved inside each bucket, and reads(e) run in
+// the launch after elect(e). index(e) and reads(e-1) share a launch safely because neither
+// writes the table. The elector writes only values of slots it owns (one bucket's keys) and
+// claims with CAS, so electors of different buckets never conflict.
 #include "internal.hpp"
 
 namespace nrg {
 
 typedef u64 u64x2 __attribute__((ext_vector_type(2)));
 
-constexpr int TPB = 256;  // B1: 36.6 us/round; 128: 36.4 (noise); 512: 37.6 (profiles/r01_variants/tpb_sweep.txt)
-constexpr u32 SIDE_SLOT = 0xFFFFFFFFu;   // put_slot value of the EMPTY_KEY key (side slot)
-constexpr u32 FULL_SLOT = 0xFFFFFFFEu;   // put_slot value of a Put that found no slot
-
-__device__ __forceinline__ u64 stamp_of(u32 epoch, u64 i) { return ((u64)epoch << 32) | (i + 1); }
+constexpr int TPB = 256;
+constexpr u32 SIDE_ID = 0x7FFFFFFFu;  // entry id of the key EMPTY_KEY (slot ids are < 2^30)
+constexpr u32 NEW_BIT = 0x80000000u;  // entry id flag: key absent when indexed (id = home slot)
+constexpr u32 ID_MASK = 0x7FFFFFFFu;
+constexpr u32 FULL_SLOT = 0xFFFFFFFFu;  // elector: no slot could be claimed (table full)
 
 // record i of a round: from a caller's buffer when given, else from the log ring
 struct RecSrc {
@@ -49,69 +53,24 @@ struct IndexJob {
     RecSrc rec;
     nrg_put* ring_out;  // log copy to write (nullptr: records already in the ring)
     u64 n;
-    u32* put_slot;
-    u32 epoch;
     u32 nblocks;
-    u64* created_acc;  // [HM_CREATED_SLOTS] keys created by index blocks
-    u64x2* bk_ent;  // bucket election (hm_elect_kernel): per index block, its distinct {slot, i+1; value}
-    u32* bk_cnt;  // entries grouped by slot bucket; [bucket][block] = offset << 16 | count
-    u32 bk_shift;  // bucket of slot s = s >> bk_shift
-    u32 bk_nb;     // buckets (power of two, <= HM_BK_MAX)
-    u32 exp;  // diagnostic knobs (NRG_EXP; results are wrong when set): 1 no stamp atomics,
-              // 2 no LDS combining (one atomic per Put), 4 no apply role, 8 no index role
-};
-struct ApplyJob {
-    RecSrc rec;
-    u64 n;
-    const u32* put_slot;
-    u32 epoch;
-    u32 nblocks;
+    u32 nb_log;    // slot buckets = 1 << nb_log
+    u32 bk_shift;  // bucket of a slot id = id >> bk_shift
+    u64x2* ent;    // [nblocks][tile] {id << 32 | i+1, value}
+    u64* ekey;     // [nblocks][tile] key
+    u32* cnt;      // [bucket][nblocks] start << 16 | count
+    u32 exp;       // diagnostic knobs (NRG_EXP; results are wrong when set): 1 no dedup, 2 no
+                   // probe (every key new), 4 no ranking/entries
 };
 struct ReadJob {
-    RecSrc rec;  // records of round `epoch` (used while its apply may be in flight); src=ring=0: none
     const u64* keys;
     u64 R;
     u64* vals;
     uint8_t* found;
-    u32 epoch;
     u32 nblocks;
 };
 
-// What a read needs of a slot: two 16-B loads to the same 128-B line, {key, val} and
-// {stamp1, created} (odd epochs) or {created, stamp0} (even epochs), issued together. The
-// empty asm pins the values at this point: otherwise hipcc sinks the second load below the
-// key compare of the probe loop, turning a Get into two dependent accesses.
-struct View {
-    u64 key, val, st;
-    u32 created;
-};
-__device__ __forceinline__ View load_view(const Slot* p, u32 par) {
-    typedef u64 u64x2 __attribute__((ext_vector_type(2)));
-    // plain loads: the second hits the line the first brought in (non-temporal loads measured
-    // 37.0 -> 44.6 us per B1 round, both going to memory)
-    const u64x2 a = *(const u64x2*)p;
-    const u64x2 b = *(const u64x2*)((const char*)p + (par ? 16 : 24));
-    u64 k = a.x, v = a.y;
-    u64 st = par ? b.x : b.y;
-    u32 cr = (u32)(par ? b.y : b.x);
-    asm volatile("" : "+v"(k), "+v"(v), "+v"(st), "+v"(cr));
-    View w;
-    w.key = k;
-    w.val = v;
-    w.st = st;
-    w.created = cr;
-    return w;
-}
-
-// The value a read of epoch ep sees in a slot (or side slot) holding its key.
-__device__ __forceinline__ bool resolve(View w, u32 ep, RecSrc rec, bool use_rec, u64* v) {
-    if (w.created == 0 || w.created > ep) return false;  // inserted by a later round (or claiming)
-    if (use_rec && (u32)(w.st >> 32) == ep)
-        *v = rec.at((u64)(u32)w.st - 1).val;  // written in round ep; apply(ep) may be in flight
-    else
-        *v = w.val;
-    return true;
-}
+__device__ __forceinline__ u32 bucket_of_id(u32 id, u32 bk_shift) { return id == SIDE_ID ? 0u : (id & ID_MASK) >> bk_shift; }
 
 // Block-wide exclusive prefix sum of one u32 per thread (TPB threads); *total gets the sum.
 __device__ __forceinline__ u32 block_scan_excl(u32 v, u32* total) {
@@ -136,268 +95,535 @@ __device__ __forceinline__ u32 block_scan_excl(u32 v, u32* total) {
     return pre + inc - v;
 }
 
-// find-or-claim k from slot s (its key already loaded as key0); returns slot or -1 if full
-__device__ __forceinline__ long long find_or_claim(Slot* table, u64 k, u64 s, u64 tmask, u64 key0, u32 epoch,
-                                                   u32* created) {
-    u64 key = key0;
+// ---- role: index(e) ---------------------------------------------------------------------------
+// Tile of a block = TPB * K1 consecutive Puts; wave w owns the 64 * K1 Puts [w*64*K1, (w+1)*64*K1)
+// of it, so the order (item q, lane) inside a wave is log order and waves follow each other.
+template <int K1>
+struct IndexLds {
+    static constexpr int TILE = TPB * K1;
+    static constexpr int HSZ = TILE * 3 / 2;  // dedup hash entries (load <= 2/3)
+    static constexpr int DEDUP_BYTES = HSZ * 12;
+    static unsigned bytes(bool dedup, u32 nb) {
+        const unsigned rank = nb * 4 + 4 * nb * 2;
+        return dedup && DEDUP_BYTES > (int)rank ? (unsigned)DEDUP_BYTES : rank;
+    }
+};
+
+template <int K1, bool DEDUP>
+__device__ __forceinline__ void index_role(const IndexJob& j, u32 blk, const Slot* __restrict__ table, u32 shift,
+                                           u64 tmask, char* lds) {
+    constexpr int WT = 64 * K1;
+    constexpr int TILE = IndexLds<K1>::TILE;
+    constexpr int HSZ = IndexLds<K1>::HSZ;
+    __shared__ u32 s_side;  // dedup of the side-slot key: largest tile position + 1
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const u64 base = (u64)blk * TILE;
+    const u32 nb = 1u << j.nb_log;
+    u64* s_hk = (u64*)lds;               // [HSZ] dedup keys
+    u32* s_hp = (u32*)(lds + HSZ * 8);   // [HSZ] largest tile position + 1 per key
+    if (DEDUP) {
+        for (int q = threadIdx.x; q < HSZ; q += TPB) {
+            s_hk[q] = EMPTY_KEY;
+            s_hp[q] = 0;
+        }
+        if (threadIdx.x == 0) s_side = 0;
+    }
+    nrg_put rec[K1];
+    u64 kk[K1];
+    u32 id[K1];
+    bool valid[K1];
+    // issue every record load, then every first probe, before waiting on any of them
+#pragma unroll
+    for (int q = 0; q < K1; q++) {
+        const u64 i = base + (u64)(w * WT + q * 64 + lane);
+        valid[q] = i < j.n;
+        rec[q] = valid[q] ? j.rec.at(i) : nrg_put{0, 0};
+    }
+#pragma unroll
+    for (int q = 0; q < K1; q++) {
+        const u64 i = base + (u64)(w * WT + q * 64 + lane);
+        if (valid[q] && j.ring_out) j.ring_out[(j.rec.lo + i) & j.rec.mask] = rec[q];
+        const bool probe = valid[q] && rec[q].key != EMPTY_KEY && !(j.exp & 2);
+        kk[q] = probe ? table[table_home(rec[q].key, shift)].key : EMPTY_KEY;
+    }
+#pragma unroll
+    for (int q = 0; q < K1; q++) {
+        id[q] = SIDE_ID;
+        if (!valid[q] || rec[q].key == EMPTY_KEY) continue;
+        const u64 k = rec[q].key;
+        const u64 home = table_home(k, shift);
+        u64 s = home;
+        u64 key = kk[q];
+        id[q] = (u32)home | NEW_BIT;  // also when the probe exhausts a full table (the claim fails)
+        for (u64 pr = 0; pr <= tmask && !(j.exp & 2); pr++) {
+            if (key == k) {
+                id[q] = (u32)s;
+                break;
+            }
+            if (key == EMPTY_KEY) break;
+            s = (s + 1) & tmask;
+            key = table[s].key;
+        }
+    }
+    // ---- drop Puts that a later Put of the same key in this block overwrites ----
+    bool emit[K1];
+    if (DEDUP && !(j.exp & 1)) {
+        __syncthreads();  // hash initialised
+        u32 hq[K1];
+#pragma unroll
+        for (int q = 0; q < K1; q++) {
+            if (!valid[q]) continue;
+            const u32 pos1 = (u32)(w * WT + q * 64 + lane) + 1;
+            if (rec[q].key == EMPTY_KEY) {
+                atomicMax(&s_side, pos1);
+                continue;
+            }
+            u32 h = (u32)(((mix64(rec[q].key) >> 32) * (u64)HSZ) >> 32);
+            for (;;) {
+                const u64 old = atomicCAS((unsigned long long*)&s_hk[h], (unsigned long long)EMPTY_KEY,
+                                          (unsigned long long)rec[q].key);
+                if (old == EMPTY_KEY || old == rec[q].key) break;
+                h = h + 1 == (u32)HSZ ? 0u : h + 1;
+            }
+            atomicMax(&s_hp[h], pos1);
+            hq[q] = h;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < K1; q++) {
+            const u32 pos1 = (u32)(w * WT + q * 64 + lane) + 1;
+            emit[q] = valid[q] && (rec[q].key == EMPTY_KEY ? s_side == pos1 : s_hp[hq[q]] == pos1);
+        }
+        __syncthreads();  // the hash region is reused below
+    } else {
+#pragma unroll
+        for (int q = 0; q < K1; q++) emit[q] = valid[q];
+    }
+    if (j.exp & 4) {
+        if (emit[0]) j.ekey[base + threadIdx.x] = id[0];
+        return;
+    }
+    // ---- stable grouping by bucket: wave-private counts, then a prefix over waves ----
+    u32* s_start = (u32*)lds;                       // [nb] bucket start in the tile
+    uint16_t* s_wc = (uint16_t*)(lds + nb * 4);     // [4][nb] per-wave counts -> wave offsets
+    for (u32 b = threadIdx.x; b < 4 * nb; b += TPB) s_wc[b] = 0;
+    __syncthreads();
+    u32 bkt[K1], rnk[K1];
+#pragma unroll
+    for (int q = 0; q < K1; q++) {
+        const u32 b = emit[q] ? bucket_of_id(id[q], j.bk_shift) : 0u;
+        u64 peers = __ballot(emit[q]);
+        for (u32 bit = 0; bit < j.nb_log; bit++) {
+            const bool one = (b >> bit) & 1u;
+            const u64 bal = __ballot(one);
+            peers &= one ? bal : ~bal;
+        }
+        bkt[q] = b;
+        if (emit[q]) {
+            const u64 below = peers & ((1ull << lane) - 1);
+            const u32 cur = s_wc[w * nb + b];
+            rnk[q] = cur + (u32)__popcll(below);
+            if (below == 0) s_wc[w * nb + b] = (uint16_t)(cur + (u32)__popcll(peers));
+        }
+    }
+    __syncthreads();
+    constexpr int PER = HM_BK_MAX / TPB;  // buckets per thread (contiguous ownership)
+    u32 tot[PER], loc = 0;
+#pragma unroll
+    for (int r = 0; r < PER; r++) {
+        const u32 b = threadIdx.x * PER + r;
+        tot[r] = 0;
+        if (b < nb) {
+            u32 run = 0;
+#pragma unroll
+            for (int v = 0; v < 4; v++) {
+                const u32 c = s_wc[v * nb + b];
+                s_wc[v * nb + b] = (uint16_t)run;
+                run += c;
+            }
+            tot[r] = run;
+            loc += run;
+        }
+    }
+    u32 off = block_scan_excl(loc, nullptr);
+#pragma unroll
+    for (int r = 0; r < PER; r++) {
+        const u32 b = threadIdx.x * PER + r;
+        if (b < nb) {
+            j.cnt[(u64)b * j.nblocks + blk] = (off << 16) | tot[r];
+            s_start[b] = off;
+        }
+        off += tot[r];
+    }
+    __syncthreads();
+    u64x2* ent = j.ent + (u64)blk * TILE;
+    u64* ekey = j.ekey + (u64)blk * TILE;
+#pragma unroll
+    for (int q = 0; q < K1; q++) {
+        if (!emit[q]) continue;
+        const u64 i = base + (u64)(w * WT + q * 64 + lane);
+        const u32 p = s_start[bkt[q]] + s_wc[w * nb + bkt[q]] + rnk[q];
+        u64x2 e;
+        e.x = ((u64)id[q] << 32) | (u64)(i + 1);
+        e.y = rec[q].val;
+        ent[p] = e;
+        ekey[p] = rec[q].key;
+    }
+}
+
+// claim (or find) k's slot from its home slot; *fresh = this call inserted it; -1: table full
+__device__ __forceinline__ long long claim_slot(Slot* table, u64 k, u64 s, u64 tmask, bool* fresh) {
+    *fresh = false;
     for (u64 pr = 0; pr <= tmask; pr++) {
+        const u64 key = ld_relaxed(&table[s].key);
         if (key == k) return (long long)s;
         if (key == EMPTY_KEY) {
-            const u64 old = atomicCAS(&table[s].key, EMPTY_KEY, k);
+            const u64 old = atomicCAS((unsigned long long*)&table[s].key, (unsigned long long)EMPTY_KEY,
+                                      (unsigned long long)k);
             if (old == EMPTY_KEY) {
-                table[s].created = epoch;
-                *created += 1;
+                *fresh = true;
                 return (long long)s;
             }
             if (old == k) return (long long)s;
         }
         s = (s + 1) & tmask;
-        key = ld_relaxed(&table[s].key);
     }
     return -1;
 }
 
-// ---- role: index(e) -------------------------------------------------------------------------
-template <int K1_ITEMS, bool BK>
-__device__ __forceinline__ void index_role(IndexJob j, u32 blk, Slot* table, u32 shift, u64 tmask,
-                                           DevCtl* ctl) {
-    constexpr int K1_TILE = TPB * K1_ITEMS;
-    constexpr int K1_LDS = 2 * K1_TILE;
-    __shared__ u32 s_slot[K1_LDS];
-    __shared__ u32 s_max[K1_LDS];
-    __shared__ u32 s_created;
-    __shared__ u32 s_bk[BK ? HM_BK_MAX : 1];
-    for (int q = threadIdx.x; q < K1_LDS; q += TPB) {
-        s_slot[q] = 0xFFFFFFFFu;
-        s_max[q] = 0;
+// ---- overlay rounds: roles index(e) -> O_e, apply(e-1) and reads(e-1) against O_{e-1} ---------
+//
+// A round of at most ov_max Puts without previous-value responses replays in ONE launch:
+//   index(e)   per block, the last Put of each key (LDS dedup), then per such key one insert into
+//              the round's overlay O_e (a small open-addressing table, 64-bit CAS on the key) and
+//              atomicMax(st, i+1): the round's last writer of every key. The main table is not
+//              touched. Inserted overlay slots are listed per block.
+//   apply(e-1) next launch, per listed slot of O_{e-1}: the winner's value (from the log record),
+//              find-or-claim of the key in the main table, store.
+//   reads(e-1) same launch: a key in O_{e-1} answers with its winner's record value (apply may be
+//              storing it concurrently), any other key from the main table. apply only claims and
+//              writes keys listed in O_{e-1}, so those reads never depend on its progress, and a
+//              claim of another key cannot hide a present key (linear probing: a key present
+//              before round e-1 lies before every slot that was empty then).
+//   clear(e-2) same launch: empties the slots O_{e-2} used (three overlays rotate).
+// Race-freedom: index(e) touches only O_e; apply/reads(e-1) read O_{e-1} (complete since the
+// previous launch); clear touches only O_{e-2}, whose apply and reads ran in the previous launch.
+struct OvIndexJob {
+    u32 exp;  // diagnostic (NRG_EXP): 16 no overlay inserts
+    RecSrc rec;
+    nrg_put* ring_out;
+    u64 n;
+    u32 nblocks;
+    OvSlot* ov;
+    u64 omask;
+    u32* list;     // [nblocks][tile] inserted overlay slots
+    u32* lcnt;     // [nblocks]
+    u64* side_st;  // &ctl->sp_st[idx]
+};
+struct OvListJob {  // apply(e-1) / clear(e-2): one thread per list position of that round
+    u32 exp;  // diagnostic (NRG_EXP): 32 no apply
+    const OvSlot* ov;
+    OvSlot* ov_w;
+    const u32* list;
+    const u32* lcnt;
+    u32 ltile;
+    u64* side_st;
+    RecSrc rec;
+    u64* created_acc;
+    u32 nblocks;
+};
+
+__device__ __forceinline__ u64 ov_home(u64 k, u64 omask) { return mix64(k) & omask; }
+
+template <int K1>
+__device__ __forceinline__ void ov_index_role(const OvIndexJob& j, u32 blk, DevCtl* ctl, char* lds) {
+    constexpr int WT = 64 * K1;
+    constexpr int TILE = IndexLds<K1>::TILE;
+    constexpr int HSZ = IndexLds<K1>::HSZ;
+    __shared__ u32 s_side;
+    __shared__ u32 s_ln;
+    __shared__ u32 s_list[TILE];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const u64 base = (u64)blk * TILE;
+    u64* s_hk = (u64*)lds;
+    u32* s_hp = (u32*)(lds + HSZ * 8);
+    for (int q = threadIdx.x; q < HSZ; q += TPB) {
+        s_hk[q] = EMPTY_KEY;
+        s_hp[q] = 0;
     }
-    if constexpr (BK)
-        for (int q = threadIdx.x; q < (int)j.bk_nb; q += TPB) s_bk[q] = 0;
+    if (threadIdx.x == 0) {
+        s_side = 0;
+        s_ln = 0;
+    }
+    nrg_put rec[K1];
+    bool valid[K1];
+#pragma unroll
+    for (int q = 0; q < K1; q++) {
+        const u64 i = base + (u64)(w * WT + q * 64 + lane);
+        valid[q] = i < j.n;
+        rec[q] = valid[q] ? j.rec.at(i) : nrg_put{0, 0};
+    }
+#pragma unroll
+    for (int q = 0; q < K1; q++) {
+        const u64 i = base + (u64)(w * WT + q * 64 + lane);
+        if (valid[q] && j.ring_out) j.ring_out[(j.rec.lo + i) & j.rec.mask] = rec[q];
+    }
+    __syncthreads();  // hash initialised
+    u32 hq[K1];
+#pragma unroll
+    for (int q = 0; q < K1; q++) {
+        if (!valid[q]) continue;
+        const u32 pos1 = (u32)(w * WT + q * 64 + lane) + 1;
+        if (rec[q].key == EMPTY_KEY) {
+            atomicMax(&s_side, pos1);
+            continue;
+        }
+        u32 h = (u32)(((mix64(rec[q].key) >> 32) * (u64)HSZ) >> 32);
+        for (;;) {
+            const u64 old = atomicCAS((unsigned long long*)&s_hk[h], (unsigned long long)EMPTY_KEY,
+                                      (unsigned long long)rec[q].key);
+            if (old == EMPTY_KEY || old == rec[q].key) break;
+            h = h + 1 == (u32)HSZ ? 0u : h + 1;
+        }
+        atomicMax(&s_hp[h], pos1);
+        hq[q] = h;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < K1; q++) {
+        if (!valid[q]) continue;
+        const u32 pos1 = (u32)(w * WT + q * 64 + lane) + 1;
+        const u64 i1 = base + pos1;  // i + 1 in the round
+        if (rec[q].key == EMPTY_KEY) {
+            if (s_side == pos1) atomicMax((unsigned long long*)j.side_st, (unsigned long long)i1);
+            continue;
+        }
+        if (s_hp[hq[q]] != pos1) continue;  // a later Put of the key in this block wins
+        if (j.exp & 16) continue;
+        const u64 k = rec[q].key;
+        u64 h = ov_home(k, j.omask);
+        bool ok = false;
+        for (u64 pr = 0; pr <= j.omask; pr++) {
+            const u64 old = atomicCAS((unsigned long long*)&j.ov[h].key, (unsigned long long)EMPTY_KEY,
+                                      (unsigned long long)k);
+            if (old == EMPTY_KEY) s_list[atomicAdd(&s_ln, 1u)] = (u32)h;
+            if (old == EMPTY_KEY || old == k) {
+                ok = true;
+                break;
+            }
+            h = (h + 1) & j.omask;
+        }
+        if (!ok) {
+            atomicOr(&ctl->err, ERR_TABLE_FULL);
+            continue;
+        }
+        atomicMax((unsigned long long*)&j.ov[h].st, (unsigned long long)i1);
+    }
+    __syncthreads();
+    const u32 ln = s_ln;
+    for (u32 q = threadIdx.x; q < ln; q += TPB) j.list[(u64)blk * TILE + q] = s_list[q];
+    if (threadIdx.x == 0) j.lcnt[blk] = ln;
+}
+
+// apply(e-1): one thread per list position of round e-1
+__device__ __forceinline__ void ov_apply_role(const OvListJob& j, u32 blk, Slot* table, u32 shift, u64 tmask,
+                                              DevCtl* ctl) {
+    __shared__ u32 s_created;
     if (threadIdx.x == 0) s_created = 0;
     __syncthreads();
-    const u32 par = j.epoch & 1;
-    const u64 base = (u64)blk * K1_TILE;
+    const u64 x = (u64)blk * TPB + threadIdx.x;
+    const u32 ib = (u32)(x / j.ltile), k = (u32)(x % j.ltile);
     u32 created = 0;
-    u64 sl_idx[K1_ITEMS];
-    u64 key0[K1_ITEMS];
-    nrg_put rec[K1_ITEMS];
-    u32 hq[K1_ITEMS];  // LDS combine entry of each record (bucket election), ~0u: none
-#pragma unroll
-    for (int q = 0; q < K1_ITEMS; q++) hq[q] = ~0u;
-    // issue every record load and every first probe before waiting on any of them
-#pragma unroll
-    for (int q = 0; q < K1_ITEMS; q++) {
-        const u64 i = base + (u64)q * TPB + threadIdx.x;
-        rec[q] = i < j.n ? j.rec.at(i) : nrg_put{EMPTY_KEY, 0};
-    }
-#pragma unroll
-    for (int q = 0; q < K1_ITEMS; q++) {
-        const u64 i = base + (u64)q * TPB + threadIdx.x;
-        if (i < j.n && j.ring_out) j.ring_out[(j.rec.lo + i) & j.rec.mask] = rec[q];
-        sl_idx[q] = table_home(rec[q].key, shift);
-        key0[q] = rec[q].key != EMPTY_KEY ? table[sl_idx[q]].key : EMPTY_KEY;
-    }
-#pragma unroll
-    for (int q = 0; q < K1_ITEMS; q++) {
-        const u64 i = base + (u64)q * TPB + threadIdx.x;
-        if (i >= j.n) continue;
-        const u64 k = rec[q].key;
-        if (k == EMPTY_KEY) {  // the side-slot key
-            if (ld_relaxed32(&ctl->sp.created) == 0 && atomicCAS(&ctl->sp.created, 0u, j.epoch) == 0u) created++;
-            atomicMax(slot_stamp(&ctl->sp, par), stamp_of(j.epoch, i));
-            j.put_slot[i] = SIDE_SLOT;
-            continue;
-        }
-        const long long s = find_or_claim(table, k, sl_idx[q], tmask, key0[q], j.epoch, &created);
-        if (s < 0) {
+    if (k < j.lcnt[ib] && !(j.exp & 32)) {
+        const u32 h = j.list[(u64)ib * j.ltile + k];
+        const u64x2 o = *(const u64x2*)&j.ov[h];
+        const u64 v = j.rec.at(o.y - 1).val;
+        bool fresh;
+        const long long sl = claim_slot(table, o.x, table_home(o.x, shift), tmask, &fresh);
+        if (sl < 0) {
             atomicOr(&ctl->err, ERR_TABLE_FULL);
-            j.put_slot[i] = FULL_SLOT;
-            continue;
+        } else {
+            table[sl].val = v;
+            created += fresh;
         }
-        j.put_slot[i] = (u32)s;
-        if (j.exp & 2) {
-            if (!(j.exp & 1)) atomicMax(slot_stamp(&table[s], par), stamp_of(j.epoch, i));
-            continue;
-        }
-        // combine in LDS: max (i+1) per slot within the block
-        u32 h = (u32)(mix64((u64)s) & (K1_LDS - 1));
-        for (;;) {
-            const u32 old = atomicCAS(&s_slot[h], 0xFFFFFFFFu, (u32)s);
-            if (old == 0xFFFFFFFFu || old == (u32)s) break;
-            h = (h + 1) & (K1_LDS - 1);
-        }
-        atomicMax(&s_max[h], (u32)(i + 1));
-        hq[q] = h;
-        sl_idx[q] = (u64)s;
     }
-    // one key-count atomic per block: a same-address atomic per thread serialises at the
-    // memory side (16k new keys cost ~16 us that way)
+    if (blk == 0 && threadIdx.x == 0) {
+        const u64 st = *j.side_st;
+        if (st) {
+            created += ctl->sp_present == 0;
+            ctl->sp_val = j.rec.at(st - 1).val;
+            ctl->sp_present = 1;
+        }
+    }
     if (created) atomicAdd(&s_created, created);
     __syncthreads();
-    if constexpr (BK) {
-        // Bucket election: no stamp atomics. The block's distinct (slot, last i+1) pairs go to
-        // its tile of bk_ent grouped by slot bucket (order inside a bucket is irrelevant: the
-        // elector takes the maximum); bk_cnt[bucket][block] says where.
-        // the block's last record per slot is the one whose i+1 won the LDS combine; its
-        // thread holds the value, so entries carry it and the elector gathers no records
-        bool win[K1_ITEMS];
-#pragma unroll
-        for (int q = 0; q < K1_ITEMS; q++) {
-            const u64 i = base + (u64)q * TPB + threadIdx.x;
-            win[q] = hq[q] != ~0u && s_max[hq[q]] == (u32)(i + 1);
-            if (win[q]) atomicAdd(&s_bk[(u32)sl_idx[q] >> j.bk_shift], 1u);
-        }
-        __syncthreads();
-        constexpr int PER = HM_BK_MAX / TPB;  // buckets per thread (bk_nb <= HM_BK_MAX)
-        u32 c[PER], loc = 0;
-#pragma unroll
-        for (int r = 0; r < PER; r++) {
-            const u32 b = threadIdx.x * PER + r;
-            c[r] = b < j.bk_nb ? s_bk[b] : 0u;
-            loc += c[r];
-        }
-        const u32 run = block_scan_excl(loc, nullptr);
-        __syncthreads();
-        u32 off = run;
-#pragma unroll
-        for (int r = 0; r < PER; r++) {
-            const u32 b = threadIdx.x * PER + r;
-            if (b < j.bk_nb) {
-                j.bk_cnt[(u64)b * j.nblocks + blk] = (off << 16) | c[r];
-                s_bk[b] = off;
-            }
-            off += c[r];
-        }
-        __syncthreads();
-        u64x2* ent = j.bk_ent + (u64)blk * K1_TILE;
-#pragma unroll
-        for (int q = 0; q < K1_ITEMS; q++) {
-            if (!win[q]) continue;
-            const u64 i = base + (u64)q * TPB + threadIdx.x;
-            u64x2 e;
-            e.x = (sl_idx[q] << 32) | (u64)(i + 1);
-            e.y = rec[q].val;
-            ent[atomicAdd(&s_bk[(u32)sl_idx[q] >> j.bk_shift], 1u)] = e;
-        }
-    } else {
-        for (int q = threadIdx.x; q < K1_LDS; q += TPB) {
-            const u32 s = s_slot[q];
-            if (s != 0xFFFFFFFFu && !(j.exp & 1))
-                atomicMax(slot_stamp(&table[s], par), ((u64)j.epoch << 32) | s_max[q]);
-        }
-    }
-    // keys created by this block: spread over HM_CREATED_SLOTS counters (summed by hm_count);
-    // one same-address atomic per block would serialise at the memory side (~88 per us)
     if (threadIdx.x == 0 && s_created) atomicAdd(&j.created_acc[blk % HM_CREATED_SLOTS], (u64)s_created);
 }
 
-// ---- role: apply(e) -------------------------------------------------------------------------
-__device__ __forceinline__ void apply_role(ApplyJob j, u32 blk, Slot* table, DevCtl* ctl) {
-    const u64 i = (u64)blk * TPB + threadIdx.x;
-    if (i >= j.n) return;
-    const u32 par = j.epoch & 1;
-    const u32 s = j.put_slot[i];
-    const u64 want = stamp_of(j.epoch, i);
-    if (s == SIDE_SLOT) {
-        if (*slot_stamp(&ctl->sp, par) == want) ctl->sp.val = j.rec.at(i).val;
-    } else if (s != FULL_SLOT) {
-        if (*slot_stamp(&table[s], par) == want) table[s].val = j.rec.at(i).val;
+// clear(e-2): empty the overlay slots round e-2 inserted
+__device__ __forceinline__ void ov_clear_role(const OvListJob& j, u32 blk) {
+    const u64 x = (u64)blk * TPB + threadIdx.x;
+    const u32 ib = (u32)(x / j.ltile), k = (u32)(x % j.ltile);
+    if (k < j.lcnt[ib]) {
+        u64x2 z;
+        z.x = EMPTY_KEY;
+        z.y = 0;
+        *(u64x2*)&j.ov_w[j.list[(u64)ib * j.ltile + k]] = z;
     }
+    if (blk == 0 && threadIdx.x == 0) *j.side_st = 0;
 }
 
-// ---- role: reads(e) -------------------------------------------------------------------------
-template <int G>
-__device__ __forceinline__ void read_role(ReadJob j, u32 blk, const Slot* table, u32 shift, u64 tmask,
-                                          const DevCtl* ctl) {
-    // G Gets per thread: all key loads, then all first-slot loads, are in flight together
-    const u32 par = j.epoch & 1;
-    const bool use_rec = j.rec.src != nullptr || j.rec.ring != nullptr;
-    const u64 jb = (u64)blk * TPB * G + threadIdx.x;
-    u64 k[G];
-    View first[G];
-#pragma unroll
-    for (int g = 0; g < G; g++) {
-        const u64 q = jb + (u64)g * TPB;
-        k[g] = q < j.R ? j.keys[q] : EMPTY_KEY;
-    }
-#pragma unroll
-    for (int g = 0; g < G; g++) first[g] = load_view(k[g] == EMPTY_KEY ? &ctl->sp : &table[table_home(k[g], shift)], par);
-#pragma unroll
-    for (int g = 0; g < G; g++) {
-        const u64 q = jb + (u64)g * TPB;
-        if (q >= j.R) break;
-        u64 v = 0;
-        bool f = false;
-        if (k[g] == EMPTY_KEY) {
-            f = resolve(first[g], j.epoch, j.rec, use_rec, &v);
+// ---- role: reads -------------------------------------------------------------------------------
+// With an overlay (reads of an overlay round, whose apply may run in the same launch): a key in
+// the overlay answers with its last writer's record value, others from the main table.
+struct OvReadCtx {
+    u32 exp;  // diagnostic (NRG_EXP): 8 reads skip the overlay
+    const OvSlot* ov;  // nullptr: no overlay round pending
+    u64 omask;
+    const u64* side_st;
+    RecSrc rec;
+};
+
+__device__ __forceinline__ void read_role(const ReadJob& j, const OvReadCtx& o, u32 blk, const Slot* table,
+                                          u32 shift, u64 tmask, const DevCtl* ctl) {
+    const u64 q = (u64)blk * TPB + threadIdx.x;
+    if (q >= j.R) return;
+    const u64 k = j.keys[q];
+    u64 v = 0;
+    bool f = false;
+    if (k == EMPTY_KEY) {
+        const u64 st = o.ov ? *o.side_st : 0;
+        if (st) {
+            f = true;
+            v = o.rec.at(st - 1).val;
         } else {
-            u64 s = table_home(k[g], shift);
-            View w = first[g];
-            for (u64 pr = 0; pr <= tmask; pr++) {
-                if (w.key == k[g]) {
-                    f = resolve(w, j.epoch, j.rec, use_rec, &v);
+            f = ctl->sp_present != 0;
+            v = f ? ctl->sp_val : 0;
+        }
+    } else {
+        u64 s = table_home(k, shift);
+        const bool use_ov = o.ov && !(o.exp & 8);
+        u64 oh = use_ov ? ov_home(k, o.omask) : 0;
+        // the overlay line and the table line are loaded together (independent addresses)
+        u64x2 ow;
+        ow.x = EMPTY_KEY;
+        if (use_ov) ow = *(const u64x2*)&o.ov[oh];
+        u64x2 w = *(const u64x2*)&table[s];
+        bool in_ov = false;
+        if (use_ov) {
+            for (u64 pr = 0; pr <= o.omask; pr++) {
+                if (ow.x == k) {
+                    in_ov = true;
                     break;
                 }
-                if (w.key == EMPTY_KEY) break;
-                s = (s + 1) & tmask;
-                w = load_view(&table[s], par);
+                if (ow.x == EMPTY_KEY) break;
+                oh = (oh + 1) & o.omask;
+                ow = *(const u64x2*)&o.ov[oh];
             }
         }
-        if (!f) v = 0;
-        j.vals[q] = v;
-        j.found[q] = f ? 1 : 0;
+        if (in_ov) {
+            f = true;
+            v = o.rec.at(ow.y - 1).val;
+        } else {
+            for (u64 pr = 0; pr <= tmask; pr++) {  // one 16-B load per probe
+                if (w.x == k) {
+                    v = w.y;
+                    f = true;
+                    break;
+                }
+                if (w.x == EMPTY_KEY) break;
+                s = (s + 1) & tmask;
+                w = *(const u64x2*)&table[s];
+            }
+        }
     }
+    j.vals[q] = v;
+    j.found[q] = f ? 1 : 0;
 }
 
-// One launch = {index(e)} + {apply(p)} + {reads(p)} over disjoint block ranges (any may be
-// empty). Index blocks come first so the latency-bound pass is dispatched first (reads first:
-// B1 37.0 -> 40.5 us, 50 % writes 66.6 -> 75.8 us; profiles/r01_variants/block_order.txt).
-template <int K1_ITEMS, int G, bool BK>
-__global__ __launch_bounds__(TPB) void hm_round_kernel(IndexJob ij, ApplyJob aj, ReadJob rj, Slot* table, u32 shift,
-                                                       u64 tmask, DevCtl* ctl) {
+// index-role kinds of a round launch
+constexpr int IX_BUCKET = 0;    // bucket round, dedup (hm_elect_kernel<false> follows)
+constexpr int IX_BUCKET_ALL = 1;  // bucket round, every Put kept (previous values)
+constexpr int IX_OVERLAY = 2;   // overlay round
+
+// One launch = {index(e)} + {apply(e-1)} + {clear(e-2)} + {reads(e-1)} over disjoint block
+// ranges (any may be empty). Index blocks come first so the latency-bound pass starts first.
+template <int K1, int IX>
+__global__ __launch_bounds__(TPB) void hm_round_kernel(IndexJob ij, OvIndexJob oj, OvListJob aj, OvListJob cj,
+                                                       ReadJob rj, OvReadCtx ro, Slot* table, u32 shift, u64 tmask,
+                                                       DevCtl* ctl) {
+    extern __shared__ __attribute__((aligned(16))) char s_lds[];
     u32 b = blockIdx.x;
-    if (b < ij.nblocks) {
-        index_role<K1_ITEMS, BK>(ij, b, table, shift, tmask, ctl);
+    const u32 nix = IX == IX_OVERLAY ? oj.nblocks : ij.nblocks;
+    if (b < nix) {
+        if constexpr (IX == IX_OVERLAY) ov_index_role<K1>(oj, b, ctl, s_lds);
+        else index_role<K1, IX == IX_BUCKET>(ij, b, table, shift, tmask, s_lds);
         return;
     }
-    b -= ij.nblocks;
+    b -= nix;
     if (b < aj.nblocks) {
-        apply_role(aj, b, table, ctl);
+        ov_apply_role(aj, b, table, shift, tmask, ctl);
         return;
     }
     b -= aj.nblocks;
-    read_role<G>(rj, b, table, shift, tmask, ctl);
+    if (b < cj.nblocks) {
+        ov_clear_role(cj, b);
+        return;
+    }
+    b -= cj.nblocks;
+    read_role(rj, ro, b, table, shift, tmask, ctl);
 }
 
-// Bucket election + apply of one round (the large-round alternative to the stamp atomics):
-// one block per slot bucket gathers the bucket's (slot, i+1) entries from every index block's
-// tile, keeps the maximum i+1 per slot in an LDS hash table (the last writer in log order) and
-// stores that record's value into the slot: one plain store per distinct key instead of a
-// scattered device atomic per Put (25.6 G/s) and a stamp re-read per Put in apply (plain
-// scattered 8-B stores run at 69 G/s, profiles/r01_get_floor.txt). A bucket whose distinct
-// slots overflow the table is redone in 2, 4, ... slot sub-ranges (the stores are idempotent).
-// The side slot (key u64::MAX) keeps its stamp; block 0 applies it.
-constexpr int HM_EL_HT = 2048;
-constexpr int HM_EL_CH = 2048;  // entries gathered per pass (one u16 tile id each in LDS)
-constexpr int HM_EL_PER = HM_EL_CH / TPB;
-__global__ __launch_bounds__(TPB) void hm_elect_kernel(const u64x2* __restrict__ ent, const u32* __restrict__ cnt,
-                                                       u32 nblocks, u32 tile, u32 bk_shift, RecSrc rec, Slot* table,
-                                                       DevCtl* ctl, u32 epoch) {
-    const u32 K1_TILE = tile;  // entries per index block (TPB x its Puts per thread)
-    extern __shared__ u32 s_dyn[];    // s_pre[nblocks + 1] entry prefix, s_off[nblocks] (u16)
-    __shared__ u32 s_hk[HM_EL_HT];
-    __shared__ u32 s_hv[HM_EL_HT];
-    __shared__ uint16_t s_tile[HM_EL_CH];
+// ---- hm_elect_kernel: last writer per key, claims of new keys, value stores -----------------------
+struct ElectJob {
+    const u64x2* ent;
+    const u64* ekey;
+    const u32* cnt;
+    u32 nblocks;
+    u32 tile;      // entries per index tile
+    u32 bk_shift;
+    Slot* table;
+    u32 shift;
+    u64 tmask;
+    DevCtl* ctl;
+    u64* created_acc;
+    u64 lo;        // log index of the round's record 0
+    u64 resp_lo, resp_hi;
+    u64* prev;     // previous-value responses for log indices [resp_lo, resp_hi)
+    uint8_t* prevf;
+    u32 exp;  // diagnostic knobs (NRG_EXP >> 8; wrong results): 1 counts only, 2 + pass 1 only, 4 no claims
+};
+
+constexpr int EL_HT = 2048;  // LDS hash entries (distinct keys of one part of a bucket)
+constexpr int EL_CH = 2048;  // entries gathered per chunk
+constexpr int EL_PER = EL_CH / TPB;
+constexpr int EL_WIN = 4;    // steps of 64 entries loaded ahead by the log-order walk
+
+__device__ __forceinline__ u32 el_hash(u64 k) { return (u32)(mix64(k) >> 40) & (EL_HT - 1); }
+
+template <bool PREV>
+__global__ __launch_bounds__(TPB) void hm_elect_kernel(ElectJob j) {
+    extern __shared__ u32 s_dyn[];  // s_pre[nblocks + 1] entry prefix, s_off[nblocks] (u16)
+    __shared__ u64 s_hk[EL_HT];
+    __shared__ u32 s_hp[EL_HT + 1];  // largest bucket position + 1 of the key; [EL_HT]: side key
+    __shared__ u32 s_hs[EL_HT + 1];  // the key's slot (SIDE_ID, FULL_SLOT)
+    __shared__ u32 s_hf[EL_HT + 1];  // bit 0: new key (claim), bit 1: s_lv holds a value
+    __shared__ u64 s_lv[PREV ? EL_HT + 1 : 1];  // PREV: the key's value so far in the walk
+    __shared__ u64 s_mk[PREV ? EL_HT + 1 : 1];  // PREV: lanes of the current walk step per key
+    __shared__ uint16_t s_tile[EL_CH];
+    __shared__ u32 s_created;
+    const u32 nblocks = j.nblocks;
     u32* s_pre = s_dyn;
     uint16_t* s_off = (uint16_t*)(s_dyn + nblocks + 1);
     const u32 b = blockIdx.x;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     // this bucket's (offset, count) in every index tile; thread owns tiles [tid*K, tid*K + K)
     const u32 K = (nblocks + TPB - 1) / TPB;
     u32 loc = 0;
     for (u32 q = 0; q < K; q++) {
         const u32 t = threadIdx.x * K + q;
         if (t < nblocks) {
-            const u32 v = cnt[(u64)b * nblocks + t];
+            const u32 v = j.cnt[(u64)b * nblocks + t];
             s_off[t] = (uint16_t)(v >> 16);
             s_pre[t] = v & 0xFFFFu;
             loc += v & 0xFFFFu;
@@ -413,145 +639,269 @@ __global__ __launch_bounds__(TPB) void hm_elect_kernel(const u64x2* __restrict__
             run += c;
         }
     }
-    if (threadIdx.x == 0) s_pre[nblocks] = total;
-    u32 lp = 0;  // parts = 2^lp slot sub-ranges of the bucket, about <= HT/2 entries each
-    while ((total >> lp) > HM_EL_HT / 2 && lp < bk_shift) lp++;
+    if (threadIdx.x == 0) {
+        s_pre[nblocks] = total;
+        s_created = 0;
+    }
+    if (total == 0 || (j.exp & 1)) return;  // uniform across the block
+    // parts = 2^lp id sub-ranges of the bucket, about <= EL_HT/2 entries each
+    u32 lp = 0;
+    while ((total >> lp) > EL_HT / 2 && lp < j.bk_shift) lp++;
     __syncthreads();
-    u64x2 x[HM_EL_PER];
-    // the chunk [base, base + CH) of this bucket's entries into registers, all loads in flight
-    auto load_chunk = [&](u32 base) {
+    // entry tile map of the chunk [base, base + EL_CH)
+    auto fill_tiles = [&](u32 base) {
         for (u32 q = 0; q < K; q++) {
             const u32 t = threadIdx.x * K + q;
             if (t >= nblocks) break;
             const u32 lo_ = s_pre[t] > base ? s_pre[t] : base;
-            const u32 hi_ = s_pre[t + 1] < base + HM_EL_CH ? s_pre[t + 1] : base + HM_EL_CH;
+            const u32 hi_ = s_pre[t + 1] < base + EL_CH ? s_pre[t + 1] : base + EL_CH;
             for (u32 i = lo_; i < hi_; i++) s_tile[i - base] = (uint16_t)t;
         }
+    };
+    auto ent_at = [&](u32 pos, u32 base) -> u64 {  // index of bucket position pos in the entry arrays
+        const u32 t = s_tile[pos - base];
+        return (u64)t * j.tile + s_off[t] + (pos - s_pre[t]);
+    };
+    u64x2 x[EL_PER];
+    u64 xk[EL_PER];
+    auto load_chunk = [&](u32 base) {
+        fill_tiles(base);
         __syncthreads();
 #pragma unroll
-        for (int r = 0; r < HM_EL_PER; r++) {
+        for (int r = 0; r < EL_PER; r++) {
             const u32 i = base + r * TPB + threadIdx.x;
-            x[r].x = ~0ull;
+            x[r].x = 0;  // i+1 = 0: no entry
             if (i < total) {
-                const u32 t = s_tile[i - base];
-                x[r] = ent[(u64)t * K1_TILE + s_off[t] + (i - s_pre[t])];
+                const u64 e = ent_at(i, base);
+                x[r] = j.ent[e];
+                xk[r] = j.ekey[e];
             }
         }
         __syncthreads();  // s_tile is reused by the next chunk
     };
-    auto in_part = [&](u32 sl, u32 p) { return !lp || ((sl >> (bk_shift - lp)) & ((1u << lp) - 1)) == p; };
-    const bool one_chunk = total <= (u32)HM_EL_CH;
+    auto in_part = [&](u32 id, u32 p) {
+        if (!lp) return true;
+        if (id == SIDE_ID) return p == 0;
+        return (((id & ID_MASK) >> (j.bk_shift - lp)) & ((1u << lp) - 1)) == p;
+    };
+    auto lookup = [&](u64 k) -> u32 {  // hash entry of a key inserted by pass 1
+        if (k == EMPTY_KEY) return (u32)EL_HT;
+        u32 h = el_hash(k);
+        while (s_hk[h] != k) h = (h + 1) & (EL_HT - 1);
+        return h;
+    };
+    const bool one_chunk = total <= (u32)EL_CH;
+    u32 created = 0;
     for (u32 p = 0; p < (1u << lp);) {
-        for (int q = threadIdx.x; q < HM_EL_HT; q += TPB) {
-            s_hk[q] = 0xFFFFFFFFu;
-            s_hv[q] = 0;
+        for (int q = threadIdx.x; q <= EL_HT; q += TPB) {
+            if (q < EL_HT) s_hk[q] = EMPTY_KEY;
+            s_hp[q] = 0;
+            s_hf[q] = 0;
+            if (PREV) s_mk[q] = 0;
         }
+        __syncthreads();
+        // pass 1: one hash entry per key, its last writer, its slot or that it is new
         bool ovf = false;
-        for (u32 base = 0; base < total; base += HM_EL_CH) {  // 1: latest i+1 per slot
-            load_chunk(base);
+        for (u32 base = 0; base < total; base += EL_CH) {
+            if (!one_chunk || p == 0) load_chunk(base);
 #pragma unroll
-            for (int r = 0; r < HM_EL_PER; r++) {
-                if (x[r].x == ~0ull) continue;
-                const u32 sl = (u32)(x[r].x >> 32);
-                if (!in_part(sl, p)) continue;
-                u32 h = (u32)(mix64(sl) & (HM_EL_HT - 1));
-                int pr = 0;
-                for (; pr < HM_EL_HT; pr++) {
-                    const u32 old = atomicCAS(&s_hk[h], 0xFFFFFFFFu, sl);
-                    if (old == 0xFFFFFFFFu || old == sl) break;
-                    h = (h + 1) & (HM_EL_HT - 1);
+            for (int r = 0; r < EL_PER; r++) {
+                if ((u32)x[r].x == 0) continue;
+                const u32 id = (u32)(x[r].x >> 32);
+                if (!in_part(id, p)) continue;
+                const u64 k = xk[r];
+                u32 h;
+                if (k == EMPTY_KEY) {
+                    h = (u32)EL_HT;
+                } else {
+                    h = el_hash(k);
+                    int pr = 0;
+                    for (; pr < EL_HT; pr++) {
+                        const u64 old = atomicCAS((unsigned long long*)&s_hk[h], (unsigned long long)EMPTY_KEY,
+                                                  (unsigned long long)k);
+                        if (old == EMPTY_KEY || old == k) break;
+                        h = (h + 1) & (EL_HT - 1);
+                    }
+                    if (pr == EL_HT) {
+                        ovf = true;
+                        continue;
+                    }
                 }
-                if (pr == HM_EL_HT) ovf = true;
-                else atomicMax(&s_hv[h], (u32)x[r].x);
+                atomicMax(&s_hp[h], base + r * TPB + threadIdx.x + 1);
+                if (id & NEW_BIT) atomicOr(&s_hf[h], 1u);
+                else s_hs[h] = id;  // the same slot for every entry of the key
             }
         }
-        if (__syncthreads_or(ovf)) {  // more distinct slots than the table holds: finer parts
+        if (j.exp & 2) return;
+        if (__syncthreads_or(ovf)) {  // more distinct keys than the table holds: finer parts
+            if (lp == j.bk_shift) {  // > EL_HT distinct new keys sharing one home slot
+                if (threadIdx.x == 0) atomicOr(&j.ctl->err, ERR_TABLE_FULL);
+                break;
+            }
             lp++;
             p = 0;
             continue;
         }
-        for (u32 base = 0; base < total; base += HM_EL_CH) {  // 2: the winners store their values
-            if (!one_chunk) load_chunk(base);
+        // slots of new keys (claims); values before the round for the previous-value walk
+        for (int h = threadIdx.x; h <= EL_HT; h += TPB) {
+            if (!s_hp[h]) continue;
+            if (h == EL_HT) {
+                s_hs[h] = SIDE_ID;
+                const bool present = j.ctl->sp_present != 0;
+                if (!present) created++;
+                if (PREV && present) {
+                    s_lv[h] = j.ctl->sp_val;
+                    s_hf[h] |= 2u;
+                }
+            } else if ((s_hf[h] & 1u) && (j.exp & 4)) {
+                s_hs[h] = FULL_SLOT;
+            } else if (s_hf[h] & 1u) {
+                const u64 k = s_hk[h];
+                bool fresh;
+                const long long sl = claim_slot(j.table, k, table_home(k, j.shift), j.tmask, &fresh);
+                if (sl < 0) {
+                    atomicOr(&j.ctl->err, ERR_TABLE_FULL);
+                    s_hs[h] = FULL_SLOT;
+                } else {
+                    s_hs[h] = (u32)sl;
+                    created += fresh;
+                    if (PREV && !fresh) {  // inserted earlier by a round not visible to index
+                        s_lv[h] = j.table[sl].val;
+                        s_hf[h] |= 2u;
+                    }
+                }
+            } else if (PREV) {
+                s_lv[h] = j.table[s_hs[h]].val;
+                s_hf[h] |= 2u;
+            }
+        }
+        __syncthreads();
+        if (!PREV) {
+            // pass 2: each key's last writer stores its value
+            for (u32 base = 0; base < total; base += EL_CH) {
+                if (!one_chunk) load_chunk(base);
 #pragma unroll
-            for (int r = 0; r < HM_EL_PER; r++) {
-                if (x[r].x == ~0ull) continue;
-                const u32 sl = (u32)(x[r].x >> 32);
-                if (!in_part(sl, p)) continue;
-                u32 h = (u32)(mix64(sl) & (HM_EL_HT - 1));
-                while (s_hk[h] != sl) h = (h + 1) & (HM_EL_HT - 1);
-                if (s_hv[h] == (u32)x[r].x) table[sl].val = x[r].y;
+                for (int r = 0; r < EL_PER; r++) {
+                    if ((u32)x[r].x == 0) continue;
+                    const u32 id = (u32)(x[r].x >> 32);
+                    if (!in_part(id, p)) continue;
+                    const u32 h = lookup(xk[r]);
+                    if (s_hp[h] != base + r * TPB + threadIdx.x + 1) continue;
+                    const u32 sl = s_hs[h];
+                    if (sl == SIDE_ID) {
+                        j.ctl->sp_val = x[r].y;
+                        j.ctl->sp_present = 1;
+                    } else if (sl != FULL_SLOT) {
+                        j.table[sl].val = x[r].y;
+                    }
+                }
+            }
+        } else {
+            // pass 2 (previous values): wave 0 walks the bucket in log order, 64 entries a step
+            for (u32 base = 0; base < total; base += EL_CH) {
+                fill_tiles(base);
+                __syncthreads();
+                const u32 end = total < base + EL_CH ? total : base + EL_CH;
+                if (w == 0) {
+                    for (u32 s0 = base; s0 < end; s0 += 64 * EL_WIN) {
+                        u64x2 ex[EL_WIN];
+                        u64 ek[EL_WIN];
+#pragma unroll
+                        for (int s = 0; s < EL_WIN; s++) {
+                            const u32 pos = s0 + s * 64 + lane;
+                            ex[s].x = 0;
+                            if (pos < end) {
+                                const u64 e = ent_at(pos, base);
+                                ex[s] = j.ent[e];
+                                ek[s] = j.ekey[e];
+                            }
+                        }
+#pragma unroll
+                        for (int s = 0; s < EL_WIN; s++) {
+                            const bool v = (u32)ex[s].x != 0 && in_part((u32)(ex[s].x >> 32), p);
+                            const u32 h = v ? lookup(ek[s]) : 0u;
+                            if (v) atomicOr((unsigned long long*)&s_mk[h], 1ull << lane);
+                            const u64 m = v ? s_mk[h] : 0ull;
+                            const u64 lower = m & ((1ull << lane) - 1);
+                            const int pl = lower ? 63 - __clzll((long long)lower) : lane;
+                            const u64 pv_lane = __shfl(ex[s].y, pl, 64);
+                            if (v) {
+                                u64 pv;
+                                uint8_t pf;
+                                if (lower) {
+                                    pv = pv_lane;
+                                    pf = 1;
+                                } else {
+                                    pf = (s_hf[h] >> 1) & 1u;
+                                    pv = pf ? s_lv[h] : 0;
+                                }
+                                const u64 g = j.lo + (u32)ex[s].x - 1;
+                                if (g >= j.resp_lo && g < j.resp_hi) {
+                                    j.prev[g - j.resp_lo] = pv;
+                                    j.prevf[g - j.resp_lo] = pf;
+                                }
+                                if ((m >> lane) == 1ull) {  // the key's last entry in this step
+                                    s_lv[h] = ex[s].y;
+                                    s_hf[h] |= 2u;
+                                    s_mk[h] = 0;
+                                }
+                            }
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+            // every key's last value
+            for (int h = threadIdx.x; h <= EL_HT; h += TPB) {
+                if (!s_hp[h]) continue;
+                const u32 sl = s_hs[h];
+                if (sl == SIDE_ID) {
+                    j.ctl->sp_val = s_lv[h];
+                    j.ctl->sp_present = 1;
+                } else if (sl != FULL_SLOT) {
+                    j.table[sl].val = s_lv[h];
+                }
             }
         }
         __syncthreads();
         p++;
     }
-    if (b == 0 && threadIdx.x == 0) {
-        const u64 st = *slot_stamp(&ctl->sp, epoch & 1);
-        if ((u32)(st >> 32) == epoch) ctl->sp.val = rec.at((u64)(u32)st - 1).val;
-    }
-}
-
-// Previous-value responses (HashMap::insert's return, nr/examples/hashmap.rs:46-50): with the
-// round's Puts stably sorted by slot, a Put's previous value is its in-group predecessor's
-// value, or the slot's value before the round (absent if the key was created in it). Runs
-// after index(e) and before apply(e), so slot values are still the pre-round ones.
-__global__ __launch_bounds__(TPB) void hm_prev_kernel(const u32* __restrict__ sk, const u32* __restrict__ sv, u64 n,
-                                                      RecSrc rec, const Slot* __restrict__ table, const DevCtl* ctl,
-                                                      u32 epoch, u64 resp_lo, u64 resp_hi, u64* __restrict__ prev,
-                                                      uint8_t* __restrict__ prevf) {
-    const u64 p = blockIdx.x * (u64)TPB + threadIdx.x;
-    if (p >= n) return;
-    const u32 s = sk[p];
-    const u64 gidx = rec.lo + sv[p];
-    if (gidx < resp_lo || gidx >= resp_hi) return;
-    u64 v = 0;
-    uint8_t f = 0;
-    if (p > 0 && sk[p - 1] == s) {
-        v = rec.at(sv[p - 1]).val;
-        f = 1;
-    } else if (s == SIDE_SLOT) {
-        const u32 cr = ctl->sp.created;
-        if (cr != 0 && cr != epoch) {
-            v = ctl->sp.val;
-            f = 1;
-        }
-    } else if (s != FULL_SLOT && table[s].created != epoch) {  // existed before the round
-        v = table[s].val;
-        f = 1;
-    }
-    prev[gidx - resp_lo] = v;
-    prevf[gidx - resp_lo] = f;
+    if (created) atomicAdd(&s_created, created);
+    __syncthreads();
+    if (threadIdx.x == 0 && s_created) atomicAdd(&j.created_acc[b % HM_CREATED_SLOTS], (u64)s_created);
 }
 
 __global__ __launch_bounds__(TPB) void hm_init_table_kernel(Slot* table, u64 slots) {
     for (u64 s = blockIdx.x * (u64)TPB + threadIdx.x; s < slots; s += (u64)gridDim.x * TPB) {
-        Slot z = {};
-        z.key = EMPTY_KEY;
-        table[s] = z;
+        u64x2 z;
+        z.x = EMPTY_KEY;
+        z.y = 0;
+        *(u64x2*)&table[s] = z;
     }
 }
 
 // NrHashMap::default (benches/hashmap.rs:91-100): keys 0..n-1 -> k + off, inserted directly.
 __global__ __launch_bounds__(TPB) void hm_prefill_range_kernel(Slot* table, u64 n, u64 off, u32 shift, u64 tmask,
-                                                               DevCtl* ctl, u32 epoch) {
+                                                               DevCtl* ctl) {
     __shared__ u32 s_ins;
     if (threadIdx.x == 0) s_ins = 0;
     __syncthreads();
     u32 inserted = 0;
     for (u64 k = blockIdx.x * (u64)TPB + threadIdx.x; k < n; k += (u64)gridDim.x * TPB) {
-        u64 s = table_home(k, shift);
-        bool done = false;
-        for (u64 pr = 0; pr <= tmask && !done; pr++) {
-            const u64 old = atomicCAS(&table[s].key, EMPTY_KEY, k);
-            if (old == EMPTY_KEY || old == k) {
-                table[s].val = k + off;
-                if (old == EMPTY_KEY) table[s].created = epoch;
-                inserted += old == EMPTY_KEY;
-                done = true;
-            }
-            s = (s + 1) & tmask;
+        if (k == EMPTY_KEY) {  // only reachable for n = 2^64, kept for the full key domain
+            inserted += ctl->sp_present == 0;
+            ctl->sp_val = k + off;
+            ctl->sp_present = 1;
+            continue;
         }
-        if (!done) atomicOr(&ctl->err, ERR_TABLE_FULL);
+        bool fresh;
+        const long long s = claim_slot(table, k, table_home(k, shift), tmask, &fresh);
+        if (s < 0) {
+            atomicOr(&ctl->err, ERR_TABLE_FULL);
+            continue;
+        }
+        table[s].val = k + off;
+        inserted += fresh;
     }
     if (inserted) atomicAdd(&s_ins, inserted);
     __syncthreads();
@@ -576,17 +926,17 @@ __global__ __launch_bounds__(TPB) void hm_count_kernel(const u64* __restrict__ a
 __global__ __launch_bounds__(TPB) void hm_dump_kernel(const Slot* __restrict__ table, u64 slots, DevCtl* ctl,
                                                       u64* __restrict__ ok, u64* __restrict__ ov) {
     const u64 gid = blockIdx.x * (u64)TPB + threadIdx.x;
-    if (gid == 0 && ctl->sp.created) {
+    if (gid == 0 && ctl->sp_present) {
         const u64 i = atomicAdd(&ctl->counter, 1ull);
         ok[i] = EMPTY_KEY;
-        ov[i] = ctl->sp.val;
+        ov[i] = ctl->sp_val;
     }
     for (u64 s = gid; s < slots; s += (u64)gridDim.x * TPB) {
-        const u64 k = table[s].key;
-        if (k != EMPTY_KEY) {
+        const u64x2 e = *(const u64x2*)&table[s];
+        if (e.x != EMPTY_KEY) {
             const u64 i = atomicAdd(&ctl->counter, 1ull);
-            ok[i] = k;
-            ov[i] = table[s].val;
+            ok[i] = e.x;
+            ov[i] = e.y;
         }
     }
 }
@@ -596,16 +946,16 @@ __global__ __launch_bounds__(TPB) void hm_digest_kernel(const Slot* __restrict__
     __shared__ u64 s_c[TPB / 64], s_s[TPB / 64], s_x[TPB / 64];
     const u64 gid = blockIdx.x * (u64)TPB + threadIdx.x;
     u64 c = 0, sm = 0, x = 0;
-    if (gid == 0 && ctl->sp.created) {
-        const u64 h = mix64(EMPTY_KEY ^ mix64(ctl->sp.val));
+    if (gid == 0 && ctl->sp_present) {
+        const u64 h = mix64(EMPTY_KEY ^ mix64(ctl->sp_val));
         c++;
         sm += h;
         x ^= h;
     }
     for (u64 s = gid; s < slots; s += (u64)gridDim.x * TPB) {
-        const u64 k = table[s].key;
-        if (k != EMPTY_KEY) {
-            const u64 h = mix64(k ^ mix64(table[s].val));
+        const u64x2 e = *(const u64x2*)&table[s];
+        if (e.x != EMPTY_KEY) {
+            const u64 h = mix64(e.x ^ mix64(e.y));
             c++;
             sm += h;
             x ^= h;
@@ -662,274 +1012,6 @@ static inline unsigned grid_for(u64 n, u64 cap = 4096) {
     return (unsigned)g;
 }
 
-// ---- owner path: partitioned replay of large rounds (no election atomics, no apply pass) -----
-//
-// A round's Puts are split by the top 8 bits of mix64(key) (the home slot's top bits) into
-// 256 buckets; every key belongs to exactly one bucket, and one block of hm_own_kernel owns
-// each (bucket, sub-bucket). That block picks every key's last writer in LDS and stores the
-// value into the slot itself, so no global atomicMax elects writers and no apply pass runs:
-//
-//   hm_part_kernel  tiles of 1024 Puts in ticket order: dedup by key in LDS (the tile's last
-//                   writer and its value), count per bucket, decoupled look-back over the
-//                   tiles' per-bucket counts (the rs_pass scheme), scatter (key, value) into
-//                   fixed-capacity bucket regions. Look-back offsets keep tile order inside a
-//                   region, so a key's last writer is its LAST entry in the region. Entries past
-//                   a region's capacity go to an overflow list with their would-be position.
-//   hm_own_kernel   per (bucket, sub-bucket): the max region position per key in LDS, then
-//                   find-or-claim the slot and store the value; the side-slot key rides the
-//                   usual stamp (one atomicMax per Put of key u64::MAX, applied by block 0).
-//
-// Reads of the round run after hm_own_kernel (next launch) and see the values in the slots.
-//
-// Status: opt-in (NRG_OWNER_MIN), parity-green, SLOWER than the stamp path on MI355X
-// (profiles/r01_variants/owner_path.txt): at 800k Puts + 900k Gets per round 135 us vs 110 us
-// (part 40 us, own 65 us); at B1 65 us vs 37 us. The part pass alone has a ~10 us latency
-// floor (load, LDS count, look-back, scatter) plus 7 us of LDS dedup at 100k Puts, so the
-// global atomics it removes (45 us at 800k) are not recovered. Kept for the next round's work
-// on the write path.
-constexpr int PT_KP = 8;
-constexpr int PT_TILE = TPB * PT_KP;  // 2048 Puts per part tile
-constexpr int PT_LDS = 2 * PT_TILE;   // dedup table entries
-constexpr int NBKT = 256;             // buckets (one look-back digit per thread)
-constexpr int OW_LDS = 2048;          // per-block key table of hm_own_kernel
-constexpr u32 OW_CLASS = 1024;        // region entries per class (table load <= 1/2)
-constexpr int OW_K = OW_LDS / TPB;    // elected keys per thread, loads issued together
-constexpr u32 PT_AGG = 1u << 30, PT_INC = 2u << 30, PT_MASK = 3u << 30, PT_CNT = (1u << 30) - 1;
-constexpr int PT_WIN = 32;
-
-__device__ __forceinline__ u32 bucket_of(u64 x) { return (u32)(x >> 56); }  // x = mix64(key)
-
-struct PartBufs {
-    u32* ticket;   // [1]
-    u32* ovf_cnt;  // [1]
-    u32* desc;     // [tiles][NBKT] look-back granules {status:2, count:30}
-    u64* bkey;     // [NBKT][cap]
-    u64* bval;     // [NBKT][cap]
-    u64* okey;     // overflow entries
-    u64* oval;
-    u32* opos;     // would-be region position
-    u32* obkt;     // bucket
-    u64 cap;
-};
-
-__global__ __launch_bounds__(TPB) void hm_part_kernel(RecSrc rec, nrg_put* ring_out, u64 n, u32 epoch, PartBufs pb,
-                                                      DevCtl* ctl) {
-    __shared__ u64 s_key[PT_LDS];
-    __shared__ u32 s_max[PT_LDS];  // 1 + the tile offset of the key's last writer
-    __shared__ u32 s_cnt[NBKT];
-    __shared__ u32 s_excl[NBKT];
-    __shared__ u32 s_tile;
-    const int t = threadIdx.x;
-    if (t == 0) s_tile = atomicAdd(pb.ticket, 1u);
-    for (int q = t; q < PT_LDS; q += TPB) {
-        s_key[q] = EMPTY_KEY;
-        s_max[q] = 0;
-    }
-    s_cnt[t] = 0;
-    __syncthreads();
-    const u32 tile = s_tile;
-    const u64 base = (u64)tile * PT_TILE;
-    const u32 par = epoch & 1;
-    nrg_put r[PT_KP];
-#pragma unroll
-    for (int q = 0; q < PT_KP; q++) {
-        const u64 i = base + (u64)q * TPB + t;
-        r[q] = i < n ? rec.at(i) : nrg_put{EMPTY_KEY, 0};
-    }
-    u32 hh[PT_KP];
-#pragma unroll
-    for (int q = 0; q < PT_KP; q++) {
-        const u64 i = base + (u64)q * TPB + t;
-        hh[q] = 0xFFFFFFFFu;
-        if (i >= n) continue;
-        if (ring_out) ring_out[(rec.lo + i) & rec.mask] = r[q];
-        const u64 k = r[q].key;
-        if (k == EMPTY_KEY) {  // the side-slot key keeps the stamp election (hm_own_kernel applies it)
-            atomicMax(slot_stamp(&ctl->sp, par), stamp_of(epoch, i));
-            continue;
-        }
-        u32 h = (u32)(mix64(k) >> 20) & (PT_LDS - 1);
-        for (;;) {
-            const u64 old = atomicCAS(&s_key[h], EMPTY_KEY, k);
-            if (old == EMPTY_KEY || old == k) break;
-            h = (h + 1) & (PT_LDS - 1);
-        }
-        atomicMax(&s_max[h], (u32)(i - base) + 1u);
-        hh[q] = h;
-    }
-    __syncthreads();
-    // per-bucket counts (the order inside a tile's run does not matter: one entry per key)
-    u32 rk[PT_LDS / TPB];
-#pragma unroll
-    for (int e = 0; e < PT_LDS / TPB; e++) {
-        const u64 k = s_key[e * TPB + t];
-        rk[e] = k != EMPTY_KEY ? atomicAdd(&s_cnt[bucket_of(mix64(k))], 1u) : 0u;
-    }
-    __syncthreads();
-    // thread t owns bucket t: publish the count, look back over earlier tiles
-    const u32 tcnt = s_cnt[t];
-    u32* my = pb.desc + (u64)tile * NBKT + t;
-    __hip_atomic_store(my, (tile == 0 ? PT_INC : PT_AGG) | tcnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    u32 excl = 0;
-    if (tile > 0) {
-        int tt = (int)tile - 1;
-        for (;;) {
-            u32 v[PT_WIN];
-#pragma unroll
-            for (int q = 0; q < PT_WIN; q++)
-                v[q] = tt - q >= 0 ? __hip_atomic_load(pb.desc + (u64)(tt - q) * NBKT + t, __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT)
-                                   : PT_INC;
-            int used = 0;
-            bool done = false;
-#pragma unroll
-            for (int q = 0; q < PT_WIN; q++) {
-                if (done || used < q) continue;
-                const u32 st = v[q] & PT_MASK;
-                if (st == 0) continue;
-                excl += v[q] & PT_CNT;
-                used = q + 1;
-                if (st == PT_INC) done = true;
-            }
-            if (done) break;
-            tt -= used;
-            if (used < PT_WIN) __builtin_amdgcn_s_sleep(1);
-        }
-        __hip_atomic_store(my, PT_INC | (excl + tcnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    s_excl[t] = excl;
-    __syncthreads();
-#pragma unroll
-    for (int e = 0; e < PT_LDS / TPB; e++) {
-        const u64 k = s_key[e * TPB + t];
-        if (k == EMPTY_KEY) continue;
-        const u32 b = bucket_of(mix64(k));
-        const u32 pos = s_excl[b] + rk[e];
-        const u64 v = rec.at(base + s_max[e * TPB + t] - 1).val;  // the tile's records are still cached
-        if (pos < pb.cap) {
-            pb.bkey[(u64)b * pb.cap + pos] = k;
-            pb.bval[(u64)b * pb.cap + pos] = v;
-        } else {
-            const u32 o = atomicAdd(pb.ovf_cnt, 1u);
-            pb.okey[o] = k;
-            pb.oval[o] = v;
-            pb.opos[o] = pos;
-            pb.obkt[o] = b;
-        }
-    }
-}
-
-__global__ __launch_bounds__(TPB) void hm_own_kernel(RecSrc rec, u32 epoch, u32 ntiles, PartBufs pb, u32 split,
-                                                     Slot* table, u32 shift, u64 tmask, DevCtl* ctl,
-                                                     u64* created_acc, u32* clear_desc, u64 clear_words,
-                                                     u32* clear_ctl) {
-    __shared__ u64 s_k[OW_LDS];
-    __shared__ u64 s_w[OW_LDS];  // max of ((region position + 1) << 32 | overflow index)
-    __shared__ uint16_t s_list[OW_LDS];
-    __shared__ u32 s_created, s_full, s_n;
-    const int t = threadIdx.x;
-    const u32 o = blockIdx.x;
-    const u32 b = o / split, sub = o % split;
-    // the other parity's buffers (used two owner rounds ago) are cleared for the next round
-    for (u64 q = (u64)o * TPB + t; q < clear_words; q += (u64)gridDim.x * TPB) clear_desc[q] = 0;
-    if (o == 0 && t < 2) clear_ctl[t] = 0;
-    const u32 total = pb.desc[(u64)(ntiles - 1) * NBKT + b] & PT_CNT;  // last tile's inclusive count
-    const u32 nin = total < pb.cap ? total : (u32)pb.cap;
-    const u32 novf = total > pb.cap ? *pb.ovf_cnt : 0u;
-    const u32 mine = (total + split - 1) / split;  // region entries of this sub-bucket, about
-    const u32 classes = mine > OW_CLASS ? (mine + OW_CLASS - 1) / OW_CLASS : 1u;
-    if (t == 0) {
-        s_created = 0;
-        s_full = 0;
-    }
-    u32 created = 0;
-    for (u32 c = 0; c < classes; c++) {
-        for (int q = t; q < OW_LDS; q += TPB) {
-            s_k[q] = EMPTY_KEY;
-            s_w[q] = 0;
-        }
-        __syncthreads();
-        for (u32 p = t; p < nin + novf; p += TPB) {
-            u64 k, w;
-            if (p < nin) {
-                k = pb.bkey[(u64)b * pb.cap + p];
-                w = ((u64)(p + 1) << 32);
-            } else {
-                const u32 q = p - nin;
-                if (pb.obkt[q] != b) continue;
-                k = pb.okey[q];
-                w = ((u64)(pb.opos[q] + 1) << 32) | q;
-            }
-            const u64 x = mix64(k);
-            if (((x >> 40) & (split - 1)) != sub) continue;
-            if (classes > 1 && (u32)((x >> 8) % classes) != c) continue;
-            u32 h = (u32)(x >> 20) & (OW_LDS - 1);
-            u32 tries = 0;
-            for (;;) {
-                const u64 old = atomicCAS(&s_k[h], EMPTY_KEY, k);
-                if (old == EMPTY_KEY || old == k) break;
-                h = (h + 1) & (OW_LDS - 1);
-                if (++tries == OW_LDS) {
-                    s_full = 1;
-                    break;
-                }
-            }
-            if (tries < OW_LDS) atomicMax(&s_w[h], w);
-        }
-        __syncthreads();
-        // compact the elected keys, then give each thread up to OW_K of them with every value
-        // load and first probe in flight together
-        if (t == 0) s_n = 0;
-        __syncthreads();
-#pragma unroll
-        for (int e = 0; e < OW_K; e++) {
-            const int q = e * TPB + t;
-            if (s_k[q] != EMPTY_KEY) s_list[atomicAdd(&s_n, 1u)] = (uint16_t)q;
-        }
-        __syncthreads();
-        const u32 nl = s_n;
-        u64 kk[OW_K], vv[OW_K], k0[OW_K], hs[OW_K];
-#pragma unroll
-        for (int e = 0; e < OW_K; e++) {
-            const u32 li = (u32)e * TPB + t;
-            kk[e] = EMPTY_KEY;
-            if (li >= nl) continue;
-            const u32 q = s_list[li];
-            kk[e] = s_k[q];
-            const u64 w = s_w[q];
-            const u32 pos = (u32)(w >> 32) - 1;
-            vv[e] = pos < pb.cap ? pb.bval[(u64)b * pb.cap + pos] : pb.oval[(u32)w];
-            hs[e] = table_home(kk[e], shift);
-            k0[e] = table[hs[e]].key;
-        }
-#pragma unroll
-        for (int e = 0; e < OW_K; e++) {
-            if (kk[e] == EMPTY_KEY) continue;
-            const long long sl = find_or_claim(table, kk[e], hs[e], tmask, k0[e], epoch, &created);
-            if (sl < 0) {
-                atomicOr(&ctl->err, ERR_TABLE_FULL);
-                continue;
-            }
-            table[sl].val = vv[e];
-        }
-        __syncthreads();
-    }
-    if (s_full) atomicOr(&ctl->err, ERR_TABLE_FULL);  // LDS table overflow (hash skew): reported, not hidden
-    if (o == 0 && t == 0) {  // the side slot
-        const u64 st = *slot_stamp(&ctl->sp, epoch & 1);
-        if ((u32)(st >> 32) == epoch) {
-            if (ctl->sp.created == 0) {
-                ctl->sp.created = epoch;
-                created++;
-            }
-            ctl->sp.val = rec.at((u64)(u32)st - 1).val;
-        }
-    }
-    if (created) atomicAdd(&s_created, created);
-    __syncthreads();
-    if (t == 0 && s_created) atomicAdd(&created_acc[o % HM_CREATED_SLOTS], (u64)s_created);
-}
-
 // ---- host side ----------------------------------------------------------------------------
 static RecSrc ring_src(nrg_ctx* c, const nrg_put* src, u64 lo) {
     RecSrc r;
@@ -940,74 +1022,110 @@ static RecSrc ring_src(nrg_ctx* c, const nrg_put* src, u64 lo) {
     return r;
 }
 
-template <int K1, int G, bool BK = false>
-static void launch_round(nrg_ctx* c, const IndexJob& ij, const ApplyJob& aj, const ReadJob& rj) {
-    const u32 blocks = ij.nblocks + aj.nblocks + rj.nblocks;
-    NRG_LAUNCH(c, "hm_round", (hm_round_kernel<K1, G, BK>), blocks, TPB, 0, c->stream, ij, aj, rj, c->d_table,
-               c->slot_shift, (u64)(c->slots - 1), c->d_ctl);
+// Puts per index thread: 2 up to 2^18 Puts per round, 4 above (fewer, larger tiles keep the
+// elector's count rows short and the per-block dedup effective on hot keys). NRG_K1 overrides.
+static u32 k1_for(const nrg_ctx* c, u64 n) {
+    u32 k = n > (1u << 18) ? 4u : 2u;
+    if (c->k1_items) k = c->k1_items >= 4 ? 4u : c->k1_items >= 2 ? 2u : 1u;
+    while (k < 4 && (n + TPB * k - 1) / (TPB * k) > HM_MAX_BATCH / (TPB * 4)) k *= 2;  // elector LDS bound
+    return k;
 }
 
-// Puts per index thread in bucket rounds: 4 below 600k Puts, 8 above (400k + 900k Gets: 64.3
-// vs 68.4 us per round; 500k + 500k: 67.9 vs 71.9; 800k + 900k: 99.7 vs 95.7). NRG_BK_K1 overrides.
-static u32 bk_k1(const nrg_ctx* c, u64 n) { return c->bk_k1 ? c->bk_k1 : (n >= 600000 ? 8u : 4u); }
+// Overlay rounds: 1 Put per index thread up to 2^17 Puts, 2 above (NRG_K1 overrides).
+static u32 ov_k1_for(const nrg_ctx* c, u64 n) {
+    if (c->k1_items) return c->k1_items >= 2 ? 2u : 1u;
+    return n > (1u << 17) ? 2u : 1u;
+}
 
-static hipError_t launch(nrg_ctx* c, IndexJob& ij, ApplyJob& aj, ReadJob& rj) {
-    // Puts per index thread: a hot key costs one same-address stamp atomic per index block
-    // that holds it (same-address atomics serialise), so large (write-heavy) rounds use fewer,
-    // bigger blocks (Zipf 0.99 at 50 % writes: 99 us with 1, 79 with 4, 65 with 8; uniform
-    // unchanged); small rounds use 2 (B1: 36.4 us with 1 or 2, 39.0 with 4; Zipf 0.99 at 10 %
-    // writes: 54.2 with 1, 47.7 with 2, 39.2 with 4). NRG_K1_ITEMS overrides.
-    const bool bk = ij.bk_ent != nullptr;  // bucket election: 8 Puts per index thread
-    const u32 k1 = bk ? bk_k1(c, ij.n) : c->k1_items ? c->k1_items : (ij.n >= (1u << 18) ? 8 : 2);
-    const u32 K1 = k1 >= 8 ? 8 : k1 >= 4 ? 4 : (k1 == 2 ? 2 : 1);
-    const u32 G = c->gets_per_thread >= 4 ? 4 : (c->gets_per_thread == 2 ? 2 : 1);
-    ij.exp = c->exp;
-    ij.created_acc = c->d_created;
-    if (c->exp & 4) aj.n = 0;
-    if (c->exp & 8) ij.n = 0;
-    ij.nblocks = (u32)((ij.n + TPB * K1 - 1) / (TPB * K1));
-    aj.nblocks = (u32)((aj.n + TPB - 1) / TPB);
-    rj.nblocks = (u32)((rj.R + TPB * G - 1) / (TPB * G));
-    if (ij.nblocks + aj.nblocks + rj.nblocks == 0) return hipSuccess;
-    if (bk) {
-        if (K1 == 4) launch_round<4, 1, true>(c, ij, aj, rj);
-        else if (K1 == 2) launch_round<2, 1, true>(c, ij, aj, rj);
-        else launch_round<8, 1, true>(c, ij, aj, rj);
-        return hipGetLastError();
+// The jobs of one hm_round_kernel launch.
+struct Launch {
+    IndexJob ij{};
+    OvIndexJob oj{};
+    OvListJob aj{};
+    OvListJob cj{};
+    ReadJob rj{};
+    OvReadCtx ro{};
+    int ix = IX_BUCKET;
+    u32 K1 = 1;
+    u32 nb = 0;
+};
+
+static u32 ov_list_blocks(const OvRound& r) {  // one thread per list position of the round
+    return (u32)(((u64)r.nblocks * r.tile + TPB - 1) / TPB);
+}
+
+// Roles every launch carries: the deferred round's apply (overlay) and reads, and the clear of
+// the overlay applied by the previous launch.
+static void attach_deferred(nrg_ctx* c, Launch& L) {
+    const HmDeferred& p = c->pend;
+    L.aj.exp = L.ro.exp = c->exp & 0xFF;
+    if (p.valid) {
+        L.rj.keys = p.keys;
+        L.rj.R = p.R;
+        L.rj.vals = p.vals;
+        L.rj.found = p.found;
+        if (p.ov.valid) {
+            const u32 x = p.ov.idx;
+            const RecSrc rs = ring_src(c, p.ov.src, p.ov.lo);
+            L.aj.ov = c->d_ov[x];
+            L.aj.list = c->d_ov_list[x];
+            L.aj.lcnt = c->d_ov_cnt[x];
+            L.aj.ltile = p.ov.tile;
+            L.aj.side_st = &c->d_ctl->sp_st[x];
+            L.aj.rec = rs;
+            L.aj.created_acc = c->d_created;
+            L.aj.nblocks = ov_list_blocks(p.ov);
+            L.ro.ov = c->d_ov[x];
+            L.ro.omask = (1ull << c->ov_log2) - 1;
+            L.ro.side_st = &c->d_ctl->sp_st[x];
+            L.ro.rec = rs;
+        }
     }
-#define NRG_RK(A, B) \
-    if (K1 == A && G == B) launch_round<A, B>(c, ij, aj, rj)
-    NRG_RK(1, 1); else NRG_RK(1, 2); else NRG_RK(1, 4); else NRG_RK(2, 1); else NRG_RK(2, 2); else NRG_RK(2, 4);
-    else NRG_RK(4, 1); else NRG_RK(4, 2); else NRG_RK(4, 4); else NRG_RK(8, 1);
+    if (c->ov_clear.valid) {
+        const u32 x = c->ov_clear.idx;
+        L.cj.ov_w = c->d_ov[x];
+        L.cj.list = c->d_ov_list[x];
+        L.cj.lcnt = c->d_ov_cnt[x];
+        L.cj.ltile = c->ov_clear.tile;
+        L.cj.side_st = &c->d_ctl->sp_st[x];
+        L.cj.nblocks = ov_list_blocks(c->ov_clear);
+    }
+    // state after this launch: the deferred half ran; the overlay it applied is cleared next
+    c->ov_clear = p.valid ? p.ov : OvRound{};
+    c->pend = HmDeferred{};
+}
+
+template <int K1, int IX>
+static void launch_round(nrg_ctx* c, const Launch& L, u32 blocks, unsigned lds) {
+    NRG_LAUNCH(c, "hm_round", (hm_round_kernel<K1, IX>), blocks, TPB, lds, c->stream, L.ij, L.oj, L.aj, L.cj, L.rj,
+               L.ro, c->d_table, c->slot_shift, (u64)(c->slots - 1), c->d_ctl);
+}
+
+static hipError_t launch(nrg_ctx* c, Launch& L) {
+    L.rj.nblocks = (u32)((L.rj.R + TPB - 1) / TPB);
+    const u32 nix = L.ix == IX_OVERLAY ? L.oj.nblocks : L.ij.nblocks;
+    const u32 blocks = nix + L.aj.nblocks + L.cj.nblocks + L.rj.nblocks;
+    if (blocks == 0) return hipSuccess;
+    const bool dedup = L.ix != IX_BUCKET_ALL;
+    const u32 nb = L.ix == IX_OVERLAY ? 0u : L.nb;
+    unsigned lds = 0;
+    if (nix) lds = L.K1 == 4 ? IndexLds<4>::bytes(dedup, nb) : L.K1 == 2 ? IndexLds<2>::bytes(dedup, nb)
+                                                                          : IndexLds<1>::bytes(dedup, nb);
+    if (!nix) launch_round<1, IX_BUCKET>(c, L, blocks, 0);
+#define NRG_RK(KK, XX) else if (L.K1 == KK && L.ix == XX) launch_round<KK, XX>(c, L, blocks, lds)
+    NRG_RK(1, IX_BUCKET); NRG_RK(1, IX_BUCKET_ALL); NRG_RK(1, IX_OVERLAY);
+    NRG_RK(2, IX_BUCKET); NRG_RK(2, IX_BUCKET_ALL); NRG_RK(2, IX_OVERLAY);
+    NRG_RK(4, IX_BUCKET); NRG_RK(4, IX_BUCKET_ALL); NRG_RK(4, IX_OVERLAY);
 #undef NRG_RK
+    else return hipErrorInvalidValue;
     return hipGetLastError();
 }
 
-static void deferred_jobs(nrg_ctx* c, ApplyJob& aj, ReadJob& rj) {
-    aj = ApplyJob{};
-    rj = ReadJob{};
-    const HmDeferred& p = c->pend;
-    if (!p.valid) return;
-    aj.rec = ring_src(c, p.src, p.lo);
-    aj.n = p.n;
-    aj.put_slot = c->d_put_slot[p.epoch & 1];
-    aj.epoch = p.epoch;
-    rj.rec = aj.rec;
-    rj.keys = p.keys;
-    rj.R = p.R;
-    rj.vals = p.vals;
-    rj.found = p.found;
-    rj.epoch = p.epoch;
-}
-
 hipError_t hm_flush(nrg_ctx* c) {
-    if (!c->pend.valid) return hipSuccess;
-    IndexJob ij{};
-    ApplyJob aj;
-    ReadJob rj;
-    deferred_jobs(c, aj, rj);
-    c->pend.valid = false;
-    return launch(c, ij, aj, rj);
+    if (!c->pend.valid && !c->ov_clear.valid) return hipSuccess;
+    Launch L;
+    attach_deferred(c, L);
+    return launch(c, L);
 }
 
 // Reads against the current state (no writes): attached to the deferred round if it has none.
@@ -1022,74 +1140,48 @@ static hipError_t hm_reads(nrg_ctx* c, const u64* keys, u64 R, u64* vals, uint8_
     }
     hipError_t e = hm_flush(c);
     if (e != hipSuccess) return e;
-    IndexJob ij{};
-    ApplyJob aj{};
-    ReadJob rj{};
-    rj.keys = keys;
-    rj.R = R;
-    rj.vals = vals;
-    rj.found = found;
-    rj.epoch = c->epoch;  // every earlier round is applied: values come from the slots
-    return launch(c, ij, aj, rj);
+    Launch L;
+    attach_deferred(c, L);  // a pending overlay clear rides along
+    L.rj.keys = keys;
+    L.rj.R = R;
+    L.rj.vals = vals;
+    L.rj.found = found;
+    return launch(c, L);
 }
 
-hipError_t hm_owner_alloc(nrg_ctx* c, u64 mb) {
-    OwnerBufs& ob = c->own;
-    ob.cap = 2 * ((mb + NBKT - 1) / NBKT) + 4096;
-    const u64 tiles = (mb + PT_TILE - 1) / PT_TILE;
+hipError_t hm_alloc(nrg_ctx* c, u64 mb) {
+    const u64 tiles = (mb + TPB - 1) / TPB;  // index tiles of >= TPB Puts
+    const u64 ents = tiles * TPB;
     hipError_t e;
-#define OB_ALLOC(P, BYTES)                     \
-    if ((e = hipMalloc(&(P), (BYTES))) != hipSuccess) return e;
-    OB_ALLOC(ob.ctl, 4 * sizeof(u32));
-    OB_ALLOC(ob.desc[0], tiles * NBKT * sizeof(u32));
-    OB_ALLOC(ob.desc[1], tiles * NBKT * sizeof(u32));
-    OB_ALLOC(ob.bkey, NBKT * ob.cap * sizeof(u64));
-    OB_ALLOC(ob.bval, NBKT * ob.cap * sizeof(u64));
-    OB_ALLOC(ob.okey, mb * sizeof(u64));
-    OB_ALLOC(ob.oval, mb * sizeof(u64));
-    OB_ALLOC(ob.opos, mb * sizeof(u32));
-    OB_ALLOC(ob.obkt, mb * sizeof(u32));
-#undef OB_ALLOC
-    if ((e = hipMemsetAsync(ob.ctl, 0, 4 * sizeof(u32), c->stream)) != hipSuccess) return e;
-    for (int i = 0; i < 2; i++)
-        if ((e = hipMemsetAsync(ob.desc[i], 0, tiles * NBKT * sizeof(u32), c->stream)) != hipSuccess) return e;
+    if ((e = hipMalloc(&c->d_bk_ent, ents * 16)) != hipSuccess) return e;
+    if ((e = hipMalloc(&c->d_bk_key, ents * 8)) != hipSuccess) return e;
+    if ((e = hipMalloc(&c->d_bk_cnt, (u64)HM_BK_MAX * tiles * sizeof(u32))) != hipSuccess) return e;
+    if (c->ov_max > mb) c->ov_max = mb;
+    if (!c->ov_max) return hipSuccess;
+    // overlays of >= 2x the largest overlay round (load <= 1/2), three in rotation
+    c->ov_log2 = 10;
+    while ((1ull << c->ov_log2) < 2 * c->ov_max) c->ov_log2++;
+    const u64 oslots = 1ull << c->ov_log2;
+    const u64 otiles = (c->ov_max + TPB - 1) / TPB + 1;
+    for (int i = 0; i < 3; i++) {
+        if ((e = hipMalloc(&c->d_ov[i], oslots * sizeof(OvSlot))) != hipSuccess) return e;
+        if ((e = hipMalloc(&c->d_ov_list[i], otiles * TPB * 4 * sizeof(u32))) != hipSuccess) return e;
+        if ((e = hipMalloc(&c->d_ov_cnt[i], otiles * sizeof(u32))) != hipSuccess) return e;
+        hm_init_table_kernel<<<grid_for(oslots, 4096), TPB, 0, c->stream>>>((Slot*)c->d_ov[i], oslots);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     return hipSuccess;
 }
 
-void hm_owner_free(nrg_ctx* c) {
-    OwnerBufs& ob = c->own;
-    void* ptrs[] = {ob.ctl, ob.desc[0], ob.desc[1], ob.bkey, ob.bval, ob.okey, ob.oval, ob.opos, ob.obkt};
-    for (void* p : ptrs)
-        if (p) (void)hipFree(p);
-    ob = OwnerBufs{};
-}
-
-// One owner-path round (see hm_part_kernel): partition, then elect + store per bucket.
-static hipError_t owner_round(nrg_ctx* c, const nrg_put* src, nrg_put* ring_out, u64 lo, u64 n, u32 epoch) {
-    OwnerBufs& ob = c->own;
-    const u32 set = c->owner_rounds++ & 1;
-    PartBufs pb;
-    pb.ticket = ob.ctl + 2 * set;
-    pb.ovf_cnt = ob.ctl + 2 * set + 1;
-    pb.desc = ob.desc[set];
-    pb.bkey = ob.bkey;
-    pb.bval = ob.bval;
-    pb.okey = ob.okey;
-    pb.oval = ob.oval;
-    pb.opos = ob.opos;
-    pb.obkt = ob.obkt;
-    pb.cap = ob.cap;
-    const u64 tiles = (n + PT_TILE - 1) / PT_TILE;
-    const RecSrc rs = ring_src(c, src, lo);
-    NRG_LAUNCH(c, "hm_part", hm_part_kernel, (unsigned)tiles, TPB, 0, c->stream, rs, ring_out, n, epoch, pb, c->d_ctl);
-    u32 split = 1;  // sub-buckets per bucket: about <= 768 region entries per owner block
-    while ((u64)split * NBKT * 768 < n && split < 64) split <<= 1;
-    NRG_LAUNCH(c, "hm_own", hm_own_kernel, NBKT * split, TPB, 0, c->stream, rs, epoch, (u32)tiles, pb, split,
-               c->d_table, c->slot_shift, (u64)(c->slots - 1), c->d_ctl, c->d_created, ob.desc[set ^ 1],
-               ob.tiles[set ^ 1] * NBKT, ob.ctl + 2 * (set ^ 1));
-    ob.tiles[set] = tiles;
-    ob.tiles[set ^ 1] = 0;  // cleared by this launch
-    return hipGetLastError();
+void hm_free(nrg_ctx* c) {
+    for (int i = 0; i < 3; i++) {
+        void* ptrs[] = {c->d_ov[i], c->d_ov_list[i], c->d_ov_cnt[i]};
+        for (void* q : ptrs)
+            if (q) (void)hipFree(q);
+        c->d_ov[i] = nullptr;
+        c->d_ov_list[i] = nullptr;
+        c->d_ov_cnt[i] = nullptr;
+    }
 }
 
 hipError_t hm_init(nrg_ctx* c) {
@@ -1101,86 +1193,111 @@ hipError_t hm_init(nrg_ctx* c) {
 // ring copy if write_ring) and answer R reads against the state after them.
 hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool write_ring, const u64* d_get_keys,
                            u64 R, u64* d_get_vals, uint8_t* d_get_found, u64 resp_lo, u64 resp_hi, u64* d_prev,
-                           uint8_t* d_prev_found, bool touch_log) {
-    (void)touch_log;
+                           uint8_t* d_prev_found) {
     if (n == 0) return hm_reads(c, d_get_keys, R, d_get_vals, d_get_found);
+    if (n > HM_MAX_BATCH) return hipErrorInvalidValue;
     const nrg_put* src = (const nrg_put*)src_recs;
     const bool want_prev = d_prev && resp_lo < lo + n && resp_hi > lo;
-    if (c->owner_min && n >= c->owner_min && !want_prev) {
-        // the previous round's apply + reads see the table before this round's stores
-        hipError_t e = hm_flush(c);
-        if (e != hipSuccess) return e;
-        const u32 epoch = ++c->epoch;
-        e = owner_round(c, src, write_ring ? (nrg_put*)c->d_ring : nullptr, lo, n, epoch);
-        if (e != hipSuccess) return e;
-        const nrg_put* keep = (src && !write_ring) ? src : nullptr;
-        HmDeferred& p = c->pend;  // reads only: the values are already in the slots
+    // records the deferred half reads: the caller's buffer only when no ring copy is written
+    const nrg_put* keep = (src && !write_ring) ? src : nullptr;
+    hipError_t e;
+    if (!want_prev && c->ov_max && n <= c->ov_max) {
+        // ---- overlay round: one launch {index(e) | apply(e-1) | clear(e-2) | reads(e-1)} ----
+        const u32 idx = c->ov_next;
+        if (c->ov_clear.valid && c->ov_clear.idx == idx && (e = hm_flush(c)) != hipSuccess) return e;
+        c->ov_next = (idx + 1) % 3;
+        const u32 K1 = ov_k1_for(c, n);
+        const u32 tile = TPB * K1;
+        Launch L;
+        L.ix = IX_OVERLAY;
+        L.K1 = K1;
+        L.oj.rec = ring_src(c, src, lo);
+        L.oj.ring_out = write_ring ? (nrg_put*)c->d_ring : nullptr;
+        L.oj.n = n;
+        L.oj.nblocks = (u32)((n + tile - 1) / tile);
+        L.oj.ov = c->d_ov[idx];
+        L.oj.omask = (1ull << c->ov_log2) - 1;
+        L.oj.list = c->d_ov_list[idx];
+        L.oj.lcnt = c->d_ov_cnt[idx];
+        L.oj.side_st = &c->d_ctl->sp_st[idx];
+        L.oj.exp = c->exp & 0xFF;
+        attach_deferred(c, L);
+        if ((e = launch(c, L)) != hipSuccess) return e;
+        c->rounds++;
+        HmDeferred& p = c->pend;
         p.valid = true;
-        p.epoch = epoch;
-        p.src = keep;
-        p.lo = lo;
-        p.n = 0;
+        p.ov.valid = true;
+        p.ov.idx = idx;
+        p.ov.src = keep;
+        p.ov.lo = lo;
+        p.ov.nblocks = L.oj.nblocks;
+        p.ov.tile = tile;
         p.keys = d_get_keys;
         p.R = R;
         p.vals = d_get_vals;
         p.found = d_get_found;
         if (!c->pipeline || keep) return hm_flush(c);
-        return hipGetLastError();
+        return hipSuccess;
     }
-    const u32 epoch = ++c->epoch;
-    IndexJob ij{};
+    // ---- bucket round: {index(e) | clear | reads(e-1)}, then hm_elect_kernel(e) ----
+    // its index pass reads the main table: a deferred overlay apply must not run beside it
+    if (c->pend.valid && c->pend.ov.valid && (e = hm_flush(c)) != hipSuccess) return e;
+    const u32 K1 = k1_for(c, n);
+    const u32 tile = TPB * K1;
+    // slot buckets of about bk_ent entries (previous values keep every Put: smaller buckets)
+    const u64 target = c->bk_ent ? c->bk_ent : (want_prev ? 256 : 512);
+    const u32 log2_slots = 64 - c->slot_shift;
+    u32 nb_log = 6;
+    while ((1ull << nb_log) * target < n && (1u << nb_log) < HM_BK_MAX) nb_log++;
+    if (nb_log > log2_slots) nb_log = log2_slots;
+    Launch L;
+    L.ix = want_prev ? IX_BUCKET_ALL : IX_BUCKET;
+    L.K1 = K1;
+    L.nb = 1u << nb_log;
+    IndexJob& ij = L.ij;
     ij.rec = ring_src(c, src, lo);
     ij.ring_out = write_ring ? (nrg_put*)c->d_ring : nullptr;
     ij.n = n;
-    ij.put_slot = c->d_put_slot[epoch & 1];
-    ij.epoch = epoch;
-    const bool bk = c->elect_min && n >= c->elect_min && !want_prev;
-    if (bk) {  // buckets of about 1024 entries (a power of two in [64, HM_BK_MAX])
-        u32 nb_log = 6;
-        while ((1ull << nb_log) * 1024 < n && (1u << nb_log) < HM_BK_MAX) nb_log++;
-        if (nb_log > 64 - c->slot_shift) nb_log = 64 - c->slot_shift;
-        ij.bk_ent = (u64x2*)c->d_bk_ent;
-        ij.bk_cnt = c->d_bk_cnt;
-        ij.bk_nb = 1u << nb_log;
-        ij.bk_shift = (64 - c->slot_shift) - nb_log;
-    }
-    ApplyJob aj;
-    ReadJob rj;
-    deferred_jobs(c, aj, rj);  // the previous round's second half rides along
-    c->pend.valid = false;
-    hipError_t e = launch(c, ij, aj, rj);
-    if (e != hipSuccess) return e;
-    // records of this round for its deferred half: the ring copy if there is one
-    const nrg_put* keep = (src && !write_ring) ? src : nullptr;
-    if (bk) {
-        const u32 nblocks = ij.nblocks;  // index tiles of TPB * bk_k1 Puts
-        NRG_LAUNCH(c, "hm_elect", hm_elect_kernel, ij.bk_nb, TPB, (nblocks + 1) * 4 + nblocks * 2, c->stream, (const u64x2*)c->d_bk_ent,
-                   c->d_bk_cnt, nblocks, TPB * bk_k1(c, n), ij.bk_shift, ring_src(c, keep, lo), c->d_table, c->d_ctl, epoch);
-        e = hipGetLastError();
-        if (e != hipSuccess) return e;
-    }
-    if (d_prev && resp_lo < lo + n && resp_hi > lo) {
-        u32 *sk = nullptr, *sv = nullptr;
-        timer_begin(c, "hm_prev", c->stream);
-        // slot ids < 2^31; the side-slot (0xFFFFFFFF) and full (0xFFFFFFFE) markers sort last
-        e = sort_pairs(c->sort, c->d_put_slot[epoch & 1], nullptr, n, 32, c->stream, &sk, &sv);
-        if (e != hipSuccess) return e;
-        hm_prev_kernel<<<(unsigned)((n + TPB - 1) / TPB), TPB, 0, c->stream>>>(
-            sk, sv, n, ring_src(c, keep, lo), c->d_table, c->d_ctl, epoch, resp_lo, resp_hi, d_prev, d_prev_found);
-        timer_end(c, "hm_prev", c->stream);
-    }
+    ij.nblocks = (u32)((n + tile - 1) / tile);
+    ij.nb_log = nb_log;
+    ij.bk_shift = log2_slots - nb_log;
+    ij.ent = (u64x2*)c->d_bk_ent;
+    ij.ekey = c->d_bk_key;
+    ij.cnt = c->d_bk_cnt;
+    ij.exp = c->exp & 0xFF;
+    attach_deferred(c, L);  // the previous round's reads ride along
+    if ((e = launch(c, L)) != hipSuccess) return e;
+    ElectJob ej{};
+    ej.ent = ij.ent;
+    ej.ekey = ij.ekey;
+    ej.cnt = ij.cnt;
+    ej.nblocks = ij.nblocks;
+    ej.tile = tile;
+    ej.bk_shift = ij.bk_shift;
+    ej.table = c->d_table;
+    ej.shift = c->slot_shift;
+    ej.tmask = c->slots - 1;
+    ej.ctl = c->d_ctl;
+    ej.created_acc = c->d_created;
+    ej.lo = lo;
+    ej.resp_lo = resp_lo;
+    ej.resp_hi = resp_hi;
+    ej.prev = d_prev;
+    ej.prevf = d_prev_found;
+    ej.exp = c->exp >> 8;
+    const unsigned dyn = (ij.nblocks + 1) * 4 + ij.nblocks * 2;
+    if (want_prev) NRG_LAUNCH(c, "hm_elect", hm_elect_kernel<true>, 1u << nb_log, TPB, dyn, c->stream, ej);
+    else NRG_LAUNCH(c, "hm_elect", hm_elect_kernel<false>, 1u << nb_log, TPB, dyn, c->stream, ej);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    c->rounds++;
     HmDeferred& p = c->pend;
     p.valid = true;
-    p.epoch = epoch;
-    p.src = keep;
-    p.lo = lo;
-    p.n = bk ? 0 : n;  // bucket rounds were applied by hm_elect_kernel: reads only
     p.keys = d_get_keys;
     p.R = R;
     p.vals = d_get_vals;
     p.found = d_get_found;
-    if (!c->pipeline || keep) return hm_flush(c);
-    return hipGetLastError();
+    if (!c->pipeline) return hm_flush(c);
+    return hipSuccess;
 }
 
 hipError_t hm_get_only(nrg_ctx* c, const u64* d_keys, u64 n, u64* d_vals, uint8_t* d_found) {
@@ -1190,10 +1307,8 @@ hipError_t hm_get_only(nrg_ctx* c, const u64* d_keys, u64 n, u64* d_vals, uint8_
 hipError_t hm_prefill_range(nrg_ctx* c, u64 n, u64 off) {
     hipError_t e = hm_flush(c);
     if (e != hipSuccess) return e;
-    // a fresh epoch: later reads see these values in the slots, not an older round's record
-    const u32 epoch = ++c->epoch;
     hm_prefill_range_kernel<<<grid_for(n, 8192), TPB, 0, c->stream>>>(c->d_table, n, off, c->slot_shift,
-                                                                      c->slots - 1, c->d_ctl, epoch);
+                                                                      c->slots - 1, c->d_ctl);
     return hipGetLastError();
 }
 

@@ -45,32 +45,26 @@ struct Staging {  // growable device scratch for the host-pointer entry points
     uint64_t bytes = 0;
 };
 
-// The apply + read half of a replayed hashmap round, kept for the next launch.
+// An overlay round of the hashmap replay (hashmap.hip): overlay `idx` holds its last writers,
+// list_idx / cnt_idx the overlay slots it inserted, per index block of `tile` Puts.
+struct OvRound {
+    bool valid = false;
+    u32 idx = 0;
+    const nrg_put* src = nullptr;  // records: src[i] if set, else ring[(lo + i) & mask]
+    u64 lo = 0;
+    u32 nblocks = 0;
+    u32 tile = 0;
+};
+
+// The second half of the last replayed hashmap round, run in the next launch (beside the next
+// round's index pass) or by a flush: its reads, and for an overlay round its apply.
 struct HmDeferred {
     bool valid = false;
-    u32 epoch = 0;
-    const nrg_put* src = nullptr;  // records of the round: src[i] if set, else ring[(lo + i) & mask]
-    u64 lo = 0, n = 0;
+    OvRound ov;                 // overlay round whose apply is deferred (ov.valid)
     const u64* keys = nullptr;  // the round's reads (R may be 0)
     u64 R = 0;
     u64* vals = nullptr;
     uint8_t* found = nullptr;
-};
-
-// Buffers of the partitioned (owner) replay of large hashmap rounds (hashmap.hip). Look-back
-// descriptors, ticket and overflow counter come in two sets used by alternate owner rounds:
-// hm_own_kernel clears the set the next owner round will use.
-struct OwnerBufs {
-    u32* ctl = nullptr;                 // [2][2]: ticket, overflow count per set
-    u32* desc[2] = {nullptr, nullptr};  // [tiles][256] per set
-    u64* bkey = nullptr;                // [256][cap] bucket regions
-    u64* bval = nullptr;
-    u64* okey = nullptr;                // [max_batch] overflow entries
-    u64* oval = nullptr;
-    u32* opos = nullptr;
-    u32* obkt = nullptr;
-    u64 cap = 0;
-    u64 tiles[2] = {0, 0};              // tiles the last round of each set used
 };
 
 struct HostRun {  // origin tags of appended log ranges (the Entry::replica field)
@@ -99,27 +93,28 @@ struct nrg_ctx {
     uint32_t slot_shift = 0;  // 64 - log2_slots
     uint64_t slots = 0;
     nrg::Slot* d_table = nullptr;
-    uint32_t* d_put_slot[2] = {nullptr, nullptr};  // per Put of a round: its slot (by epoch parity)
-    uint32_t epoch = 0;              // replay rounds so far (stamps carry the round's epoch)
-    uint32_t k1_items = 0;           // Puts per thread in the index role (0: by round size; NRG_K1_ITEMS)
-    uint32_t gets_per_thread = 1;    // Gets per thread in the read role (tuning knob NRG_GETS)
-    uint32_t exp = 0;                // diagnostic knobs (NRG_EXP), see hashmap.hip IndexJob::exp
-    // Deferred second half of the last replayed round (apply its values, answer its reads):
-    // launched together with the next round's index pass, or by nrg_join / nrg_sync / any call
-    // that reads the table. With pipeline == false it is flushed at the end of every call.
+    uint64_t rounds = 0;             // replay rounds launched (statistics)
+    uint32_t k1_items = 0;           // Puts per index thread (0: by round size; NRG_K1 overrides)
+    uint32_t bk_ent = 0;             // target entries per elector bucket (0: default; NRG_BK_ENT)
+    uint32_t exp = 0;                // diagnostic knobs (NRG_EXP; see hashmap.hip IndexJob/ElectJob)
+    // Reads of the last replayed round: answered in the next launch beside the next round's
+    // index pass, or by nrg_join / nrg_sync / any call that reads the table. With
+    // pipeline == false they are flushed at the end of every call.
     bool pipeline = false;
     nrg::HmDeferred pend;
     uint64_t* d_created = nullptr;  // [HM_CREATED_SLOTS] keys created by replay rounds
-    // Rounds of >= owner_min Puts take the partitioned path (0: never; NRG_OWNER_MIN).
-    uint64_t owner_min = 0;
-    uint32_t owner_rounds = 0;
-    // Rounds of >= elect_min Puts elect last writers per slot bucket in LDS (hm_elect_kernel)
-    // instead of stamp atomics (0: never; NRG_ELECT_MIN overrides the default).
-    uint64_t elect_min = 0;
-    uint32_t bk_k1 = 0;  // Puts per index thread in bucket rounds (0: by size; 2, 4, 8: NRG_BK_K1)
-    void* d_bk_ent = nullptr;      // [tiles of 2048] 16-B {slot << 32 | i+1, value} per index block
-    uint32_t* d_bk_cnt = nullptr;  // [HM_BK_MAX][tiles] offset << 16 | count
-    nrg::OwnerBufs own;
+    void* d_bk_ent = nullptr;       // [index tiles][tile] 16-B {id << 32 | i+1, value}
+    uint64_t* d_bk_key = nullptr;   // [index tiles][tile] key of each entry
+    uint32_t* d_bk_cnt = nullptr;   // [bucket][index tiles] offset << 16 | count
+    // Overlay rounds (<= ov_max Puts, no previous values): three rotating overlays, lists of the
+    // overlay slots each round inserted; ov_clear = applied overlay round still to be cleared.
+    uint64_t ov_max = 0;
+    uint32_t ov_log2 = 0;
+    uint32_t ov_next = 0;
+    nrg::OvRound ov_clear;
+    nrg::OvSlot* d_ov[3] = {nullptr, nullptr, nullptr};
+    uint32_t* d_ov_list[3] = {nullptr, nullptr, nullptr};
+    uint32_t* d_ov_cnt[3] = {nullptr, nullptr, nullptr};
     // Zipf generator cache: zeta(zipf_n, zipf_theta)
     uint64_t zipf_n = 0;
     double zipf_theta = 0.0, zipf_zetan = 0.0;
@@ -167,18 +162,19 @@ bool timer_events(nrg_ctx* c, const char* name, hipEvent_t* start, hipEvent_t* s
         else                                                                                            \
             KERNEL<<<(GRID), (BLOCK), (SHMEM), (STREAM)>>>(__VA_ARGS__);                                \
     } while (0)
-// launch the deferred apply + reads of the last hashmap round, if any (hashmap.hip)
+// make the context's device current for this thread (runtime.cpp; cached per thread)
+int ctx_use_device(nrg_ctx* c);
+// launch the deferred reads of the last hashmap round, if any (hashmap.hip)
 hipError_t hm_flush(nrg_ctx* c);
 
 // hashmap.hip
 hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool write_ring,
                            const u64* d_get_keys, u64 R, u64* d_get_vals, uint8_t* d_get_found,
-                           u64 resp_lo, u64 resp_hi, u64* d_prev, uint8_t* d_prev_found,
-                           bool touch_log);
+                           u64 resp_lo, u64 resp_hi, u64* d_prev, uint8_t* d_prev_found);
 hipError_t hm_get_only(nrg_ctx* c, const u64* d_keys, u64 n, u64* d_vals, uint8_t* d_found);
 hipError_t hm_init(nrg_ctx* c);
-hipError_t hm_owner_alloc(nrg_ctx* c, u64 max_batch);
-void hm_owner_free(nrg_ctx* c);
+hipError_t hm_alloc(nrg_ctx* c, u64 max_batch);  // per-round scratch (entries, counts, overlays)
+void hm_free(nrg_ctx* c);
 hipError_t hm_prefill_range(nrg_ctx* c, u64 n, u64 off);
 hipError_t hm_dump(nrg_ctx* c, u64* d_keys, u64* d_vals);
 hipError_t hm_count(nrg_ctx* c);  // DevCtl::nkeys_total = number of keys

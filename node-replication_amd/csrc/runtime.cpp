@@ -72,9 +72,10 @@ int use_device(nrg_ctx* c) {
 hipError_t hm_flush_if(nrg_ctx* c) { return c->cfg.ds_kind == NRG_DS_HASHMAP ? hm_flush(c) : hipSuccess; }
 
 // Log GC boundary: the slowest replica's tail (this replica's ltail), held back to the first
-// record of a deferred hashmap round, whose apply still reads its records from the ring.
+// record of a deferred hashmap overlay round, whose apply and reads take values from the ring.
 uint64_t gc_head(const nrg_ctx* c) {
-    if (c->pend.valid && !c->pend.src && c->pend.lo < c->ltail) return c->pend.lo;
+    const nrg::OvRound& o = c->pend.ov;
+    if (c->pend.valid && o.valid && !o.src && o.lo < c->ltail) return o.lo;
     return c->ltail;
 }
 
@@ -110,7 +111,7 @@ int exec_range(nrg_ctx* c, uint64_t resp_lo, uint64_t resp_hi, void* d_resp, uin
         switch (c->cfg.ds_kind) {
             case NRG_DS_HASHMAP:
                 e = hm_replay_chunk(c, nullptr, lo, n, false, nullptr, 0, nullptr, nullptr, resp_lo, resp_hi,
-                                    (u64*)d_resp, d_some, true);
+                                    (u64*)d_resp, d_some);
                 break;
             case NRG_DS_STACK:
                 e = st_replay_chunk(c, lo, n, resp_lo, resp_hi, (uint32_t*)d_resp, d_some);
@@ -184,6 +185,7 @@ int staging(nrg_ctx* c, Staging& st, uint64_t bytes) {
 }  // namespace
 
 namespace nrg {
+int ctx_use_device(nrg_ctx* c) { return use_device(c); }
 // c->timing_only: empty (time every kernel) or a comma-separated list of kernel names
 static bool timer_match(const nrg_ctx* c, const char* name) {
     if (c->timing_only.empty()) return true;
@@ -269,11 +271,12 @@ const char* nrg_strerror(int code) {
         case NRG_E_NOT_SYNCED: return "replica not synced to the log tail";
         case NRG_E_CAPACITY: return "capacity exceeded";
         case NRG_E_NODEV: return "no such HIP device";
+        case NRG_E_COMM: return "RCCL unavailable or a collective failed";
         default: return "unknown error";
     }
 }
 
-const char* nrg_version(void) { return "nrgpu 0.1 gfx950"; }
+const char* nrg_version(void) { return "nrgpu 0.2 gfx950"; }
 
 int nrg_device_count(void) {
     int n = 0;
@@ -325,37 +328,25 @@ int nrg_open(int dev, const nrg_config* cfg_in, nrg_ctx** out) {
 
     const uint64_t mb = cf.max_batch;
     if (cf.ds_kind == NRG_DS_HASHMAP) {
-        // slot ids are u32 with two reserved values: at most 2^31 slots (64 GiB)
-        if (cf.log2_slots < 4 || cf.log2_slots > 31) { nrg_close(c); return NRG_E_INVAL; }
+        // slot ids are < 2^30 (entry ids carry two flag values above them, hashmap.hip);
+        // replay chunks are bounded by the elector's per-tile LDS tables (HM_MAX_BATCH)
+        if (cf.log2_slots < 4 || cf.log2_slots > 30 || mb > HM_MAX_BATCH) { nrg_close(c); return NRG_E_INVAL; }
         c->slots = 1ull << cf.log2_slots;
         c->slot_shift = 64 - cf.log2_slots;
         OPEN_CHK(hipMalloc(&c->d_table, c->slots * sizeof(Slot)));
         OPEN_CHK(hm_init(c));
-        OPEN_CHK(hipMalloc(&c->d_put_slot[0], mb * sizeof(uint32_t)));
-        OPEN_CHK(hipMalloc(&c->d_put_slot[1], mb * sizeof(uint32_t)));
         OPEN_CHK(hipMalloc(&c->d_created, HM_CREATED_SLOTS * sizeof(uint64_t)));
         OPEN_CHK(hipMemsetAsync(c->d_created, 0, HM_CREATED_SLOTS * sizeof(uint64_t), c->stream));
-        if (const char* e = std::getenv("NRG_K1_ITEMS")) c->k1_items = (uint32_t)std::atoi(e);
-        if (const char* e = std::getenv("NRG_GETS")) c->gets_per_thread = (uint32_t)std::atoi(e);
+        // rounds of <= ov_max Puts without previous values replay in one launch (overlay rounds)
+        c->ov_max = 1u << 18;
+        if (const char* e = std::getenv("NRG_OV_MAX")) c->ov_max = (uint64_t)std::atoll(e);
+        OPEN_CHK(hm_alloc(c, mb));
+        // tuning knobs: Puts per index thread, target entries per elector bucket
+        if (const char* e = std::getenv("NRG_K1")) c->k1_items = (uint32_t)std::atoi(e);
+        if (const char* e = std::getenv("NRG_BK_ENT")) c->bk_ent = (uint32_t)std::atoi(e);
         if (const char* e = std::getenv("NRG_EXP")) c->exp = (uint32_t)std::atoi(e);
-        if (const char* e = std::getenv("NRG_OWNER_MIN")) c->owner_min = (uint64_t)std::atoll(e);
-        if (c->owner_min) OPEN_CHK(hm_owner_alloc(c, mb));  // buffers only when the path is enabled
-        // Rounds of >= 250k Puts elect per slot bucket (hm_elect_kernel) instead of stamp atomics:
-        // measured crossover between 200k Puts (+ 900k Gets: 45.7 us stamp vs 49.3 bucket) and
-        // 300k (61.3 vs 56.2); 800k: 112.5 vs 94.3; Zipf 0.99 at 50 % writes: 64.9 vs 47.4.
-        // profiles/r01_bucket_election.txt
-        c->elect_min = 250000;
-        if (const char* e = std::getenv("NRG_ELECT_MIN")) c->elect_min = (uint64_t)std::atoll(e);
-        if (const char* e = std::getenv("NRG_BK_K1")) c->bk_k1 = std::atoi(e) >= 8 ? 8 : std::atoi(e) >= 4 ? 4 : 2;
-        if (c->elect_min && mb >= c->elect_min) {
-            const uint64_t tiles = (mb + 511) / 512;  // index tiles of 256 x (2, 4 or 8) Puts
-            OPEN_CHK(hipMalloc(&c->d_bk_ent, tiles * 512 * 2 * sizeof(uint64_t)));
-            OPEN_CHK(hipMalloc(&c->d_bk_cnt, (uint64_t)HM_BK_MAX * tiles * sizeof(uint32_t)));
-        }
         c->pipeline = cf.pipeline != 0;
         if (const char* e = std::getenv("NRG_PIPELINE")) c->pipeline = std::atoi(e) != 0;
-        c->epoch = 1;  // epoch 1 = the state built by prefill; replay rounds start at 2
-        if (sort_alloc(c->sort, mb) != NRG_OK) { nrg_close(c); return NRG_E_NOMEM; }
     } else if (cf.ds_kind == NRG_DS_STACK) {
         // max_batch <= 2^24: st_cross_kernel stages one minimum per 2048-op tile in LDS
         if (!cf.stack_capacity || cf.stack_capacity >= (1ull << 31) || mb > (1ull << 24)) {
@@ -370,7 +361,6 @@ int nrg_open(int dev, const nrg_config* cfg_in, nrg_ctx** out) {
         OPEN_CHK(hipMalloc(&c->d_scan_desc, c->scan_desc_words * 4));
         OPEN_CHK(hipMemsetAsync(c->d_scan_desc, 0, c->scan_desc_words * 4, c->stream));
         OPEN_CHK(hipMalloc(&c->d_st_aux, st_aux_bytes(mb)));
-        if (const char* e = std::getenv("NRG_EXP")) c->exp = (uint32_t)std::atoi(e);
     } else {
         const uint64_t T = cf.synth_hot_writes + cf.synth_cold_writes;
         if (!cf.synth_n || cf.synth_hot_reads == 0 || cf.synth_n <= cf.synth_hot_reads || T == 0 || T > 64 ||
@@ -387,7 +377,6 @@ int nrg_open(int dev, const nrg_config* cfg_in, nrg_ctx** out) {
         OPEN_CHK(hipMalloc(&c->d_scan_desc, c->scan_desc_words * 4));
         if (sort_alloc(c->sort, mb * T) != NRG_OK) { nrg_close(c); return NRG_E_NOMEM; }
         // sort-free bucket replay where the config allows it; NRG_SY_SORT=1 keeps the sort path
-        if (const char* e = std::getenv("NRG_EXP")) c->exp = (uint32_t)std::atoi(e);
         const char* force_sort = std::getenv("NRG_SY_SORT");
         if (sy_bucket_eligible(cf) && !(force_sort && std::atoi(force_sort)))
             OPEN_CHK(hipMalloc(&c->d_sy_aux, sy_bucket_aux_bytes(cf)));
@@ -405,13 +394,13 @@ int nrg_close(nrg_ctx* c) {
     g_dev_set = c->device;
     if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
     if (c->stream && c->stream != c->own_stream) (void)hipStreamSynchronize(c->stream);
-    void* ptrs[] = {c->d_ring,    c->d_ctl,      c->d_table,   c->d_put_slot[0], c->d_put_slot[1],
-                    c->d_stack,   c->d_words,    c->d_sort_aux, c->d_tmp_u64,    c->d_scan_desc,
-                    c->d_created, c->d_st_aux,   c->d_sy_aux,   c->d_bk_ent,     c->d_bk_cnt};
+    void* ptrs[] = {c->d_ring,    c->d_ctl,      c->d_table,    c->d_stack,  c->d_words,
+                    c->d_sort_aux, c->d_tmp_u64, c->d_scan_desc, c->d_created, c->d_st_aux,
+                    c->d_sy_aux,  c->d_bk_ent,   c->d_bk_key,   c->d_bk_cnt};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     sort_free(c->sort);
-    hm_owner_free(c);
+    hm_free(c);
     Staging* s = stg(c);
     for (int i = 0; i < 4; i++)
         if (s[i].p) (void)hipFree(s[i].p);
@@ -424,10 +413,23 @@ int nrg_close(nrg_ctx* c) {
 
 int nrg_set_stream(nrg_ctx* c, void* s) {
     if (!c) return NRG_E_INVAL;
+    int r = use_device(c);
+    if (r) return r;
     // deferred hashmap work belongs to the old stream: launch it there first
     hipError_t e = hm_flush_if(c);
     if (e != hipSuccess) return hip_fail(e);
-    c->stream = (hipStream_t)s;  // NULL: the device's null stream, as in HIP
+    hipStream_t ns = (hipStream_t)s;  // NULL: the device's null stream, as in HIP
+    if (ns != c->stream) {
+        // everything already queued on the old stream (the replica's table, ring and scratch)
+        // comes before anything the new stream runs from now on
+        hipEvent_t ev;
+        HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        e = hipEventRecord(ev, c->stream);
+        if (e == hipSuccess) e = hipStreamWaitEvent(ns, ev, 0);
+        (void)hipEventDestroy(ev);
+        if (e != hipSuccess) return hip_fail(e);
+    }
+    c->stream = ns;
     return NRG_OK;
 }
 
@@ -555,6 +557,10 @@ int nrg_log_state(const nrg_ctx* c, nrg_log_info* o) {
 
 int nrg_log_reset(nrg_ctx* c) {
     if (!c) return NRG_E_INVAL;
+    int r = use_device(c);
+    if (r) return r;
+    // a deferred hashmap read batch belongs to the log positions being reset: answer it now
+    HIPCHK(hm_flush_if(c));
     c->head = c->tail = c->ctail = c->ltail = 0;
     c->origins.clear();
     return NRG_OK;
@@ -603,7 +609,7 @@ int nrg_hashmap_round_async(nrg_ctx* c, const nrg_put* d_puts, uint64_t W, uint3
     const uint64_t lo = c->tail;
     if (!d_prev || !d_prev_found) d_prev = nullptr, d_prev_found = nullptr;
     HIPCHK(hm_replay_chunk(c, d_puts, lo, W, true, d_get_keys, R, d_get_vals, d_get_found, lo, lo + W, d_prev,
-                           d_prev_found, true));
+                           d_prev_found));
     if (W) note_origin(c, lo, W, origin);
     c->tail = lo + W;
     c->ltail = c->tail;
@@ -622,7 +628,7 @@ static int hm_exec_with_gets(nrg_ctx* c, uint64_t resp_lo, uint64_t resp_hi, uin
         const bool last = lo + n == c->tail;
         HIPCHK(hm_replay_chunk(c, nullptr, lo, n, false, last ? d_get_keys : nullptr, last ? R : 0,
                                last ? d_get_vals : nullptr, last ? d_get_found : nullptr, resp_lo, resp_hi, d_prev,
-                               d_prevf, true));
+                               d_prevf));
         c->ltail = lo + n;
     }
     if (c->ctail < c->ltail) c->ctail = c->ltail;
@@ -655,7 +661,7 @@ int nrg_hashmap_round_segments_async(nrg_ctx* c, const nrg_put* d_base, uint32_t
         // the gathered segments are already the contiguous round W_0 || W_1 || ...: replay them
         // in place while K1 writes the log copy (no separate append pass)
         HIPCHK(hm_replay_chunk(c, d_base, lo, total, true, d_get_keys, R, d_get_vals, d_get_found, rlo, rhi, d_prev,
-                               d_prev_found, true));
+                               d_prev_found));
         for (uint32_t s = 0, off = 0; s < nseg; off += (uint32_t)lens[s], s++)
             if (lens[s]) note_origin(c, lo + off, lens[s], origins ? origins[s] : s + 1);
         c->tail = lo + total;
@@ -689,8 +695,7 @@ int nrg_hashmap_prefill(nrg_ctx* c, const uint64_t* keys, const uint64_t* vals, 
         if (e != hipSuccess) return hip_fail(e);
         // direct insert (no log traffic): replay the records through the round pipeline
         // with a private log position, so duplicate keys keep last-writer-wins order.
-        HIPCHK(hm_replay_chunk(c, s[0].p, 0, m, false, nullptr, 0, nullptr, nullptr, 0, 0, nullptr, nullptr,
-                               false));
+        HIPCHK(hm_replay_chunk(c, s[0].p, 0, m, false, nullptr, 0, nullptr, nullptr, 0, 0, nullptr, nullptr));
         done += m;
     }
     HIPCHK(sync_all(c));
@@ -795,6 +800,10 @@ int nrg_stack_len(nrg_ctx* c, uint64_t* n) {
     long long d = 0;
     HIPCHK(hipMemcpyAsync(&d, &c->d_ctl->depth, sizeof(d), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(sync_all(c));
+    // an overflowing chunk latches ERR_CAPACITY once but keeps counting: never report (or
+    // let dump/peek copy) more elements than the allocation holds
+    if (d < 0) d = 0;
+    if ((uint64_t)d > c->cfg.stack_capacity) d = (long long)c->cfg.stack_capacity;
     *n = (uint64_t)d;
     return check_err(c);
 }

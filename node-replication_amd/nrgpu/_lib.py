@@ -28,6 +28,8 @@ NRG_E_NOMEM = -5
 NRG_E_NOT_SYNCED = -6
 NRG_E_CAPACITY = -7
 NRG_E_NODEV = -8
+NRG_E_COMM = -9
+NRG_GROUP_ID_BYTES = 128
 
 NRG_DS_HASHMAP = 1
 NRG_DS_STACK = 2
@@ -74,6 +76,21 @@ class LogInfo(C.Structure):
         ("ltail", C.c_uint64),
         ("replica_id", C.c_uint32),
         ("ds_kind", C.c_uint32),
+    ]
+
+
+class Round(C.Structure):
+    """nrg_round: one group member's part of a round (device pointers on its GPU)."""
+
+    _fields_ = [
+        ("recs", C.c_void_p),
+        ("n", C.c_uint64),
+        ("resp", C.c_void_p),
+        ("some", C.c_void_p),
+        ("get_keys", C.c_void_p),
+        ("n_gets", C.c_uint64),
+        ("get_vals", C.c_void_p),
+        ("get_found", C.c_void_p),
     ]
 
 
@@ -133,6 +150,15 @@ SIGNATURES = {
     "nrg_kernel_timing": (C.c_int, [vp, C.c_int]),
     "nrg_kernel_timing_only": (C.c_int, [vp, C.c_char_p]),
     "nrg_kernel_time": (C.c_int, [vp, C.c_char_p, u64p, C.POINTER(C.c_double)]),
+    "nrg_group_unique_id": (C.c_int, [vp]),
+    "nrg_group_join": (C.c_int, [vp, vp, C.c_int, C.c_int, C.POINTER(vp)]),
+    "nrg_group_open": (C.c_int, [C.POINTER(C.c_int), C.c_int, C.POINTER(Config), C.POINTER(vp)]),
+    "nrg_group_close": (C.c_int, [vp]),
+    "nrg_group_info": (C.c_int, [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "nrg_group_replica": (vp, [vp, C.c_int]),
+    "nrg_group_set_input_stream": (C.c_int, [vp, C.c_int, vp]),
+    "nrg_group_round_async": (C.c_int, [vp, C.POINTER(Round), u64p]),
+    "nrg_group_sync": (C.c_int, [vp]),
 }
 
 # include/nrgpu_testing.h (kernel unit-test hooks)

@@ -3,21 +3,96 @@
 In NR every replica replays every write (nr/src/log.rs:473-524, one exec loop per replica
 over the shared log); the reference shares the log through cache-coherent memory across
 NUMA nodes. Here each GPU is a NUMA node: per round, every rank contributes the write segment
-its clients produced, the segments are all-gathered (torch.distributed all_gather_into_tensor,
-i.e. RCCL over xGMI with the "nccl" backend), and every replica replays the identical global
-log W_0 || W_1 || ... || W_{G-1} (concatenation by rank = the deterministic log order of the
-round), then answers its own reads against the post-round state. Responses to writes go only
-to the origin rank (nr/src/replica.rs:576-578). Reads never leave their GPU.
+its clients produced, the segments are all-gathered, and every replica replays the identical
+global log W_0 || W_1 || ... || W_{G-1} (concatenation by rank = the deterministic log order
+of the round), then answers its own reads against the post-round state. Responses to writes go
+only to the origin rank (nr/src/replica.rs:576-578). Reads never leave their GPU.
 
-The exchange is the only collective on the path; it is backend-agnostic so the
-host logic runs under `gloo` on CPU (tests) and `nccl` (RCCL) on MI355X.
+Two transports, one round semantics:
+  ReplicaGroup      the C ABI's group (nrg_group_join / nrg_group_round_async): RCCL over xGMI,
+                    called from libnrgpu.so on a library-owned stream per GPU, all-gather of
+                    round e+1 overlapping the replay of round e. The MI355X path.
+  ReplicatedLog /   the same rounds with the all-gather done by torch.distributed (gloo), for
+  ReplicatedHashMap multi-process tests on hosts without GPUs-per-rank (CPU `gloo` tests, the
+                    1-GPU box rehearsal); the replay is the same C-ABI call
+                    (nrg_hashmap_round_segments_async / append_segments + exec).
 """
 from __future__ import annotations
 
-from typing import Optional
+import ctypes as C
+from typing import Optional, Sequence
 
 import torch
 import torch.distributed as dist
+
+from . import _lib as L
+
+
+def _ptr(t) -> int:
+    if t is None:
+        return 0
+    return t if isinstance(t, int) else t.data_ptr()
+
+
+class ReplicaGroup:
+    """This process's replica as one member of a libnrgpu.so replica group (RCCL).
+
+    The group id (ncclUniqueId) is created by rank 0 and broadcast over the default
+    torch.distributed process group; every rank then joins with its own replica
+    (nrg_group_join, ncclCommInitRank on the replica's GPU)."""
+
+    def __init__(self, replica, rank: Optional[int] = None, world: Optional[int] = None,
+                 pg: Optional[dist.ProcessGroup] = None):
+        lib = L.load()
+        self.replica = replica
+        self.rank = dist.get_rank(pg) if rank is None else rank
+        self.world = dist.get_world_size(pg) if world is None else world
+        uid = (C.c_uint8 * L.NRG_GROUP_ID_BYTES)()
+        if self.rank == 0:
+            L.check(lib.nrg_group_unique_id(uid), "nrg_group_unique_id")
+        if self.world > 1:
+            obj = [bytes(uid)]
+            dist.broadcast_object_list(obj, src=0, group=pg)
+            uid = (C.c_uint8 * L.NRG_GROUP_ID_BYTES).from_buffer_copy(obj[0])
+        h = C.c_void_p()
+        L.check(lib.nrg_group_join(replica.handle, uid, self.world, self.rank, C.byref(h)), "nrg_group_join")
+        self._h = h
+        self._lib = lib
+        self._round = L.Round()
+        self._lens = None
+
+    def set_input_stream(self, stream_ptr: int):
+        """All-gathers wait only for work on this stream (where the inputs are produced)."""
+        L.check(self._lib.nrg_group_set_input_stream(self._h, 0, C.c_void_p(stream_ptr)))
+
+    def round_async(self, recs, n: int, resp=None, some=None, get_keys=None, n_gets: int = 0, get_vals=None,
+                    get_found=None, seg_lens: Optional[Sequence[int]] = None):
+        """One NR round (device tensors or raw pointers): all-gather + replay + local reads."""
+        r = self._round
+        r.recs, r.n, r.resp, r.some = _ptr(recs), n, _ptr(resp), _ptr(some)
+        r.get_keys, r.n_gets, r.get_vals, r.get_found = _ptr(get_keys), n_gets, _ptr(get_vals), _ptr(get_found)
+        lens = None
+        if seg_lens is not None:
+            if self._lens is None or list(self._lens) != list(seg_lens):
+                self._lens = (C.c_uint64 * self.world)(*seg_lens)
+            lens = self._lens
+        rc = self._lib.nrg_group_round_async(self._h, C.byref(r), lens)
+        if rc:
+            L.check(rc, "nrg_group_round_async")
+
+    def sync(self):
+        L.check(self._lib.nrg_group_sync(self._h), "nrg_group_sync")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.nrg_group_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
 
 
 class Gathered:
@@ -30,20 +105,16 @@ class Gathered:
 
     def wait(self):
         if self.work is not None:
-            self.work.wait()  # nccl: the current stream waits for the collective (host does not block)
+            self.work.wait()
             self.work = None
 
 
 class ReplicatedLog:
-    """One replica per rank of any NR data structure, driven in rounds of write segments.
+    """One replica per rank of any NR data structure, driven in rounds of write segments, with
+    the all-gather done by torch.distributed (gloo; see ReplicaGroup for RCCL).
 
-    round() = gather_async() + replay(). Callers that know the next round's writes early call
-    gather_async(next) before replay(current): the all-gather of round e+1 then runs on the
-    collective stream while round e replays (the replica's kernels copy the gathered records
-    into their own log ring, so a gathered buffer is free once its replay was enqueued; torch's
-    ProcessGroupNCCL orders each collective after the work already on the current stream).
-    Records are int64 tensors [W, words] (words = record bytes / 8: hashmap 2, stack 1).
-    """
+    round() = gather_async() + replay(). Records are int64 tensors [W, words] (words = record
+    bytes / 8: hashmap 2, stack 1, synthetic 4)."""
 
     NBUF = 3  # gathered-log buffers in rotation
 
@@ -53,29 +124,28 @@ class ReplicatedLog:
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.device = device if device is not None else torch.device("cpu")
-        self.backend = dist.get_backend(group)
         self.origins = [r + 1 for r in range(self.world)]  # replica ids start at 1 (nr/src/log.rs:272-292)
         self._bufs = [None] * self.NBUF
         self._next = 0
 
-    def _buf(self, need: int, device) -> torch.Tensor:
+    def _buf(self, need: int) -> torch.Tensor:
         i = self._next
         self._next = (i + 1) % self.NBUF
         b = self._bufs[i]
-        if b is None or b.numel() < need or b.device != device:
-            b = torch.empty(need, dtype=torch.int64, device=device)
+        if b is None or b.numel() < need:
+            b = torch.empty(need, dtype=torch.int64)
             self._bufs[i] = b
         return b[:need]
 
     def exchange_lengths(self, W: int):
-        t = torch.tensor([W], dtype=torch.int64, device=self.device if self.backend == "nccl" else "cpu")
+        t = torch.tensor([W], dtype=torch.int64)
         out = [torch.zeros_like(t) for _ in range(self.world)]
         dist.all_gather(out, t, group=self.group)
         return [int(x.item()) for x in out]
 
     def gather_async(self, recs: torch.Tensor, stride: Optional[int] = None, lens=None) -> Gathered:
-        """Start the all-gather of this rank's write segment (records in issue order). Fixed-size
-        rounds pass `stride` (segment capacity) and skip the length exchange."""
+        """All-gather this rank's write segment (records in issue order). Fixed-size rounds pass
+        `stride` (segment capacity) and skip the length exchange."""
         if recs.dim() == 1:
             recs = recs.reshape(-1, 1)
         W, words = recs.shape
@@ -83,19 +153,11 @@ class ReplicatedLog:
             lens = [W] * self.world if stride is not None else self.exchange_lengths(W)
         if stride is None:
             stride = max(lens) if lens else 0
-        seg = recs
-        if W < stride:
-            seg = torch.zeros((stride, words), dtype=torch.int64, device=recs.device)
-            seg[:W] = recs
-        seg = seg.reshape(-1)
-        need = self.world * stride * words
-        if self.backend == "gloo" and seg.device.type != "cpu":
-            out = self._buf(need, torch.device("cpu"))
-            dist.all_gather_into_tensor(out, seg.cpu(), group=self.group)
-            return Gathered(out.to(seg.device), None, stride, lens, words)
-        out = self._buf(need, seg.device)
-        work = dist.all_gather_into_tensor(out, seg.contiguous(), group=self.group, async_op=True)
-        return Gathered(out, work, stride, lens, words)
+        seg = torch.zeros((stride, words), dtype=torch.int64)
+        seg[:W] = recs.cpu()
+        out = self._buf(self.world * stride * words)
+        dist.all_gather_into_tensor(out, seg.reshape(-1), group=self.group)
+        return Gathered(out.to(recs.device), None, stride, lens, words)
 
     def replay(self, g: Gathered, resp: Optional[torch.Tensor] = None, some: Optional[torch.Tensor] = None):
         """Log::append of the gathered segments in rank order (the round's global log order),

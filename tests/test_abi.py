@@ -9,7 +9,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADERS = [os.path.join(ROOT, "include", h) for h in ("nrgpu.h", "nrgpu_testing.h")]
-DECL = re.compile(r"^\s*(?:const\s+)?(?:int|void|char)\s*\**\s*(nrg_\w+)\s*\(", re.M)
+DECL = re.compile(r"^\s*(?:const\s+)?(?:int|void|char|nrg_ctx)\s*\**\s*(nrg_\w+)\s*\(", re.M)
 
 
 def declared():
@@ -32,7 +32,9 @@ def test_header_parse_finds_the_abi():
     for must in ("nrg_open", "nrg_close", "nrg_log_append", "nrg_log_exec", "nrg_hashmap_get",
                  "nrg_hashmap_round_segments_async", "nrg_stack_peek", "nrg_synth_read", "nrg_test_sort_pairs"):
         assert must in names
-    assert len(names) >= 40
+    for must in ("nrg_group_open", "nrg_group_join", "nrg_group_round_async", "nrg_group_replica"):
+        assert must in names
+    assert len(names) >= 50
 
 
 def test_every_declared_symbol_is_exported(lib):
@@ -55,7 +57,7 @@ def test_non_compute_queries(lib):
     from nrgpu import _lib as L
 
     assert lib.nrg_version().decode().endswith("gfx950")
-    for code in range(0, -9, -1):
+    for code in range(0, -10, -1):
         assert lib.nrg_strerror(code)
     assert lib.nrg_device_count() >= 0
     cfg = L.Config()
@@ -95,3 +97,20 @@ def test_scaleout_csv_format(tmp_path):
                        "exp_time_in_sec", "iterations"]
     assert len(rows) == 5 and rows[1][6] == "0" and rows[2][6] == "1"
     assert int(rows[1][9]) == 2_000_000_000
+
+
+def test_group_api_argument_checks(lib):
+    """The RCCL group entry points reject bad arguments before touching RCCL or a device."""
+    from nrgpu import _lib as L
+
+    out = C.c_void_p()
+    assert lib.nrg_group_close(None) == L.NRG_E_INVAL
+    assert lib.nrg_group_sync(None) == L.NRG_E_INVAL
+    assert lib.nrg_group_round_async(None, None, None) == L.NRG_E_INVAL
+    assert lib.nrg_group_replica(None, 0) is None
+    assert lib.nrg_group_join(None, None, 2, 0, C.byref(out)) == L.NRG_E_INVAL
+    cfg = L.default_config(L.NRG_DS_HASHMAP)
+    assert lib.nrg_group_open(None, 1, C.byref(cfg), C.byref(out)) == L.NRG_E_INVAL
+    devs = (C.c_int * 1)(0)
+    assert lib.nrg_group_open(devs, 0, C.byref(cfg), C.byref(out)) == L.NRG_E_INVAL
+    assert lib.nrg_strerror(L.NRG_E_COMM).decode().startswith("RCCL")

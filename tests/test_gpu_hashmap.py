@@ -136,13 +136,17 @@ def test_fused_round_device(nrg, orc):
     _check_state(dev, om)
 
 
-def test_pipelined_rounds_back_to_back(nrg, orc):
-    """config.pipeline = 1: rounds enqueued back to back, no host sync in between. Each
-    round's reads run on the side stream overlapping the next round's index pass and must
-    still see exactly their own round's state (keys created by later rounds invisible,
-    values overwritten by later rounds not yet applied)."""
+@pytest.mark.parametrize("path", ["overlay", "bucket"])
+def test_pipelined_rounds_back_to_back(nrg, orc, monkeypatch, path):
+    """config.pipeline = 1: rounds enqueued back to back, no host sync in between. Each round's
+    reads run in the next round's launch, beside its index pass (and, for overlay rounds,
+    beside the apply of their own round's writes), and must see exactly their own round's
+    state (keys created by later rounds invisible, values overwritten later not yet there).
+    NRG_OV_MAX=0 sends every round through the bucket elector instead."""
     import torch
 
+    if path == "bucket":
+        monkeypatch.setenv("NRG_OV_MAX", "0")
     dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=17, max_batch=1 << 14, pipeline=1)
     dev.use_torch_stream()
     om = orc.HashMap()
@@ -273,20 +277,18 @@ def _mix64(x):
         return x ^ (x >> np.uint64(31))
 
 
-def test_owner_path_rounds(nrg, orc, monkeypatch):
-    """The opt-in partitioned replay (NRG_OWNER_MIN): pipelined rounds with side-slot keys, a
-    Zipf round, and a round whose keys all fall in ONE bucket (region overflow list and the
-    multi-class LDS election), each against the sequential oracle."""
+def test_one_bucket_rounds(nrg, orc):
+    """Pipelined rounds whose keys all fall into ONE elector bucket (many chunks, finer parts,
+    duplicates across index tiles), with side-slot keys and a Zipf round, against the oracle."""
     import torch
 
-    monkeypatch.setenv("NRG_OWNER_MIN", "1")
     dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=17, max_batch=8192, pipeline=1)
     dev.use_torch_stream()
     om = orc.HashMap()
     dev.hm_prefill_range(3000, 1)
     om.prefill_range(3000, 1)
     cand = np.arange(1, 4_000_000, dtype=np.uint64)
-    one_bucket = cand[(_mix64(cand) >> np.uint64(56)) == 0][:6000]  # 6000 > region capacity 4160
+    one_bucket = cand[(_mix64(cand) >> np.uint64(58)) == 0][:6000]  # top 6 home bits 0: bucket 0 of 64
     assert len(one_bucket) == 6000
     rounds = [orc.gen_uniform(6000, 240 + r, 9000) for r in range(3)]
     rounds.append(orc.gen_zipf(8000, 250, 20000, 0.99))
@@ -342,9 +344,8 @@ def _bucket_rounds(nrg, orc, dev, om, rounds):
 
 
 def test_bucket_election_default_rounds(nrg, orc):
-    """Rounds of >= 250k Puts take the bucket election by default (hm_elect_kernel): pipelined
-    uniform and Zipf rounds with side-slot keys, a stamp round in between (mode switch both
-    ways), against the sequential oracle."""
+    """Large pipelined rounds (4 Puts per index thread above 2^18 Puts): uniform and Zipf rounds
+    with side-slot keys and a small round in between, against the sequential oracle."""
     dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=22, max_batch=1 << 19, pipeline=1)
     dev.use_torch_stream()
     om = orc.HashMap()
@@ -357,11 +358,10 @@ def test_bucket_election_default_rounds(nrg, orc):
     _bucket_rounds(nrg, orc, dev, om, rounds)
 
 
-def test_bucket_election_part_overflow(nrg, orc, monkeypatch):
-    """2500 keys of a round home into the first 4096 slots of one bucket: the elector's first
+def test_bucket_election_part_overflow(nrg, orc):
+    """2500 new keys of a round home into the first 4096 slots of one bucket: the elector's first
     split (4096-slot parts) overflows its 2048-entry LDS table, and the bucket is redone in
     2048-slot parts."""
-    monkeypatch.setenv("NRG_ELECT_MIN", "1")
     dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=20, max_batch=1 << 14, pipeline=1)
     dev.use_torch_stream()
     om = orc.HashMap()
