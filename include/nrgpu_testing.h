@@ -17,6 +17,10 @@ int nrg_test_sort_pairs(nrg_ctx* ctx, const uint32_t* d_keys, const uint32_t* d_
 /* M[p] = max{q <= p : q == 0 || keys[q-1] != keys[q] || (vals[q] & 0x80000000)} */
 int nrg_test_maxscan(nrg_ctx* ctx, const uint32_t* d_keys, const uint32_t* d_vals, uint64_t n,
                      uint32_t* d_out);
+/* copy the record stored at PHYSICAL ring position `phys` (< log size) to host memory `out`
+ * (rec bytes per ds kind); syncs first. Lets tests check Log::index (nr/src/log.rs:528-530)
+ * against what the replica's HBM ring actually holds. */
+int nrg_test_ring_read(nrg_ctx* ctx, uint64_t phys, void* out);
 #ifdef __cplusplus
 }
 #endif

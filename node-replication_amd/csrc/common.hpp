@@ -41,36 +41,39 @@ __device__ __forceinline__ u64 mulhi64(u64 a, u64 b) { return __umul64hi(a, b); 
 // Home slot of a key: top bits of the mixed key.
 __device__ __forceinline__ u64 table_home(u64 key, u32 shift) { return mix64(key) >> shift; }
 
-// 16-byte table slot {key, value}, eight per 128-B line: 2^26 slots = 1 GiB. Nothing else lives
-// in the table: a replay round never writes a slot while the same launch reads it (hashmap.hip:
-// the index pass only reads, the elector launch claims keys and stores values), so no epochs,
-// stamps or creation marks are needed, and the footprint a random Get ranges over is 4x smaller
-// than with the 64-B slots of the first design (1 GiB vs 4 GiB: 23.8 vs 27.5 us per 1M Gets,
-// profiles/r01_get_footprint.txt).
-struct __attribute__((aligned(16))) Slot {
+// 32-byte table slot, four per 128-B line (2^26 slots = 2 GiB). A random read costs one 128-B
+// line at the memory side whatever its width (profiles/r01_rdreq_size.txt), so the replay's
+// per-key bookkeeping rides in the key's line: a Get reads {key, val} and the stamp of its
+// round's parity, two 16-B loads of one line.
+//   st[p]  stamp of the last round of parity p that wrote or created the key:
+//          epoch << 32 | (i+1) for the round's last writer (raised with atomicMax), or
+//          epoch << 32 | 0 as the mark a round leaves in the OTHER parity when it creates the key.
+//          0 = never stamped: a slot whose claim is still in flight reads as absent.
+// Epoch 1 means "present since before any replay round" (prefill, bucket-round claims); replay
+// rounds take epochs 2, 3, ... and are renormalised before the 32-bit epoch wraps.
+// A Get of round ep reads st[ep & 1]:  0 or epoch > ep -> absent (created by a later round);
+// epoch == ep -> the round's last writer (its record); epoch < ep -> present, value in `val`.
+struct __attribute__((aligned(32))) Slot {
     u64 key;  // EMPTY_KEY when free
     u64 val;
+    u64 st[2];
 };
+__host__ __device__ __forceinline__ u64 stamp_make(u32 epoch, u64 i1) { return ((u64)epoch << 32) | i1; }
+__host__ __device__ __forceinline__ u32 stamp_epoch(u64 st) { return (u32)(st >> 32); }
+constexpr u64 STAMP_PRESENT = 1ull << 32;  // epoch 1, no writer: present since before the replay rounds
 
 // One replica-wide control block in HBM.
 struct __attribute__((aligned(64))) DevCtl {
     u32 err;          // latched ERR_* bits
-    u32 sp_present;   // hashmap: the key EMPTY_KEY is present (its value is sp_val)
+    u32 sp_claim;     // hashmap: the key EMPTY_KEY has been inserted (its slot is `sp`)
     u64 nkeys;        // hashmap: keys inserted directly (prefill)
     long long depth;  // stack: current length
     u64 counter;      // scratch counter (dump compaction)
     u64 nkeys_total;  // hashmap: nkeys + keys created by replay rounds (hm_count)
     long long depth0;      // stack: length before the chunk being replayed
     long long depth_next;  // stack: length after it (st_commit_kernel moves it to depth)
-    u64 sp_val;       // hashmap: value of the key EMPTY_KEY (side slot)
-    u64 sp_st[3];     // hashmap overlay rounds: last writer (i+1) of EMPTY_KEY, per overlay
-};
-
-// Overlay slot (hashmap.hip overlay rounds): a key written by the round and the largest i+1
-// among its Puts (the round's last writer of the key, raised with atomicMax).
-struct __attribute__((aligned(16))) OvSlot {
-    u64 key;  // EMPTY_KEY when free
-    u64 st;   // i + 1 of the last writer
+    u64 pad;
+    Slot sp;          // hashmap: side slot of the key EMPTY_KEY (val, stamps; key unused)
 };
 
 __device__ __forceinline__ u64 ld_relaxed(const u64* p) {

@@ -4,31 +4,32 @@
 // benches/hashmap.rs:114-119, nr/examples/hashmap.rs:46-50) and the read path
 // Replica::read_only -> dispatch (nr/src/replica.rs:483-497, benches/hashmap.rs:107-111).
 //
-// Table: 2^k open-addressing slots of 16 B {key, value} (common.hpp), linear probing from
-// mix64(key) >> (64 - k); the one key equal to the empty marker lives in DevCtl (side slot).
-// A replay round covers the log records [lo, lo+n) and takes two launches:
+// Table: 2^k open-addressing slots of 32 B {key, value, stamp[2]} (common.hpp), linear probing
+// from mix64(key) >> (64 - k); the one key equal to the empty marker lives in DevCtl::sp. Every
+// replay round covers the log records [lo, lo+n) and takes a fresh epoch e. Two schedules:
 //
-//   hm_round_kernel  index(e) on its first blocks, reads(e-1) on the rest. index(e) only READS
-//                    the table: per Put it finds the key's slot, or notes that the key is new
-//                    (id = its home slot), drops Puts that a later Put of the same key in the
-//                    same block overwrites, and writes one 24-B entry {id, i+1, value; key} per
-//                    surviving Put into its tile, grouped by slot bucket and in log order inside
-//                    each bucket. reads(e-1) answer the previous round's Gets from the slots.
-//   hm_elect_kernel  one block per slot bucket gathers the bucket's entries from every tile in
-//                    log order, keeps one LDS hash entry per key (the largest i+1 = the round's
-//                    last writer), claims a slot for every new key (64-bit CAS) and stores each
-//                    key's final value: one plain scattered store per distinct key. With
-//                    previous-value responses wanted (HashMap::insert's return) every Put keeps
-//                    its entry and one wave walks the bucket in log order: a Put's previous
-//                    value is its predecessor's in the bucket walk, or the slot's value before
-//                    the round, or None for a key the round created.
-//
-// Why this is the sequential replay: every key lives in exactly one bucket (found keys by
-// slot, new keys by home slot; within one round all Puts of a key agree, since nothing claims
-// slots while index(e) runs), log order is preserved inside each bucket, and reads(e) run in
-// the launch after elect(e). index(e) and reads(e-1) share a launch safely because neither
-// writes the table. The elector writes only values of slots it owns (one bucket's keys) and
-// claims with CAS, so electors of different buckets never conflict.
+// Stamp rounds (<= stamp_max Puts, no previous-value responses): ONE launch per round,
+//   {index(e) | apply(e-1) | reads(e-1)} on disjoint block ranges of hm_round_kernel:
+//   index(e)   per Put: find the key's slot or claim an empty one (64-bit CAS; a fresh slot is
+//              marked in the other parity, stamp (e, 0), so the reads of round e-1 running in
+//              the same launch see it as absent); elect the round's last writer of every key
+//              with atomicMax(st[e&1], e << 32 | i+1), pre-combined per block in LDS.
+//   apply(e-1) per Put: the elected writer (st == (e-1, i+1)) stores its value.
+//   reads(e-1) a key is present iff its stamp of parity e-1 is nonzero with epoch <= e-1; if the
+//              epoch is e-1 the value is the elected record's (apply may be storing it).
+//   index(e) touches only st[e&1], claims of empty slots and values apply never reads; apply and
+//   reads look only at st[(e-1)&1]. The latency-bound index pass overlaps the reads.
+// Bucket rounds (larger rounds, and rounds that return HashMap::insert's previous values):
+//   hm_round_kernel {index(e) | apply(e-1) | reads(e-1)} where index(e) only READS the table and
+//   writes one entry {id, i+1, value; key} per surviving Put into its tile, grouped by slot
+//   bucket in log order; then hm_elect_kernel: one block per bucket gathers its entries from
+//   every tile in log order, keeps one LDS hash entry per key (the largest i+1 = last writer),
+//   claims slots for new keys and stores each key's final value -- no device atomics per Put.
+//   With previous values wanted every Put keeps its entry and one wave walks the bucket in log
+//   order: a Put's previous value is its predecessor's, or the slot's value before the round, or
+//   None for a key the round created. A key lives in exactly one bucket (found keys by slot, new
+//   keys by home slot: nothing claims slots while a bucket index pass runs, so all Puts of a key
+//   agree), and the round's reads run in the launch after the elector.
 #include "internal.hpp"
 
 namespace nrg {
@@ -68,6 +69,9 @@ struct ReadJob {
     u64* vals;
     uint8_t* found;
     u32 nblocks;
+    u32 epoch;    // the reads see the state after round `epoch`
+    bool use_rec; // that round's apply may run in the same launch: take its winners' records
+    RecSrc rec;
 };
 
 __device__ __forceinline__ u32 bucket_of_id(u32 id, u32 bk_shift) { return id == SIDE_ID ? 0u : (id & ID_MASK) >> bk_shift; }
@@ -291,287 +295,215 @@ __device__ __forceinline__ long long claim_slot(Slot* table, u64 k, u64 s, u64 t
     return -1;
 }
 
-// ---- overlay rounds: roles index(e) -> O_e, apply(e-1) and reads(e-1) against O_{e-1} ---------
-//
-// A round of at most ov_max Puts without previous-value responses replays in ONE launch:
-//   index(e)   per block, the last Put of each key (LDS dedup), then per such key one insert into
-//              the round's overlay O_e (a small open-addressing table, 64-bit CAS on the key) and
-//              atomicMax(st, i+1): the round's last writer of every key. The main table is not
-//              touched. Inserted overlay slots are listed per block.
-//   apply(e-1) next launch, per listed slot of O_{e-1}: the winner's value (from the log record),
-//              find-or-claim of the key in the main table, store.
-//   reads(e-1) same launch: a key in O_{e-1} answers with its winner's record value (apply may be
-//              storing it concurrently), any other key from the main table. apply only claims and
-//              writes keys listed in O_{e-1}, so those reads never depend on its progress, and a
-//              claim of another key cannot hide a present key (linear probing: a key present
-//              before round e-1 lies before every slot that was empty then).
-//   clear(e-2) same launch: empties the slots O_{e-2} used (three overlays rotate).
-// Race-freedom: index(e) touches only O_e; apply/reads(e-1) read O_{e-1} (complete since the
-// previous launch); clear touches only O_{e-2}, whose apply and reads ran in the previous launch.
-struct OvIndexJob {
-    u32 exp;  // diagnostic (NRG_EXP): 16 no overlay inserts
+// ---- stamp rounds: index(e) with claims and stamps, apply(e-1) ------------------------------------
+struct StampJob {
     RecSrc rec;
     nrg_put* ring_out;
     u64 n;
     u32 nblocks;
-    OvSlot* ov;
-    u64 omask;
-    u32* list;     // [nblocks][tile] inserted overlay slots
-    u32* lcnt;     // [nblocks]
-    u64* side_st;  // &ctl->sp_st[idx]
-};
-struct OvListJob {  // apply(e-1) / clear(e-2): one thread per list position of that round
-    u32 exp;  // diagnostic (NRG_EXP): 32 no apply
-    const OvSlot* ov;
-    OvSlot* ov_w;
-    const u32* list;
-    const u32* lcnt;
-    u32 ltile;
-    u64* side_st;
-    RecSrc rec;
+    u32 epoch;
+    u32* put_slot;  // [n] slot of each Put (SIDE_SLOT, FULL_SLOT)
     u64* created_acc;
+};
+struct ApplyJob {
+    RecSrc rec;
+    u64 n;
+    const u32* put_slot;
+    u32 epoch;
     u32 nblocks;
 };
-
-__device__ __forceinline__ u64 ov_home(u64 k, u64 omask) { return mix64(k) & omask; }
+constexpr u32 SIDE_SLOT = 0xFFFFFFFEu;  // put_slot of the key EMPTY_KEY
 
 template <int K1>
-__device__ __forceinline__ void ov_index_role(const OvIndexJob& j, u32 blk, DevCtl* ctl, char* lds) {
-    constexpr int WT = 64 * K1;
-    constexpr int TILE = IndexLds<K1>::TILE;
-    constexpr int HSZ = IndexLds<K1>::HSZ;
-    __shared__ u32 s_side;
-    __shared__ u32 s_ln;
-    __shared__ u32 s_list[TILE];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const u64 base = (u64)blk * TILE;
-    u64* s_hk = (u64*)lds;
-    u32* s_hp = (u32*)(lds + HSZ * 8);
-    for (int q = threadIdx.x; q < HSZ; q += TPB) {
-        s_hk[q] = EMPTY_KEY;
-        s_hp[q] = 0;
-    }
-    if (threadIdx.x == 0) {
-        s_side = 0;
-        s_ln = 0;
-    }
-    nrg_put rec[K1];
-    bool valid[K1];
-#pragma unroll
-    for (int q = 0; q < K1; q++) {
-        const u64 i = base + (u64)(w * WT + q * 64 + lane);
-        valid[q] = i < j.n;
-        rec[q] = valid[q] ? j.rec.at(i) : nrg_put{0, 0};
-    }
-#pragma unroll
-    for (int q = 0; q < K1; q++) {
-        const u64 i = base + (u64)(w * WT + q * 64 + lane);
-        if (valid[q] && j.ring_out) j.ring_out[(j.rec.lo + i) & j.rec.mask] = rec[q];
-    }
-    __syncthreads();  // hash initialised
-    u32 hq[K1];
-#pragma unroll
-    for (int q = 0; q < K1; q++) {
-        if (!valid[q]) continue;
-        const u32 pos1 = (u32)(w * WT + q * 64 + lane) + 1;
-        if (rec[q].key == EMPTY_KEY) {
-            atomicMax(&s_side, pos1);
-            continue;
-        }
-        u32 h = (u32)(((mix64(rec[q].key) >> 32) * (u64)HSZ) >> 32);
-        for (;;) {
-            const u64 old = atomicCAS((unsigned long long*)&s_hk[h], (unsigned long long)EMPTY_KEY,
-                                      (unsigned long long)rec[q].key);
-            if (old == EMPTY_KEY || old == rec[q].key) break;
-            h = h + 1 == (u32)HSZ ? 0u : h + 1;
-        }
-        atomicMax(&s_hp[h], pos1);
-        hq[q] = h;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < K1; q++) {
-        if (!valid[q]) continue;
-        const u32 pos1 = (u32)(w * WT + q * 64 + lane) + 1;
-        const u64 i1 = base + pos1;  // i + 1 in the round
-        if (rec[q].key == EMPTY_KEY) {
-            if (s_side == pos1) atomicMax((unsigned long long*)j.side_st, (unsigned long long)i1);
-            continue;
-        }
-        if (s_hp[hq[q]] != pos1) continue;  // a later Put of the key in this block wins
-        if (j.exp & 16) continue;
-        const u64 k = rec[q].key;
-        u64 h = ov_home(k, j.omask);
-        bool ok = false;
-        for (u64 pr = 0; pr <= j.omask; pr++) {
-            const u64 old = atomicCAS((unsigned long long*)&j.ov[h].key, (unsigned long long)EMPTY_KEY,
+struct StampLds {
+    static constexpr int TILE = TPB * K1;
+    static constexpr int HT = 2 * TILE;  // LDS combine table (slot -> largest i+1)
+    static constexpr unsigned BYTES = HT * 8;
+};
+
+// find k from its home slot s (first key loaded: key0), or claim an empty slot; a slot this
+// call claims is marked in the other parity (stamp (e, 0)) so the concurrent reads of round
+// e-1 see it as absent; -1: table full
+__device__ __forceinline__ long long find_or_claim_marked(Slot* table, u64 k, u64 s, u64 tmask, u64 key0, u32 e,
+                                                          u32* created) {
+    u64 key = key0;
+    for (u64 pr = 0; pr <= tmask; pr++) {
+        if (key == k) return (long long)s;
+        if (key == EMPTY_KEY) {
+            const u64 old = atomicCAS((unsigned long long*)&table[s].key, (unsigned long long)EMPTY_KEY,
                                       (unsigned long long)k);
-            if (old == EMPTY_KEY) s_list[atomicAdd(&s_ln, 1u)] = (u32)h;
-            if (old == EMPTY_KEY || old == k) {
-                ok = true;
-                break;
+            if (old == EMPTY_KEY) {
+                table[s].st[(e - 1) & 1] = stamp_make(e, 0);
+                *created += 1;
+                return (long long)s;
             }
-            h = (h + 1) & j.omask;
+            if (old == k) return (long long)s;
         }
-        if (!ok) {
-            atomicOr(&ctl->err, ERR_TABLE_FULL);
-            continue;
-        }
-        atomicMax((unsigned long long*)&j.ov[h].st, (unsigned long long)i1);
+        s = (s + 1) & tmask;
+        key = ld_relaxed(&table[s].key);
     }
-    __syncthreads();
-    const u32 ln = s_ln;
-    for (u32 q = threadIdx.x; q < ln; q += TPB) j.list[(u64)blk * TILE + q] = s_list[q];
-    if (threadIdx.x == 0) j.lcnt[blk] = ln;
+    return -1;
 }
 
-// apply(e-1): one thread per list position of round e-1
-__device__ __forceinline__ void ov_apply_role(const OvListJob& j, u32 blk, Slot* table, u32 shift, u64 tmask,
-                                              DevCtl* ctl) {
-    __shared__ u32 s_created;
-    if (threadIdx.x == 0) s_created = 0;
-    __syncthreads();
-    const u64 x = (u64)blk * TPB + threadIdx.x;
-    const u32 ib = (u32)(x / j.ltile), k = (u32)(x % j.ltile);
-    u32 created = 0;
-    if (k < j.lcnt[ib] && !(j.exp & 32)) {
-        const u32 h = j.list[(u64)ib * j.ltile + k];
-        const u64x2 o = *(const u64x2*)&j.ov[h];
-        const u64 v = j.rec.at(o.y - 1).val;
-        bool fresh;
-        const long long sl = claim_slot(table, o.x, table_home(o.x, shift), tmask, &fresh);
-        if (sl < 0) {
-            atomicOr(&ctl->err, ERR_TABLE_FULL);
-        } else {
-            table[sl].val = v;
-            created += fresh;
-        }
+template <int K1>
+__device__ __forceinline__ void stamp_index_role(const StampJob& j, u32 blk, Slot* table, u32 shift, u64 tmask,
+                                                 DevCtl* ctl, char* lds) {
+    constexpr int TILE = StampLds<K1>::TILE;
+    constexpr int HT = StampLds<K1>::HT;
+    __shared__ u32 s_side, s_created;
+    u32* s_slot = (u32*)lds;        // [HT] slot ids, ~0u free
+    u32* s_max = (u32*)lds + HT;    // [HT] largest i+1 per slot in this block
+    for (int q = threadIdx.x; q < HT; q += TPB) {
+        s_slot[q] = 0xFFFFFFFFu;
+        s_max[q] = 0;
     }
-    if (blk == 0 && threadIdx.x == 0) {
-        const u64 st = *j.side_st;
-        if (st) {
-            created += ctl->sp_present == 0;
-            ctl->sp_val = j.rec.at(st - 1).val;
-            ctl->sp_present = 1;
+    if (threadIdx.x == 0) s_side = s_created = 0;
+    const u32 e = j.epoch, par = e & 1;
+    const u64 base = (u64)blk * TILE;
+    nrg_put rec[K1];
+    u64 home[K1], key0[K1];
+    // every record load, then every first probe, in flight before waiting on any of them
+#pragma unroll
+    for (int q = 0; q < K1; q++) {
+        const u64 i = base + (u64)q * TPB + threadIdx.x;
+        rec[q] = i < j.n ? j.rec.at(i) : nrg_put{EMPTY_KEY, 0};
+    }
+#pragma unroll
+    for (int q = 0; q < K1; q++) {
+        const u64 i = base + (u64)q * TPB + threadIdx.x;
+        if (i < j.n && j.ring_out) j.ring_out[(j.rec.lo + i) & j.rec.mask] = rec[q];
+        home[q] = table_home(rec[q].key, shift);
+        key0[q] = i < j.n && rec[q].key != EMPTY_KEY ? table[home[q]].key : EMPTY_KEY;
+    }
+    __syncthreads();  // LDS table initialised
+    u32 created = 0;
+#pragma unroll
+    for (int q = 0; q < K1; q++) {
+        const u64 i = base + (u64)q * TPB + threadIdx.x;
+        if (i >= j.n) continue;
+        const u64 k = rec[q].key;
+        if (k == EMPTY_KEY) {  // the side-slot key
+            if (ld_relaxed32(&ctl->sp_claim) == 0 && atomicCAS(&ctl->sp_claim, 0u, 1u) == 0u) {
+                ctl->sp.st[(e - 1) & 1] = stamp_make(e, 0);
+                created++;
+            }
+            atomicMax(&s_side, (u32)(i + 1));
+            j.put_slot[i] = SIDE_SLOT;
+            continue;
         }
+        const long long s = find_or_claim_marked(table, k, home[q], tmask, key0[q], e, &created);
+        if (s < 0) {
+            atomicOr(&ctl->err, ERR_TABLE_FULL);
+            j.put_slot[i] = FULL_SLOT;
+            continue;
+        }
+        j.put_slot[i] = (u32)s;
+        u32 h = (u32)(mix64((u64)s) & (HT - 1));
+        for (;;) {
+            const u32 old = atomicCAS(&s_slot[h], 0xFFFFFFFFu, (u32)s);
+            if (old == 0xFFFFFFFFu || old == (u32)s) break;
+            h = (h + 1) & (HT - 1);
+        }
+        atomicMax(&s_max[h], (u32)(i + 1));
     }
     if (created) atomicAdd(&s_created, created);
     __syncthreads();
-    if (threadIdx.x == 0 && s_created) atomicAdd(&j.created_acc[blk % HM_CREATED_SLOTS], (u64)s_created);
+    // one stamp atomic per distinct slot of the block (a hot key costs one per block)
+    for (int q = threadIdx.x; q < HT; q += TPB) {
+        const u32 sl = s_slot[q];
+        if (sl != 0xFFFFFFFFu)
+            atomicMax((unsigned long long*)&table[sl].st[par], (unsigned long long)stamp_make(e, s_max[q]));
+    }
+    if (threadIdx.x == 0) {
+        if (s_side) atomicMax((unsigned long long*)&ctl->sp.st[par], (unsigned long long)stamp_make(e, s_side));
+        if (s_created) atomicAdd(&j.created_acc[blk % HM_CREATED_SLOTS], (u64)s_created);
+    }
 }
 
-// clear(e-2): empty the overlay slots round e-2 inserted
-__device__ __forceinline__ void ov_clear_role(const OvListJob& j, u32 blk) {
-    const u64 x = (u64)blk * TPB + threadIdx.x;
-    const u32 ib = (u32)(x / j.ltile), k = (u32)(x % j.ltile);
-    if (k < j.lcnt[ib]) {
-        u64x2 z;
-        z.x = EMPTY_KEY;
-        z.y = 0;
-        *(u64x2*)&j.ov_w[j.list[(u64)ib * j.ltile + k]] = z;
+// apply(e): per Put, the elected writer stores its value
+__device__ __forceinline__ void apply_role(const ApplyJob& j, u32 blk, Slot* table, DevCtl* ctl) {
+    const u64 i = (u64)blk * TPB + threadIdx.x;
+    if (i >= j.n) return;
+    const u32 par = j.epoch & 1;
+    const u32 s = j.put_slot[i];
+    const u64 want = stamp_make(j.epoch, i + 1);
+    if (s == SIDE_SLOT) {
+        if (ctl->sp.st[par] == want) ctl->sp.val = j.rec.at(i).val;
+    } else if (s != FULL_SLOT) {
+        if (table[s].st[par] == want) table[s].val = j.rec.at(i).val;
     }
-    if (blk == 0 && threadIdx.x == 0) *j.side_st = 0;
 }
 
 // ---- role: reads -------------------------------------------------------------------------------
-// With an overlay (reads of an overlay round, whose apply may run in the same launch): a key in
-// the overlay answers with its last writer's record value, others from the main table.
-struct OvReadCtx {
-    u32 exp;  // diagnostic (NRG_EXP): 8 reads skip the overlay
-    const OvSlot* ov;  // nullptr: no overlay round pending
-    u64 omask;
-    const u64* side_st;
-    RecSrc rec;
-};
+// Present iff the stamp of the round's parity is nonzero with epoch <= ep (0: claim in flight;
+// a later epoch: created by the concurrent round); epoch == ep: written by round ep, whose
+// elected record holds the value while its apply may run in this launch.
+__device__ __forceinline__ bool resolve(u64 val, u64 st, const ReadJob& j, u64* v) {
+    const u32 se = stamp_epoch(st);
+    if (st == 0 || se > j.epoch) return false;
+    *v = (se == j.epoch && j.use_rec) ? j.rec.at((u32)st - 1).val : val;
+    return true;
+}
 
-__device__ __forceinline__ void read_role(const ReadJob& j, const OvReadCtx& o, u32 blk, const Slot* table,
-                                          u32 shift, u64 tmask, const DevCtl* ctl) {
+__device__ __forceinline__ void read_role(const ReadJob& j, u32 blk, const Slot* table, u32 shift, u64 tmask,
+                                          const DevCtl* ctl) {
     const u64 q = (u64)blk * TPB + threadIdx.x;
     if (q >= j.R) return;
     const u64 k = j.keys[q];
+    const u32 par = j.epoch & 1;
     u64 v = 0;
     bool f = false;
     if (k == EMPTY_KEY) {
-        const u64 st = o.ov ? *o.side_st : 0;
-        if (st) {
-            f = true;
-            v = o.rec.at(st - 1).val;
-        } else {
-            f = ctl->sp_present != 0;
-            v = f ? ctl->sp_val : 0;
-        }
+        if (ctl->sp_claim) f = resolve(ctl->sp.val, ctl->sp.st[par], j, &v);
     } else {
         u64 s = table_home(k, shift);
-        const bool use_ov = o.ov && !(o.exp & 8);
-        u64 oh = use_ov ? ov_home(k, o.omask) : 0;
-        // the overlay line and the table line are loaded together (independent addresses)
-        u64x2 ow;
-        ow.x = EMPTY_KEY;
-        if (use_ov) ow = *(const u64x2*)&o.ov[oh];
-        u64x2 w = *(const u64x2*)&table[s];
-        bool in_ov = false;
-        if (use_ov) {
-            for (u64 pr = 0; pr <= o.omask; pr++) {
-                if (ow.x == k) {
-                    in_ov = true;
-                    break;
-                }
-                if (ow.x == EMPTY_KEY) break;
-                oh = (oh + 1) & o.omask;
-                ow = *(const u64x2*)&o.ov[oh];
+        for (u64 pr = 0; pr <= tmask; pr++) {
+            // {key, val} and the stamp: two loads of one line, issued together
+            const u64x2 w = *(const u64x2*)&table[s];
+            u64 st = table[s].st[par];
+            u64 kk = w.x, vv = w.y;
+            asm volatile("" : "+v"(kk), "+v"(vv), "+v"(st));
+            if (kk == k) {
+                f = resolve(vv, st, j, &v);
+                break;
             }
-        }
-        if (in_ov) {
-            f = true;
-            v = o.rec.at(ow.y - 1).val;
-        } else {
-            for (u64 pr = 0; pr <= tmask; pr++) {  // one 16-B load per probe
-                if (w.x == k) {
-                    v = w.y;
-                    f = true;
-                    break;
-                }
-                if (w.x == EMPTY_KEY) break;
-                s = (s + 1) & tmask;
-                w = *(const u64x2*)&table[s];
-            }
+            if (kk == EMPTY_KEY) break;
+            s = (s + 1) & tmask;
         }
     }
+    if (!f) v = 0;
     j.vals[q] = v;
     j.found[q] = f ? 1 : 0;
 }
 
 // index-role kinds of a round launch
-constexpr int IX_BUCKET = 0;    // bucket round, dedup (hm_elect_kernel<false> follows)
+constexpr int IX_BUCKET = 0;      // bucket round, dedup (hm_elect_kernel<false> follows)
 constexpr int IX_BUCKET_ALL = 1;  // bucket round, every Put kept (previous values)
-constexpr int IX_OVERLAY = 2;   // overlay round
+constexpr int IX_STAMP = 2;       // stamp round
 
-// One launch = {index(e)} + {apply(e-1)} + {clear(e-2)} + {reads(e-1)} over disjoint block
-// ranges (any may be empty). Index blocks come first so the latency-bound pass starts first.
+// One launch = {index(e)} + {apply(e-1)} + {reads(e-1)} over disjoint block ranges (any may be
+// empty). Index blocks come first so the latency-bound pass starts first.
+// <= 80 SGPRs: 256-thread blocks are admitted 8 per CU only up to 80 SGPRs (82-96: 7 per CU,
+// MI355X_MICROARCH.md "Residency"), and the read role needs every resident wave.
 template <int K1, int IX>
-__global__ __launch_bounds__(TPB) void hm_round_kernel(IndexJob ij, OvIndexJob oj, OvListJob aj, OvListJob cj,
-                                                       ReadJob rj, OvReadCtx ro, Slot* table, u32 shift, u64 tmask,
-                                                       DevCtl* ctl) {
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_num_sgpr(80))) void hm_round_kernel(IndexJob ij, StampJob sj,
+                                                                                             ApplyJob aj, ReadJob rj,
+                                                       Slot* table, u32 shift, u64 tmask, DevCtl* ctl) {
     extern __shared__ __attribute__((aligned(16))) char s_lds[];
     u32 b = blockIdx.x;
-    const u32 nix = IX == IX_OVERLAY ? oj.nblocks : ij.nblocks;
+    const u32 nix = IX == IX_STAMP ? sj.nblocks : ij.nblocks;
     if (b < nix) {
-        if constexpr (IX == IX_OVERLAY) ov_index_role<K1>(oj, b, ctl, s_lds);
+        if constexpr (IX == IX_STAMP) stamp_index_role<K1>(sj, b, table, shift, tmask, ctl, s_lds);
         else index_role<K1, IX == IX_BUCKET>(ij, b, table, shift, tmask, s_lds);
         return;
     }
     b -= nix;
     if (b < aj.nblocks) {
-        ov_apply_role(aj, b, table, shift, tmask, ctl);
+        apply_role(aj, b, table, ctl);
         return;
     }
     b -= aj.nblocks;
-    if (b < cj.nblocks) {
-        ov_clear_role(cj, b);
-        return;
-    }
-    b -= cj.nblocks;
-    read_role(rj, ro, b, table, shift, tmask, ctl);
+    read_role(rj, b, table, shift, tmask, ctl);
 }
 
 // ---- hm_elect_kernel: last writer per key, claims of new keys, value stores -----------------------
@@ -747,10 +679,14 @@ __global__ __launch_bounds__(TPB) void hm_elect_kernel(ElectJob j) {
             if (!s_hp[h]) continue;
             if (h == EL_HT) {
                 s_hs[h] = SIDE_ID;
-                const bool present = j.ctl->sp_present != 0;
-                if (!present) created++;
+                const bool present = j.ctl->sp_claim != 0;
+                if (!present) {  // created by this round (no reads run beside the elector)
+                    created++;
+                    j.ctl->sp_claim = 1;
+                    j.ctl->sp.st[0] = j.ctl->sp.st[1] = STAMP_PRESENT;
+                }
                 if (PREV && present) {
-                    s_lv[h] = j.ctl->sp_val;
+                    s_lv[h] = j.ctl->sp.val;
                     s_hf[h] |= 2u;
                 }
             } else if ((s_hf[h] & 1u) && (j.exp & 4)) {
@@ -765,6 +701,7 @@ __global__ __launch_bounds__(TPB) void hm_elect_kernel(ElectJob j) {
                 } else {
                     s_hs[h] = (u32)sl;
                     created += fresh;
+                    if (fresh) j.table[sl].st[0] = j.table[sl].st[1] = STAMP_PRESENT;
                     if (PREV && !fresh) {  // inserted earlier by a round not visible to index
                         s_lv[h] = j.table[sl].val;
                         s_hf[h] |= 2u;
@@ -789,8 +726,7 @@ __global__ __launch_bounds__(TPB) void hm_elect_kernel(ElectJob j) {
                     if (s_hp[h] != base + r * TPB + threadIdx.x + 1) continue;
                     const u32 sl = s_hs[h];
                     if (sl == SIDE_ID) {
-                        j.ctl->sp_val = x[r].y;
-                        j.ctl->sp_present = 1;
+                        j.ctl->sp.val = x[r].y;
                     } else if (sl != FULL_SLOT) {
                         j.table[sl].val = x[r].y;
                     }
@@ -856,8 +792,7 @@ __global__ __launch_bounds__(TPB) void hm_elect_kernel(ElectJob j) {
                 if (!s_hp[h]) continue;
                 const u32 sl = s_hs[h];
                 if (sl == SIDE_ID) {
-                    j.ctl->sp_val = s_lv[h];
-                    j.ctl->sp_present = 1;
+                    j.ctl->sp.val = s_lv[h];
                 } else if (sl != FULL_SLOT) {
                     j.table[sl].val = s_lv[h];
                 }
@@ -877,7 +812,21 @@ __global__ __launch_bounds__(TPB) void hm_init_table_kernel(Slot* table, u64 slo
         z.x = EMPTY_KEY;
         z.y = 0;
         *(u64x2*)&table[s] = z;
+        z.x = z.y = 0;
+        *(u64x2*)&table[s].st[0] = z;
     }
+}
+
+// Epoch renormalisation (before the 32-bit epoch wraps): every present key becomes "present
+// since before the replay rounds" (epoch 1); claims in flight do not exist at this point.
+__global__ __launch_bounds__(TPB) void hm_renorm_kernel(Slot* table, u64 slots, DevCtl* ctl) {
+    for (u64 s = blockIdx.x * (u64)TPB + threadIdx.x; s < slots; s += (u64)gridDim.x * TPB) {
+        if (table[s].key == EMPTY_KEY) continue;
+        u64x2 z;
+        z.x = z.y = STAMP_PRESENT;
+        *(u64x2*)&table[s].st[0] = z;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0 && ctl->sp_claim) ctl->sp.st[0] = ctl->sp.st[1] = STAMP_PRESENT;
 }
 
 // NrHashMap::default (benches/hashmap.rs:91-100): keys 0..n-1 -> k + off, inserted directly.
@@ -889,9 +838,10 @@ __global__ __launch_bounds__(TPB) void hm_prefill_range_kernel(Slot* table, u64 
     u32 inserted = 0;
     for (u64 k = blockIdx.x * (u64)TPB + threadIdx.x; k < n; k += (u64)gridDim.x * TPB) {
         if (k == EMPTY_KEY) {  // only reachable for n = 2^64, kept for the full key domain
-            inserted += ctl->sp_present == 0;
-            ctl->sp_val = k + off;
-            ctl->sp_present = 1;
+            inserted += ctl->sp_claim == 0;
+            ctl->sp.val = k + off;
+            ctl->sp.st[0] = ctl->sp.st[1] = STAMP_PRESENT;
+            ctl->sp_claim = 1;
             continue;
         }
         bool fresh;
@@ -901,6 +851,7 @@ __global__ __launch_bounds__(TPB) void hm_prefill_range_kernel(Slot* table, u64 
             continue;
         }
         table[s].val = k + off;
+        table[s].st[0] = table[s].st[1] = STAMP_PRESENT;
         inserted += fresh;
     }
     if (inserted) atomicAdd(&s_ins, inserted);
@@ -926,10 +877,10 @@ __global__ __launch_bounds__(TPB) void hm_count_kernel(const u64* __restrict__ a
 __global__ __launch_bounds__(TPB) void hm_dump_kernel(const Slot* __restrict__ table, u64 slots, DevCtl* ctl,
                                                       u64* __restrict__ ok, u64* __restrict__ ov) {
     const u64 gid = blockIdx.x * (u64)TPB + threadIdx.x;
-    if (gid == 0 && ctl->sp_present) {
+    if (gid == 0 && ctl->sp_claim) {
         const u64 i = atomicAdd(&ctl->counter, 1ull);
         ok[i] = EMPTY_KEY;
-        ov[i] = ctl->sp_val;
+        ov[i] = ctl->sp.val;
     }
     for (u64 s = gid; s < slots; s += (u64)gridDim.x * TPB) {
         const u64x2 e = *(const u64x2*)&table[s];
@@ -946,8 +897,8 @@ __global__ __launch_bounds__(TPB) void hm_digest_kernel(const Slot* __restrict__
     __shared__ u64 s_c[TPB / 64], s_s[TPB / 64], s_x[TPB / 64];
     const u64 gid = blockIdx.x * (u64)TPB + threadIdx.x;
     u64 c = 0, sm = 0, x = 0;
-    if (gid == 0 && ctl->sp_present) {
-        const u64 h = mix64(EMPTY_KEY ^ mix64(ctl->sp_val));
+    if (gid == 0 && ctl->sp_claim) {
+        const u64 h = mix64(EMPTY_KEY ^ mix64(ctl->sp.val));
         c++;
         sm += h;
         x ^= h;
@@ -1022,7 +973,7 @@ static RecSrc ring_src(nrg_ctx* c, const nrg_put* src, u64 lo) {
     return r;
 }
 
-// Puts per index thread: 2 up to 2^18 Puts per round, 4 above (fewer, larger tiles keep the
+// Bucket rounds, Puts per index thread: 2 up to 2^18 Puts per round, 4 above (fewer, larger tiles keep the
 // elector's count rows short and the per-block dedup effective on hot keys). NRG_K1 overrides.
 static u32 k1_for(const nrg_ctx* c, u64 n) {
     u32 k = n > (1u << 18) ? 4u : 2u;
@@ -1031,98 +982,79 @@ static u32 k1_for(const nrg_ctx* c, u64 n) {
     return k;
 }
 
-// Overlay rounds: 1 Put per index thread up to 2^17 Puts, 2 above (NRG_K1 overrides).
-static u32 ov_k1_for(const nrg_ctx* c, u64 n) {
-    if (c->k1_items) return c->k1_items >= 2 ? 2u : 1u;
-    return n > (1u << 17) ? 2u : 1u;
+// Stamp rounds: 2 Puts per index thread (B1: 1 and 2 measured equal in round 1, 4 slower;
+// Zipf rounds gain from fewer blocks per hot key). NRG_K1 overrides.
+static u32 stamp_k1_for(const nrg_ctx* c) {
+    if (c->k1_items) return c->k1_items >= 4 ? 4u : c->k1_items >= 2 ? 2u : 1u;
+    return 2u;
 }
 
 // The jobs of one hm_round_kernel launch.
 struct Launch {
     IndexJob ij{};
-    OvIndexJob oj{};
-    OvListJob aj{};
-    OvListJob cj{};
+    StampJob sj{};
+    ApplyJob aj{};
     ReadJob rj{};
-    OvReadCtx ro{};
     int ix = IX_BUCKET;
     u32 K1 = 1;
     u32 nb = 0;
 };
 
-static u32 ov_list_blocks(const OvRound& r) {  // one thread per list position of the round
-    return (u32)(((u64)r.nblocks * r.tile + TPB - 1) / TPB);
-}
-
-// Roles every launch carries: the deferred round's apply (overlay) and reads, and the clear of
-// the overlay applied by the previous launch.
+// The deferred half of the last round rides in this launch: its apply (stamp rounds) and reads.
 static void attach_deferred(nrg_ctx* c, Launch& L) {
     const HmDeferred& p = c->pend;
-    L.aj.exp = L.ro.exp = c->exp & 0xFF;
+    L.rj.epoch = c->epoch;  // reads without a deferred round: every round applied
     if (p.valid) {
+        const RecSrc rs = ring_src(c, p.src, p.lo);
         L.rj.keys = p.keys;
         L.rj.R = p.R;
         L.rj.vals = p.vals;
         L.rj.found = p.found;
-        if (p.ov.valid) {
-            const u32 x = p.ov.idx;
-            const RecSrc rs = ring_src(c, p.ov.src, p.ov.lo);
-            L.aj.ov = c->d_ov[x];
-            L.aj.list = c->d_ov_list[x];
-            L.aj.lcnt = c->d_ov_cnt[x];
-            L.aj.ltile = p.ov.tile;
-            L.aj.side_st = &c->d_ctl->sp_st[x];
+        L.rj.epoch = p.epoch;
+        L.rj.use_rec = p.apply;
+        L.rj.rec = rs;
+        if (p.apply) {
             L.aj.rec = rs;
-            L.aj.created_acc = c->d_created;
-            L.aj.nblocks = ov_list_blocks(p.ov);
-            L.ro.ov = c->d_ov[x];
-            L.ro.omask = (1ull << c->ov_log2) - 1;
-            L.ro.side_st = &c->d_ctl->sp_st[x];
-            L.ro.rec = rs;
+            L.aj.n = p.n;
+            L.aj.put_slot = c->d_put_slot[p.epoch & 1];
+            L.aj.epoch = p.epoch;
+            L.aj.nblocks = (u32)((p.n + TPB - 1) / TPB);
         }
     }
-    if (c->ov_clear.valid) {
-        const u32 x = c->ov_clear.idx;
-        L.cj.ov_w = c->d_ov[x];
-        L.cj.list = c->d_ov_list[x];
-        L.cj.lcnt = c->d_ov_cnt[x];
-        L.cj.ltile = c->ov_clear.tile;
-        L.cj.side_st = &c->d_ctl->sp_st[x];
-        L.cj.nblocks = ov_list_blocks(c->ov_clear);
-    }
-    // state after this launch: the deferred half ran; the overlay it applied is cleared next
-    c->ov_clear = p.valid ? p.ov : OvRound{};
     c->pend = HmDeferred{};
 }
 
 template <int K1, int IX>
 static void launch_round(nrg_ctx* c, const Launch& L, u32 blocks, unsigned lds) {
-    NRG_LAUNCH(c, "hm_round", (hm_round_kernel<K1, IX>), blocks, TPB, lds, c->stream, L.ij, L.oj, L.aj, L.cj, L.rj,
-               L.ro, c->d_table, c->slot_shift, (u64)(c->slots - 1), c->d_ctl);
+    NRG_LAUNCH(c, "hm_round", (hm_round_kernel<K1, IX>), blocks, TPB, lds, c->stream, L.ij, L.sj, L.aj, L.rj,
+               c->d_table, c->slot_shift, (u64)(c->slots - 1), c->d_ctl);
 }
 
 static hipError_t launch(nrg_ctx* c, Launch& L) {
     L.rj.nblocks = (u32)((L.rj.R + TPB - 1) / TPB);
-    const u32 nix = L.ix == IX_OVERLAY ? L.oj.nblocks : L.ij.nblocks;
-    const u32 blocks = nix + L.aj.nblocks + L.cj.nblocks + L.rj.nblocks;
+    const u32 nix = L.ix == IX_STAMP ? L.sj.nblocks : L.ij.nblocks;
+    const u32 blocks = nix + L.aj.nblocks + L.rj.nblocks;
     if (blocks == 0) return hipSuccess;
-    const bool dedup = L.ix != IX_BUCKET_ALL;
-    const u32 nb = L.ix == IX_OVERLAY ? 0u : L.nb;
     unsigned lds = 0;
-    if (nix) lds = L.K1 == 4 ? IndexLds<4>::bytes(dedup, nb) : L.K1 == 2 ? IndexLds<2>::bytes(dedup, nb)
-                                                                          : IndexLds<1>::bytes(dedup, nb);
+    if (nix && L.ix == IX_STAMP) {
+        lds = L.K1 == 4 ? StampLds<4>::BYTES : L.K1 == 2 ? StampLds<2>::BYTES : StampLds<1>::BYTES;
+    } else if (nix) {
+        const bool dedup = L.ix == IX_BUCKET;
+        lds = L.K1 == 4 ? IndexLds<4>::bytes(dedup, L.nb) : L.K1 == 2 ? IndexLds<2>::bytes(dedup, L.nb)
+                                                                       : IndexLds<1>::bytes(dedup, L.nb);
+    }
     if (!nix) launch_round<1, IX_BUCKET>(c, L, blocks, 0);
 #define NRG_RK(KK, XX) else if (L.K1 == KK && L.ix == XX) launch_round<KK, XX>(c, L, blocks, lds)
-    NRG_RK(1, IX_BUCKET); NRG_RK(1, IX_BUCKET_ALL); NRG_RK(1, IX_OVERLAY);
-    NRG_RK(2, IX_BUCKET); NRG_RK(2, IX_BUCKET_ALL); NRG_RK(2, IX_OVERLAY);
-    NRG_RK(4, IX_BUCKET); NRG_RK(4, IX_BUCKET_ALL); NRG_RK(4, IX_OVERLAY);
+    NRG_RK(1, IX_BUCKET); NRG_RK(1, IX_BUCKET_ALL); NRG_RK(1, IX_STAMP);
+    NRG_RK(2, IX_BUCKET); NRG_RK(2, IX_BUCKET_ALL); NRG_RK(2, IX_STAMP);
+    NRG_RK(4, IX_BUCKET); NRG_RK(4, IX_BUCKET_ALL); NRG_RK(4, IX_STAMP);
 #undef NRG_RK
     else return hipErrorInvalidValue;
     return hipGetLastError();
 }
 
 hipError_t hm_flush(nrg_ctx* c) {
-    if (!c->pend.valid && !c->ov_clear.valid) return hipSuccess;
+    if (!c->pend.valid) return hipSuccess;
     Launch L;
     attach_deferred(c, L);
     return launch(c, L);
@@ -1141,7 +1073,7 @@ static hipError_t hm_reads(nrg_ctx* c, const u64* keys, u64 R, u64* vals, uint8_
     hipError_t e = hm_flush(c);
     if (e != hipSuccess) return e;
     Launch L;
-    attach_deferred(c, L);  // a pending overlay clear rides along
+    attach_deferred(c, L);
     L.rj.keys = keys;
     L.rj.R = R;
     L.rj.vals = vals;
@@ -1156,37 +1088,35 @@ hipError_t hm_alloc(nrg_ctx* c, u64 mb) {
     if ((e = hipMalloc(&c->d_bk_ent, ents * 16)) != hipSuccess) return e;
     if ((e = hipMalloc(&c->d_bk_key, ents * 8)) != hipSuccess) return e;
     if ((e = hipMalloc(&c->d_bk_cnt, (u64)HM_BK_MAX * tiles * sizeof(u32))) != hipSuccess) return e;
-    if (c->ov_max > mb) c->ov_max = mb;
-    if (!c->ov_max) return hipSuccess;
-    // overlays of >= 2x the largest overlay round (load <= 1/2), three in rotation
-    c->ov_log2 = 10;
-    while ((1ull << c->ov_log2) < 2 * c->ov_max) c->ov_log2++;
-    const u64 oslots = 1ull << c->ov_log2;
-    const u64 otiles = (c->ov_max + TPB - 1) / TPB + 1;
-    for (int i = 0; i < 3; i++) {
-        if ((e = hipMalloc(&c->d_ov[i], oslots * sizeof(OvSlot))) != hipSuccess) return e;
-        if ((e = hipMalloc(&c->d_ov_list[i], otiles * TPB * 4 * sizeof(u32))) != hipSuccess) return e;
-        if ((e = hipMalloc(&c->d_ov_cnt[i], otiles * sizeof(u32))) != hipSuccess) return e;
-        hm_init_table_kernel<<<grid_for(oslots, 4096), TPB, 0, c->stream>>>((Slot*)c->d_ov[i], oslots);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-    }
+    if (c->stamp_max > mb) c->stamp_max = mb;
+    for (int i = 0; i < 2 && c->stamp_max; i++)
+        if ((e = hipMalloc(&c->d_put_slot[i], c->stamp_max * sizeof(u32))) != hipSuccess) return e;
     return hipSuccess;
 }
 
 void hm_free(nrg_ctx* c) {
-    for (int i = 0; i < 3; i++) {
-        void* ptrs[] = {c->d_ov[i], c->d_ov_list[i], c->d_ov_cnt[i]};
-        for (void* q : ptrs)
-            if (q) (void)hipFree(q);
-        c->d_ov[i] = nullptr;
-        c->d_ov_list[i] = nullptr;
-        c->d_ov_cnt[i] = nullptr;
+    for (int i = 0; i < 2; i++) {
+        if (c->d_put_slot[i]) (void)hipFree(c->d_put_slot[i]);
+        c->d_put_slot[i] = nullptr;
     }
 }
 
 hipError_t hm_init(nrg_ctx* c) {
     hm_init_table_kernel<<<grid_for(c->slots, 16384), TPB, 0, c->stream>>>(c->d_table, c->slots);
     return hipGetLastError();
+}
+
+// The next round's epoch; before the 32-bit epoch wraps, every stamp is renormalised to epoch 1.
+static hipError_t next_epoch(nrg_ctx* c, u32* e) {
+    if (c->epoch >= c->epoch_limit) {
+        hipError_t r = hm_flush(c);
+        if (r != hipSuccess) return r;
+        hm_renorm_kernel<<<grid_for(c->slots, 16384), TPB, 0, c->stream>>>(c->d_table, c->slots, c->d_ctl);
+        if ((r = hipGetLastError()) != hipSuccess) return r;
+        c->epoch = 1;
+    }
+    *e = ++c->epoch;
+    return hipSuccess;
 }
 
 // Replay the records [lo, lo+n) (from `src_recs` if given, else from the ring; writing the
@@ -1201,102 +1131,87 @@ hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool
     // records the deferred half reads: the caller's buffer only when no ring copy is written
     const nrg_put* keep = (src && !write_ring) ? src : nullptr;
     hipError_t e;
-    if (!want_prev && c->ov_max && n <= c->ov_max) {
-        // ---- overlay round: one launch {index(e) | apply(e-1) | clear(e-2) | reads(e-1)} ----
-        const u32 idx = c->ov_next;
-        if (c->ov_clear.valid && c->ov_clear.idx == idx && (e = hm_flush(c)) != hipSuccess) return e;
-        c->ov_next = (idx + 1) % 3;
-        const u32 K1 = ov_k1_for(c, n);
+    u32 epoch;
+    if ((e = next_epoch(c, &epoch)) != hipSuccess) return e;
+    Launch L;
+    const bool stamp = !want_prev && c->stamp_max && n <= c->stamp_max;
+    if (stamp) {
+        // ---- stamp round: one launch {index(e) | apply(e-1) | reads(e-1)} ----
+        const u32 K1 = stamp_k1_for(c);
         const u32 tile = TPB * K1;
-        Launch L;
-        L.ix = IX_OVERLAY;
+        L.ix = IX_STAMP;
         L.K1 = K1;
-        L.oj.rec = ring_src(c, src, lo);
-        L.oj.ring_out = write_ring ? (nrg_put*)c->d_ring : nullptr;
-        L.oj.n = n;
-        L.oj.nblocks = (u32)((n + tile - 1) / tile);
-        L.oj.ov = c->d_ov[idx];
-        L.oj.omask = (1ull << c->ov_log2) - 1;
-        L.oj.list = c->d_ov_list[idx];
-        L.oj.lcnt = c->d_ov_cnt[idx];
-        L.oj.side_st = &c->d_ctl->sp_st[idx];
-        L.oj.exp = c->exp & 0xFF;
+        L.sj.rec = ring_src(c, src, lo);
+        L.sj.ring_out = write_ring ? (nrg_put*)c->d_ring : nullptr;
+        L.sj.n = n;
+        L.sj.nblocks = (u32)((n + tile - 1) / tile);
+        L.sj.epoch = epoch;
+        L.sj.put_slot = c->d_put_slot[epoch & 1];
+        L.sj.created_acc = c->d_created;
         attach_deferred(c, L);
         if ((e = launch(c, L)) != hipSuccess) return e;
-        c->rounds++;
-        HmDeferred& p = c->pend;
-        p.valid = true;
-        p.ov.valid = true;
-        p.ov.idx = idx;
-        p.ov.src = keep;
-        p.ov.lo = lo;
-        p.ov.nblocks = L.oj.nblocks;
-        p.ov.tile = tile;
-        p.keys = d_get_keys;
-        p.R = R;
-        p.vals = d_get_vals;
-        p.found = d_get_found;
-        if (!c->pipeline || keep) return hm_flush(c);
-        return hipSuccess;
+    } else {
+        // ---- bucket round: {index(e) | apply(e-1) | reads(e-1)}, then hm_elect_kernel(e) ----
+        const u32 K1 = k1_for(c, n);
+        const u32 tile = TPB * K1;
+        // slot buckets of about bk_ent entries (previous values keep every Put: smaller buckets)
+        const u64 target = c->bk_ent ? c->bk_ent : (want_prev ? 256 : 512);
+        const u32 log2_slots = 64 - c->slot_shift;
+        u32 nb_log = 6;
+        while ((1ull << nb_log) * target < n && (1u << nb_log) < HM_BK_MAX) nb_log++;
+        if (nb_log > log2_slots) nb_log = log2_slots;
+        L.ix = want_prev ? IX_BUCKET_ALL : IX_BUCKET;
+        L.K1 = K1;
+        L.nb = 1u << nb_log;
+        IndexJob& ij = L.ij;
+        ij.rec = ring_src(c, src, lo);
+        ij.ring_out = write_ring ? (nrg_put*)c->d_ring : nullptr;
+        ij.n = n;
+        ij.nblocks = (u32)((n + tile - 1) / tile);
+        ij.nb_log = nb_log;
+        ij.bk_shift = log2_slots - nb_log;
+        ij.ent = (u64x2*)c->d_bk_ent;
+        ij.ekey = c->d_bk_key;
+        ij.cnt = c->d_bk_cnt;
+        ij.exp = c->exp & 0xFF;
+        attach_deferred(c, L);  // the previous round's apply and reads ride along (index only reads)
+        if ((e = launch(c, L)) != hipSuccess) return e;
+        ElectJob ej{};
+        ej.ent = ij.ent;
+        ej.ekey = ij.ekey;
+        ej.cnt = ij.cnt;
+        ej.nblocks = ij.nblocks;
+        ej.tile = tile;
+        ej.bk_shift = ij.bk_shift;
+        ej.table = c->d_table;
+        ej.shift = c->slot_shift;
+        ej.tmask = c->slots - 1;
+        ej.ctl = c->d_ctl;
+        ej.created_acc = c->d_created;
+        ej.lo = lo;
+        ej.resp_lo = resp_lo;
+        ej.resp_hi = resp_hi;
+        ej.prev = d_prev;
+        ej.prevf = d_prev_found;
+        ej.exp = c->exp >> 8;
+        const unsigned dyn = (ij.nblocks + 1) * 4 + ij.nblocks * 2;
+        if (want_prev) NRG_LAUNCH(c, "hm_elect", hm_elect_kernel<true>, 1u << nb_log, TPB, dyn, c->stream, ej);
+        else NRG_LAUNCH(c, "hm_elect", hm_elect_kernel<false>, 1u << nb_log, TPB, dyn, c->stream, ej);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    // ---- bucket round: {index(e) | clear | reads(e-1)}, then hm_elect_kernel(e) ----
-    // its index pass reads the main table: a deferred overlay apply must not run beside it
-    if (c->pend.valid && c->pend.ov.valid && (e = hm_flush(c)) != hipSuccess) return e;
-    const u32 K1 = k1_for(c, n);
-    const u32 tile = TPB * K1;
-    // slot buckets of about bk_ent entries (previous values keep every Put: smaller buckets)
-    const u64 target = c->bk_ent ? c->bk_ent : (want_prev ? 256 : 512);
-    const u32 log2_slots = 64 - c->slot_shift;
-    u32 nb_log = 6;
-    while ((1ull << nb_log) * target < n && (1u << nb_log) < HM_BK_MAX) nb_log++;
-    if (nb_log > log2_slots) nb_log = log2_slots;
-    Launch L;
-    L.ix = want_prev ? IX_BUCKET_ALL : IX_BUCKET;
-    L.K1 = K1;
-    L.nb = 1u << nb_log;
-    IndexJob& ij = L.ij;
-    ij.rec = ring_src(c, src, lo);
-    ij.ring_out = write_ring ? (nrg_put*)c->d_ring : nullptr;
-    ij.n = n;
-    ij.nblocks = (u32)((n + tile - 1) / tile);
-    ij.nb_log = nb_log;
-    ij.bk_shift = log2_slots - nb_log;
-    ij.ent = (u64x2*)c->d_bk_ent;
-    ij.ekey = c->d_bk_key;
-    ij.cnt = c->d_bk_cnt;
-    ij.exp = c->exp & 0xFF;
-    attach_deferred(c, L);  // the previous round's reads ride along
-    if ((e = launch(c, L)) != hipSuccess) return e;
-    ElectJob ej{};
-    ej.ent = ij.ent;
-    ej.ekey = ij.ekey;
-    ej.cnt = ij.cnt;
-    ej.nblocks = ij.nblocks;
-    ej.tile = tile;
-    ej.bk_shift = ij.bk_shift;
-    ej.table = c->d_table;
-    ej.shift = c->slot_shift;
-    ej.tmask = c->slots - 1;
-    ej.ctl = c->d_ctl;
-    ej.created_acc = c->d_created;
-    ej.lo = lo;
-    ej.resp_lo = resp_lo;
-    ej.resp_hi = resp_hi;
-    ej.prev = d_prev;
-    ej.prevf = d_prev_found;
-    ej.exp = c->exp >> 8;
-    const unsigned dyn = (ij.nblocks + 1) * 4 + ij.nblocks * 2;
-    if (want_prev) NRG_LAUNCH(c, "hm_elect", hm_elect_kernel<true>, 1u << nb_log, TPB, dyn, c->stream, ej);
-    else NRG_LAUNCH(c, "hm_elect", hm_elect_kernel<false>, 1u << nb_log, TPB, dyn, c->stream, ej);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
     c->rounds++;
     HmDeferred& p = c->pend;
     p.valid = true;
+    p.epoch = epoch;
+    p.apply = stamp;
+    p.src = keep;
+    p.lo = lo;
+    p.n = n;
     p.keys = d_get_keys;
     p.R = R;
     p.vals = d_get_vals;
     p.found = d_get_found;
-    if (!c->pipeline) return hm_flush(c);
+    if (!c->pipeline || (stamp && keep)) return hm_flush(c);
     return hipSuccess;
 }
 

@@ -45,23 +45,15 @@ struct Staging {  // growable device scratch for the host-pointer entry points
     uint64_t bytes = 0;
 };
 
-// An overlay round of the hashmap replay (hashmap.hip): overlay `idx` holds its last writers,
-// list_idx / cnt_idx the overlay slots it inserted, per index block of `tile` Puts.
-struct OvRound {
-    bool valid = false;
-    u32 idx = 0;
-    const nrg_put* src = nullptr;  // records: src[i] if set, else ring[(lo + i) & mask]
-    u64 lo = 0;
-    u32 nblocks = 0;
-    u32 tile = 0;
-};
-
 // The second half of the last replayed hashmap round, run in the next launch (beside the next
-// round's index pass) or by a flush: its reads, and for an overlay round its apply.
+// round's index pass) or by a flush: its reads and, for a stamp round, its apply.
 struct HmDeferred {
     bool valid = false;
-    OvRound ov;                 // overlay round whose apply is deferred (ov.valid)
-    const u64* keys = nullptr;  // the round's reads (R may be 0)
+    u32 epoch = 0;
+    bool apply = false;            // stamp round: the elected writers still store their values
+    const nrg_put* src = nullptr;  // records: src[i] if set, else ring[(lo + i) & mask]
+    u64 lo = 0, n = 0;
+    const u64* keys = nullptr;     // the round's reads (R may be 0)
     u64 R = 0;
     u64* vals = nullptr;
     uint8_t* found = nullptr;
@@ -106,15 +98,11 @@ struct nrg_ctx {
     void* d_bk_ent = nullptr;       // [index tiles][tile] 16-B {id << 32 | i+1, value}
     uint64_t* d_bk_key = nullptr;   // [index tiles][tile] key of each entry
     uint32_t* d_bk_cnt = nullptr;   // [bucket][index tiles] offset << 16 | count
-    // Overlay rounds (<= ov_max Puts, no previous values): three rotating overlays, lists of the
-    // overlay slots each round inserted; ov_clear = applied overlay round still to be cleared.
-    uint64_t ov_max = 0;
-    uint32_t ov_log2 = 0;
-    uint32_t ov_next = 0;
-    nrg::OvRound ov_clear;
-    nrg::OvSlot* d_ov[3] = {nullptr, nullptr, nullptr};
-    uint32_t* d_ov_list[3] = {nullptr, nullptr, nullptr};
-    uint32_t* d_ov_cnt[3] = {nullptr, nullptr, nullptr};
+    // Stamp rounds (<= stamp_max Puts, no previous values): per-Put slot ids by epoch parity.
+    uint64_t stamp_max = 0;
+    uint32_t epoch = 1;  // epoch of the last replay round (1: prefill / before any round)
+    uint32_t epoch_limit = 0xFFFFFFF0u;  // renormalise stamps here (NRG_EPOCH_LIMIT for tests)
+    uint32_t* d_put_slot[2] = {nullptr, nullptr};
     // Zipf generator cache: zeta(zipf_n, zipf_theta)
     uint64_t zipf_n = 0;
     double zipf_theta = 0.0, zipf_zetan = 0.0;

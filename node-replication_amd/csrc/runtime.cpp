@@ -72,10 +72,10 @@ int use_device(nrg_ctx* c) {
 hipError_t hm_flush_if(nrg_ctx* c) { return c->cfg.ds_kind == NRG_DS_HASHMAP ? hm_flush(c) : hipSuccess; }
 
 // Log GC boundary: the slowest replica's tail (this replica's ltail), held back to the first
-// record of a deferred hashmap overlay round, whose apply and reads take values from the ring.
+// record of a deferred hashmap stamp round, whose apply and reads take values from the ring.
 uint64_t gc_head(const nrg_ctx* c) {
-    const nrg::OvRound& o = c->pend.ov;
-    if (c->pend.valid && o.valid && !o.src && o.lo < c->ltail) return o.lo;
+    const nrg::HmDeferred& p = c->pend;
+    if (p.valid && p.apply && !p.src && p.lo < c->ltail) return p.lo;
     return c->ltail;
 }
 
@@ -337,9 +337,11 @@ int nrg_open(int dev, const nrg_config* cfg_in, nrg_ctx** out) {
         OPEN_CHK(hm_init(c));
         OPEN_CHK(hipMalloc(&c->d_created, HM_CREATED_SLOTS * sizeof(uint64_t)));
         OPEN_CHK(hipMemsetAsync(c->d_created, 0, HM_CREATED_SLOTS * sizeof(uint64_t), c->stream));
-        // rounds of <= ov_max Puts without previous values replay in one launch (overlay rounds)
-        c->ov_max = 1u << 18;
-        if (const char* e = std::getenv("NRG_OV_MAX")) c->ov_max = (uint64_t)std::atoll(e);
+        // rounds of <= stamp_max Puts without previous values replay in one launch (stamp
+        // rounds); larger ones and previous-value rounds take the bucket elector
+        c->stamp_max = 250000;
+        if (const char* e = std::getenv("NRG_STAMP_MAX")) c->stamp_max = (uint64_t)std::atoll(e);
+        if (const char* e = std::getenv("NRG_EPOCH_LIMIT")) c->epoch_limit = (uint32_t)std::atoll(e);
         OPEN_CHK(hm_alloc(c, mb));
         // tuning knobs: Puts per index thread, target entries per elector bucket
         if (const char* e = std::getenv("NRG_K1")) c->k1_items = (uint32_t)std::atoi(e);
@@ -1007,5 +1009,14 @@ extern "C" int nrg_test_maxscan(nrg_ctx* c, const uint32_t* d_keys, const uint32
     if (c->cfg.ds_kind == NRG_DS_STACK)
         HIPCHK(hipMemsetAsync(c->d_scan_desc, 0, c->scan_desc_words * 4, c->stream));
     HIPCHK(sync_all(c));
+    return NRG_OK;
+}
+
+extern "C" int nrg_test_ring_read(nrg_ctx* c, uint64_t phys, void* out) {
+    if (!c || !out || phys >= c->log_size) return NRG_E_INVAL;
+    int r = use_device(c);
+    if (r) return r;
+    HIPCHK(sync_all(c));
+    HIPCHK(hipMemcpy(out, (const char*)c->d_ring + phys * c->rec_bytes, c->rec_bytes, hipMemcpyDeviceToHost));
     return NRG_OK;
 }

@@ -49,7 +49,6 @@ __device__ __forceinline__ long long fn_apply(Fn f, long long x) {
 }
 
 constexpr u64 D_AGG = 1ull << 62;
-constexpr u64 D_INC = 2ull << 62;
 constexpr u64 D_MASK = 3ull << 62;
 
 // identity of fn_then (a = -infinity for max(a, x + b))
@@ -181,43 +180,44 @@ __global__ __launch_bounds__(ST_TPB) void st_tile_kernel(const nrg_stack_op* __r
     for (int i = 0; i < w; i++) wpre = fn_then(wpre, Fn{s_wb[i], s_wa[i]});
     const Fn tpre = fn_then(wpre, ex);
     if (w == 0) {
-        // Wave 0 publishes the tile's aggregate and does the look-back with all 64 lanes:
-        // lane l reads tile (tt - l)'s descriptor, so one memory round trip covers 64
-        // predecessors.
+        // Wave 0 publishes the tile's aggregate, then composes the aggregates of ALL earlier
+        // tiles itself (64 per wave instruction, every load of a group in flight at once)
+        // instead of waiting for an inclusive prefix to ripple down the chain of tiles: each
+        // tile publishes its aggregate right after its loads, so the prefix of the last tile is
+        // ready one round trip after the last predecessor has loaded its ops.
         Fn tagg = {0, 0};
         for (int i = 0; i < 4; i++) tagg = fn_then(tagg, Fn{s_wb[i], s_wa[i]});
-        long long dbase = d0;
-        if (tile == 0) {
-            if (lane == 0)
-                __hip_atomic_store(&desc[0], D_INC | (u64)fn_apply(tagg, dbase), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            if (lane == 0) __hip_atomic_store(&desc[tile], pack_agg(tagg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            Fn acc = FN_ID;  // composition of the predecessors consumed so far (older ones apply first)
-            int tt = (int)tile - 1;
-            for (;;) {
-                const int idx = tt - lane;
-                const u64 v = idx >= 0 ? __hip_atomic_load(&desc[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-                const u64 st = v & D_MASK;
-                const u64 nr = __ballot(st == 0);
-                const u64 ic = __ballot(st == D_INC);
-                const int first_nr = nr ? __ffsll((unsigned long long)nr) - 1 : 64;
-                const int first_ic = ic ? __ffsll((unsigned long long)ic) - 1 : 64;
-                const int use = first_ic < first_nr ? first_ic : first_nr;  // aggregates usable now
-                const Fn f = lane < use ? unpack_agg(v) : FN_ID;
-                acc = fn_then(wave_compose(f), acc);
-                if (first_ic < first_nr) {
-                    const long long incv = (long long)(__shfl(v, first_ic, 64) & ~D_MASK);
-                    dbase = fn_apply(acc, incv);
-                    break;
-                }
-                tt -= use;
-                if (use < 64) __builtin_amdgcn_s_sleep(1);
+        if (lane == 0) __hip_atomic_store(&desc[tile], pack_agg(tagg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        Fn acc = {0, 0};  // composition of tiles [0, c0) (oldest applied first)
+        constexpr int G = 8;  // groups of 64 descriptors with their loads in flight together
+        for (int c0 = 0; c0 < (int)tile; c0 += 64 * G) {
+            u64 v[G];
+#pragma unroll
+            for (int gq = 0; gq < G; gq++) {
+                // lane l of group gq holds tile c0 + 64 gq + 63 - l: the highest lane is the oldest
+                const int idx = c0 + 64 * gq + 63 - lane;
+                v[gq] = idx < (int)tile ? __hip_atomic_load(&desc[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                        : D_AGG;  // past the predecessors: identity (b = a = 0 packed below)
             }
-            if (lane == 0)
-                __hip_atomic_store(&desc[tile], D_INC | (u64)fn_apply(tagg, dbase), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+            for (int gq = 0; gq < G; gq++) {
+                const int idx = c0 + 64 * gq + 63 - lane;
+                if (idx < (int)tile) {
+                    u32 spins = 0;
+                    while (!(v[gq] & D_MASK)) {  // not published yet (its tile is still loading)
+                        __builtin_amdgcn_s_sleep(1);
+                        v[gq] = __hip_atomic_load(&desc[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (++spins == (1u << 26)) {  // bounded: never hang the device
+                            atomicOr(&ctl->err, ERR_CAPACITY);
+                            break;
+                        }
+                    }
+                }
+                const Fn f = idx < (int)tile ? unpack_agg(v[gq]) : FN_ID;
+                acc = fn_then(acc, wave_compose(f));
+            }
         }
+        const long long dbase = fn_apply(acc, d0);
         if (lane == 0) {
             const u64 ntiles = (n + ST_TILE - 1) / ST_TILE;
             if ((u64)tile == ntiles - 1) {

@@ -461,6 +461,7 @@ class Log:
             size <<= 1
         self.bytes = nbytes
         self.size = size
+        self.head = 0
         self.tail = 0
         self.ctail = 0
         self._next = 1
@@ -472,13 +473,37 @@ class Log:
         with self.lock:
             if self._next >= MAX_REPLICAS:
                 return None
+            # each replica's copy of the log starts empty: a late replica could not catch up on
+            # entries appended before it (checked before any state changes)
+            if self.tail != 0:
+                raise RuntimeError("register replicas before appending to the log")
             idx = self._next
             self._next += 1
             self._replicas.append(replica)
-            # a late replica's copy starts at the current tail only if nothing was appended yet
-            if self.tail != 0:
-                raise RuntimeError("register replicas before appending to the log")
             return idx
+
+    def _ltails(self):
+        return [r.dev.log_state()["ltail"] for r in self._replicas]
+
+    def get_ctail(self) -> int:
+        """Log::get_ctail (nr/src/log.rs:677-679): the largest tail any replica has replayed."""
+        with self.lock:
+            self.ctail = max([self.ctail] + self._ltails())
+            return self.ctail
+
+    def is_replica_synced_for_reads(self, replica: "Replica", ctail: Optional[int] = None) -> bool:
+        """Log::is_replica_synced_for_reads (nr/src/log.rs:671-673): ltail >= ctail."""
+        c = self.get_ctail() if ctail is None else ctail
+        return replica.dev.log_state()["ltail"] >= c
+
+    def advance_head(self) -> int:
+        """Log::advance_head (nr/src/log.rs:536-580): head = min over replicas' ltails (each
+        device replica's own ring is garbage-collected up to its ltail by libnrgpu.so)."""
+        with self.lock:
+            lt = self._ltails()
+            if lt:
+                self.head = max(self.head, min(lt))
+            return self.head
 
     def append(self, recs: np.ndarray, idx: int) -> int:
         """Log::append: the same records at the same logical indices in every copy."""

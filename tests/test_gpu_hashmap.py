@@ -136,17 +136,17 @@ def test_fused_round_device(nrg, orc):
     _check_state(dev, om)
 
 
-@pytest.mark.parametrize("path", ["overlay", "bucket"])
+@pytest.mark.parametrize("path", ["stamp", "bucket"])
 def test_pipelined_rounds_back_to_back(nrg, orc, monkeypatch, path):
     """config.pipeline = 1: rounds enqueued back to back, no host sync in between. Each round's
-    reads run in the next round's launch, beside its index pass (and, for overlay rounds,
-    beside the apply of their own round's writes), and must see exactly their own round's
-    state (keys created by later rounds invisible, values overwritten later not yet there).
-    NRG_OV_MAX=0 sends every round through the bucket elector instead."""
+    reads run in the next round's launch, beside its index pass (and, for stamp rounds, beside
+    the apply of their own round's writes), and must see exactly their own round's state (keys
+    created by later rounds invisible, values overwritten later not yet there).
+    NRG_STAMP_MAX=0 sends every round through the bucket elector instead."""
     import torch
 
     if path == "bucket":
-        monkeypatch.setenv("NRG_OV_MAX", "0")
+        monkeypatch.setenv("NRG_STAMP_MAX", "0")
     dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=17, max_batch=1 << 14, pipeline=1)
     dev.use_torch_stream()
     om = orc.HashMap()
@@ -404,3 +404,41 @@ def test_b1_full_size_rounds(nrg, orc):
         np.testing.assert_array_equal(gf.cpu().numpy(), want[r][1], err_msg=f"round {r} found")
         np.testing.assert_array_equal(gv.cpu().numpy().view(np.uint64), want[r][0], err_msg=f"round {r} vals")
     assert dev.hm_digest() == om.digest()
+
+
+def test_epoch_renormalisation(nrg, orc, monkeypatch):
+    """Replay epochs are 32-bit; before they wrap every stamp is renormalised to epoch 1. A limit
+    of 6 (NRG_EPOCH_LIMIT) renormalises every few rounds: pipelined stamp and bucket rounds with
+    new keys, overwrites and side-slot keys across several renormalisations, against the oracle."""
+    import torch
+
+    monkeypatch.setenv("NRG_EPOCH_LIMIT", "6")
+    monkeypatch.setenv("NRG_STAMP_MAX", "5000")
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=16, max_batch=8192, pipeline=1)
+    dev.use_torch_stream()
+    om = orc.HashMap()
+    dev.hm_prefill_range(500, 1)
+    om.prefill_range(500, 1)
+    outs, want = [], []
+    for r in range(17):
+        W = 3000 if r % 3 else 7000  # 7000 > NRG_STAMP_MAX: bucket rounds in between
+        keys = orc.gen_uniform(W, 900 + r, 4000 + 150 * r)
+        keys[::113] = EMPTY
+        vals = orc.gen_raw(W, 950 + r)
+        R = 3000
+        gk = orc.gen_uniform(R, 990 + r, 7000)
+        gk[::127] = EMPTY
+        d_puts = torch.from_numpy(_puts(keys, vals).view(np.int64).copy()).cuda()
+        d_gk = torch.from_numpy(gk.view(np.int64)).cuda()
+        d_gv = torch.full((R,), -1, dtype=torch.int64, device="cuda")
+        d_gf = torch.full((R,), 7, dtype=torch.uint8, device="cuda")
+        dev.hm_round_device(d_puts, W, 1, d_gk, R, d_gv, d_gf, None, None)
+        outs.append((d_puts, d_gk, d_gv, d_gf))
+        om.replay(keys, vals)
+        want.append(om.get_batch(gk))
+    dev.join()
+    for r, (_, _, gv, gf) in enumerate(outs):
+        np.testing.assert_array_equal(gf.cpu().numpy(), want[r][1], err_msg=f"round {r} found")
+        np.testing.assert_array_equal(gv.cpu().numpy().view(np.uint64), want[r][0], err_msg=f"round {r} vals")
+    dev.sync()
+    _check_state(dev, om)
