@@ -97,3 +97,94 @@ def test_ring_full_is_an_error(nrg):
     st = dev.log_state()
     assert st["tail"] == 0  # nothing was appended
     dev.close()
+
+
+def _round(nrg, dev, keys, vals, gk):
+    import torch
+
+    d_p = torch.from_numpy(_puts(nrg, keys, vals).view(np.int64).copy()).cuda()
+    d_gk = torch.from_numpy(np.ascontiguousarray(gk).view(np.int64)).cuda()
+    gv = torch.full((len(gk),), -1, dtype=torch.int64, device="cuda")
+    gf = torch.full((len(gk),), 9, dtype=torch.uint8, device="cuda")
+    dev.hm_round_device(d_p, len(keys), 1, d_gk, len(gk), gv, gf)
+    return d_p, d_gk, gv, gf
+
+
+def test_log_reset_with_a_deferred_round(nrg, orc):
+    """pipeline=1: round, Log::reset, round. The first round's deferred half (apply + reads)
+    must run before the reset lets the next round reuse log positions 0.. (advisor finding on
+    nrg_log_reset); every read and the final digest against the oracle."""
+    import torch
+
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=14, max_batch=4096, pipeline=1)
+    dev.use_torch_stream()
+    om = orc.HashMap()
+    outs, want = [], []
+    for r in range(4):
+        keys = orc.gen_uniform(2000, 40 + r, 3000)
+        vals = orc.gen_raw(2000, 50 + r)
+        gk = orc.gen_uniform(1500, 60 + r, 3500)
+        outs.append(_round(nrg, dev, keys, vals, gk))
+        om.replay(keys, vals)
+        want.append(om.get_batch(gk))
+        if r % 2 == 0:
+            dev.log_reset()
+            st = dev.log_state()
+            assert st["tail"] == st["head"] == st["ltail"] == 0
+    dev.join()
+    torch.cuda.synchronize()
+    for r, (_, _, gv, gf) in enumerate(outs):
+        np.testing.assert_array_equal(gf.cpu().numpy(), want[r][1], err_msg=f"round {r} found")
+        np.testing.assert_array_equal(gv.cpu().numpy().view(np.uint64), want[r][0], err_msg=f"round {r} vals")
+    assert dev.hm_digest() == om.digest()
+    dev.close()
+
+
+def test_stream_switch_between_async_rounds(nrg, orc):
+    """nrg_set_stream between async rounds orders everything queued on the old stream before
+    the new stream's work (advisor finding): rounds alternate between two torch streams with no
+    host synchronisation in between."""
+    import torch
+
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=15, max_batch=8192, pipeline=1)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    om = orc.HashMap()
+    outs, want = [], []
+    for r in range(6):
+        s = s1 if r % 2 == 0 else s2
+        with torch.cuda.stream(s):
+            keys = orc.gen_uniform(6000, 70 + r, 9000)
+            vals = orc.gen_raw(6000, 80 + r)
+            gk = orc.gen_uniform(5000, 90 + r, 9500)
+            dev.set_stream(s.cuda_stream)
+            outs.append(_round(nrg, dev, keys, vals, gk))
+            om.replay(keys, vals)
+            want.append(om.get_batch(gk))
+    dev.join()
+    torch.cuda.synchronize()
+    for r, (_, _, gv, gf) in enumerate(outs):
+        np.testing.assert_array_equal(gf.cpu().numpy(), want[r][1], err_msg=f"round {r} found")
+        np.testing.assert_array_equal(gv.cpu().numpy().view(np.uint64), want[r][0], err_msg=f"round {r} vals")
+    assert dev.hm_digest() == om.digest()
+    dev.close()
+
+
+def test_stack_overflow_then_dump_and_peek(nrg):
+    """A chunk that pushes past stack_capacity latches NRG_E_CAPACITY once; afterwards len,
+    dump and peek never report or copy more than the capacity (advisor finding)."""
+    cap = 1000
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_STACK, 0, max_batch=4096, stack_capacity=cap)
+    recs = np.zeros(1500, nrg.STACK_OP_DTYPE)
+    recs["val"] = np.arange(1500, dtype=np.uint32)
+    recs["op"] = 1
+    dev.log_append(recs, 1)
+    with pytest.raises(nrg.NrgError) as e:
+        dev.log_exec()
+    assert e.value.code == nrg._lib.NRG_E_CAPACITY
+    n = dev.st_len()
+    assert n <= cap
+    out = dev.st_dump()
+    assert len(out) == n <= cap
+    top = dev.st_peek()
+    assert top is None or 0 <= top < 1500
+    dev.close()
