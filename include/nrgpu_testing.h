@@ -21,6 +21,8 @@ int nrg_test_maxscan(nrg_ctx* ctx, const uint32_t* d_keys, const uint32_t* d_val
  * (rec bytes per ds kind); syncs first. Lets tests check Log::index (nr/src/log.rs:528-530)
  * against what the replica's HBM ring actually holds. */
 int nrg_test_ring_read(nrg_ctx* ctx, uint64_t phys, void* out);
+/* diagnostic phase timestamps of the last replay (contexts opened with NRG_EXP & 2) */
+int nrg_test_debug_read(nrg_ctx* ctx, uint64_t* out, uint64_t words);
 #ifdef __cplusplus
 }
 #endif

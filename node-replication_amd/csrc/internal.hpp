@@ -124,6 +124,7 @@ struct nrg_ctx {
     uint64_t scan_desc_words = 0;
 
     nrg::Staging stg[4];
+    uint64_t* d_dbg = nullptr;  // diagnostic phase timestamps (NRG_EXP & 2), [tiles][16]
 
     // ---- timing ----
     bool timing = false;

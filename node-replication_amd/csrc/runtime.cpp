@@ -356,13 +356,12 @@ int nrg_open(int dev, const nrg_config* cfg_in, nrg_ctx** out) {
             return NRG_E_INVAL;
         }
         OPEN_CHK(hipMalloc(&c->d_stack, cf.stack_capacity * sizeof(uint32_t)));
-        OPEN_CHK(hipMalloc(&c->d_tmp_u64, mb * sizeof(uint64_t)));  // last-Push window: 2 * mb u32
-        OPEN_CHK(hipMemsetAsync(c->d_tmp_u64, 0, mb * sizeof(uint64_t), c->stream));
-        c->tmp_words = mb;
         c->scan_desc_words = 2 * (32 + (mb + 2047) / 2048);
         OPEN_CHK(hipMalloc(&c->d_scan_desc, c->scan_desc_words * 4));
         OPEN_CHK(hipMemsetAsync(c->d_scan_desc, 0, c->scan_desc_words * 4, c->stream));
         OPEN_CHK(hipMalloc(&c->d_st_aux, st_aux_bytes(mb)));
+        if (const char* e = std::getenv("NRG_EXP")) c->exp = (uint32_t)std::atoi(e);
+        if (c->exp & 2) OPEN_CHK(hipMalloc(&c->d_dbg, ((mb + 2047) / 2048) * 16 * sizeof(uint64_t)));
     } else {
         const uint64_t T = cf.synth_hot_writes + cf.synth_cold_writes;
         if (!cf.synth_n || cf.synth_hot_reads == 0 || cf.synth_n <= cf.synth_hot_reads || T == 0 || T > 64 ||
@@ -398,7 +397,7 @@ int nrg_close(nrg_ctx* c) {
     if (c->stream && c->stream != c->own_stream) (void)hipStreamSynchronize(c->stream);
     void* ptrs[] = {c->d_ring,    c->d_ctl,      c->d_table,    c->d_stack,  c->d_words,
                     c->d_sort_aux, c->d_tmp_u64, c->d_scan_desc, c->d_created, c->d_st_aux,
-                    c->d_sy_aux,  c->d_bk_ent,   c->d_bk_key,   c->d_bk_cnt};
+                    c->d_sy_aux,  c->d_bk_ent,   c->d_bk_key,   c->d_bk_cnt, c->d_dbg};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     sort_free(c->sort);
@@ -1018,5 +1017,15 @@ extern "C" int nrg_test_ring_read(nrg_ctx* c, uint64_t phys, void* out) {
     if (r) return r;
     HIPCHK(sync_all(c));
     HIPCHK(hipMemcpy(out, (const char*)c->d_ring + phys * c->rec_bytes, c->rec_bytes, hipMemcpyDeviceToHost));
+    return NRG_OK;
+}
+
+extern "C" int nrg_test_debug_read(nrg_ctx* c, uint64_t* out, uint64_t words) {
+    if (!c || !out) return NRG_E_INVAL;
+    if (!c->d_dbg) return NRG_E_INVAL;
+    int r = use_device(c);
+    if (r) return r;
+    HIPCHK(sync_all(c));
+    HIPCHK(hipMemcpy(out, c->d_dbg, words * 8, hipMemcpyDeviceToHost));
     return NRG_OK;
 }

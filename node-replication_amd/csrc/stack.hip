@@ -18,8 +18,10 @@
 //     tile, the slot's content before the chunk.
 // Each tile publishes its minimum depth and a table "last Push to slot tmin + r" (u16
 // positions), so the cross-tile Pops (a few percent for random ops) walk back over tile minima
-// only. The chunk's final content of a slot is its last Push, picked with one atomicMax per
-// (tile, pushed slot) in a window of 2n slots around the chunk's starting depth.
+// only. The chunk's final content of a slot s below the final depth is its last Push, which
+// lies in the LAST tile whose minimum depth is <= s (the walk never comes back down to s after
+// it); that tile's table already holds it, so st_finish_kernel commits, per tile, the levels
+// [tmin, min(tile end depth, minimum depth of every later tile)).
 //
 // Kernels: st_tile_kernel (scan + in-tile pairing + tables), st_finish_kernel (cross-tile
 // Pops, last Pushes -> stack, depth update).
@@ -84,6 +86,7 @@ __device__ __forceinline__ Fn unpack_agg(u64 v) {
 // Per-tile results of st_tile_kernel, read by st_cross_kernel.
 struct StTiles {
     long long* tmin;   // [tiles] minimum depth reached in the tile (start and end included)
+    u32* tend;         // [tiles] end depth of the tile - tmin
     u32* table;        // [tiles][ST_TILE] value of the tile's last Push to slot tmin + r, for the
                        // slots below the tile's end depth (the only ones ever looked up)
     u32* ucnt;         // [tiles] Pops whose Push is outside the tile
@@ -111,9 +114,13 @@ constexpr u32 ST_INF = 0xFFFFu;
 __global__ __launch_bounds__(ST_TPB) void st_tile_kernel(const nrg_stack_op* __restrict__ src, nrg_stack_op* ring,
                                                          u64 ring_mask, u64 lo,
                                                          u64 n, DevCtl* ctl, u64* desc, u32* ticket, StTiles tl,
-                                                         u32* __restrict__ last, const u32* __restrict__ stack,
+                                                         const u32* __restrict__ stack,
                                                          u64 cap, u64 resp_lo, u64 resp_hi, int push_resp,
-                                                         u32* __restrict__ resp, uint8_t* __restrict__ some) {
+                                                         u32* __restrict__ resp, uint8_t* __restrict__ some, u32 exp,
+                                                         u64* __restrict__ dbg) {
+#define ST_MARK(K) \
+    if (dbg && threadIdx.x == 0) dbg[(u64)blockIdx.x * 16 + (K)] = wall_clock64()
+    ST_MARK(0);
     __shared__ long long s_wb[4], s_wa[4], s_wmin[4];
     __shared__ u32 s_tile, s_ucnt, s_aend;
     __shared__ long long s_dbase;
@@ -126,10 +133,11 @@ __global__ __launch_bounds__(ST_TPB) void st_tile_kernel(const nrg_stack_op* __r
     __shared__ u32 s_q[4][ST_ITEMS * 64];      // per wave: Pops answered beyond their thread
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     if (t == 0) {
-        s_tile = atomicAdd(ticket, 1u);
+        s_tile = (exp & 1) ? blockIdx.x : atomicAdd(ticket, 1u);  // exp 1: diagnostic only
         s_ucnt = 0;
     }
     __syncthreads();
+    ST_MARK(1);
     const u32 tile = s_tile;
     const u64 tbase = (u64)tile * ST_TILE;
     const u64 base = tbase + (u64)t * ST_ITEMS;
@@ -178,6 +186,7 @@ __global__ __launch_bounds__(ST_TPB) void st_tile_kernel(const nrg_stack_op* __r
     __syncthreads();
     Fn wpre = {0, 0};
     for (int i = 0; i < w; i++) wpre = fn_then(wpre, Fn{s_wb[i], s_wa[i]});
+    ST_MARK(2);
     const Fn tpre = fn_then(wpre, ex);
     if (w == 0) {
         // Wave 0 publishes the tile's aggregate, then composes the aggregates of ALL earlier
@@ -188,35 +197,38 @@ __global__ __launch_bounds__(ST_TPB) void st_tile_kernel(const nrg_stack_op* __r
         Fn tagg = {0, 0};
         for (int i = 0; i < 4; i++) tagg = fn_then(tagg, Fn{s_wb[i], s_wa[i]});
         if (lane == 0) __hip_atomic_store(&desc[tile], pack_agg(tagg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        Fn acc = {0, 0};  // composition of tiles [0, c0) (oldest applied first)
-        constexpr int G = 8;  // groups of 64 descriptors with their loads in flight together
-        for (int c0 = 0; c0 < (int)tile; c0 += 64 * G) {
-            u64 v[G];
+        // lane l composes the run of predecessors [r*G, r*G + G), r = 63 - l, in registers (older
+        // first); one wave composition then joins the runs (the highest lane holds the oldest)
+        const int np = (int)tile;
+        const int G = (np + 63) / 64;
+        const int r0 = (63 - lane) * G;
+        Fn acc = FN_ID;
+        constexpr int B = 8;  // descriptor loads in flight per lane
+        for (int g0 = 0; g0 < G; g0 += B) {
+            u64 v[B];
 #pragma unroll
-            for (int gq = 0; gq < G; gq++) {
-                // lane l of group gq holds tile c0 + 64 gq + 63 - l: the highest lane is the oldest
-                const int idx = c0 + 64 * gq + 63 - lane;
-                v[gq] = idx < (int)tile ? __hip_atomic_load(&desc[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                        : D_AGG;  // past the predecessors: identity (b = a = 0 packed below)
+            for (int q = 0; q < B; q++) {
+                const int idx = r0 + g0 + q;
+                v[q] = (g0 + q < G && idx < np) ? __hip_atomic_load(&desc[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                                 : 0ull;
             }
 #pragma unroll
-            for (int gq = 0; gq < G; gq++) {
-                const int idx = c0 + 64 * gq + 63 - lane;
-                if (idx < (int)tile) {
-                    u32 spins = 0;
-                    while (!(v[gq] & D_MASK)) {  // not published yet (its tile is still loading)
-                        __builtin_amdgcn_s_sleep(1);
-                        v[gq] = __hip_atomic_load(&desc[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        if (++spins == (1u << 26)) {  // bounded: never hang the device
-                            atomicOr(&ctl->err, ERR_CAPACITY);
-                            break;
-                        }
+            for (int q = 0; q < B; q++) {
+                const int idx = r0 + g0 + q;
+                if (g0 + q >= G || idx >= np) continue;
+                u32 spins = 0;
+                while (!(v[q] & D_MASK)) {  // not published yet (its tile is still loading)
+                    __builtin_amdgcn_s_sleep(1);
+                    v[q] = __hip_atomic_load(&desc[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (++spins == (1u << 26)) {  // bounded: never hang the device
+                        atomicOr(&ctl->err, ERR_CAPACITY);
+                        break;
                     }
                 }
-                const Fn f = idx < (int)tile ? unpack_agg(v[gq]) : FN_ID;
-                acc = fn_then(acc, wave_compose(f));
+                acc = fn_then(acc, unpack_agg(v[q]));
             }
         }
+        acc = np ? wave_compose(acc) : Fn{0, 0};
         const long long dbase = fn_apply(acc, d0);
         if (lane == 0) {
             const u64 ntiles = (n + ST_TILE - 1) / ST_TILE;
@@ -229,6 +241,7 @@ __global__ __launch_bounds__(ST_TPB) void st_tile_kernel(const nrg_stack_op* __r
     }
     __syncthreads();
 
+    ST_MARK(3);
     // Depth after each op, relative to the tile's minimum (start and end included: <= 2048).
     const long long dbase = s_dbase;
     const long long dstart = fn_apply(tpre, dbase);
@@ -246,6 +259,7 @@ __global__ __launch_bounds__(ST_TPB) void st_tile_kernel(const nrg_stack_op* __r
     }
     if (over) atomicOr(&ctl->err, ERR_CAPACITY);
     const long long tmin = block_min4(dmin, s_wmin, w, lane);
+    ST_MARK(4);
     u32 a[ST_ITEMS];  // relative depth after each of this thread's ops
     u32 amin = ST_INF;
     dd = dstart;
@@ -284,6 +298,7 @@ __global__ __launch_bounds__(ST_TPB) void st_tile_kernel(const nrg_stack_op* __r
             __syncthreads();
         }
     }
+    ST_MARK(5);
     u32 after = __shfl_down(sfx, 1, 64);  // min over later threads in the wave
     if (lane == 63) after = ST_INF;
     for (int i = w + 1; i < 4; i++) after = s_sw[i] < after ? s_sw[i] : after;
@@ -342,6 +357,7 @@ __global__ __launch_bounds__(ST_TPB) void st_tile_kernel(const nrg_stack_op* __r
         prv = a[q];
     }
     __syncthreads();
+    ST_MARK(6);
     for (u32 i = lane; i < qn; i += 64) {
         const u32 e = s_q[w][i];
         const u32 s = e >> 11, pos = e & 2047u;
@@ -374,56 +390,53 @@ __global__ __launch_bounds__(ST_TPB) void st_tile_kernel(const nrg_stack_op* __r
             some[g - resp_lo] = 1;
         }
     }
+    ST_MARK(7);
     if (t == ST_TPB - 1) s_aend = a[ST_ITEMS - 1];
     __syncthreads();
     // Levels [tmin, end depth) each have a last Push (suffix records); no other level has one.
     u32* tab = tl.table + (u64)tile * ST_TILE;
-    for (u32 r = t; r < s_aend; r += ST_TPB) {
-        const uint16_t p = s_tab[r];
-        tab[r] = s_val[p];
-        atomicMax(&last[(u64)(tmin + r - d0 + (long long)n)], ((tile << 11) | p) + 1u);
-    }
+    for (u32 r = t; r < s_aend; r += ST_TPB) tab[r] = s_val[s_tab[r]];
     if (t == 0) {
         tl.tmin[tile] = tmin;
+        tl.tend[tile] = s_aend;
         tl.ucnt[tile] = s_ucnt;
     }
+    ST_MARK(8);
+#undef ST_MARK
 }
 
 // One block per tile after st_tile_kernel. Every block stages all tile minima in LDS (with the
-// minimum of every 64-tile group) and then
-//   * commits: for the slots any tile pushed — [min tmin, max tmin + 2048) of the window
-//     [depth0 - n, depth0 + n) — writes the chunk's last Push and clears the window entry;
+// minimum of every 8- and 64-tile group) and then
+//   * commits: the tile's levels [tmin, min(end depth, min of every later tile's minimum)) are
+//     the slots whose last Push of the chunk is this tile's, held in its table;
 //   * resolves the tile's Pops whose Push lies in an earlier tile: the nearest earlier tile
 //     whose minimum is <= the slot (a walk that skips 8- and 64-tile groups whose minimum is
 //     above the slot), or the pre-chunk content st_tile_kernel read.
 // Block 0 publishes the new depth.
-__global__ __launch_bounds__(256) void st_finish_kernel(const nrg_stack_op* __restrict__ ring, u64 ring_mask, u64 lo,
-                                                        u64 n, DevCtl* ctl, StTiles tl, u32* __restrict__ last,
+__global__ __launch_bounds__(256) void st_finish_kernel(u64 lo, u64 n, DevCtl* ctl, StTiles tl,
                                                         u32* __restrict__ stack, u64 cap, u64 resp_lo, u64 resp_hi,
                                                         u32* __restrict__ resp, uint8_t* __restrict__ some,
                                                         u64* desc, u32* ticket) {
     extern __shared__ long long s_tm[];  // [tiles] tile minima, [tiles/8 + 1] and [tiles/64 + 1] group minima
-    __shared__ long long s_lo[4], s_hi[4];
+    __shared__ long long s_lo[4];
     const u32 tiles = gridDim.x;
     const u32 tile = blockIdx.x;
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     // independent loads first: they overlap the staging below
-    const long long d0 = ctl->depth0;
     const u32 cnt = resp ? tl.ucnt[tile] : 0u;
     const u32 v0 = tl.upop[(u64)tile * ST_TILE + t];
     const u32 uv0 = tl.uval[(u64)tile * ST_TILE + t];
+    const u32 tend = tl.tend[tile];
     if (t == 0) desc[tile] = 0;  // ready for the next chunk (the tile kernel is done)
     if (tile == 0 && t == 0) *ticket = 0;
     const u32 ngr = (tiles + 63) / 64;
     long long* s_g8 = s_tm + tiles;
     long long* s_gm = s_g8 + tiles / 8 + 1;
-    long long mn = 1ll << 62, mx = -(1ll << 62);
+    long long later = 1ll << 62;  // minimum over the tiles after this one
     for (u32 k = t; k < ngr * 64; k += 256) {
         const long long v = k < tiles ? tl.tmin[k] : (1ll << 62);
-        if (k < tiles) {
-            s_tm[k] = v;
-            mx = v > mx ? v : mx;
-        }
+        if (k < tiles) s_tm[k] = v;
+        if (k > tile) later = v < later ? v : later;
         long long m = v;
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {
@@ -432,36 +445,23 @@ __global__ __launch_bounds__(256) void st_finish_kernel(const nrg_stack_op* __re
             if (off == 4 && (lane & 7) == 0 && (k >> 3) <= tiles / 8) s_g8[k >> 3] = m;
         }
         if (lane == 0) s_gm[k >> 6] = m;
-        mn = m < mn ? m : mn;
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
-        const long long x = __shfl_xor(mx, off, 64);
-        mx = x > mx ? x : mx;
+        const long long x = __shfl_xor(later, off, 64);
+        later = x < later ? x : later;
     }
-    if (lane == 0) {
-        s_lo[w] = mn;
-        s_hi[w] = mx;
-    }
+    if (lane == 0) s_lo[w] = later;
     __syncthreads();
     if (tile == 0 && t == 0) ctl->depth = ctl->depth_next;
     {
-        long long smin = s_lo[0], smax = s_hi[0];
-        for (int i = 1; i < 4; i++) {
-            smin = s_lo[i] < smin ? s_lo[i] : smin;
-            smax = s_hi[i] > smax ? s_hi[i] : smax;
-        }
-        long long ilo = smin - d0 + (long long)n, ihi = smax + ST_TILE - d0 + (long long)n;
-        ilo = ilo < 0 ? 0 : ilo;
-        ihi = ihi > 2 * (long long)n ? 2 * (long long)n : ihi;
-        for (long long i = ilo + tile * 256ll + t; i < ihi; i += (long long)tiles * 256) {
-            const u32 x = last[i];
-            if (!x) continue;
-            last[i] = 0;
-            const long long slot = i + d0 - (long long)n;
-            if ((u64)slot < cap)
-                stack[slot] = ring[(lo + (u64)((x - 1) >> 11) * ST_TILE + ((x - 1) & 2047u)) & ring_mask].val;
-        }
+        for (int i = 0; i < 4; i++) later = s_lo[i] < later ? s_lo[i] : later;
+        const long long tm = s_tm[tile];
+        long long hi = tm + (long long)tend;
+        hi = hi < later ? hi : later;
+        const u32* tab = tl.table + (u64)tile * ST_TILE;
+        for (long long sl = tm + t; sl < hi; sl += 256)
+            if ((u64)sl < cap) stack[sl] = tab[sl - tm];
     }
     const long long tmin = s_tm[tile];
     for (u32 j = t; j < cnt; j += 256) {
@@ -507,18 +507,19 @@ hipError_t st_replay_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 resp_hi, 
     StTiles tl;
     tl.tmin = (long long*)c->d_st_aux;
     tl.ucnt = (u32*)(tl.tmin + mt);
-    tl.upop = tl.ucnt + mt;
+    tl.tend = tl.ucnt + mt;
+    tl.upop = tl.tend + mt;
     tl.uval = tl.upop + mt * ST_TILE;
     tl.table = tl.uval + mt * ST_TILE;
-    u32* last = (u32*)c->d_tmp_u64;  // 2 * max_batch u32, zero between chunks
     const bool want = d_resp != nullptr && resp_lo < lo + n && resp_hi > lo;
     const u64 rlo = want ? resp_lo : 0, rhi = want ? resp_hi : 0;
     timer_begin(c, "st_replay");
-    st_tile_kernel<<<(unsigned)tiles, ST_TPB, 0, st>>>(src, ring, ring_mask, lo, n, c->d_ctl, desc, ticket, tl, last,
+    st_tile_kernel<<<(unsigned)tiles, ST_TPB, 0, st>>>(src, ring, ring_mask, lo, n, c->d_ctl, desc, ticket, tl,
                                                       c->d_stack, c->cfg.stack_capacity, rlo, rhi,
-                                                      (int)c->cfg.stack_push_resp, d_resp, d_some);
+                                                      (int)c->cfg.stack_push_resp, d_resp, d_some, c->exp,
+                                                      (c->exp & 2) ? c->d_dbg : nullptr);
     st_finish_kernel<<<(unsigned)tiles, 256, (tiles + tiles / 8 + tiles / 64 + 2) * 8, st>>>(
-        ring, ring_mask, lo, n, c->d_ctl, tl, last, c->d_stack, c->cfg.stack_capacity, rlo, rhi,
+        lo, n, c->d_ctl, tl, c->d_stack, c->cfg.stack_capacity, rlo, rhi,
         want ? d_resp : nullptr, d_some, desc, ticket);
     timer_end(c, "st_replay");
     return hipGetLastError();
@@ -526,7 +527,7 @@ hipError_t st_replay_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 resp_hi, 
 
 u64 st_aux_bytes(u64 max_batch) {
     const u64 mt = (max_batch + ST_TILE - 1) / ST_TILE;
-    return mt * (8 + 4) + mt * ST_TILE * (4 + 4 + 4);
+    return mt * (8 + 4 + 4) + mt * ST_TILE * (4 + 4 + 4);
 }
 
 }  // namespace nrg

@@ -166,6 +166,7 @@ TEST_SIGNATURES = {
     "nrg_test_sort_pairs": (C.c_int, [vp, vp, vp, u64, C.c_int, vp, vp]),
     "nrg_test_maxscan": (C.c_int, [vp, vp, vp, u64, vp]),
     "nrg_test_ring_read": (C.c_int, [vp, u64, vp]),
+    "nrg_test_debug_read": (C.c_int, [vp, vp, u64]),
 }
 
 _lib = None
