@@ -27,7 +27,7 @@ dev.gen_stack_ops_device(ops, N, 12345)
 resp = torch.empty(N, dtype=torch.int32, device="cuda")
 some = torch.empty(N, dtype=torch.uint8, device="cuda")
 tiles = (N + 2047) // 2048
-names = ["ticket", "loads+scan", "lookback", "depths+min", "sparse table", "pairing", "queue+cross", "tables+last"]
+names = ["ticket", "loads+scan", "depths+min", "sparse table", "pairing", "queue", "lookback", "emit+tables"]
 acc = np.zeros((tiles, 9))
 R = 20
 for r in range(R + 3):

@@ -188,209 +188,250 @@ __global__ __launch_bounds__(ST_TPB) void st_tile_kernel(const nrg_stack_op* __r
     for (int i = 0; i < w; i++) wpre = fn_then(wpre, Fn{s_wb[i], s_wa[i]});
     ST_MARK(2);
     const Fn tpre = fn_then(wpre, ex);
-    if (w == 0) {
-        // Wave 0 publishes the tile's aggregate, then composes the aggregates of ALL earlier
-        // tiles itself (64 per wave instruction, every load of a group in flight at once)
-        // instead of waiting for an inclusive prefix to ripple down the chain of tiles: each
-        // tile publishes its aggregate right after its loads, so the prefix of the last tile is
-        // ready one round trip after the last predecessor has loaded its ops.
-        Fn tagg = {0, 0};
-        for (int i = 0; i < 4; i++) tagg = fn_then(tagg, Fn{s_wb[i], s_wa[i]});
-        if (lane == 0) __hip_atomic_store(&desc[tile], pack_agg(tagg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // lane l composes the run of predecessors [r*G, r*G + G), r = 63 - l, in registers (older
-        // first); one wave composition then joins the runs (the highest lane holds the oldest)
-        const int np = (int)tile;
-        const int G = (np + 63) / 64;
-        const int r0 = (63 - lane) * G;
-        Fn acc = FN_ID;
-        constexpr int B = 8;  // descriptor loads in flight per lane
-        for (int g0 = 0; g0 < G; g0 += B) {
-            u64 v[B];
+    Fn tagg = {0, 0};
+    for (int i = 0; i < 4; i++) tagg = fn_then(tagg, Fn{s_wb[i], s_wa[i]});
+    if (t == 0) __hip_atomic_store(&desc[tile], pack_agg(tagg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+
+    // Pass 0 pairs the tile speculatively on the UNCLAMPED walk relative to the tile's start:
+    // Push/Pop pairing depends only on relative depths, and it is the real pairing unless the
+    // stack runs empty inside the tile (a Pop at depth 0 is a no-op). Whether it does needs the
+    // tile's start depth, i.e. the look-back, which therefore runs after pass 0 and finds its
+    // predecessors' aggregates already published. Pass 1 (a stack within 2048 of empty) redoes
+    // the pairing on the clamped walk from the known start depth.
+    long long dstart = tpre.b;
+    bool clamp = false;
+    long long tmin = 0;   // minimum of the walk, start and end included (pass 0: relative)
+    u32 a[ST_ITEMS];      // depth after each of this thread's ops - tmin
+    u32 astart = 0;       // depth before this thread's first op - tmin
+    u32 rv[ST_ITEMS];     // response per op:
+    uint8_t rk[ST_ITEMS]; //   0 none (padding, or queued below), 1 Some(rv), 2 None
+    u32 qe[ST_ITEMS], qv[ST_ITEMS];  // queued Pops this lane resolved: entry and value,
+    bool qx[ST_ITEMS];               //   or outside the tile (qx)
+    u32 qn = 0;                      // wave-uniform queue length
+    for (int pass = 0;; pass++) {
+        long long dd = dstart, dmin = dd;
 #pragma unroll
-            for (int q = 0; q < B; q++) {
-                const int idx = r0 + g0 + q;
-                v[q] = (g0 + q < G && idx < np) ? __hip_atomic_load(&desc[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                                 : 0ull;
+        for (int q = 0; q < ST_ITEMS; q++) {
+            if (ops[q].op == 1) dd += 1;
+            else if (ops[q].op == 0 && (!clamp || dd > 0)) dd -= 1;
+            dmin = dd < dmin ? dd : dmin;
+        }
+        tmin = block_min4(dmin, s_wmin, w, lane);
+        ST_MARK(3);
+        u32 amin = ST_INF;
+        dd = dstart;
+#pragma unroll
+        for (int q = 0; q < ST_ITEMS; q++) {
+            if (ops[q].op == 1) dd += 1;
+            else if (ops[q].op == 0 && (!clamp || dd > 0)) dd -= 1;
+            a[q] = (u32)(dd - tmin);
+            amin = a[q] < amin ? a[q] : amin;
+            s_A[t * ST_ITEMS + q + 1] = (uint16_t)a[q];
+            s_val[t * ST_ITEMS + q] = ops[q].val;
+        }
+        astart = (u32)(dstart - tmin);
+        if (t == 0) s_A[0] = (uint16_t)astart;
+        s_sp[0][t] = (uint16_t)amin;
+        // suffix minimum over the threads after this one (exclusive), for the last-Push records
+        u32 sfx = amin;  // inclusive suffix min within the wave
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const u32 o = __shfl_down(sfx, off, 64);
+            if (lane + off < 64) sfx = o < sfx ? o : sfx;
+        }
+        if (lane == 0) s_sw[w] = (uint16_t)sfx;
+        for (int r = t; r < ST_TILE; r += ST_TPB) s_tab[r] = ST_NO_PUSH;
+        __syncthreads();
+        {
+            u32 m = amin;
+#pragma unroll
+            for (int j = 1; j < 9; j++) {
+                const int h = 1 << (j - 1);
+                if (t >= h) {
+                    const u32 o = s_sp[j - 1][t - h];
+                    m = o < m ? o : m;
+                }
+                s_sp[j][t] = (uint16_t)m;
+                __syncthreads();
             }
+        }
+        ST_MARK(4);
+        u32 after = __shfl_down(sfx, 1, 64);  // min over later threads in the wave
+        if (lane == 63) after = ST_INF;
+        for (int i = w + 1; i < 4; i++) after = s_sw[i] < after ? s_sw[i] : after;
+
+        // Last Push to each slot below the tile's end depth: after the last time the walk is at
+        // (or below) a level it pushes that level, i.e. at i + 1 for every suffix-record low i.
+        {
+            u32 cur = after;
+            const bool lastthr = t == ST_TPB - 1;
 #pragma unroll
-            for (int q = 0; q < B; q++) {
-                const int idx = r0 + g0 + q;
-                if (g0 + q >= G || idx >= np) continue;
-                u32 spins = 0;
-                while (!(v[q] & D_MASK)) {  // not published yet (its tile is still loading)
-                    __builtin_amdgcn_s_sleep(1);
-                    v[q] = __hip_atomic_load(&desc[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (++spins == (1u << 26)) {  // bounded: never hang the device
-                        atomicOr(&ctl->err, ERR_CAPACITY);
-                        break;
+            for (int q = ST_ITEMS - 1; q >= 0; q--) {
+                const bool final = lastthr && q == ST_ITEMS - 1;  // nothing follows position 2047
+                if (!final && a[q] < cur) s_tab[a[q]] = (uint16_t)(t * ST_ITEMS + q + 1);
+                cur = a[q] < cur ? a[q] : cur;
+            }
+            if (t == 0 && astart < cur) s_tab[astart] = 0;
+        }
+
+        // Each Pop returns the Push right after the last earlier position whose depth is <= the
+        // depth the Pop leaves (a previous-smaller-or-equal query over the tile). Pops that the
+        // thread cannot answer from its own ops are queued per wave and answered with all lanes.
+        u32 prv = astart;
+        qn = 0;
+#pragma unroll
+        for (int q = 0; q < ST_ITEMS; q++) {
+            const u32 pos = (u32)(t * ST_ITEMS + q);
+            const bool pop = ops[q].op == 0 && prv > a[q];  // a non-empty Pop (empty: depth stays 0)
+            rk[q] = 0;
+            rv[q] = 0;
+            if (ops[q].op == 0 && !pop) {
+                rk[q] = 2;  // Pop on an empty stack: None
+            } else if (ops[q].op == 1) {
+                rk[q] = push_resp ? 1 : 2;
+                rv[q] = ops[q].val;
+            }
+            bool need = false;
+            if (pop) {
+                const u32 s = a[q];
+                int r = astart <= s ? t * ST_ITEMS - 1 : -2;
+#pragma unroll
+                for (int qq = 0; qq < ST_ITEMS; qq++)
+                    if (qq < q && a[qq] <= s) r = t * ST_ITEMS + qq;
+                if (r != -2) {
+                    rk[q] = 1;
+                    rv[q] = s_val[r + 1];
+                } else {
+                    need = true;
+                }
+            }
+            const u64 m = __ballot(need);
+            if (need) s_q[w][qn + __popcll(m & ((1ull << lane) - 1))] = (a[q] << 11) | pos;
+            qn += (u32)__popcll(m);
+            prv = a[q];
+        }
+        __syncthreads();
+        ST_MARK(5);
+#pragma unroll
+        for (int j = 0; j < ST_ITEMS; j++) {
+            const u32 i = (u32)lane + 64u * j;
+            if (i >= qn) continue;
+            const u32 e = s_q[w][i];
+            const u32 s = e >> 11, pos = e & 2047u;
+            // nearest earlier thread whose minimum is <= s: binary lifting, 9 steps
+            int k = (int)(pos / ST_ITEMS) - 1;
+            int r = -2;
+#pragma unroll
+            for (int jj = 8; jj >= 0; jj--)
+                if (k >= 0 && s_sp[jj][k] > s) k -= 1 << jj;
+            if (k >= 0) {
+                u32 v[ST_ITEMS];
+#pragma unroll
+                for (int qq = 0; qq < ST_ITEMS; qq++) v[qq] = s_A[k * ST_ITEMS + qq + 1];
+#pragma unroll
+                for (int qq = 0; qq < ST_ITEMS; qq++)
+                    if (v[qq] <= s) r = k * ST_ITEMS + qq;
+            } else if (s_A[0] <= s) {
+                r = -1;
+            }
+            qe[j] = e;
+            qx[j] = r == -2;  // the Push is in an earlier tile or before the chunk
+            qv[j] = r == -2 ? 0u : s_val[r + 1];
+        }
+        ST_MARK(6);
+        if (pass == 1) break;
+
+        if (w == 0) {
+            // Wave 0 composes the aggregates of ALL earlier tiles itself (64 per wave
+            // instruction, every load of a group in flight at once) instead of waiting for an
+            // inclusive prefix to ripple down the chain of tiles. Lane l composes the run of
+            // predecessors [r*G, r*G + G), r = 63 - l, in registers (older first); one wave
+            // composition then joins the runs (the highest lane holds the oldest).
+            const int np = (int)tile;
+            const int G = (np + 63) / 64;
+            const int r0 = (63 - lane) * G;
+            Fn acc = FN_ID;
+            constexpr int B = 8;  // descriptor loads in flight per lane
+            for (int g0 = 0; g0 < G; g0 += B) {
+                u64 v[B];
+#pragma unroll
+                for (int q = 0; q < B; q++) {
+                    const int idx = r0 + g0 + q;
+                    v[q] = (g0 + q < G && idx < np)
+                               ? __hip_atomic_load(&desc[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                               : 0ull;
+                }
+#pragma unroll
+                for (int q = 0; q < B; q++) {
+                    const int idx = r0 + g0 + q;
+                    if (g0 + q >= G || idx >= np) continue;
+                    u32 spins = 0;
+                    while (!(v[q] & D_MASK)) {  // not published yet (its tile is still loading)
+                        __builtin_amdgcn_s_sleep(1);
+                        v[q] = __hip_atomic_load(&desc[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (++spins == (1u << 26)) {  // bounded: never hang the device
+                            atomicOr(&ctl->err, ERR_CAPACITY);
+                            break;
+                        }
                     }
+                    acc = fn_then(acc, unpack_agg(v[q]));
                 }
-                acc = fn_then(acc, unpack_agg(v[q]));
             }
-        }
-        acc = np ? wave_compose(acc) : Fn{0, 0};
-        const long long dbase = fn_apply(acc, d0);
-        if (lane == 0) {
-            const u64 ntiles = (n + ST_TILE - 1) / ST_TILE;
-            if ((u64)tile == ntiles - 1) {
-                ctl->depth_next = fn_apply(tagg, dbase);
-                ctl->depth0 = d0;
-            }
-            s_dbase = dbase;
-        }
-    }
-    __syncthreads();
-
-    ST_MARK(3);
-    // Depth after each op, relative to the tile's minimum (start and end included: <= 2048).
-    const long long dbase = s_dbase;
-    const long long dstart = fn_apply(tpre, dbase);
-    long long dd = dstart, dmin = dd;
-    bool over = false;
-#pragma unroll
-    for (int q = 0; q < ST_ITEMS; q++) {
-        if (ops[q].op == 1) {
-            over |= (u64)dd >= cap;
-            dd += 1;
-        } else if (ops[q].op == 0 && dd > 0) {
-            dd -= 1;
-        }
-        dmin = dd < dmin ? dd : dmin;
-    }
-    if (over) atomicOr(&ctl->err, ERR_CAPACITY);
-    const long long tmin = block_min4(dmin, s_wmin, w, lane);
-    ST_MARK(4);
-    u32 a[ST_ITEMS];  // relative depth after each of this thread's ops
-    u32 amin = ST_INF;
-    dd = dstart;
-#pragma unroll
-    for (int q = 0; q < ST_ITEMS; q++) {
-        if (ops[q].op == 1) dd += 1;
-        else if (ops[q].op == 0 && dd > 0) dd -= 1;
-        a[q] = (u32)(dd - tmin);
-        amin = a[q] < amin ? a[q] : amin;
-        s_A[t * ST_ITEMS + q + 1] = (uint16_t)a[q];
-        s_val[t * ST_ITEMS + q] = ops[q].val;
-    }
-    const u32 astart = (u32)(dstart - tmin);  // relative depth before this thread's first op
-    if (t == 0) s_A[0] = (uint16_t)astart;
-    s_sp[0][t] = (uint16_t)amin;
-    // suffix minimum over the threads after this one (exclusive), for the last-Push records
-    u32 sfx = amin;  // inclusive suffix min within the wave
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const u32 o = __shfl_down(sfx, off, 64);
-        if (lane + off < 64) sfx = o < sfx ? o : sfx;
-    }
-    if (lane == 0) s_sw[w] = (uint16_t)sfx;
-    for (int r = t; r < ST_TILE; r += ST_TPB) s_tab[r] = ST_NO_PUSH;
-    __syncthreads();
-    {
-        u32 m = amin;
-#pragma unroll
-        for (int j = 1; j < 9; j++) {
-            const int h = 1 << (j - 1);
-            if (t >= h) {
-                const u32 o = s_sp[j - 1][t - h];
-                m = o < m ? o : m;
-            }
-            s_sp[j][t] = (uint16_t)m;
-            __syncthreads();
-        }
-    }
-    ST_MARK(5);
-    u32 after = __shfl_down(sfx, 1, 64);  // min over later threads in the wave
-    if (lane == 63) after = ST_INF;
-    for (int i = w + 1; i < 4; i++) after = s_sw[i] < after ? s_sw[i] : after;
-
-    // Last Push to each slot below the tile's end depth: after the last time the walk is at
-    // (or below) a level it pushes that level, i.e. at i + 1 for every suffix-record low i.
-    {
-        u32 cur = after;
-        const bool lastthr = t == ST_TPB - 1;
-#pragma unroll
-        for (int q = ST_ITEMS - 1; q >= 0; q--) {
-            const bool final = lastthr && q == ST_ITEMS - 1;  // nothing follows position 2047
-            if (!final && a[q] < cur) s_tab[a[q]] = (uint16_t)(t * ST_ITEMS + q + 1);
-            cur = a[q] < cur ? a[q] : cur;
-        }
-        if (t == 0 && astart < cur) s_tab[astart] = 0;
-    }
-
-    // Each Pop returns the Push right after the last earlier position whose depth is <= the
-    // depth the Pop leaves (a previous-smaller-or-equal query over the tile). Pops that the
-    // thread cannot answer from its own ops are queued per wave and answered with all lanes.
-    u32 prv = astart;
-    u32 qn = 0;  // wave-uniform queue length
-#pragma unroll
-    for (int q = 0; q < ST_ITEMS; q++) {
-        const u32 pos = (u32)(t * ST_ITEMS + q);
-        const u64 g = lo + tbase + pos;
-        const bool inwin = g >= resp_lo && g < resp_hi;
-        const bool pop = ops[q].op == 0 && prv > a[q];  // a non-empty Pop (empty: depth stays 0)
-        if (ops[q].op == 0 && !pop && inwin) {            // Pop on an empty stack: None
-            resp[g - resp_lo] = 0;
-            some[g - resp_lo] = 0;
-        } else if (ops[q].op == 1 && inwin) {
-            resp[g - resp_lo] = push_resp ? ops[q].val : 0u;
-            some[g - resp_lo] = push_resp ? 1 : 0;
-        }
-        bool need = false;
-        if (pop) {
-            const u32 s = a[q];
-            int r = astart <= s ? t * ST_ITEMS - 1 : -2;
-#pragma unroll
-            for (int qq = 0; qq < ST_ITEMS; qq++)
-                if (qq < q && a[qq] <= s) r = t * ST_ITEMS + qq;
-            if (r != -2) {
-                if (inwin) {
-                    resp[g - resp_lo] = s_val[r + 1];
-                    some[g - resp_lo] = 1;
+            acc = np ? wave_compose(acc) : Fn{0, 0};
+            const long long dbase = fn_apply(acc, d0);
+            if (lane == 0) {
+                const u64 ntiles = (n + ST_TILE - 1) / ST_TILE;
+                if ((u64)tile == ntiles - 1) {
+                    ctl->depth_next = fn_apply(tagg, dbase);
+                    ctl->depth0 = d0;
                 }
-            } else {
-                need = true;
+                s_dbase = dbase;
             }
         }
-        const u64 m = __ballot(need);
-        if (need) s_q[w][qn + __popcll(m & ((1ull << lane) - 1))] = (a[q] << 11) | pos;
-        qn += (u32)__popcll(m);
-        prv = a[q];
-    }
-    __syncthreads();
-    ST_MARK(6);
-    for (u32 i = lane; i < qn; i += 64) {
-        const u32 e = s_q[w][i];
-        const u32 s = e >> 11, pos = e & 2047u;
-        // nearest earlier thread whose minimum is <= s: binary lifting, 9 steps
-        int k = (int)(pos / ST_ITEMS) - 1;
-        int r = -2;
-#pragma unroll
-        for (int j = 8; j >= 0; j--)
-            if (k >= 0 && s_sp[j][k] > s) k -= 1 << j;
-        if (k >= 0) {
-            u32 v[ST_ITEMS];
-#pragma unroll
-            for (int qq = 0; qq < ST_ITEMS; qq++) v[qq] = s_A[k * ST_ITEMS + qq + 1];
-#pragma unroll
-            for (int qq = 0; qq < ST_ITEMS; qq++)
-                if (v[qq] <= s) r = k * ST_ITEMS + qq;
-        } else if (s_A[0] <= s) {
-            r = -1;
+        __syncthreads();
+        ST_MARK(7);
+        const long long D = s_dbase;  // depth before the tile
+        if (D + tmin >= 0) {          // the walk never reaches an empty stack: pass 0 holds
+            tmin += D;
+            break;
         }
-        const u64 g = lo + tbase + pos;
-        if (r == -2) {  // the Push is in an earlier tile or before the chunk
-            // No tile writes the stack before st_finish_kernel, so read the pre-chunk
-            // content now; it is the answer when no earlier tile of the chunk pushed s.
-            const u32 h = atomicAdd(&s_ucnt, 1u);
-            const long long slot = tmin + s;
-            tl.upop[(u64)tile * ST_TILE + h] = e;
-            tl.uval[(u64)tile * ST_TILE + h] = slot < d0 && (u64)slot < cap ? stack[slot] : 0u;
-        } else if (g >= resp_lo && g < resp_hi) {
-            resp[g - resp_lo] = s_val[r + 1];
-            some[g - resp_lo] = 1;
+        dstart = fn_apply(tpre, D);
+        clamp = true;
+    }
+
+    // Responses, the capacity check, cross-tile Pops (with the slot's pre-chunk content: no
+    // tile writes the stack before st_finish_kernel), then the last-Push table.
+    {
+        bool over = false;
+        u32 prv = astart;
+#pragma unroll
+        for (int q = 0; q < ST_ITEMS; q++) {
+            const u64 g = lo + tbase + (u64)(t * ST_ITEMS + q);
+            over |= ops[q].op == 1 && (u64)(tmin + (long long)prv) >= cap;
+            if (rk[q] && g >= resp_lo && g < resp_hi) {
+                resp[g - resp_lo] = rk[q] == 1 ? rv[q] : 0u;
+                some[g - resp_lo] = rk[q] == 1 ? 1 : 0;
+            }
+            prv = a[q];
+        }
+        if (over) atomicOr(&ctl->err, ERR_CAPACITY);
+#pragma unroll
+        for (int j = 0; j < ST_ITEMS; j++) {
+            const u32 i = (u32)lane + 64u * j;
+            if (i >= qn) continue;
+            const u32 e = qe[j];
+            const u64 g = lo + tbase + (e & 2047u);
+            if (qx[j]) {
+                const u32 h = atomicAdd(&s_ucnt, 1u);
+                const long long slot = tmin + (long long)(e >> 11);
+                tl.upop[(u64)tile * ST_TILE + h] = e;
+                tl.uval[(u64)tile * ST_TILE + h] = slot < d0 && (u64)slot < cap ? stack[slot] : 0u;
+            } else if (g >= resp_lo && g < resp_hi) {
+                resp[g - resp_lo] = qv[j];
+                some[g - resp_lo] = 1;
+            }
         }
     }
-    ST_MARK(7);
     if (t == ST_TPB - 1) s_aend = a[ST_ITEMS - 1];
     __syncthreads();
     // Levels [tmin, end depth) each have a last Push (suffix records); no other level has one.

@@ -113,3 +113,37 @@ def test_stack_bench_size_rounds(nrg, orc):
         np.testing.assert_array_equal(some.cpu().numpy(), osome)
         np.testing.assert_array_equal(resp.cpu().numpy().view(np.uint32), oresp)
     np.testing.assert_array_equal(dev.st_dump(), os_.dump())
+
+
+@pytest.mark.parametrize("init_n", [50_000, 0])
+def test_stack_eight_segment_round(nrg, orc, init_n):
+    """configs[4] on 8 GPUs: every replica replays the all-gathered round of 8 x 1M ops (8M ops in
+    one chunk, nr/src/log.rs:473-524) and answers only its own segment (nr/src/replica.rs:576-578).
+    Two rounds through nrg_log_append_segments_async + nrg_log_exec_async; with init_n = 0 the
+    stack starts empty, so the first tiles pop an empty stack (Pop -> None, depth stays 0)."""
+    import torch
+
+    G, W = 8, 1_000_000
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_STACK, 0, max_batch=G * W, stack_capacity=1 << 24,
+                            log_bytes=64 * 2 * G * W)
+    init = np.arange(init_n, dtype=np.uint32)
+    dev.st_init(init)
+    os_ = orc.Stack(init)
+    for r, own in enumerate([2, 7]):
+        segs = [orc.gen_stack_ops(W, 0x8E5 + 10 * r + g) for g in range(G)]
+        base = np.concatenate([_ops(v, o) for v, o in segs])
+        d_base = torch.from_numpy(base.view(np.int64).copy()).cuda()
+        firsts = dev.log_append_segments(d_base, W, [W] * G, [g + 1 for g in range(G)])
+        assert firsts == [r * G * W + g * W for g in range(G)]
+        resp = torch.full((W,), -1, dtype=torch.int32, device="cuda")
+        some = torch.full((W,), 7, dtype=torch.uint8, device="cuda")
+        dev.log_exec_device(firsts[own], firsts[own] + W, resp, some)
+        torch.cuda.synchronize()
+        for g, (v, o) in enumerate(segs):
+            oresp, osome = os_.replay(v, o)
+            if g == own:
+                np.testing.assert_array_equal(some.cpu().numpy(), osome, err_msg=f"round {r} some")
+                np.testing.assert_array_equal(resp.cpu().numpy().view(np.uint32), oresp, err_msg=f"round {r} resp")
+        assert dev.st_len() == len(os_.dump())
+    np.testing.assert_array_equal(dev.st_dump(), os_.dump())
+    dev.close()
