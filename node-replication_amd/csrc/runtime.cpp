@@ -381,6 +381,8 @@ int nrg_open(int dev, const nrg_config* cfg_in, nrg_ctx** out) {
         const char* force_sort = std::getenv("NRG_SY_SORT");
         if (sy_bucket_eligible(cf) && !(force_sort && std::atoi(force_sort)))
             OPEN_CHK(hipMalloc(&c->d_sy_aux, sy_bucket_aux_bytes(cf)));
+        if (const char* e = std::getenv("NRG_EXP")) c->exp = (uint32_t)std::atoi(e);
+        if (c->exp & 2) OPEN_CHK(hipMalloc(&c->d_dbg, 1024 * 16 * sizeof(uint64_t)));  // <= 1024 buckets
         OPEN_CHK(sy_init(c));
     }
     OPEN_CHK(hipStreamSynchronize(c->stream));

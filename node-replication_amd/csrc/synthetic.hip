@@ -223,7 +223,7 @@ __global__ __launch_bounds__(256) void sy_read_kernel(const nrg_synth_rd* __rest
 //               sy_sum_kernel adds them per op with LDS atomics (coalesced responses).
 // Replaces expand + 3 radix passes + max-scan + scattered u64 atomics (620 us per 1M ops).
 constexpr u32 SYB_SHIFT = 9;
-constexpr u32 SYB_WORDS = 1u << SYB_SHIFT;
+constexpr u32 SYB_WORDS = 1u << SYB_SHIFT;  // LDS words per bucket (a bucket holds W <= 512 of them)
 constexpr int SYA_TPB = 512, SYA_WAVES = SYA_TPB / 64, SYA_OROUNDS = 4;
 constexpr u32 SYA_OPS = SYA_WAVES * SYA_OROUNDS * 64;  // ops per tile (11 bits)
 constexpr u32 SY_MAX_NB = 512, SY_MAX_HOT = 16, SY_MAX_TILES = 4096, SY_MAX_CW = 8;
@@ -231,6 +231,12 @@ constexpr int SYB_TPB = 512, SYB_WAVES = SYB_TPB / 64, SYB_PER = 8;
 constexpr u32 SYB_PASS = SYB_TPB * SYB_PER;  // touches per pass of a bucket workgroup
 constexpr int SYC_TPB = 512;
 constexpr u32 NOTOUCH = 0xFFFFFFFFu;
+
+// Cold word x (relative to hot_reads) lives in bucket x / W, W = ceil(span / 512): ~512 buckets,
+// so the bucket kernel's workgroups spread evenly over the 256 CUs (2 per CU) instead of a
+// power-of-two bucket size leaving some CUs one workgroup and others two. The division is
+// (x * ceil(2^40 / W)) >> 40, exact for x < 2^31 and W <= 512.
+__device__ __forceinline__ u32 bucket_of(u32 x, u64 wm) { return (u32)(((u64)x * wm) >> 40); }
 
 // A cold touch in the tile layout, 4 bytes: word within its bucket (9 bits), SET (1), cold
 // index k (3), op within its tile (11). The bucket and tile are implied by the position.
@@ -305,7 +311,7 @@ template <int CW>
 // log copy itself (lane-contiguous). nullptr: the ops are in the ring.
 __global__ __launch_bounds__(SYA_TPB) void sy_part_kernel(const nrg_synth_op* __restrict__ src, nrg_synth_op* ring,
                                                           u64 ring_mask, u64 lo,
-                                                          u64 n, u64 span, u64 span_m, u32 HR, u64 hr_m, u32 HW, u32 NB,
+                                                          u64 n, u64 span, u64 span_m, u32 HR, u64 hr_m, u32 HW, u32 NB, u32 W, u64 wm,
                                                           u32 ntiles, u32* __restrict__ E, u32* __restrict__ cnt_bt,
                                                           SyHot* __restrict__ hot) {
     __shared__ unsigned short s_wcnt[SYA_WAVES][SY_MAX_NB];
@@ -389,7 +395,7 @@ __global__ __launch_bounds__(SYA_TPB) void sy_part_kernel(const nrg_synth_op* __
         for (int r = 0; r < CW; r++) {
             const u32 v = s_u.r.words[w][r * 64 + lane];
             const bool tv = v != NOTOUCH;
-            const u32 b = tv ? (((v & ~SETBIT) - HR) >> SYB_SHIFT) : 0u;
+            const u32 b = tv ? bucket_of((v & ~SETBIT) - HR, wm) : 0u;
             u64 peers;
             const u32 rank = wave_rank(tv, b, lane, s_u.r.mask[w], s_wcnt[w], &peers);
             xs[orr * CW + r] = v;
@@ -435,7 +441,7 @@ __global__ __launch_bounds__(SYA_TPB) void sy_part_kernel(const nrg_synth_op* __
             const u32 p = pk[orr * CW + r];
             const u32 t = r * 64 + lane;
             const u32 opl = (u32)(w * SYA_OROUNDS + orr) * 64 + t / CW;
-            const u32 xl = ((v & ~SETBIT) - HR) & (SYB_WORDS - 1);
+            const u32 xl = (v & ~SETBIT) - HR - (p >> 16) * W;
             s_u.stage[s_wcnt[w][p >> 16] + (p & 0xFFFFu)] = ent_make(xl, (v & SETBIT) != 0, t % CW, opl);
         }
     }
@@ -451,30 +457,45 @@ __global__ __launch_bounds__(SYA_TPB) void sy_part_kernel(const nrg_synth_op* __
 // WriteOnly in it is applied wave by wave instead (values depend on the last SET).
 __global__ __launch_bounds__(SYB_TPB) void sy_bucket_kernel(const u32* __restrict__ E, const u32* __restrict__ cnt_bt,
                                                             u32 ntiles, u32 tile_entries, u64* __restrict__ V,
-                                                            u64* __restrict__ words, u64 N, u32 HR,
-                                                            const nrg_synth_op* __restrict__ ring, u64 ring_mask, u64 lo) {
+                                                            u64* __restrict__ words, u64 N, u32 HR, u32 W,
+                                                            const nrg_synth_op* __restrict__ ring, u64 ring_mask, u64 lo,
+                                                            u64* __restrict__ dbg) {
+    // dbg (NRG_EXP & 2, diagnostic): per block, thread 0's wall clock at the phase edges
+    // [0] start [1] prologue loaded [2] scanned, then summed over passes [3] tile map [4] gather
+    // [5] rank + place [6] stores, [7] end, [8] passes
+    u64 tm_acc[4] = {0, 0, 0, 0}, tm_last = 0;
+#define SY_MARK(K) \
+    if (dbg && threadIdx.x == 0) dbg[(u64)blockIdx.x * 16 + (K)] = tm_last = wall_clock64()
+#define SY_ACC(K)                                  \
+    if (dbg && threadIdx.x == 0) {                 \
+        const u64 now_ = wall_clock64();           \
+        tm_acc[K] += now_ - tm_last;               \
+        tm_last = now_;                            \
+    }
+    SY_MARK(0);
     extern __shared__ u32 s_dyn[];  // s_pre[ntiles + 1], s_off[ntiles] (u16)
     __shared__ u64 s_cur[SYB_WORDS];
     __shared__ u32 s_wc[SYB_WAVES][SYB_WORDS];
     __shared__ u64 s_mk[SYB_WAVES][SYB_WORDS];
-    __shared__ unsigned short s_tile[SYB_PASS];
+    __shared__ unsigned short s_tile[2][SYB_PASS];  // tile of every touch of a pass (double buffered)
     __shared__ u32 s_part[SYB_WAVES];
     u32* s_pre = s_dyn;
     unsigned short* s_off = (unsigned short*)(s_dyn + ntiles + 1);
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const u32 b = blockIdx.x;
-    const u64 w0 = (u64)HR + (u64)b * SYB_WORDS;
+    const u64 w0 = (u64)HR + (u64)b * W;
     for (u32 t = tid; t < ntiles; t += SYB_TPB) {
         const u32 p = cnt_bt[(u64)b * ntiles + t];
         s_off[t] = (unsigned short)(p >> 16);
         s_pre[t] = p & 0xFFFFu;
     }
-    for (u32 i = tid; i < SYB_WORDS; i += SYB_TPB) s_cur[i] = w0 + i < N ? words[w0 + i] : 0ull;
+    for (u32 i = tid; i < SYB_WORDS; i += SYB_TPB) s_cur[i] = i < W && w0 + i < N ? words[w0 + i] : 0ull;
     for (u32 i = tid; i < SYB_WAVES * SYB_WORDS; i += SYB_TPB) {
         (&s_wc[0][0])[i] = 0;
         (&s_mk[0][0])[i] = 0;
     }
     __syncthreads();
+    SY_MARK(1);
     // exclusive scan of the per-tile counts: thread owns tiles [tid*K, tid*K + K)
     const u32 K = (ntiles + SYB_TPB - 1) / SYB_TPB;
     u32 loc = 0;
@@ -504,30 +525,51 @@ __global__ __launch_bounds__(SYB_TPB) void sy_bucket_kernel(const u32* __restric
     }
     if (tid == 0) s_pre[ntiles] = total;
     __syncthreads();
-    for (u32 base = 0; base < total; base += SYB_PASS) {
-        // tile of every touch of the pass
+    SY_MARK(2);
+    // The pass starting at `base`: the tile of each of its touches, then this thread's entries.
+    auto map_pass = [&](u32 base, unsigned short* map) {
         for (u32 t = tid; t < ntiles; t += SYB_TPB) {
             const u32 a = s_pre[t] > base ? s_pre[t] : base;
             const u32 z = s_pre[t + 1] < base + SYB_PASS ? s_pre[t + 1] : base + SYB_PASS;
-            for (u32 j = a; j < z; j++) s_tile[j - base] = (unsigned short)t;
+            for (u32 j = a; j < z; j++) map[j - base] = (unsigned short)t;
         }
+    };
+    u32 nent[SYB_PER], ngpos[SYB_PER];
+    auto load_pass = [&](u32 base, const unsigned short* map) {
+#pragma unroll
+        for (int q = 0; q < SYB_PER; q++) {
+            const u32 i = base + (u32)w * (SYB_PER * 64) + q * 64 + lane;
+            ngpos[q] = 0;
+            nent[q] = 0;
+            if (i < total) {
+                const u32 t = map[i - base];
+                ngpos[q] = t * tile_entries + s_off[t] + (i - s_pre[t]);
+                nent[q] = E[ngpos[q]];
+            }
+        }
+    };
+    if (total) {
+        map_pass(0, s_tile[0]);
         __syncthreads();
+        load_pass(0, s_tile[0]);
+    }
+    // Software pipelined: the next pass's entries are in flight while this pass is ranked.
+    for (u32 base = 0, pb = 0; base < total; base += SYB_PASS, pb ^= 1) {
         u32 ent[SYB_PER], gpos[SYB_PER];
         u64 sv[SYB_PER];
         bool myset = false;
 #pragma unroll
         for (int q = 0; q < SYB_PER; q++) {
-            const u32 i = base + (u32)w * (SYB_PER * 64) + q * 64 + lane;
-            gpos[q] = 0;
-            ent[q] = 0;
-            if (i < total) {
-                const u32 t = s_tile[i - base];
-                gpos[q] = t * tile_entries + s_off[t] + (i - s_pre[t]);
-                ent[q] = E[gpos[q]];
-                myset |= ent_set(ent[q]);
-            }
+            ent[q] = nent[q];
+            gpos[q] = ngpos[q];
+            myset |= ent_set(ent[q]);
         }
-        const int anyset = __syncthreads_or(myset);
+        SY_ACC(1);
+        const u32 nb = base + SYB_PASS;
+        if (nb < total) map_pass(nb, s_tile[pb ^ 1]);
+        const int anyset = __syncthreads_or(myset);  // also publishes the next pass's tile map
+        if (nb < total) load_pass(nb, s_tile[pb ^ 1]);
+        SY_ACC(0);
         if (!anyset) {
 #pragma unroll
             for (int q = 0; q < SYB_PER; q++) {
@@ -593,13 +635,25 @@ __global__ __launch_bounds__(SYB_TPB) void sy_bucket_kernel(const u32* __restric
                 __syncthreads();
             }
         }
+        SY_ACC(2);
 #pragma unroll
         for (int q = 0; q < SYB_PER; q++)
             if (base + (u32)w * (SYB_PER * 64) + q * 64 + lane < total) V[gpos[q]] = sv[q];
+        SY_ACC(3);
     }
     __syncthreads();
-    for (u32 i = tid; i < SYB_WORDS; i += SYB_TPB)
+    for (u32 i = tid; i < W; i += SYB_TPB)
         if (w0 + i < N) words[w0 + i] = s_cur[i];
+    if (dbg && threadIdx.x == 0) {
+        for (int k = 0; k < 4; k++) dbg[(u64)blockIdx.x * 16 + 3 + k] = tm_acc[k];
+        dbg[(u64)blockIdx.x * 16 + 8] = (total + SYB_PASS - 1) / SYB_PASS;
+        dbg[(u64)blockIdx.x * 16 + 9] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+        dbg[(u64)blockIdx.x * 16 + 10] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+        dbg[(u64)blockIdx.x * 16 + 11] = total;
+    }
+    SY_MARK(7);
+#undef SY_MARK
+#undef SY_ACC
 }
 
 __global__ __launch_bounds__(SYC_TPB) void sy_sum_kernel(const u32* __restrict__ E, const u64* __restrict__ V, u32 CW,
@@ -657,12 +711,13 @@ __global__ __launch_bounds__(SYC_TPB) void sy_sum_kernel(const u32* __restrict__
 bool sy_bucket_eligible(const nrg_config& cf) {
     const u64 span = cf.synth_n - cf.synth_hot_reads;
     return cf.synth_cold_writes >= 1 && cf.synth_cold_writes <= SY_MAX_CW && cf.synth_hot_reads <= SY_MAX_HOT &&
-           (span + SYB_WORDS - 1) / SYB_WORDS <= SY_MAX_NB && cf.max_batch <= (u64)SY_MAX_TILES * SYA_OPS;
+           span <= (u64)SY_MAX_NB * SYB_WORDS && cf.max_batch <= (u64)SY_MAX_TILES * SYA_OPS;
 }
 
 u64 sy_bucket_aux_bytes(const nrg_config& cf) {
     const u64 span = cf.synth_n - cf.synth_hot_reads;
-    const u64 NB = (span + SYB_WORDS - 1) / SYB_WORDS;
+    const u64 W = (span + SY_MAX_NB - 1) / SY_MAX_NB;
+    const u64 NB = (span + W - 1) / W;
     const u64 tiles = (cf.max_batch + SYA_OPS - 1) / SYA_OPS;
     return tiles * SYA_OPS * cf.synth_cold_writes * 12 + NB * tiles * 4 + tiles * cf.synth_hot_reads * sizeof(SyHot) +
            256;
@@ -674,7 +729,9 @@ static hipError_t sy_bucket_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 re
     const nrg_config& cf = c->cfg;
     const u32 HW = cf.synth_hot_writes, CW = cf.synth_cold_writes, HR = cf.synth_hot_reads;
     const u64 span = cf.synth_n - HR;
-    const u32 NB = (u32)((span + SYB_WORDS - 1) / SYB_WORDS);
+    const u32 W = (u32)((span + SY_MAX_NB - 1) / SY_MAX_NB);  // words per bucket, <= 512
+    const u32 NB = (u32)((span + W - 1) / W);
+    const u64 wm = ((1ull << 40) + W - 1) / W;
     const u64 span_m = ~0ull / span, hr_m = ~0ull / HR;
     const u32 ntiles = (u32)((n + SYA_OPS - 1) / SYA_OPS);
     const u64 max_tiles = (cf.max_batch + SYA_OPS - 1) / SYA_OPS;
@@ -687,8 +744,8 @@ static hipError_t sy_bucket_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 re
     timer_begin(c, "sy_replay");
 #define SY_PART(CWV)                                                                                               \
     case CWV:                                                                                                      \
-        sy_part_kernel<CWV><<<ntiles, SYA_TPB, 0, st>>>(src, ring, ring_mask, lo, n, span, span_m, HR, hr_m, HW, NB, ntiles, \
-                                                        E, cnt, hot);                                              \
+        sy_part_kernel<CWV><<<ntiles, SYA_TPB, 0, st>>>(src, ring, ring_mask, lo, n, span, span_m, HR, hr_m, HW, NB, W, wm, \
+                                                        ntiles, E, cnt, hot);                                              \
         break
     switch (CW) {
         SY_PART(1); SY_PART(2); SY_PART(3); SY_PART(4); SY_PART(5); SY_PART(6); SY_PART(7); SY_PART(8);
@@ -696,8 +753,8 @@ static hipError_t sy_bucket_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 re
     }
 #undef SY_PART
     const size_t dyn = (size_t)(ntiles + 1) * 4 + (size_t)ntiles * 2;
-    sy_bucket_kernel<<<NB, SYB_TPB, dyn, st>>>(E, cnt, ntiles, SYA_OPS * CW, V, c->d_words, cf.synth_n, HR, ring,
-                                               ring_mask, lo);
+    sy_bucket_kernel<<<NB, SYB_TPB, dyn, st>>>(E, cnt, ntiles, SYA_OPS * CW, V, c->d_words, cf.synth_n, HR, W, ring,
+                                               ring_mask, lo, (c->exp & 2) ? c->d_dbg : nullptr);
     const bool want = d_resp != nullptr && resp_lo < lo + n && resp_hi > lo;
     u32 t0 = 0, t1 = 1;
     if (want) {
