@@ -142,3 +142,19 @@ def test_synth_bench_size_rounds(nrg, orc):
         oresp = os_.replay(np.stack([ops["tid"], ops["r1"], ops["r2"], ops["op"]], axis=1))
         np.testing.assert_array_equal(resp.cpu().numpy().view(np.uint64), oresp)
     np.testing.assert_array_equal(dev.sy_dump(), os_.dump())
+
+
+@pytest.mark.parametrize("wo", [0, 40])
+def test_synth_heavy_buckets(nrg, orc, monkeypatch, wo):
+    """Skewed rounds: tid 0 (whose cold touches start at word hot_reads) on 30 % of the ops and
+    r2 = 0 (all of an op's cold touches on one word) on 5 %, so a few buckets carry several times
+    the mean and take many passes; WriteOnly ops make the values depend on each word's last SET."""
+    monkeypatch.delenv("NRG_SY_SORT", raising=False)
+
+    def tweak(ops):
+        ops["tid"][::3] = 0
+        ops["r2"][::20] = 0
+
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_SYNTHETIC, 0, max_batch=1 << 18)
+    _check_rounds(nrg, orc, dev, orc.Synthetic(), 4, 200_000, 0x4EA + wo, list(range(64)), wo, tweak)
+    dev.close()
