@@ -145,12 +145,13 @@ def cpu_baseline(seconds: float, write_ratio: int, key_space: int, prefill: int)
                    f"(one per NUMA node); {res.ops} ops"),
         "host": host_topology(),
     }
-    c0, c0_cpus, c0_groups = _nr_cpu_run(5.0, 10, 5_000_000, 1 << 22)
+    side = min(5.0, seconds)  # the configs[0] and 1-thread legs
+    c0, c0_cpus, c0_groups = _nr_cpu_run(side, 10, 5_000_000, 1 << 22)
     out["configs0"] = {"value": round(c0.ops / c0.seconds / 1e6, 3), "unit": "Mops/s", "cores": len(c0_cpus),
                        "replicas": len(c0_groups),
-                       "sample": "BASELINE configs[0]: 5M keys, prefill [0,2^22), uniform, 10% writes, %.1f s" %
-                                 c0.seconds}
-    t1, _, _ = _nr_cpu_run(5.0, write_ratio, key_space, prefill, threads=1)
+                       "sample": f"BASELINE configs[0]: 5M keys, prefill [0,2^22), uniform, 10% writes, "
+                                 f"{c0.seconds:.1f} s"}
+    t1, _, _ = _nr_cpu_run(side, write_ratio, key_space, prefill, threads=1)
     out["one_thread"] = {"value": round(t1.ops / t1.seconds / 1e6, 3), "unit": "Mops/s", "cores": 1,
                          "sample": "the B1 stream on 1 thread, 1 replica, %.1f s" % t1.seconds}
     return out
