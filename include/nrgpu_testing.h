@@ -23,6 +23,9 @@ int nrg_test_maxscan(nrg_ctx* ctx, const uint32_t* d_keys, const uint32_t* d_val
 int nrg_test_ring_read(nrg_ctx* ctx, uint64_t phys, void* out);
 /* diagnostic phase timestamps of the last replay (contexts opened with NRG_EXP & 2) */
 int nrg_test_debug_read(nrg_ctx* ctx, uint64_t* out, uint64_t words);
+// Hashmap: 1 when the sampled key skew sends rounds to the bucket elector (hashmap.hip
+// skew_sample), 0 when they take the one-launch stamp rounds.
+int nrg_test_hm_skewed(nrg_ctx* ctx, int* out);
 #ifdef __cplusplus
 }
 #endif

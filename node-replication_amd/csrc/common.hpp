@@ -20,6 +20,8 @@ constexpr u32 ERR_CAPACITY = 4u;
 
 // Counters of keys created by replay rounds (elector blocks add to slot blk % HM_CREATED_SLOTS).
 constexpr u64 HM_CREATED_SLOTS = 8192;
+// Counters of Puts combined inside their index block (key skew statistic, hm_dup_sample_kernel).
+constexpr u64 HM_DUP_SLOTS = 64;
 // Slot buckets of a replay round (hashmap.hip hm_elect_kernel): at most this many.
 constexpr u32 HM_BK_MAX = 1024;
 // Largest hashmap replay chunk: keeps the elector's per-tile LDS tables (one u32 + one u16

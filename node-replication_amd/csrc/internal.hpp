@@ -103,6 +103,14 @@ struct nrg_ctx {
     uint32_t epoch = 1;  // epoch of the last replay round (1: prefill / before any round)
     uint32_t epoch_limit = 0xFFFFFFF0u;  // renormalise stamps here (NRG_EPOCH_LIMIT for tests)
     uint32_t* d_put_slot[2] = {nullptr, nullptr};
+    // Key skew (hm_dup_sample_kernel): Puts combined inside their index block, sampled every
+    // dup_every rounds into mapped host memory; a skewed stream takes the bucket rounds.
+    uint64_t* d_dup = nullptr;            // [HM_DUP_SLOTS]
+    volatile uint64_t* h_dup = nullptr;   // {seq, dups}, mapped pinned host memory
+    uint64_t* h_dup_dev = nullptr;        // its device address
+    uint64_t dup_seq = 0, dup_puts = 0, dup_puts_sampled = 0;
+    uint32_t dup_rounds = 0, dup_every = 16;
+    bool skewed = false;
     // Zipf generator cache: zeta(zipf_n, zipf_theta)
     uint64_t zipf_n = 0;
     double zipf_theta = 0.0, zipf_zetan = 0.0;

@@ -9,6 +9,7 @@
 // makes every copy identical), so head = min over replicas = this ltail.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -337,10 +338,12 @@ int nrg_open(int dev, const nrg_config* cfg_in, nrg_ctx** out) {
         OPEN_CHK(hm_init(c));
         OPEN_CHK(hipMalloc(&c->d_created, HM_CREATED_SLOTS * sizeof(uint64_t)));
         OPEN_CHK(hipMemsetAsync(c->d_created, 0, HM_CREATED_SLOTS * sizeof(uint64_t), c->stream));
-        // rounds of <= stamp_max Puts without previous values replay in one launch (stamp
-        // rounds); larger ones and previous-value rounds take the bucket elector
-        c->stamp_max = 250000;
+        // rounds without previous values replay in one launch (stamp rounds) unless the key
+        // stream is skewed (hashmap.hip skew_sample); skewed and previous-value rounds take the
+        // bucket elector
+        c->stamp_max = HM_MAX_BATCH;  // every size; skewed streams switch to bucket rounds
         if (const char* e = std::getenv("NRG_STAMP_MAX")) c->stamp_max = (uint64_t)std::atoll(e);
+        if (const char* e = std::getenv("NRG_SKEW_EVERY")) c->dup_every = (uint32_t)std::max(1, std::atoi(e));
         if (const char* e = std::getenv("NRG_EPOCH_LIMIT")) c->epoch_limit = (uint32_t)std::atoll(e);
         OPEN_CHK(hm_alloc(c, mb));
         // tuning knobs: Puts per index thread, target entries per elector bucket
@@ -1019,6 +1022,12 @@ extern "C" int nrg_test_ring_read(nrg_ctx* c, uint64_t phys, void* out) {
     if (r) return r;
     HIPCHK(sync_all(c));
     HIPCHK(hipMemcpy(out, (const char*)c->d_ring + phys * c->rec_bytes, c->rec_bytes, hipMemcpyDeviceToHost));
+    return NRG_OK;
+}
+
+extern "C" int nrg_test_hm_skewed(nrg_ctx* c, int* out) {
+    if (!c || !out || c->cfg.ds_kind != NRG_DS_HASHMAP) return NRG_E_INVAL;
+    *out = c->skewed ? 1 : 0;
     return NRG_OK;
 }
 

@@ -167,6 +167,7 @@ TEST_SIGNATURES = {
     "nrg_test_maxscan": (C.c_int, [vp, vp, vp, u64, vp]),
     "nrg_test_ring_read": (C.c_int, [vp, u64, vp]),
     "nrg_test_debug_read": (C.c_int, [vp, vp, u64]),
+    "nrg_test_hm_skewed": (C.c_int, [vp, vp]),
 }
 
 _lib = None

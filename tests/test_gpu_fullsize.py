@@ -90,10 +90,12 @@ def test_b1_rounds_with_previous_values(nrg, orc):
     dev.close()
 
 
-def test_configs2_per_gpu_round(nrg, orc):
+@pytest.mark.parametrize("prev", [True, False])
+def test_configs2_per_gpu_round(nrg, orc, prev):
     """configs[2]'s per-GPU work: 8 segments x 500k Puts (the all-gathered round of 8 ranks at 50 %
-    writes, 4M Puts replayed in place) + this rank's 500k Gets, previous values for the rank's own
-    segment, two pipelined rounds through nrg_hashmap_round_segments_async."""
+    writes, 4M Puts replayed in place) + this rank's 500k Gets, two pipelined rounds through
+    nrg_hashmap_round_segments_async; with previous values for the rank's own segment (bucket
+    elector) or without (Ok(None), 4M-Put stamp rounds)."""
     import torch
 
     G, W, R = 8, 500_000, 500_000
@@ -108,7 +110,7 @@ def test_configs2_per_gpu_round(nrg, orc):
         d = dict(base=_cuda(base), gk=_cuda(gk), gv=_out(R, torch.int64, -1), gf=_out(R, torch.uint8, 7),
                  pv=_out(W, torch.int64, -1), pf=_out(W, torch.uint8, 7))
         dev.hm_round_segments_device(d["base"], W, [W] * G, [g + 1 for g in range(G)], own, d["gk"], R, d["gv"],
-                                     d["gf"], d["pv"], d["pf"])
+                                     d["gf"], d["pv"] if prev else None, d["pf"] if prev else None)
         exp = None
         for g, (k, v) in enumerate(segs):
             p = om.replay(k, v)
@@ -117,8 +119,9 @@ def test_configs2_per_gpu_round(nrg, orc):
         outs.append((d, exp, om.get_batch(gk)))
     dev.join()
     for r, (d, (pv, pf), (gv, gf)) in enumerate(outs):
-        _check(d["pf"], pf, f"round {r} prev found")
-        _check(d["pv"], pv, f"round {r} prev vals")
+        if prev:
+            _check(d["pf"], pf, f"round {r} prev found")
+            _check(d["pv"], pv, f"round {r} prev vals")
         _check(d["gf"], gf, f"round {r} get found")
         _check(d["gv"], gv, f"round {r} get vals")
     assert dev.hm_digest() == om.digest()

@@ -442,3 +442,49 @@ def test_epoch_renormalisation(nrg, orc, monkeypatch):
         np.testing.assert_array_equal(gv.cpu().numpy().view(np.uint64), want[r][0], err_msg=f"round {r} vals")
     dev.sync()
     _check_state(dev, om)
+
+
+def test_skew_switches_round_kind(nrg, orc, monkeypatch):
+    """Stamp rounds (one launch, one stamp atomic per distinct key per block) are faster for
+    uniform keys, bucket rounds (no atomics per Put) for skewed ones; the replica switches from
+    the sampled share of Puts combined inside their block (every 2 rounds here). Uniform rounds,
+    then Zipf(0.99), then uniform again, pipelined: every Get and the final state bit-exact
+    across both switches, and the switches happen."""
+    import ctypes as C
+
+    import torch
+
+    monkeypatch.setenv("NRG_SKEW_EVERY", "2")
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=19, max_batch=1 << 15, pipeline=1)
+    dev.use_torch_stream()
+    om = orc.HashMap()
+    dev.hm_prefill_range(5000, 1)
+    om.prefill_range(5000, 1)
+    W, R, span = 8000, 16000, 200_000
+    kinds, outs, want = [], [], []
+    for r in range(18):
+        zipf = 6 <= r < 12
+        keys = orc.gen_zipf(W, 300 + r, span, 0.99) if zipf else orc.gen_uniform(W, 300 + r, span)
+        vals = orc.gen_raw(W, 330 + r)
+        gk = orc.gen_zipf(R, 360 + r, span, 0.99) if zipf else orc.gen_uniform(R, 360 + r, span)
+        d_puts = torch.from_numpy(_puts(keys, vals).view(np.int64).copy()).cuda()
+        d_gk = torch.from_numpy(gk.view(np.int64)).cuda()
+        d_gv = torch.full((R,), -1, dtype=torch.int64, device="cuda")
+        d_gf = torch.full((R,), 7, dtype=torch.uint8, device="cuda")
+        dev.hm_round_device(d_puts, W, 1, d_gk, R, d_gv, d_gf, None, None)
+        outs.append((d_puts, d_gk, d_gv, d_gf))
+        om.replay(keys, vals)
+        want.append(om.get_batch(gk))
+        torch.cuda.synchronize()  # the skew sample lands before the next decision
+        flag = C.c_int(-1)
+        nrg._lib.check(nrg.load().nrg_test_hm_skewed(dev.handle, C.byref(flag)))
+        kinds.append(flag.value)
+    dev.join()
+    for r, (_, _, gv, gf) in enumerate(outs):
+        np.testing.assert_array_equal(gf.cpu().numpy(), want[r][1], err_msg=f"round {r} found")
+        np.testing.assert_array_equal(gv.cpu().numpy().view(np.uint64), want[r][0], err_msg=f"round {r} vals")
+    dev.sync()
+    _check_state(dev, om)
+    assert kinds[:6] == [0] * 6, kinds
+    assert kinds[11] == 1, kinds
+    assert kinds[17] == 0, kinds
