@@ -22,6 +22,9 @@
  *   nrg_synth_*                   AbstractDataStructure Dispatch     benches/synthetic.rs:60-195
  *   nrg_group_*                   the shared Log across NUMA nodes   nr/src/log.rs:494-511 (every replica
  *                                 (RCCL all-gather of write segments) replays every entry), :473-524
+ *   nrg_key_owner, nrg_hashmap_partition*, nrg_group_partitioned_round
+ *                                 cnr's key-partitioned logs         cnr/src/lib.rs:134-167 (LogMapper::hash),
+ *                                 (one log per GPU, RCCL send/recv)  cnr/src/replica.rs:430-445, :673-736
  *
  * Conventions
  *   - Every function returns NRG_OK (0) or a negative NRG_E_* code. Nothing throws or aborts.
@@ -314,6 +317,37 @@ int nrg_group_set_input_stream(nrg_group* g, int member, void* hip_stream);
 int nrg_group_round_async(nrg_group* g, const nrg_round* rounds, const uint64_t* seg_lens);
 /* Wait for all queued group work and report latched device errors of every local replica. */
 int nrg_group_sync(nrg_group* g);
+
+/* ---- cnr-style key-partitioned NrHashMap ---------------------------------
+ * cnr maps each operation to one of several logs with LogMapper::hash() (cnr/src/lib.rs:134-167);
+ * the operations of one key share a log, so the logs replay independently
+ * (cnr/src/replica.rs:430-445 hash -> log, :673-736 combine(hashidx)). Across GPUs, partition p's
+ * log lives on GPU p, which holds only the keys it owns (no full replication): a round's Puts and
+ * Gets travel to their owners, each owner replays the Puts it received in rank order -- for every
+ * key the same order as the NR global log W_0 || W_1 || ... -- and answers the Gets it received,
+ * and answers and previous values travel back in the caller's order. The answers are identical
+ * to NR's; the replicas are not (each holds one partition). */
+#define NRG_MAX_PARTS 64
+/* Owner partition of a key: (low 32 bits of splitmix64(key)) * parts >> 32. */
+uint32_t nrg_key_owner(uint64_t key, uint32_t parts);
+/* Stable partition of W Puts and R Get keys by owner (device buffers, the replica's stream):
+ * puts_out / keys_out hold them grouped by owner, each group in issue order; put_pos[i] / get_pos[i]
+ * = where record i went; counts[p] = Puts of owner p, counts[parts + p] = Gets of owner p (u64).
+ * W, R < 2^32. */
+int nrg_hashmap_partition_async(nrg_ctx* ctx, const nrg_put* d_puts, uint64_t W, const uint64_t* d_keys, uint64_t R,
+                                uint32_t parts, nrg_put* d_puts_out, uint32_t* d_put_pos, uint64_t* d_keys_out,
+                                uint32_t* d_get_pos, uint64_t* d_counts);
+/* dst[i] = src[pos[i]] (u64 and/or u8 arrays; either pair may be NULL): answers back in order. */
+int nrg_route_back_async(nrg_ctx* ctx, const uint64_t* d_src, const uint8_t* d_src8, const uint32_t* d_pos, uint64_t n,
+                         uint64_t* d_dst, uint8_t* d_dst8);
+/* NrHashMap::default restricted to a partition: keys k < n with nrg_key_owner(k, parts) == part. */
+int nrg_hashmap_prefill_partition(nrg_ctx* ctx, uint64_t n, uint64_t off, uint32_t part, uint32_t parts);
+/* One partitioned round on every local member (group of hashmap replicas, one partition each,
+ * rank = partition): rounds[i].recs / n = the member's Puts (nrg_put), get_keys / n_gets its Gets;
+ * get_vals / get_found and (nullable) resp / some = the Gets' answers and the Puts' previous values,
+ * in the member's order. Exchanges with ncclSend / ncclRecv; returns after the counts exchange
+ * (one host round trip), the rest is stream ordered (nrg_group_sync waits). */
+int nrg_group_partitioned_round(nrg_group* g, const nrg_round* rounds);
 
 /* ---- device memory helpers (for callers without their own allocator) ----------------- */
 int nrg_dev_alloc(nrg_ctx* ctx, uint64_t bytes, void** d_ptr);

@@ -40,6 +40,13 @@ __host__ __device__ __forceinline__ u64 sm64_at(u64 seed, u64 i) {
 }
 __device__ __forceinline__ u64 mulhi64(u64 a, u64 b) { return __umul64hi(a, b); }
 
+// Owner of a key among `parts` key partitions (partition.hip): the low 32 bits of the mixed key
+// scaled to [0, parts), independent of the home-slot bits below.
+constexpr u32 PT_MAX_PARTS = 64;
+__host__ __device__ __forceinline__ u32 key_owner(u64 key, u32 parts) {
+    return (u32)(((mix64(key) & 0xFFFFFFFFull) * parts) >> 32);
+}
+
 // Home slot of a key: top bits of the mixed key.
 __device__ __forceinline__ u64 table_home(u64 key, u32 shift) { return mix64(key) >> shift; }
 

@@ -35,6 +35,8 @@ struct Rccl {
     decltype(&ncclGroupStart) group_start = nullptr;
     decltype(&ncclGroupEnd) group_end = nullptr;
     decltype(&ncclCommDestroy) destroy = nullptr;
+    decltype(&ncclSend) send = nullptr;  // partitioned rounds only
+    decltype(&ncclRecv) recv = nullptr;
 };
 
 std::mutex g_rccl_mu;
@@ -58,6 +60,8 @@ const Rccl* rccl() {
             r.group_start = (decltype(r.group_start))dlsym(h, "ncclGroupStart");
             r.group_end = (decltype(r.group_end))dlsym(h, "ncclGroupEnd");
             r.destroy = (decltype(r.destroy))dlsym(h, "ncclCommDestroy");
+            r.send = (decltype(r.send))dlsym(h, "ncclSend");
+            r.recv = (decltype(r.recv))dlsym(h, "ncclRecv");
             g_rccl_ok = r.get_unique_id && r.init_rank && r.init_all && r.all_gather && r.group_start &&
                         r.group_end && r.destroy;
             if (g_rccl_ok) g_rccl = r;
@@ -67,6 +71,16 @@ const Rccl* rccl() {
 }
 
 constexpr int NBUF = 3;  // gathered-log buffers in rotation per member
+
+// A device buffer grown on demand; a reallocation first drains the streams that may use it.
+struct DBuf {
+    void* p = nullptr;
+    uint64_t bytes = 0;
+};
+
+// Partitioned rounds (nrg_group_partitioned_round): buffers of one member.
+enum PtBuf { PB_POUT, PB_PPOS, PB_KOUT, PB_GPOS, PB_CNT, PB_ALLCNT, PB_RPUT, PB_RKEY, PB_RVAL, PB_RFOUND, PB_RPREV,
+             PB_RPREVF, PB_AVAL, PB_AFOUND, PB_APREV, PB_APREVF, PB_N };
 
 struct Member {
     nrg_ctx* ctx = nullptr;
@@ -83,6 +97,9 @@ struct Member {
     bool used[NBUF] = {};
     void* sbuf = nullptr;  // padded send copy when a segment is shorter than the stride
     uint64_t sbytes = 0;
+    DBuf pt[PB_N];               // partitioned rounds
+    std::vector<uint64_t> hcnt;  // [nranks][2 * nranks + 1] counts (and previous-value flags)
+    hipEvent_t pt_ev = nullptr;
 };
 
 int hip_rc(hipError_t e) { return e == hipSuccess ? NRG_OK : (e == hipErrorOutOfMemory ? NRG_E_NOMEM : NRG_E_HIP); }
@@ -98,6 +115,7 @@ int member_init(Member& m) {
     if (r) return r;
     GCHK(hipStreamCreateWithFlags(&m.cstream, hipStreamNonBlocking));
     GCHK(hipEventCreateWithFlags(&m.in_ev, hipEventDisableTiming));
+    GCHK(hipEventCreateWithFlags(&m.pt_ev, hipEventDisableTiming));
     for (int b = 0; b < NBUF; b++) {
         GCHK(hipEventCreateWithFlags(&m.gathered[b], hipEventDisableTiming));
         GCHK(hipEventCreateWithFlags(&m.freed[b], hipEventDisableTiming));
@@ -116,6 +134,9 @@ void member_free(Member& m, const Rccl* R) {
         if (m.freed[b]) (void)hipEventDestroy(m.freed[b]);
     }
     if (m.sbuf) (void)hipFree(m.sbuf);
+    for (DBuf& d : m.pt)
+        if (d.p) (void)hipFree(d.p);
+    if (m.pt_ev) (void)hipEventDestroy(m.pt_ev);
     if (m.in_ev) (void)hipEventDestroy(m.in_ev);
     if (m.cstream) (void)hipStreamDestroy(m.cstream);
     m = Member{};
@@ -336,6 +357,205 @@ int nrg_group_round_async(nrg_group* g, const nrg_round* rounds, const uint64_t*
         }
     }
     g->round++;
+    return NRG_OK;
+}
+
+// ---- cnr-style key-partitioned rounds (cnr/src/replica.rs:430-445, :673-736) ----
+
+static int grow(Member& m, PtBuf k, uint64_t bytes) {
+    DBuf& d = m.pt[k];
+    if (d.bytes >= bytes) return NRG_OK;
+    GCHK(hipStreamSynchronize(m.cstream));
+    GCHK(hipStreamSynchronize(m.ctx->stream));
+    if (d.p) GCHK(hipFree(d.p));
+    d.p = nullptr;
+    d.bytes = 0;
+    uint64_t b = bytes < 4096 ? 4096 : bytes + bytes / 4;  // headroom: rounds vary in size
+    GCHK(hipMalloc(&d.p, b));
+    d.bytes = b;
+    return NRG_OK;
+}
+
+// `to` waits for the work queued on `from` so far
+static int order(Member& m, hipStream_t from, hipStream_t to) {
+    GCHK(hipEventRecord(m.pt_ev, from));
+    GCHK(hipStreamWaitEvent(to, m.pt_ev, 0));
+    return NRG_OK;
+}
+
+#define RCHK(x)                                   \
+    do {                                          \
+        int _r = (x);                             \
+        if (_r != NRG_OK) return _r;              \
+    } while (0)
+
+int nrg_group_partitioned_round(nrg_group* g, const nrg_round* rounds) {
+    if (!g || !rounds) return NRG_E_INVAL;
+    const Rccl* R = rccl();
+    if (!R || !R->send || !R->recv) return NRG_E_COMM;
+    const int G = g->nranks, nl = (int)g->m.size();
+    if (G > NRG_MAX_PARTS) return NRG_E_INVAL;
+    const uint64_t CW = 2 * (uint64_t)G + 1;  // per rank: Puts per owner, Gets per owner, wants previous values
+    for (int i = 0; i < nl; i++) {
+        const nrg_round& x = rounds[i];
+        if (g->m[i].ctx->cfg.ds_kind != NRG_DS_HASHMAP || (x.n && !x.recs) ||
+            (x.n_gets && (!x.get_keys || !x.get_vals || !x.get_found)))
+            return NRG_E_INVAL;
+        if (x.n >= (1ull << 32) || x.n_gets >= (1ull << 32)) return NRG_E_CAPACITY;
+    }
+    // 1. partition each member's Puts and Gets by owner (its stream, after its inputs)
+    for (int i = 0; i < nl; i++) {
+        Member& m = g->m[i];
+        const nrg_round& x = rounds[i];
+        nrg_ctx* c = m.ctx;
+        RCHK(nrg::ctx_use_device(c));
+        RCHK(grow(m, PB_POUT, x.n * 16));
+        RCHK(grow(m, PB_PPOS, x.n * 4));
+        RCHK(grow(m, PB_KOUT, x.n_gets * 8));
+        RCHK(grow(m, PB_GPOS, x.n_gets * 4));
+        RCHK(grow(m, PB_CNT, CW * 8));
+        RCHK(grow(m, PB_ALLCNT, (uint64_t)G * CW * 8));
+        if (m.in_set && m.in_stream != c->stream) RCHK(order(m, m.in_stream, c->stream));
+        RCHK(nrg_hashmap_partition_async(c, (const nrg_put*)x.recs, x.n, x.get_keys, x.n_gets, (uint32_t)G,
+                                         (nrg_put*)m.pt[PB_POUT].p, (uint32_t*)m.pt[PB_PPOS].p,
+                                         (uint64_t*)m.pt[PB_KOUT].p, (uint32_t*)m.pt[PB_GPOS].p,
+                                         (uint64_t*)m.pt[PB_CNT].p));
+        // word 2G: 1 when this rank wants its Puts' previous values (little-endian u64)
+        void* flag = (uint64_t*)m.pt[PB_CNT].p + 2 * G;
+        GCHK(hipMemsetAsync(flag, 0, 8, c->stream));
+        if (x.resp && x.some) GCHK(hipMemsetAsync(flag, 1, 1, c->stream));
+        RCHK(order(m, c->stream, m.cstream));
+    }
+    // 2. every rank's counts to every rank; the host needs them to size the exchanges
+    if (R->group_start() != ncclSuccess) return NRG_E_COMM;
+    ncclResult_t res = ncclSuccess;
+    for (int i = 0; i < nl && res == ncclSuccess; i++)
+        res = R->all_gather(g->m[i].pt[PB_CNT].p, g->m[i].pt[PB_ALLCNT].p, CW, ncclUint64, g->m[i].comm, g->m[i].cstream);
+    if (R->group_end() != ncclSuccess || res != ncclSuccess) return NRG_E_COMM;
+    for (int i = 0; i < nl; i++) {
+        Member& m = g->m[i];
+        RCHK(nrg::ctx_use_device(m.ctx));
+        m.hcnt.resize((size_t)G * CW);
+        GCHK(hipMemcpyAsync(m.hcnt.data(), m.pt[PB_ALLCNT].p, (uint64_t)G * CW * 8, hipMemcpyDeviceToHost, m.cstream));
+        GCHK(hipStreamSynchronize(m.cstream));
+    }
+    bool any_prev = false;
+    for (int s = 0; s < G; s++) any_prev |= g->m[0].hcnt[(size_t)s * CW + 2 * G] != 0;
+    // 3. Puts and Get keys to their owners: member rank r sends its owner-o group to o and receives
+    //    rank s's group for r at offset sum_{s' < s} (rank order = the global log order)
+    struct Plan {
+        std::vector<uint64_t> pto, gto, pfrom, gfrom, pto_off, gto_off, pfrom_off, gfrom_off;
+        uint64_t rp = 0, rk = 0;
+    };
+    std::vector<Plan> plan(nl);
+    for (int i = 0; i < nl; i++) {
+        Member& m = g->m[i];
+        Plan& P = plan[i];
+        const int r = m.rank;
+        const uint64_t* h = m.hcnt.data();
+        P.pto.resize(G), P.gto.resize(G), P.pfrom.resize(G), P.gfrom.resize(G);
+        P.pto_off.resize(G), P.gto_off.resize(G), P.pfrom_off.resize(G), P.gfrom_off.resize(G);
+        uint64_t a = 0, b = 0, cq = 0, d = 0;
+        for (int o = 0; o < G; o++) {
+            P.pto[o] = h[(size_t)r * CW + o];
+            P.gto[o] = h[(size_t)r * CW + G + o];
+            P.pfrom[o] = h[(size_t)o * CW + r];
+            P.gfrom[o] = h[(size_t)o * CW + G + r];
+            P.pto_off[o] = a, a += P.pto[o];
+            P.gto_off[o] = b, b += P.gto[o];
+            P.pfrom_off[o] = cq, cq += P.pfrom[o];
+            P.gfrom_off[o] = d, d += P.gfrom[o];
+        }
+        if (a != rounds[i].n || b != rounds[i].n_gets) return NRG_E_HIP;  // counts disagree with the inputs
+        P.rp = cq;
+        P.rk = d;
+        const nrg_round& x = rounds[i];
+        RCHK(grow(m, PB_RPUT, P.rp * 16));
+        RCHK(grow(m, PB_RKEY, P.rk * 8));
+        RCHK(grow(m, PB_RVAL, P.rk * 8));
+        RCHK(grow(m, PB_RFOUND, P.rk));
+        RCHK(grow(m, PB_RPREV, P.rp * 8));
+        RCHK(grow(m, PB_RPREVF, P.rp));
+        RCHK(grow(m, PB_AVAL, x.n_gets * 8));
+        RCHK(grow(m, PB_AFOUND, x.n_gets));
+        RCHK(grow(m, PB_APREV, x.n * 8));
+        RCHK(grow(m, PB_APREVF, x.n));
+    }
+    auto at = [](const DBuf& d, uint64_t off) { return (void*)((char*)d.p + off); };
+    if (R->group_start() != ncclSuccess) return NRG_E_COMM;
+    for (int i = 0; i < nl && res == ncclSuccess; i++) {
+        Member& m = g->m[i];
+        const Plan& P = plan[i];
+        for (int o = 0; o < G && res == ncclSuccess; o++) {
+            if (P.pto[o]) res = R->send(at(m.pt[PB_POUT], P.pto_off[o] * 16), P.pto[o] * 2, ncclUint64, o, m.comm, m.cstream);
+            if (res == ncclSuccess && P.pfrom[o])
+                res = R->recv(at(m.pt[PB_RPUT], P.pfrom_off[o] * 16), P.pfrom[o] * 2, ncclUint64, o, m.comm, m.cstream);
+            if (res == ncclSuccess && P.gto[o])
+                res = R->send(at(m.pt[PB_KOUT], P.gto_off[o] * 8), P.gto[o], ncclUint64, o, m.comm, m.cstream);
+            if (res == ncclSuccess && P.gfrom[o])
+                res = R->recv(at(m.pt[PB_RKEY], P.gfrom_off[o] * 8), P.gfrom[o], ncclUint64, o, m.comm, m.cstream);
+        }
+    }
+    if (R->group_end() != ncclSuccess || res != ncclSuccess) return NRG_E_COMM;
+    // 4. each owner replays the Puts it received (rank order) and answers the Gets it received
+    for (int i = 0; i < nl; i++) {
+        Member& m = g->m[i];
+        const Plan& P = plan[i];
+        nrg_ctx* c = m.ctx;
+        RCHK(nrg::ctx_use_device(c));
+        RCHK(order(m, m.cstream, c->stream));
+        if (P.rp || P.rk)
+            RCHK(nrg_hashmap_round_async(c, (const nrg_put*)m.pt[PB_RPUT].p, P.rp, (uint32_t)m.rank + 1,
+                                         (const uint64_t*)m.pt[PB_RKEY].p, P.rk, (uint64_t*)m.pt[PB_RVAL].p,
+                                         (uint8_t*)m.pt[PB_RFOUND].p, any_prev ? (uint64_t*)m.pt[PB_RPREV].p : nullptr,
+                                         any_prev ? (uint8_t*)m.pt[PB_RPREVF].p : nullptr));
+        RCHK(nrg_join(c));
+        RCHK(order(m, c->stream, m.cstream));
+    }
+    // 5. answers back to the ranks that asked, into their owner-grouped order
+    if (R->group_start() != ncclSuccess) return NRG_E_COMM;
+    for (int i = 0; i < nl && res == ncclSuccess; i++) {
+        Member& m = g->m[i];
+        const Plan& P = plan[i];
+        const bool mine = rounds[i].resp && rounds[i].some;
+        for (int o = 0; o < G && res == ncclSuccess; o++) {
+            const bool theirs = m.hcnt[(size_t)o * CW + 2 * G] != 0;
+            if (P.gfrom[o]) {
+                res = R->send(at(m.pt[PB_RVAL], P.gfrom_off[o] * 8), P.gfrom[o], ncclUint64, o, m.comm, m.cstream);
+                if (res == ncclSuccess)
+                    res = R->send(at(m.pt[PB_RFOUND], P.gfrom_off[o]), P.gfrom[o], ncclUint8, o, m.comm, m.cstream);
+            }
+            if (res == ncclSuccess && P.gto[o]) {
+                res = R->recv(at(m.pt[PB_AVAL], P.gto_off[o] * 8), P.gto[o], ncclUint64, o, m.comm, m.cstream);
+                if (res == ncclSuccess)
+                    res = R->recv(at(m.pt[PB_AFOUND], P.gto_off[o]), P.gto[o], ncclUint8, o, m.comm, m.cstream);
+            }
+            if (res == ncclSuccess && theirs && P.pfrom[o]) {
+                res = R->send(at(m.pt[PB_RPREV], P.pfrom_off[o] * 8), P.pfrom[o], ncclUint64, o, m.comm, m.cstream);
+                if (res == ncclSuccess)
+                    res = R->send(at(m.pt[PB_RPREVF], P.pfrom_off[o]), P.pfrom[o], ncclUint8, o, m.comm, m.cstream);
+            }
+            if (res == ncclSuccess && mine && P.pto[o]) {
+                res = R->recv(at(m.pt[PB_APREV], P.pto_off[o] * 8), P.pto[o], ncclUint64, o, m.comm, m.cstream);
+                if (res == ncclSuccess)
+                    res = R->recv(at(m.pt[PB_APREVF], P.pto_off[o]), P.pto[o], ncclUint8, o, m.comm, m.cstream);
+            }
+        }
+    }
+    if (R->group_end() != ncclSuccess || res != ncclSuccess) return NRG_E_COMM;
+    // 6. back into the caller's order
+    for (int i = 0; i < nl; i++) {
+        Member& m = g->m[i];
+        const nrg_round& x = rounds[i];
+        nrg_ctx* c = m.ctx;
+        RCHK(nrg::ctx_use_device(c));
+        RCHK(order(m, m.cstream, c->stream));
+        RCHK(nrg_route_back_async(c, (const uint64_t*)m.pt[PB_AVAL].p, (const uint8_t*)m.pt[PB_AFOUND].p,
+                                  (const uint32_t*)m.pt[PB_GPOS].p, x.n_gets, x.get_vals, x.get_found));
+        if (x.resp && x.some)
+            RCHK(nrg_route_back_async(c, (const uint64_t*)m.pt[PB_APREV].p, (const uint8_t*)m.pt[PB_APREVF].p,
+                                      (const uint32_t*)m.pt[PB_PPOS].p, x.n, (uint64_t*)x.resp, x.some));
+    }
     return NRG_OK;
 }
 

@@ -846,12 +846,13 @@ __global__ __launch_bounds__(TPB) void hm_renorm_kernel(Slot* table, u64 slots, 
 
 // NrHashMap::default (benches/hashmap.rs:91-100): keys 0..n-1 -> k + off, inserted directly.
 __global__ __launch_bounds__(TPB) void hm_prefill_range_kernel(Slot* table, u64 n, u64 off, u32 shift, u64 tmask,
-                                                               DevCtl* ctl) {
+                                                               DevCtl* ctl, u32 part, u32 parts) {
     __shared__ u32 s_ins;
     if (threadIdx.x == 0) s_ins = 0;
     __syncthreads();
     u32 inserted = 0;
     for (u64 k = blockIdx.x * (u64)TPB + threadIdx.x; k < n; k += (u64)gridDim.x * TPB) {
+        if (parts > 1 && key_owner(k, parts) != part) continue;  // a key partition's share only
         if (k == EMPTY_KEY) {  // only reachable for n = 2^64, kept for the full key domain
             inserted += ctl->sp_claim == 0;
             ctl->sp.val = k + off;
@@ -1281,11 +1282,11 @@ hipError_t hm_get_only(nrg_ctx* c, const u64* d_keys, u64 n, u64* d_vals, uint8_
     return hm_reads(c, d_keys, n, d_vals, d_found);
 }
 
-hipError_t hm_prefill_range(nrg_ctx* c, u64 n, u64 off) {
+hipError_t hm_prefill_range(nrg_ctx* c, u64 n, u64 off, u32 part, u32 parts) {
     hipError_t e = hm_flush(c);
     if (e != hipSuccess) return e;
     hm_prefill_range_kernel<<<grid_for(n, 8192), TPB, 0, c->stream>>>(c->d_table, n, off, c->slot_shift,
-                                                                      c->slots - 1, c->d_ctl);
+                                                                      c->slots - 1, c->d_ctl, part, parts);
     return hipGetLastError();
 }
 

@@ -106,6 +106,8 @@ struct nrg_ctx {
     // Key skew (hm_dup_sample_kernel): Puts combined inside their index block, sampled every
     // dup_every rounds into mapped host memory; a skewed stream takes the bucket rounds.
     uint64_t* d_dup = nullptr;            // [HM_DUP_SLOTS]
+    void* d_pt = nullptr;                 // partition.hip tile counts / offsets
+    uint64_t pt_words = 0;
     volatile uint64_t* h_dup = nullptr;   // {seq, dups}, mapped pinned host memory
     uint64_t* h_dup_dev = nullptr;        // its device address
     uint64_t dup_seq = 0, dup_puts = 0, dup_puts_sampled = 0;
@@ -172,7 +174,10 @@ hipError_t hm_get_only(nrg_ctx* c, const u64* d_keys, u64 n, u64* d_vals, uint8_
 hipError_t hm_init(nrg_ctx* c);
 hipError_t hm_alloc(nrg_ctx* c, u64 max_batch);  // per-round scratch (entries, counts, overlays)
 void hm_free(nrg_ctx* c);
-hipError_t hm_prefill_range(nrg_ctx* c, u64 n, u64 off);
+hipError_t hm_prefill_range(nrg_ctx* c, u64 n, u64 off, u32 part = 0, u32 parts = 1);
+// partition.hip: stable partition of records (key in word 0) by key owner; answers routed back
+hipError_t pt_partition(nrg_ctx* c, const u64* in, u64 n, u32 words, u32 parts, u64* out, u32* pos, u64* total);
+hipError_t pt_gather(nrg_ctx* c, const u64* src, const uint8_t* src8, const u32* pos, u64 n, u64* dst, uint8_t* dst8);
 hipError_t hm_dump(nrg_ctx* c, u64* d_keys, u64* d_vals);
 hipError_t hm_count(nrg_ctx* c);  // DevCtl::nkeys_total = number of keys
 hipError_t hm_digest(nrg_ctx* c, u64* d_out3);

@@ -1,0 +1,186 @@
+// partition.hip — cnr-style key partitioning of hashmap rounds across replicas.
+//
+// cnr (cnr/src/lib.rs:134-167) maps every operation to one of several logs with
+// LogMapper::hash(); conflicting operations (the same key) share a log, so each log replays
+// independently (cnr/src/replica.rs:430-445 hash -> log, :673-736 combine(hashidx)). Across GPUs
+// the log of partition p lives on GPU p, which holds only the keys it owns: a round's Puts and
+// Gets are routed to their owners, each owner replays the Puts it received in rank order (the
+// global log order restricted to its keys, so every key sees its writes in the same order as an
+// NR replay of W_0 || W_1 || ...), answers the Gets it received, and the answers travel back.
+//
+// Owner of a key: the low 32 bits of mix64(key) scaled to [0, parts). The table's home slot uses
+// the top bits of the same mix (common.hpp table_home), so a partition's keys still spread over
+// its whole table.
+//
+// Kernels (records of `words` u64 with the key in word 0: Puts 2, Get keys 1):
+//   pt_count_kernel    per 2048-record tile: records per owner
+//   pt_scan_kernel     per owner: exclusive scan of the tile counts, and the owner's total
+//   pt_scatter_kernel  per tile: stable rank of each record among its owner's records of the
+//                      tile (per wave, one ballot per distinct owner in a 64-record round; the
+//                      per-owner counts of a wave live in lane `owner`), then out[dest] = record
+//                      and pos[i] = dest, dest = owner start + tile offset + wave offset + rank
+//   pt_gather_kernel   answers back to the caller's order: dst[i] = src[pos[i]]
+#include "internal.hpp"
+
+namespace nrg {
+
+constexpr int PT_TPB = 256;
+constexpr int PT_WAVES = PT_TPB / 64;
+constexpr int PT_ROUNDS = 8;                             // 64-record rounds per wave
+constexpr u32 PT_TILE = PT_TPB * PT_ROUNDS;              // 2048 records per tile
+
+__global__ __launch_bounds__(PT_TPB) void pt_count_kernel(const u64* __restrict__ in, u64 n, u32 words, u32 parts,
+                                                          u32* __restrict__ tcnt) {
+    __shared__ u32 s_c[PT_MAX_PARTS];
+    if (threadIdx.x < PT_MAX_PARTS) s_c[threadIdx.x] = 0;
+    __syncthreads();
+    const u64 t0 = (u64)blockIdx.x * PT_TILE;
+    for (u32 k = threadIdx.x; k < PT_TILE; k += PT_TPB) {
+        const u64 i = t0 + k;
+        if (i < n) atomicAdd(&s_c[key_owner(in[i * words], parts)], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < parts) tcnt[(u64)blockIdx.x * parts + threadIdx.x] = s_c[threadIdx.x];
+}
+
+// one block per owner p: toff[t][p] = sum of tcnt[t'][p], t' < t; total[p]
+__global__ __launch_bounds__(PT_TPB) void pt_scan_kernel(const u32* __restrict__ tcnt, u32 ntiles, u32 parts,
+                                                         u32* __restrict__ toff, u64* __restrict__ total) {
+    __shared__ u32 s_w[PT_WAVES];
+    const u32 p = blockIdx.x;
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    const u32 K = (ntiles + PT_TPB - 1) / PT_TPB;  // tiles [t*K, t*K + K) per thread
+    u32 loc = 0;
+    for (u32 q = 0; q < K; q++) {
+        const u32 tile = t * K + q;
+        if (tile < ntiles) loc += tcnt[(u64)tile * parts + p];
+    }
+    u32 inc = loc;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const u32 y = __shfl_up(inc, off, 64);
+        if (lane >= off) inc += y;
+    }
+    if (lane == 63) s_w[w] = inc;
+    __syncthreads();
+    u32 run = inc - loc;
+    for (int i = 0; i < w; i++) run += s_w[i];
+    for (u32 q = 0; q < K; q++) {
+        const u32 tile = t * K + q;
+        if (tile < ntiles) {
+            const u32 c = tcnt[(u64)tile * parts + p];
+            toff[(u64)tile * parts + p] = run;
+            run += c;
+        }
+    }
+    if (t == PT_TPB - 1) {
+        u32 all = 0;
+        for (int i = 0; i < PT_WAVES; i++) all += s_w[i];
+        total[p] = all;
+    }
+}
+
+__global__ __launch_bounds__(PT_TPB) void pt_scatter_kernel(const u64* __restrict__ in, u64 n, u32 words, u32 parts,
+                                                            const u32* __restrict__ toff, const u64* __restrict__ total,
+                                                            u64* __restrict__ out, u32* __restrict__ pos) {
+    __shared__ u32 s_base[PT_MAX_PARTS];          // owner start: exclusive prefix of the totals
+    __shared__ u32 s_wc[PT_WAVES][PT_MAX_PARTS];  // per wave counts, then wave offsets
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    if (t == 0) {
+        u32 acc = 0;
+        for (u32 p = 0; p < parts; p++) {
+            s_base[p] = acc;
+            acc += (u32)total[p];
+        }
+    }
+    const u64 t0 = (u64)blockIdx.x * PT_TILE + (u64)w * (PT_ROUNDS * 64);
+    u32 own[PT_ROUNDS], rank[PT_ROUNDS];
+    u32 cnt = 0;  // lane p: this wave's records of owner p so far
+#pragma unroll
+    for (int r = 0; r < PT_ROUNDS; r++) {
+        const u64 i = t0 + (u64)r * 64 + lane;
+        const bool valid = i < n;
+        const u32 o = valid ? key_owner(in[i * words], parts) : 0u;
+        own[r] = o;
+        rank[r] = 0;
+        u64 act = __ballot(valid);
+        while (act) {  // one ballot per distinct owner among the 64 records (wave-uniform loop)
+            const int leader = __ffsll((long long)act) - 1;
+            const u32 ol = (u32)__shfl((int)o, leader, 64);
+            const u64 m = __ballot(valid && o == ol);
+            const u32 c0 = (u32)__shfl((int)cnt, (int)ol, 64);
+            if (valid && o == ol) rank[r] = c0 + (u32)__popcll(m & ((1ull << lane) - 1));
+            if ((u32)lane == ol) cnt += (u32)__popcll(m);
+            act &= ~m;
+        }
+    }
+    if ((u32)lane < parts) s_wc[w][lane] = cnt;
+    __syncthreads();
+    if (t < (int)parts) {
+        u32 acc = 0;
+        for (int i = 0; i < PT_WAVES; i++) {
+            const u32 c = s_wc[i][t];
+            s_wc[i][t] = acc;
+            acc += c;
+        }
+    }
+    __syncthreads();
+    const u32* to = toff + (u64)blockIdx.x * parts;
+#pragma unroll
+    for (int r = 0; r < PT_ROUNDS; r++) {
+        const u64 i = t0 + (u64)r * 64 + lane;
+        if (i >= n) continue;
+        const u32 o = own[r];
+        const u32 dest = s_base[o] + to[o] + s_wc[w][o] + rank[r];
+        for (u32 k = 0; k < words; k++) out[(u64)dest * words + k] = in[i * words + k];
+        pos[i] = dest;
+    }
+}
+
+__global__ __launch_bounds__(PT_TPB) void pt_gather_kernel(const u64* __restrict__ src, const uint8_t* __restrict__ src8,
+                                                           const u32* __restrict__ pos, u64 n, u64* __restrict__ dst,
+                                                           uint8_t* __restrict__ dst8) {
+    for (u64 i = blockIdx.x * (u64)PT_TPB + threadIdx.x; i < n; i += (u64)gridDim.x * PT_TPB) {
+        const u32 p = pos[i];
+        if (dst) dst[i] = src[p];
+        if (dst8) dst8[i] = src8[p];
+    }
+}
+
+// Scratch for the tile counts and offsets, grown on demand (the replica's stream is drained
+// before a reallocation).
+static hipError_t pt_scratch(nrg_ctx* c, u64 words) {
+    if (c->pt_words >= words) return hipSuccess;
+    hipError_t e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return e;
+    if (c->d_pt) (void)hipFree(c->d_pt);
+    c->d_pt = nullptr;
+    c->pt_words = 0;
+    if ((e = hipMalloc(&c->d_pt, words * sizeof(u32))) != hipSuccess) return e;
+    c->pt_words = words;
+    return hipSuccess;
+}
+
+hipError_t pt_partition(nrg_ctx* c, const u64* in, u64 n, u32 words, u32 parts, u64* out, u32* pos, u64* total) {
+    if (parts == 0 || parts > PT_MAX_PARTS) return hipErrorInvalidValue;
+    if (n == 0) return hipMemsetAsync(total, 0, parts * sizeof(u64), c->stream);
+    const u64 ntiles = (n + PT_TILE - 1) / PT_TILE;
+    if (ntiles > 0xFFFFFFFFull || n > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    hipError_t e = pt_scratch(c, 2 * ntiles * parts);
+    if (e != hipSuccess) return e;
+    u32* tcnt = (u32*)c->d_pt;
+    u32* toff = tcnt + ntiles * parts;
+    pt_count_kernel<<<(unsigned)ntiles, PT_TPB, 0, c->stream>>>(in, n, words, parts, tcnt);
+    pt_scan_kernel<<<parts, PT_TPB, 0, c->stream>>>(tcnt, (u32)ntiles, parts, toff, total);
+    pt_scatter_kernel<<<(unsigned)ntiles, PT_TPB, 0, c->stream>>>(in, n, words, parts, toff, total, out, pos);
+    return hipGetLastError();
+}
+
+hipError_t pt_gather(nrg_ctx* c, const u64* src, const uint8_t* src8, const u32* pos, u64 n, u64* dst, uint8_t* dst8) {
+    if (n == 0) return hipSuccess;
+    const u64 blocks = (n + PT_TPB - 1) / PT_TPB;
+    pt_gather_kernel<<<(unsigned)(blocks < 4096 ? blocks : 4096), PT_TPB, 0, c->stream>>>(src, src8, pos, n, dst, dst8);
+    return hipGetLastError();
+}
+
+}  // namespace nrg

@@ -402,7 +402,7 @@ int nrg_close(nrg_ctx* c) {
     if (c->stream && c->stream != c->own_stream) (void)hipStreamSynchronize(c->stream);
     void* ptrs[] = {c->d_ring,    c->d_ctl,      c->d_table,    c->d_stack,  c->d_words,
                     c->d_sort_aux, c->d_tmp_u64, c->d_scan_desc, c->d_created, c->d_st_aux,
-                    c->d_sy_aux,  c->d_bk_ent,   c->d_bk_key,   c->d_bk_cnt, c->d_dbg};
+                    c->d_sy_aux,  c->d_bk_ent,   c->d_bk_key,   c->d_bk_cnt, c->d_dbg,     c->d_pt};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     sort_free(c->sort);
@@ -712,6 +712,42 @@ int nrg_hashmap_prefill_range(nrg_ctx* c, uint64_t n, uint64_t off) {
     int r = need(c, NRG_DS_HASHMAP);
     if (r) return r;
     HIPCHK(hm_prefill_range(c, n, off));
+    HIPCHK(sync_all(c));
+    return check_err(c);
+}
+
+// ---- cnr-style key partitioning (partition.hip) ----------------------------
+uint32_t nrg_key_owner(uint64_t key, uint32_t parts) { return parts ? nrg::key_owner(key, parts) : 0u; }
+
+int nrg_hashmap_partition_async(nrg_ctx* c, const nrg_put* d_puts, uint64_t W, const uint64_t* d_keys, uint64_t R,
+                                uint32_t parts, nrg_put* d_puts_out, uint32_t* d_put_pos, uint64_t* d_keys_out,
+                                uint32_t* d_get_pos, uint64_t* d_counts) {
+    int r = need(c, NRG_DS_HASHMAP);
+    if (r) return r;
+    if (parts == 0 || parts > NRG_MAX_PARTS || !d_counts) return NRG_E_INVAL;
+    if ((W && (!d_puts || !d_puts_out || !d_put_pos)) || (R && (!d_keys || !d_keys_out || !d_get_pos)))
+        return NRG_E_INVAL;
+    if (W >= (1ull << 32) || R >= (1ull << 32)) return NRG_E_CAPACITY;
+    HIPCHK(pt_partition(c, (const u64*)d_puts, W, 2, parts, (u64*)d_puts_out, d_put_pos, d_counts));
+    HIPCHK(pt_partition(c, d_keys, R, 1, parts, d_keys_out, d_get_pos, d_counts + parts));
+    return NRG_OK;
+}
+
+int nrg_route_back_async(nrg_ctx* c, const uint64_t* d_src, const uint8_t* d_src8, const uint32_t* d_pos, uint64_t n,
+                         uint64_t* d_dst, uint8_t* d_dst8) {
+    if (!c) return NRG_E_INVAL;
+    int r = use_device(c);
+    if (r) return r;
+    if (n && (!d_pos || (d_dst && !d_src) || (d_dst8 && !d_src8))) return NRG_E_INVAL;
+    HIPCHK(pt_gather(c, d_src, d_src8, d_pos, n, d_dst, d_dst8));
+    return NRG_OK;
+}
+
+int nrg_hashmap_prefill_partition(nrg_ctx* c, uint64_t n, uint64_t off, uint32_t part, uint32_t parts) {
+    int r = need(c, NRG_DS_HASHMAP);
+    if (r) return r;
+    if (parts == 0 || parts > NRG_MAX_PARTS || part >= parts) return NRG_E_INVAL;
+    HIPCHK(hm_prefill_range(c, n, off, part, parts));
     HIPCHK(sync_all(c));
     return check_err(c);
 }

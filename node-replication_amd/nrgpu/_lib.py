@@ -30,6 +30,7 @@ NRG_E_CAPACITY = -7
 NRG_E_NODEV = -8
 NRG_E_COMM = -9
 NRG_GROUP_ID_BYTES = 128
+NRG_MAX_PARTS = 64
 
 NRG_DS_HASHMAP = 1
 NRG_DS_STACK = 2
@@ -159,6 +160,11 @@ SIGNATURES = {
     "nrg_group_set_input_stream": (C.c_int, [vp, C.c_int, vp]),
     "nrg_group_round_async": (C.c_int, [vp, C.POINTER(Round), u64p]),
     "nrg_group_sync": (C.c_int, [vp]),
+    "nrg_key_owner": (C.c_uint32, [u64, C.c_uint32]),
+    "nrg_hashmap_partition_async": (C.c_int, [vp, vp, u64, vp, u64, C.c_uint32, vp, vp, vp, vp, vp]),
+    "nrg_route_back_async": (C.c_int, [vp, vp, vp, vp, u64, vp, vp]),
+    "nrg_hashmap_prefill_partition": (C.c_int, [vp, u64, u64, C.c_uint32, C.c_uint32]),
+    "nrg_group_partitioned_round": (C.c_int, [vp, C.POINTER(Round)]),
 }
 
 # include/nrgpu_testing.h (kernel unit-test hooks)

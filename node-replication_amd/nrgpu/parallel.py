@@ -192,3 +192,104 @@ class ReplicatedHashMap(ReplicatedLog):
         g = self.gather_async(puts, stride, lens)
         self.replay(g, get_keys, get_vals, get_found, prev, prev_found)
         return g.buf.view(-1, 2)
+
+
+# ---- cnr-style key-partitioned NrHashMap ----------------------------------
+# cnr maps every operation to one of several logs with LogMapper::hash (cnr/src/lib.rs:134-167,
+# cnr/src/replica.rs:430-445) and each log replays on its own (:673-736). Here partition p's log
+# lives on rank p, which holds only the keys it owns: a round routes Puts and Gets to their
+# owners, every owner replays what it received in rank order (for each key the NR global-log
+# order) and answers its Gets, and the answers come back in the caller's order. Answers equal
+# NR's; the replicas hold one partition each (their digests add up to the NR replica's).
+
+_M1, _M2 = 0xBF58476D1CE4E5B9, 0x94D049BB133111EB
+
+
+def key_owner(keys, parts: int):
+    """nrg_key_owner over an array: (low 32 bits of splitmix64(key)) * parts >> 32."""
+    import numpy as np
+
+    z = np.ascontiguousarray(keys).view(np.uint64).copy()
+    with np.errstate(over="ignore"):
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(_M1)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(_M2)
+        z = z ^ (z >> np.uint64(31))
+    return ((z & np.uint64(0xFFFFFFFF)) * np.uint64(parts) >> np.uint64(32)).astype(np.int64)
+
+
+class PartitionedGroup(ReplicaGroup):
+    """This rank's replica as partition `rank` of a key-partitioned group (libnrgpu.so, RCCL
+    send/recv): nrg_group_partitioned_round."""
+
+    def round(self, puts, n: int, get_keys, n_gets: int, get_vals, get_found, prev=None, prev_found=None):
+        r = self._round
+        r.recs, r.n, r.resp, r.some = _ptr(puts), n, _ptr(prev), _ptr(prev_found)
+        r.get_keys, r.n_gets, r.get_vals, r.get_found = _ptr(get_keys), n_gets, _ptr(get_vals), _ptr(get_found)
+        rc = self._lib.nrg_group_partitioned_round(self._h, C.byref(r))
+        if rc:
+            L.check(rc, "nrg_group_partitioned_round")
+
+
+class PartitionedHashMap:
+    """Key-partitioned rounds with the exchanges done by torch.distributed (all_to_all_single;
+    gloo on CPU tests, see PartitionedGroup for RCCL). `replica` must provide
+    partitioned_replay(puts [p, 2] int64, keys [k] int64, want_prev) -> (vals, found, prev, prev_found)
+    (DeviceReplica does; CPU tests use an oracle-backed double)."""
+
+    def __init__(self, replica, group: Optional[dist.ProcessGroup] = None):
+        self.replica = replica
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+
+    def _split(self, keys: torch.Tensor):
+        """Stable partition by owner: (order, counts); order[j] = index of the j-th routed item."""
+        import numpy as np
+
+        own = key_owner(keys.cpu().numpy(), self.world)
+        order = np.argsort(own, kind="stable")
+        counts = np.bincount(own, minlength=self.world)
+        return torch.from_numpy(order), [int(c) for c in counts]
+
+    def _a2a(self, send: torch.Tensor, send_counts, recv_counts):
+        out = torch.empty((sum(recv_counts),) + tuple(send.shape[1:]), dtype=send.dtype)
+        dist.all_to_all_single(out, send.contiguous(), [c for c in recv_counts], [c for c in send_counts],
+                               group=self.group)
+        return out
+
+    def round(self, puts: torch.Tensor, get_keys: torch.Tensor, get_vals: torch.Tensor, get_found: torch.Tensor,
+              prev: Optional[torch.Tensor] = None, prev_found: Optional[torch.Tensor] = None):
+        """puts [W, 2] int64 (key, value) and get_keys [R] in issue order, on any device; answers
+        land in get_vals / get_found (and prev / prev_found) in that order."""
+        dev = get_vals.device
+        p_cpu, k_cpu = puts.reshape(-1, 2).cpu(), get_keys.reshape(-1).cpu()
+        p_order, p_cnt = self._split(p_cpu[:, 0])
+        k_order, k_cnt = self._split(k_cpu)
+        want = torch.tensor([1 if prev is not None else 0], dtype=torch.int64)
+        sizes = torch.tensor(p_cnt + k_cnt + [int(want.item())], dtype=torch.int64)
+        allsz = [torch.zeros_like(sizes) for _ in range(self.world)]
+        dist.all_gather(allsz, sizes, group=self.group)  # every rank's counts (and wants-prev flag)
+        w = self.world
+        p_from = [int(allsz[s][self.rank]) for s in range(w)]
+        k_from = [int(allsz[s][w + self.rank]) for s in range(w)]
+        any_prev = any(int(allsz[s][2 * w]) for s in range(w))
+        rput = self._a2a(p_cpu[p_order], p_cnt, p_from)      # received in rank order = log order
+        rkey = self._a2a(k_cpu[k_order], k_cnt, k_from)
+        vals, found, pv, pf = self.replica.partitioned_replay(rput, rkey, any_prev)
+        a_vals = self._a2a(vals.cpu(), k_from, k_cnt)
+        a_found = self._a2a(found.cpu(), k_from, k_cnt)
+        back_v = torch.empty_like(a_vals)
+        back_f = torch.empty_like(a_found)
+        back_v[k_order] = a_vals
+        back_f[k_order] = a_found
+        get_vals.copy_(back_v.to(dev))
+        get_found.copy_(back_f.to(dev))
+        if any_prev:
+            a_pv = self._a2a(pv.cpu(), p_from, p_cnt)
+            a_pf = self._a2a(pf.cpu(), p_from, p_cnt)
+            if prev is not None:
+                bv, bf = torch.empty_like(a_pv), torch.empty_like(a_pf)
+                bv[p_order] = a_pv
+                bf[p_order] = a_pf
+                prev.copy_(bv.to(prev.device))
+                prev_found.copy_(bf.to(prev_found.device))

@@ -198,6 +198,39 @@ class DeviceReplica:
     def hm_prefill_range(self, n: int, off: int = 1):
         L.check(self._lib.nrg_hashmap_prefill_range(self._h, n, off), "prefill_range")
 
+    def hm_prefill_partition(self, n: int, off: int, part: int, parts: int):
+        """NrHashMap::default restricted to key partition `part` of `parts` (nrg_key_owner)."""
+        L.check(self._lib.nrg_hashmap_prefill_partition(self._h, n, off, part, parts), "prefill_partition")
+
+    def hm_partition_device(self, d_puts, W, d_keys, R, parts, d_puts_out, d_put_pos, d_keys_out, d_get_pos, d_counts):
+        """Stable partition of a round's Puts and Get keys by owner (nrg_hashmap_partition_async)."""
+        L.check(self._lib.nrg_hashmap_partition_async(self._h, _dptr(d_puts), W, _dptr(d_keys), R, parts,
+                                                      _dptr(d_puts_out), _dptr(d_put_pos), _dptr(d_keys_out),
+                                                      _dptr(d_get_pos), _dptr(d_counts)), "partition")
+
+    def route_back_device(self, d_src, d_src8, d_pos, n, d_dst, d_dst8):
+        L.check(self._lib.nrg_route_back_async(self._h, _dptr(d_src), _dptr(d_src8), _dptr(d_pos), n, _dptr(d_dst),
+                                               _dptr(d_dst8)), "route_back")
+
+    def partitioned_replay(self, puts, keys, want_prev: bool):
+        """One owner's share of a key-partitioned round (nrgpu.parallel.PartitionedHashMap): replay
+        the received Puts [p, 2] in the given (rank) order, answer the received Gets after them."""
+        import torch
+
+        dev = torch.device("cuda", self.device) if torch.cuda.is_available() else torch.device("cpu")
+        p = puts.reshape(-1, 2).to(dev).contiguous()
+        k = keys.reshape(-1).to(dev).contiguous()
+        n, r = p.shape[0], k.shape[0]
+        vals = torch.zeros(r, dtype=torch.int64, device=dev)
+        found = torch.zeros(r, dtype=torch.uint8, device=dev)
+        pv = torch.zeros(n, dtype=torch.int64, device=dev) if want_prev else None
+        pf = torch.zeros(n, dtype=torch.uint8, device=dev) if want_prev else None
+        self.use_torch_stream()
+        self.hm_round_device(p, n, int(self.cfg.replica_id) or 1, k, r, vals, found, pv, pf)
+        self.join()
+        torch.cuda.synchronize(dev)
+        return vals, found, pv, pf
+
     def hm_size(self) -> int:
         n = C.c_uint64()
         L.check(self._lib.nrg_hashmap_size(self._h, C.byref(n)))

@@ -11,6 +11,10 @@ digests are compared across ranks.
 --backend cpu : the replica is an oracle-backed test double (host logic only, runs anywhere)
 --backend gpu : the replica is nrgpu.DeviceReplica on cuda:0 (every rank shares the one GPU
                 of the box; the exchange still goes through gloo)
+--mode partitioned : cnr-style key partitions instead (nrgpu.parallel.PartitionedHashMap): rank
+                p holds only the keys it owns, Puts and Gets travel to their owners
+                (all_to_all_single), answers come back. Every answer must still equal the NR
+                replay of the global log, and the partitions' digests must add up to its digest.
 """
 import argparse
 import json
@@ -53,6 +57,29 @@ class OracleReplica:
         return tuple(self.m.digest())
 
 
+class OraclePartition:
+    """Test double for one key partition: partitioned_replay() as DeviceReplica's, on the oracle."""
+
+    def __init__(self, prefill, part, parts):
+        from nrgpu.parallel import key_owner
+
+        self.m = oracle.HashMap()
+        k = np.arange(prefill, dtype=np.uint64)
+        k = k[key_owner(k, parts) == part]
+        self.m.replay(k, k + np.uint64(1))  # NrHashMap::default restricted to the partition
+
+    def partitioned_replay(self, puts, keys, want_prev):
+        p = puts.reshape(-1, 2).numpy().view(np.uint64)
+        pv, pf = self.m.replay(p[:, 0].copy(), p[:, 1].copy())
+        v, f = self.m.get_batch(keys.numpy().view(np.uint64).copy())
+        return (torch.from_numpy(v.view(np.int64).copy()), torch.from_numpy(f.astype(np.uint8)),
+                torch.from_numpy(pv.view(np.int64).copy()) if want_prev else None,
+                torch.from_numpy(pf.astype(np.uint8)) if want_prev else None)
+
+    def hm_digest(self):
+        return tuple(self.m.digest())
+
+
 def segment(rank, rnd, span):
     W = 300 + 137 * rank + 61 * rnd  # ragged: ranks contribute different lengths each round
     if rnd == 1 and rank == 0:
@@ -72,11 +99,14 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--span", type=int, default=3000)
     ap.add_argument("--prefill", type=int, default=1000)
+    ap.add_argument("--mode", choices=["replicated", "partitioned"], default="replicated")
     a = ap.parse_args()
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     from nrgpu.parallel import ReplicatedHashMap
 
+    if a.mode == "partitioned":
+        return partitioned(a, rank, world)
     if a.backend == "gpu":
         import nrgpu
 
@@ -122,6 +152,59 @@ def main():
     dist.all_gather_object(digs, dig)
     ok &= all(d == digs[0] for d in digs)  # replicas_are_equal (nr/tests/stack.rs:434-489)
     print(json.dumps({"rank": rank, "ok": bool(ok), "digest": dig}), flush=True)
+    dist.destroy_process_group()
+    if a.backend == "gpu":
+        rep.close()
+    sys.exit(0 if ok else 1)
+
+
+def partitioned(a, rank, world):
+    from nrgpu.parallel import PartitionedHashMap
+
+    if a.backend == "gpu":
+        import nrgpu
+
+        dev_t = torch.device("cuda", 0)
+        torch.cuda.set_device(0)
+        rep = nrgpu.DeviceReplica(nrgpu._lib.NRG_DS_HASHMAP, 0, log2_slots=16, max_batch=1 << 14,
+                                  replica_id=rank + 1)
+        rep.hm_prefill_partition(a.prefill, 1, rank, world)
+    else:
+        dev_t = torch.device("cpu")
+        rep = OraclePartition(a.prefill, rank, world)
+    pm = PartitionedHashMap(rep)
+    model = oracle.HashMap()  # the NR replay of the global log
+    model.prefill_range(a.prefill, 1)
+    ok = True
+    for rnd in range(a.rounds):
+        k, v = segment(rank, rnd, a.span)
+        W = len(k)
+        puts = torch.from_numpy(np.stack([k, v], 1).view(np.int64).copy()).reshape(W, 2).to(dev_t)
+        gk = torch.from_numpy(reads(rank, rnd, a.span).view(np.int64).copy()).to(dev_t)
+        R = gk.shape[0]
+        gv = torch.full((R,), -1, dtype=torch.int64, device=dev_t)
+        gf = torch.full((R,), 7, dtype=torch.uint8, device=dev_t)
+        want = rnd != 1 or rank != 1  # a rank without previous values in round 1
+        pv = torch.full((W,), -1, dtype=torch.int64, device=dev_t) if want else None
+        pf = torch.full((W,), 7, dtype=torch.uint8, device=dev_t) if want else None
+        pm.round(puts, gk, gv, gf, pv, pf)
+        for r in range(world):
+            kr, vr = segment(r, rnd, a.span)
+            p, f = model.replay(kr, vr)
+            if r == rank and want:
+                ok &= np.array_equal(pv.cpu().numpy().view(np.uint64), p)
+                ok &= np.array_equal(pf.cpu().numpy(), f.astype(np.uint8))
+        ev, ef = model.get_batch(reads(rank, rnd, a.span))
+        ok &= np.array_equal(gv.cpu().numpy().view(np.uint64), ev)
+        ok &= np.array_equal(gf.cpu().numpy(), ef.astype(np.uint8))
+    dig = [int(x) for x in rep.hm_digest()]
+    digs = [None] * world
+    dist.all_gather_object(digs, dig)
+    total = [sum(d[0] for d in digs), sum(d[1] for d in digs) % (1 << 64), 0]
+    for d in digs:
+        total[2] ^= d[2]
+    ok &= total == [int(x) for x in model.digest()]  # the partitions add up to the NR replica
+    print(json.dumps({"rank": rank, "ok": bool(ok), "digest": total}), flush=True)
     dist.destroy_process_group()
     if a.backend == "gpu":
         rep.close()

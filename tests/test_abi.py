@@ -114,3 +114,26 @@ def test_group_api_argument_checks(lib):
     devs = (C.c_int * 1)(0)
     assert lib.nrg_group_open(devs, 0, C.byref(cfg), C.byref(out)) == L.NRG_E_INVAL
     assert lib.nrg_strerror(L.NRG_E_COMM).decode().startswith("RCCL")
+
+
+def test_key_owner_matches_the_python_mirror(lib):
+    """nrg_key_owner (the C ABI's partition function) == nrgpu.parallel.key_owner (numpy), and it
+    spreads keys evenly over the partitions (SURVEY.md §8 f4 routing)."""
+    import numpy as np
+
+    from nrgpu.parallel import key_owner
+
+    rng = np.random.default_rng(7)
+    keys = np.concatenate([np.arange(2000, dtype=np.uint64), rng.integers(0, 2**64 - 1, 3000, dtype=np.uint64),
+                           np.array([2**64 - 1, 2**63], dtype=np.uint64)])
+    for parts in (1, 2, 3, 7, 8, 64):
+        mine = key_owner(keys, parts)
+        theirs = [lib.nrg_key_owner(C.c_uint64(int(k)), parts) for k in keys]
+        assert mine.tolist() == theirs
+        assert mine.min() >= 0 and mine.max() < parts
+    counts = np.bincount(key_owner(np.arange(80000, dtype=np.uint64), 8), minlength=8)
+    assert counts.min() > 0.9 * 10000 and counts.max() < 1.1 * 10000
+    from nrgpu import _lib as L
+
+    assert lib.nrg_group_partitioned_round(None, None) == L.NRG_E_INVAL
+    assert lib.nrg_hashmap_partition_async(None, None, 0, None, 0, 2, None, None, None, None, None) == L.NRG_E_INVAL

@@ -49,6 +49,17 @@ def test_replicated_rounds_gloo_cpu(world):
     run_ranks(world, "cpu")
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_partitioned_rounds_gloo_cpu(world):
+    """cnr-style key partitions: answers equal the NR replay, partitions add up."""
+    run_ranks(world, "cpu", extra=("--mode", "partitioned", "--rounds", "4"))
+
+
+@pytest.mark.gpu
+def test_partitioned_rounds_gloo_gpu():
+    run_ranks(2, "gpu", timeout=110, extra=("--mode", "partitioned"))
+
+
 @pytest.mark.gpu
 def test_replicated_rounds_gloo_gpu():
     # two replicas (two processes) on the box's one GPU; exchange over gloo
