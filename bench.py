@@ -162,9 +162,10 @@ def traffic_key(args):
         return "stack_ops%d_init%d_n%d" % (args.ops_per_gpu, args.stack_init, int(os.environ.get("WORLD_SIZE", "1")))
     if args.workload == "synthetic":
         return "synthetic_ops%d_n%d" % (args.ops_per_gpu, int(os.environ.get("WORLD_SIZE", "1")))
-    return "w%d_ops%d_ks%d_pf%d_s%d_%s_n%d" % (args.write_ratio, args.ops_per_gpu, args.key_space, args.prefill,
-                                              args.log2_slots, key_dist_name(args),
-                                              int(os.environ.get("WORLD_SIZE", "1")))
+    return "w%d_ops%d_ks%d_pf%d_s%d_%s_n%d%s" % (args.write_ratio, args.ops_per_gpu, args.key_space, args.prefill,
+                                                args.log2_slots, key_dist_name(args),
+                                                int(os.environ.get("WORLD_SIZE", "1")),
+                                                "_part" if getattr(args, "partitioned", False) else "")
 
 
 def key_dist_name(args):
@@ -296,7 +297,10 @@ def run_hashmap(args, env):
     rep = nrgpu.DeviceReplica(L.NRG_DS_HASHMAP, env.local, log2_slots=args.log2_slots, max_batch=max(Wg, 1),
                               log_bytes=64 * 4 * max(Wg, 8192), replica_id=rank + 1, pipeline=args.pipeline)
     rep.use_torch_stream()
-    rep.hm_prefill_range(args.prefill, 1)
+    if args.partitioned:  # cnr-style: this rank holds only the keys it owns
+        rep.hm_prefill_partition(args.prefill, 1, rank, world)
+    else:
+        rep.hm_prefill_range(args.prefill, 1)
 
     # ---- inputs: a pool of distinct batches generated on device (seeds per rank/batch) ----
     P = max(1, min(args.pool, args.steps + args.warmup))
@@ -336,8 +340,15 @@ def run_hashmap(args, env):
     else:
         u_w = u_w_local
 
-    group = cgroup = None
-    if world > 1 and args.backend == "nccl":
+    group = cgroup = pgroup = None
+    if args.partitioned:
+        # Puts and Gets routed to their key's owner (RCCL send/recv in libnrgpu.so)
+        from nrgpu.parallel import PartitionedGroup
+
+        if args.backend != "nccl":
+            raise SystemExit("--partitioned needs --backend nccl (RCCL send/recv)")
+        pgroup = PartitionedGroup(rep, rank, world)
+    elif world > 1 and args.backend == "nccl":
         # the C ABI's replica group: RCCL all-gather on a library-owned stream, replay on ours
         from nrgpu.parallel import ReplicaGroup
 
@@ -360,7 +371,10 @@ def run_hashmap(args, env):
     def step(i):
         p = i % P
         prev = mode["prev"]
-        if cgroup is not None:
+        if pgroup is not None:
+            pp, gp = ptrs[p]
+            pgroup.round(pp, W, gp, R, gv_p, gf_p, pv_p if prev else None, pf_p if prev else None)
+        elif cgroup is not None:
             pp, gp = ptrs[p]
             cgroup.round_async(pp, W, pv_p if prev else None, pf_p if prev else None, gp, R, gv_p, gf_p)
         elif group is None:
@@ -419,14 +433,18 @@ def run_hashmap(args, env):
     dist_txt = ("uniform keys over %d" % args.key_space if args.dist == "uniform" else
                 "Zipf(theta=%g%s) keys over %d" % (args.theta, ", scrambled" if args.scramble else ", hot keys adjacent",
                                                    args.key_space))
-    res = common_fields(args, env, value, elapsed * 1e3 / args.steps, METRIC, "u64", {
+    metric = METRIC if not args.partitioned else (
+        "Mops/s whole node, NrHashMap key-partitioned rounds (cnr-style, SURVEY.md 8 f4; not the NR headline)")
+    res = common_fields(args, env, value, elapsed * 1e3 / args.steps, metric, "u64", {
         "workload": ("NrHashMap replica per GPU: 2^%d-slot table, %s, prefill [0,%d)->k+1, rounds of %d ops/GPU "
                      "= %d Put + %d Get%s" % (
                          args.log2_slots, dist_txt, args.prefill, args.ops_per_gpu, W, R,
                          "; write segments all-gathered (%s), every replica replays all %d Puts" % (
                              "RCCL over xGMI from libnrgpu.so's replica group" if args.backend == "nccl"
                              else "gloo rehearsal", Wg)
-                         if world > 1 else "")),
+                         if world > 1 and not args.partitioned else "") +
+                     ("; key-partitioned: rank p holds the keys with nrg_key_owner(k, %d) == p, Puts and Gets "
+                      "routed to their owners and answers back (RCCL send/recv)" % world if args.partitioned else "")),
         "baseline_config": "configs[1] (B1)" if (world == 1 and args.write_ratio == 10 and args.dist == "uniform")
         else ("configs[2] (B8 weak scaling)" if args.dist == "uniform" else "configs[3] (Z)"),
         "write_ratio_pct": args.write_ratio,
@@ -445,7 +463,7 @@ def run_hashmap(args, env):
     }
     if prev_value is not None:
         res["variants"] = {"prev_value_responses_Mops": round(prev_value, 3)}
-    if not args.no_cpu_baseline and world == 1 and args.dist == "uniform":
+    if not args.no_cpu_baseline and world == 1 and args.dist == "uniform" and not args.partitioned:
         log(f"cpu baseline: {args.cpu_seconds}s ...")
         try:
             res["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.write_ratio, args.key_space, args.prefill)
@@ -719,6 +737,8 @@ def main():
     ap.add_argument("--prefill", type=int, default=1 << 23)
     ap.add_argument("--log2-slots", type=int, default=26)
     ap.add_argument("--stack-init", type=int, default=50_000)
+    ap.add_argument("--partitioned", action="store_true",
+                    help="hashmap: cnr-style key-partitioned rounds (SURVEY.md 8 f4) instead of full replication")
     ap.add_argument("--pool", type=int, default=64, help="distinct pre-generated input batches")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
