@@ -539,6 +539,7 @@ struct ElectJob {
     u64* prev;     // previous-value responses for log indices [resp_lo, resp_hi)
     uint8_t* prevf;
     u32 exp;  // diagnostic knobs (NRG_EXP >> 8; wrong results): 1 counts only, 2 + pass 1 only, 4 no claims
+    u64* dbg; // NRG_EXP & 0x10000 (diagnostic): per block, thread 0's wall clock at the phase edges
 };
 
 constexpr int EL_HT = 2048;  // LDS hash entries (distinct keys of one part of a bucket)
@@ -546,24 +547,34 @@ constexpr int EL_CH = 2048;  // entries gathered per chunk
 constexpr int EL_PER = EL_CH / TPB;
 constexpr int EL_WIN = 4;    // steps of 64 entries loaded ahead by the log-order walk
 
-__device__ __forceinline__ u32 el_hash(u64 k) { return (u32)(mix64(k) >> 40) & (EL_HT - 1); }
+__device__ __forceinline__ u32 el_hash(u64 k, u32 ht) { return (u32)(mix64(k) >> 40) & (ht - 1); }
 
 template <bool PREV>
 __global__ __launch_bounds__(TPB) void hm_elect_kernel(ElectJob j) {
+    // Previous-value buckets are small (about 256 entries): a 1024-entry hash leaves LDS for the
+    // bucket's entries, staged in pass 1 for the log-order walk (no second gather).
+    constexpr int HT = PREV ? 1024 : EL_HT;
+    constexpr int ST = PREV ? 1024 : 1;  // staged entries
+    constexpr uint16_t NOH = 0xFFFFu;    // staged entry outside the current part
     extern __shared__ u32 s_dyn[];  // s_pre[nblocks + 1] entry prefix, s_off[nblocks] (u16)
-    __shared__ u64 s_hk[EL_HT];
-    __shared__ u32 s_hp[EL_HT + 1];  // largest bucket position + 1 of the key; [EL_HT]: side key
-    __shared__ u32 s_hs[EL_HT + 1];  // the key's slot (SIDE_ID, FULL_SLOT)
-    __shared__ u32 s_hf[EL_HT + 1];  // bit 0: new key (claim), bit 1: s_lv holds a value
-    __shared__ u64 s_lv[PREV ? EL_HT + 1 : 1];  // PREV: the key's value so far in the walk
-    __shared__ u64 s_mk[PREV ? EL_HT + 1 : 1];  // PREV: lanes of the current walk step per key
+    __shared__ u64 s_hk[HT];
+    __shared__ u32 s_hp[HT + 1];  // largest bucket position + 1 of the key; [HT]: side key
+    __shared__ u32 s_hs[HT + 1];  // the key's slot (SIDE_ID, FULL_SLOT)
+    __shared__ u32 s_hf[HT + 1];  // bit 0: new key (claim), bit 1: s_lv holds a value
+    __shared__ u64 s_lv[PREV ? HT + 1 : 1];  // PREV: the key's value so far in the walk
+    __shared__ u64 s_mk[PREV ? HT + 1 : 1];  // PREV: lanes of the current walk step per key
     __shared__ uint16_t s_tile[EL_CH];
+    __shared__ u64x2 s_sx[ST];      // PREV: the bucket's entries in log order (total <= ST)
+    __shared__ uint16_t s_sh[ST];   // their hash entries (NOH: not in this part)
     __shared__ u32 s_created;
     const u32 nblocks = j.nblocks;
     u32* s_pre = s_dyn;
     uint16_t* s_off = (uint16_t*)(s_dyn + nblocks + 1);
     const u32 b = blockIdx.x;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#define EL_MARK(K) \
+    if (j.dbg && threadIdx.x == 0) j.dbg[(u64)blockIdx.x * 16 + (K)] = wall_clock64()
+    EL_MARK(0);
     // this bucket's (offset, count) in every index tile; thread owns tiles [tid*K, tid*K + K)
     const u32 K = (nblocks + TPB - 1) / TPB;
     u32 loc = 0;
@@ -590,10 +601,11 @@ __global__ __launch_bounds__(TPB) void hm_elect_kernel(ElectJob j) {
         s_pre[nblocks] = total;
         s_created = 0;
     }
+    EL_MARK(1);
     if (total == 0 || (j.exp & 1)) return;  // uniform across the block
-    // parts = 2^lp id sub-ranges of the bucket, about <= EL_HT/2 entries each
+    // parts = 2^lp id sub-ranges of the bucket, about <= HT/2 entries each
     u32 lp = 0;
-    while ((total >> lp) > EL_HT / 2 && lp < j.bk_shift) lp++;
+    while ((total >> lp) > HT / 2 && lp < j.bk_shift) lp++;
     __syncthreads();
     // entry tile map of the chunk [base, base + EL_CH)
     auto fill_tiles = [&](u32 base) {
@@ -632,56 +644,82 @@ __global__ __launch_bounds__(TPB) void hm_elect_kernel(ElectJob j) {
         return (((id & ID_MASK) >> (j.bk_shift - lp)) & ((1u << lp) - 1)) == p;
     };
     auto lookup = [&](u64 k) -> u32 {  // hash entry of a key inserted by pass 1
-        if (k == EMPTY_KEY) return (u32)EL_HT;
-        u32 h = el_hash(k);
-        while (s_hk[h] != k) h = (h + 1) & (EL_HT - 1);
+        if (k == EMPTY_KEY) return (u32)HT;
+        u32 h = el_hash(k, HT);
+        while (s_hk[h] != k) h = (h + 1) & (HT - 1);
         return h;
     };
     const bool one_chunk = total <= (u32)EL_CH;
+    const bool staged = PREV && total <= (u32)ST;
     u32 created = 0;
     for (u32 p = 0; p < (1u << lp);) {
-        for (int q = threadIdx.x; q <= EL_HT; q += TPB) {
-            if (q < EL_HT) s_hk[q] = EMPTY_KEY;
+        for (int q = threadIdx.x; q <= HT; q += TPB) {
+            if (q < HT) s_hk[q] = EMPTY_KEY;
             s_hp[q] = 0;
             s_hf[q] = 0;
             if (PREV) s_mk[q] = 0;
         }
         __syncthreads();
-        // pass 1: one hash entry per key, its last writer, its slot or that it is new
+        // pass 1: one hash entry per key, its last writer, its slot or that it is new. With
+        // previous values, an existing key's value before the round is loaded here too (its
+        // slot is the entry's id), in flight while the hash is built.
         bool ovf = false;
         for (u32 base = 0; base < total; base += EL_CH) {
             if (!one_chunk || p == 0) load_chunk(base);
+            u64 ov[PREV ? EL_PER : 1];
+            if (PREV) {
+#pragma unroll
+                for (int r = 0; r < EL_PER; r++) {
+                    const u32 id = (u32)(x[r].x >> 32);
+                    ov[r] = ((u32)x[r].x != 0 && !(id & NEW_BIT) && id != SIDE_ID && in_part(id, p))
+                                ? j.table[id].val : 0ull;
+                }
+            }
 #pragma unroll
             for (int r = 0; r < EL_PER; r++) {
+                const u32 pos = base + r * TPB + threadIdx.x;
+                if (staged && pos < total) {
+                    s_sx[pos] = x[r];
+                    s_sh[pos] = NOH;
+                }
                 if ((u32)x[r].x == 0) continue;
                 const u32 id = (u32)(x[r].x >> 32);
                 if (!in_part(id, p)) continue;
                 const u64 k = xk[r];
                 u32 h;
                 if (k == EMPTY_KEY) {
-                    h = (u32)EL_HT;
+                    h = (u32)HT;
                 } else {
-                    h = el_hash(k);
+                    h = el_hash(k, HT);
                     int pr = 0;
-                    for (; pr < EL_HT; pr++) {
+                    for (; pr < HT; pr++) {
                         const u64 old = atomicCAS((unsigned long long*)&s_hk[h], (unsigned long long)EMPTY_KEY,
                                                   (unsigned long long)k);
                         if (old == EMPTY_KEY || old == k) break;
-                        h = (h + 1) & (EL_HT - 1);
+                        h = (h + 1) & (HT - 1);
                     }
-                    if (pr == EL_HT) {
+                    if (pr == HT) {
                         ovf = true;
                         continue;
                     }
                 }
                 atomicMax(&s_hp[h], base + r * TPB + threadIdx.x + 1);
-                if (id & NEW_BIT) atomicOr(&s_hf[h], 1u);
-                else s_hs[h] = id;  // the same slot for every entry of the key
+                if (staged) s_sh[pos] = (uint16_t)h;
+                if (id & NEW_BIT) {
+                    atomicOr(&s_hf[h], 1u);
+                } else {
+                    s_hs[h] = id;  // the same slot for every entry of the key
+                    if (PREV && id != SIDE_ID) {  // the same value too (nothing writes it yet)
+                        s_lv[h] = ov[r];
+                        atomicOr(&s_hf[h], 2u);
+                    }
+                }
             }
         }
         if (j.exp & 2) return;
+        EL_MARK(2);
         if (__syncthreads_or(ovf)) {  // more distinct keys than the table holds: finer parts
-            if (lp == j.bk_shift) {  // > EL_HT distinct new keys sharing one home slot
+            if (lp == j.bk_shift) {  // > HT distinct new keys sharing one home slot
                 if (threadIdx.x == 0) atomicOr(&j.ctl->err, ERR_TABLE_FULL);
                 break;
             }
@@ -689,10 +727,33 @@ __global__ __launch_bounds__(TPB) void hm_elect_kernel(ElectJob j) {
             p = 0;
             continue;
         }
-        // slots of new keys (claims); values before the round for the previous-value walk
-        for (int h = threadIdx.x; h <= EL_HT; h += TPB) {
-            if (!s_hp[h]) continue;
-            if (h == EL_HT) {
+        // slots of new keys (claims). A thread owns hash entries tid + q*TPB: all their home-slot
+        // loads are issued first, then all CASes on empty home slots, then the results are
+        // resolved (one or two memory round trips instead of one or two per entry).
+        constexpr int HQ = (HT + TPB) / TPB;  // entries per thread, the side entry included
+        u64 kh[HQ], cas[HQ];
+#pragma unroll
+        for (int q = 0; q < HQ; q++) {
+            const int h = threadIdx.x + q * TPB;
+            kh[q] = 0;
+            if (h >= HT || !s_hp[h]) continue;
+            if (s_hf[h] & 1u) {
+                if (!(j.exp & 4)) kh[q] = ld_relaxed(&j.table[table_home(s_hk[h], j.shift)].key);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < HQ; q++) {
+            const int h = threadIdx.x + q * TPB;
+            cas[q] = 0;
+            if (h < HT && s_hp[h] && (s_hf[h] & 1u) && !(j.exp & 4) && kh[q] == EMPTY_KEY)
+                cas[q] = atomicCAS((unsigned long long*)&j.table[table_home(s_hk[h], j.shift)].key,
+                                   (unsigned long long)EMPTY_KEY, (unsigned long long)s_hk[h]);
+        }
+#pragma unroll
+        for (int q = 0; q < HQ; q++) {
+            const int h = threadIdx.x + q * TPB;
+            if (h > HT || !s_hp[h]) continue;
+            if (h == HT) {
                 s_hs[h] = SIDE_ID;
                 const bool present = j.ctl->sp_claim != 0;
                 if (!present) {  // created by this round (no reads run beside the elector)
@@ -708,8 +769,17 @@ __global__ __launch_bounds__(TPB) void hm_elect_kernel(ElectJob j) {
                 s_hs[h] = FULL_SLOT;
             } else if (s_hf[h] & 1u) {
                 const u64 k = s_hk[h];
-                bool fresh;
-                const long long sl = claim_slot(j.table, k, table_home(k, j.shift), j.tmask, &fresh);
+                const u64 home = table_home(k, j.shift);
+                bool fresh = false;
+                long long sl;
+                if (kh[q] == EMPTY_KEY && cas[q] == EMPTY_KEY) {
+                    sl = (long long)home;
+                    fresh = true;
+                } else if (kh[q] == k || (kh[q] == EMPTY_KEY && cas[q] == k)) {
+                    sl = (long long)home;
+                } else {  // home slot holds another key: walk the probe chain from the next slot
+                    sl = claim_slot(j.table, k, (home + 1) & j.tmask, j.tmask, &fresh);
+                }
                 if (sl < 0) {
                     atomicOr(&j.ctl->err, ERR_TABLE_FULL);
                     s_hs[h] = FULL_SLOT;
@@ -722,12 +792,10 @@ __global__ __launch_bounds__(TPB) void hm_elect_kernel(ElectJob j) {
                         s_hf[h] |= 2u;
                     }
                 }
-            } else if (PREV) {
-                s_lv[h] = j.table[s_hs[h]].val;
-                s_hf[h] |= 2u;
-            }
+            }  // existing keys: slot and (previous values) value set in pass 1
         }
         __syncthreads();
+        EL_MARK(3);
         if (!PREV) {
             // pass 2: each key's last writer stores its value
             for (u32 base = 0; base < total; base += EL_CH) {
@@ -749,28 +817,39 @@ __global__ __launch_bounds__(TPB) void hm_elect_kernel(ElectJob j) {
             }
         } else {
             // pass 2 (previous values): wave 0 walks the bucket in log order, 64 entries a step
+            // (from the staged entries when the bucket fits, else gathered again)
             for (u32 base = 0; base < total; base += EL_CH) {
-                fill_tiles(base);
-                __syncthreads();
+                if (!staged) {
+                    fill_tiles(base);
+                    __syncthreads();
+                }
                 const u32 end = total < base + EL_CH ? total : base + EL_CH;
                 if (w == 0) {
                     for (u32 s0 = base; s0 < end; s0 += 64 * EL_WIN) {
                         u64x2 ex[EL_WIN];
                         u64 ek[EL_WIN];
+                        uint16_t eh[EL_WIN];
 #pragma unroll
                         for (int s = 0; s < EL_WIN; s++) {
                             const u32 pos = s0 + s * 64 + lane;
                             ex[s].x = 0;
+                            eh[s] = NOH;
                             if (pos < end) {
-                                const u64 e = ent_at(pos, base);
-                                ex[s] = j.ent[e];
-                                ek[s] = j.ekey[e];
+                                if (staged) {
+                                    ex[s] = s_sx[pos];
+                                    eh[s] = s_sh[pos];
+                                } else {
+                                    const u64 e = ent_at(pos, base);
+                                    ex[s] = j.ent[e];
+                                    ek[s] = j.ekey[e];
+                                }
                             }
                         }
 #pragma unroll
                         for (int s = 0; s < EL_WIN; s++) {
-                            const bool v = (u32)ex[s].x != 0 && in_part((u32)(ex[s].x >> 32), p);
-                            const u32 h = v ? lookup(ek[s]) : 0u;
+                            const bool v = staged ? eh[s] != NOH
+                                                  : (u32)ex[s].x != 0 && in_part((u32)(ex[s].x >> 32), p);
+                            const u32 h = !v ? 0u : staged ? (u32)eh[s] : lookup(ek[s]);
                             if (v) atomicOr((unsigned long long*)&s_mk[h], 1ull << lane);
                             const u64 m = v ? s_mk[h] : 0ull;
                             const u64 lower = m & ((1ull << lane) - 1);
@@ -802,8 +881,9 @@ __global__ __launch_bounds__(TPB) void hm_elect_kernel(ElectJob j) {
                 }
                 __syncthreads();
             }
+            EL_MARK(4);
             // every key's last value
-            for (int h = threadIdx.x; h <= EL_HT; h += TPB) {
+            for (int h = threadIdx.x; h <= HT; h += TPB) {
                 if (!s_hp[h]) continue;
                 const u32 sl = s_hs[h];
                 if (sl == SIDE_ID) {
@@ -819,6 +899,9 @@ __global__ __launch_bounds__(TPB) void hm_elect_kernel(ElectJob j) {
     if (created) atomicAdd(&s_created, created);
     __syncthreads();
     if (threadIdx.x == 0 && s_created) atomicAdd(&j.created_acc[b % HM_CREATED_SLOTS], (u64)s_created);
+    EL_MARK(5);
+    if (j.dbg && threadIdx.x == 0) j.dbg[(u64)blockIdx.x * 16 + 6] = total;
+#undef EL_MARK
 }
 
 __global__ __launch_bounds__(TPB) void hm_init_table_kernel(Slot* table, u64 slots) {
@@ -1254,7 +1337,8 @@ hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool
         ej.resp_hi = resp_hi;
         ej.prev = d_prev;
         ej.prevf = d_prev_found;
-        ej.exp = c->exp >> 8;
+        ej.exp = (c->exp >> 8) & 0xFF;
+        ej.dbg = (c->exp & 0x10000) ? c->d_dbg : nullptr;
         const unsigned dyn = (ij.nblocks + 1) * 4 + ij.nblocks * 2;
         if (want_prev) NRG_LAUNCH(c, "hm_elect", hm_elect_kernel<true>, 1u << nb_log, TPB, dyn, c->stream, ej);
         else NRG_LAUNCH(c, "hm_elect", hm_elect_kernel<false>, 1u << nb_log, TPB, dyn, c->stream, ej);

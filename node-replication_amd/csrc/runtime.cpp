@@ -350,6 +350,7 @@ int nrg_open(int dev, const nrg_config* cfg_in, nrg_ctx** out) {
         if (const char* e = std::getenv("NRG_K1")) c->k1_items = (uint32_t)std::atoi(e);
         if (const char* e = std::getenv("NRG_BK_ENT")) c->bk_ent = (uint32_t)std::atoi(e);
         if (const char* e = std::getenv("NRG_EXP")) c->exp = (uint32_t)std::atoi(e);
+        if (c->exp & 0x10000) OPEN_CHK(hipMalloc(&c->d_dbg, HM_BK_MAX * 16 * sizeof(uint64_t)));
         c->pipeline = cf.pipeline != 0;
         if (const char* e = std::getenv("NRG_PIPELINE")) c->pipeline = std::atoi(e) != 0;
     } else if (cf.ds_kind == NRG_DS_STACK) {
