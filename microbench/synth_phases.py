@@ -29,8 +29,8 @@ ops[:, 3] = 1
 resp = torch.empty(N, dtype=torch.int64, device="cuda")
 some = torch.empty(N, dtype=torch.uint8, device="cuda")
 SPAN = 200_000 - 2  # hot_reads = 2
-W = -(-SPAN // 512)
-NB = -(-SPAN // W)
+W = -(-(SPAN - 1) // 511)
+NB = 1 + -(-(SPAN - 1) // W)  # bucket 0: cold word 0 alone
 R = 20
 acc = np.zeros((NB, 9))
 hw = None

@@ -232,11 +232,14 @@ constexpr u32 SYB_PASS = SYB_TPB * SYB_PER;  // touches per pass of a bucket wor
 constexpr int SYC_TPB = 512;
 constexpr u32 NOTOUCH = 0xFFFFFFFFu;
 
-// Cold word x (relative to hot_reads) lives in bucket x / W, W = ceil(span / 512): ~512 buckets,
-// so the bucket kernel's workgroups spread evenly over the 256 CUs (2 per CU) instead of a
-// power-of-two bucket size leaving some CUs one workgroup and others two. The division is
+// Buckets of cold words (x relative to hot_reads). Cold word 0 has bucket 0 to itself: an op's
+// cold touches start at r1 * tid, so every op of core tid 0 touches cold word 0
+// (benches/synthetic.rs:165-171) -- 1/64 of all ops on one word, which as part of an ordinary
+// bucket made it 2.5x the mean and the kernel's straggler. Words 1.. go to buckets 1.. of
+// W = ceil((span - 1) / 511) words: 512 buckets, 2 workgroups per CU. The division is
 // (x * ceil(2^40 / W)) >> 40, exact for x < 2^31 and W <= 512.
-__device__ __forceinline__ u32 bucket_of(u32 x, u64 wm) { return (u32)(((u64)x * wm) >> 40); }
+__device__ __forceinline__ u32 bucket_of(u32 x, u64 wm) { return x ? 1u + (u32)(((u64)(x - 1) * wm) >> 40) : 0u; }
+__device__ __forceinline__ u32 word_in_bucket(u32 x, u32 b, u32 W) { return x ? (x - 1) - (b - 1) * W : 0u; }
 
 // A cold touch in the tile layout, 4 bytes: word within its bucket (9 bits), SET (1), cold
 // index k (3), op within its tile (11). The bucket and tile are implied by the position.
@@ -441,7 +444,7 @@ __global__ __launch_bounds__(SYA_TPB) void sy_part_kernel(const nrg_synth_op* __
             const u32 p = pk[orr * CW + r];
             const u32 t = r * 64 + lane;
             const u32 opl = (u32)(w * SYA_OROUNDS + orr) * 64 + t / CW;
-            const u32 xl = (v & ~SETBIT) - HR - (p >> 16) * W;
+            const u32 xl = word_in_bucket((v & ~SETBIT) - HR, p >> 16, W);
             s_u.stage[s_wcnt[w][p >> 16] + (p & 0xFFFFu)] = ent_make(xl, (v & SETBIT) != 0, t % CW, opl);
         }
     }
@@ -455,7 +458,8 @@ __global__ __launch_bounds__(SYA_TPB) void sy_part_kernel(const nrg_synth_op* __
 // w-th contiguous SYB_PER rounds of 64: wave-private per-word counts rank the wave's
 // touches without barriers, then per-word prefixes over the waves place them. A pass with a
 // WriteOnly in it is applied wave by wave instead (values depend on the last SET).
-__global__ __launch_bounds__(SYB_TPB) void sy_bucket_kernel(const u32* __restrict__ E, const u32* __restrict__ cnt_bt,
+// (<= 128 VGPRs: two 8-wave workgroups per CU)
+__global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) void sy_bucket_kernel(const u32* __restrict__ E, const u32* __restrict__ cnt_bt,
                                                             u32 ntiles, u32 tile_entries, u64* __restrict__ V,
                                                             u64* __restrict__ words, u64 N, u32 HR, u32 W,
                                                             const nrg_synth_op* __restrict__ ring, u64 ring_mask, u64 lo,
@@ -483,13 +487,14 @@ __global__ __launch_bounds__(SYB_TPB) void sy_bucket_kernel(const u32* __restric
     unsigned short* s_off = (unsigned short*)(s_dyn + ntiles + 1);
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const u32 b = blockIdx.x;
-    const u64 w0 = (u64)HR + (u64)b * W;
+    const u64 w0 = b ? (u64)HR + 1 + (u64)(b - 1) * W : (u64)HR;  // bucket 0: cold word 0 alone
+    const u32 nw = b ? W : 1u;
     for (u32 t = tid; t < ntiles; t += SYB_TPB) {
         const u32 p = cnt_bt[(u64)b * ntiles + t];
         s_off[t] = (unsigned short)(p >> 16);
         s_pre[t] = p & 0xFFFFu;
     }
-    for (u32 i = tid; i < SYB_WORDS; i += SYB_TPB) s_cur[i] = i < W && w0 + i < N ? words[w0 + i] : 0ull;
+    for (u32 i = tid; i < SYB_WORDS; i += SYB_TPB) s_cur[i] = i < nw && w0 + i < N ? words[w0 + i] : 0ull;
     for (u32 i = tid; i < SYB_WAVES * SYB_WORDS; i += SYB_TPB) {
         (&s_wc[0][0])[i] = 0;
         (&s_mk[0][0])[i] = 0;
@@ -571,11 +576,19 @@ __global__ __launch_bounds__(SYB_TPB) void sy_bucket_kernel(const u32* __restric
         if (nb < total) load_pass(nb, s_tile[pb ^ 1]);
         SY_ACC(0);
         if (!anyset) {
+            if (b == 0) {  // one word: a touch's rank in its wave is its position there
+                const u32 w0i = base + (u32)w * (SYB_PER * 64);
 #pragma unroll
-            for (int q = 0; q < SYB_PER; q++) {
-                const u32 i = base + (u32)w * (SYB_PER * 64) + q * 64 + lane;
-                u64 peers;
-                sv[q] = wave_rank(i < total, ent_word(ent[q]), lane, s_mk[w], s_wc[w], &peers);
+                for (int q = 0; q < SYB_PER; q++) sv[q] = (u64)(q * 64 + lane);
+                if (lane == 0)
+                    s_wc[w][0] = total > w0i ? (total - w0i < SYB_PER * 64 ? total - w0i : SYB_PER * 64) : 0u;
+            } else {
+#pragma unroll
+                for (int q = 0; q < SYB_PER; q++) {
+                    const u32 i = base + (u32)w * (SYB_PER * 64) + q * 64 + lane;
+                    u64 peers;
+                    sv[q] = wave_rank(i < total, ent_word(ent[q]), lane, s_mk[w], s_wc[w], &peers);
+                }
             }
             __syncthreads();
             u64 totw = 0;
@@ -642,7 +655,7 @@ __global__ __launch_bounds__(SYB_TPB) void sy_bucket_kernel(const u32* __restric
         SY_ACC(3);
     }
     __syncthreads();
-    for (u32 i = tid; i < W; i += SYB_TPB)
+    for (u32 i = tid; i < nw; i += SYB_TPB)
         if (w0 + i < N) words[w0 + i] = s_cur[i];
     if (dbg && threadIdx.x == 0) {
         for (int k = 0; k < 4; k++) dbg[(u64)blockIdx.x * 16 + 3 + k] = tm_acc[k];
@@ -711,13 +724,13 @@ __global__ __launch_bounds__(SYC_TPB) void sy_sum_kernel(const u32* __restrict__
 bool sy_bucket_eligible(const nrg_config& cf) {
     const u64 span = cf.synth_n - cf.synth_hot_reads;
     return cf.synth_cold_writes >= 1 && cf.synth_cold_writes <= SY_MAX_CW && cf.synth_hot_reads <= SY_MAX_HOT &&
-           span <= (u64)SY_MAX_NB * SYB_WORDS && cf.max_batch <= (u64)SY_MAX_TILES * SYA_OPS;
+           span <= 1 + (u64)(SY_MAX_NB - 1) * SYB_WORDS && cf.max_batch <= (u64)SY_MAX_TILES * SYA_OPS;
 }
 
 u64 sy_bucket_aux_bytes(const nrg_config& cf) {
     const u64 span = cf.synth_n - cf.synth_hot_reads;
-    const u64 W = (span + SY_MAX_NB - 1) / SY_MAX_NB;
-    const u64 NB = (span + W - 1) / W;
+    const u64 W = span > 1 ? (span - 1 + SY_MAX_NB - 2) / (SY_MAX_NB - 1) : 1;
+    const u64 NB = 1 + (span - 1 + W - 1) / W;
     const u64 tiles = (cf.max_batch + SYA_OPS - 1) / SYA_OPS;
     return tiles * SYA_OPS * cf.synth_cold_writes * 12 + NB * tiles * 4 + tiles * cf.synth_hot_reads * sizeof(SyHot) +
            256;
@@ -729,8 +742,9 @@ static hipError_t sy_bucket_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 re
     const nrg_config& cf = c->cfg;
     const u32 HW = cf.synth_hot_writes, CW = cf.synth_cold_writes, HR = cf.synth_hot_reads;
     const u64 span = cf.synth_n - HR;
-    const u32 W = (u32)((span + SY_MAX_NB - 1) / SY_MAX_NB);  // words per bucket, <= 512
-    const u32 NB = (u32)((span + W - 1) / W);
+    // bucket 0: cold word 0 alone; buckets 1..: W words each (<= 512, sy_bucket_eligible)
+    const u32 W = span > 1 ? (u32)((span - 1 + SY_MAX_NB - 2) / (SY_MAX_NB - 1)) : 1u;
+    const u32 NB = 1 + (u32)((span - 1 + W - 1) / W);
     const u64 wm = ((1ull << 40) + W - 1) / W;
     const u64 span_m = ~0ull / span, hr_m = ~0ull / HR;
     const u32 ntiles = (u32)((n + SYA_OPS - 1) / SYA_OPS);
