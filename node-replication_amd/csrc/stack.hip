@@ -29,10 +29,13 @@
 
 namespace nrg {
 
-constexpr int ST_TPB = 256;
-constexpr int ST_ITEMS = 8;
-constexpr int ST_TILE = ST_TPB * ST_ITEMS;  // 2048 ops: positions and relative slots fit 11 bits
-constexpr uint16_t ST_NO_PUSH = 0xFFFFu;
+constexpr int SW_OPS = 32;                  // ops per lane, replayed in order by that lane
+constexpr int ST_WAVES = 4;                 // a tile is one workgroup of 4 waves
+constexpr int ST_LANES = 64 * ST_WAVES;     // 256 lanes
+constexpr int ST_TILE = ST_LANES * SW_OPS;  // 8192 ops
+constexpr int ST_PB = 13;                   // bits of a position in the tile
+constexpr u32 ST_PMASK = (1u << ST_PB) - 1;
+static_assert(ST_TILE == 1 << ST_PB, "positions");
 
 struct Fn {
     long long b;
@@ -90,360 +93,433 @@ struct StTiles {
     u32* table;        // [tiles][ST_TILE] value of the tile's last Push to slot tmin + r, for the
                        // slots below the tile's end depth (the only ones ever looked up)
     u32* ucnt;         // [tiles] Pops whose Push is outside the tile
-    u32* upop;         // [tiles][ST_TILE] those Pops: (slot - tmin) << 11 | position
+    u32* upop;         // [tiles][ST_TILE] those Pops: (slot - tmin) << ST_PB | position
     u32* uval;         // [tiles][ST_TILE] their slot's content before the chunk (if below it)
 };
 
-__device__ __forceinline__ long long block_min4(long long x, long long* s_w, int w, int lane) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        const long long o = __shfl_xor(x, off, 64);
-        x = o < x ? o : x;
-    }
-    if (lane == 0) s_w[w] = x;
-    __syncthreads();
-    long long m = s_w[0];
-    for (int i = 1; i < 4; i++) m = s_w[i] < m ? s_w[i] : m;
-    return m;
+__device__ __forceinline__ void wave_sync() {  // LDS written by other lanes of this wave
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-constexpr u32 ST_INF = 0xFFFFu;
+// (m, e) of a clamped ±1 walk: unclamped minimum m <= 0 and end e; from start x it ends at
+// max(x + e, e - m). Composition, f then g: (min(m_f, e_f + m_g), e_f + e_g).
+__device__ __forceinline__ void me_then(int& m, int& e, int m2, int e2) {
+    const int t = e + m2;
+    m = m < t ? m : t;
+    e += e2;
+}
 
-// src: the chunk's records in a caller buffer (nrg_stack_round_async); the kernel then writes
-// the log copy itself (Log::append fused into the replay). nullptr: records are in the ring.
-__global__ __launch_bounds__(ST_TPB) void st_tile_kernel(const nrg_stack_op* __restrict__ src, nrg_stack_op* ring,
-                                                         u64 ring_mask, u64 lo,
-                                                         u64 n, DevCtl* ctl, u64* desc, u32* ticket, StTiles tl,
-                                                         const u32* __restrict__ stack,
-                                                         u64 cap, u64 resp_lo, u64 resp_hi, int push_resp,
-                                                         u32* __restrict__ resp, uint8_t* __restrict__ some, u32 exp,
-                                                         u64* __restrict__ dbg) {
-#define ST_MARK(K) \
-    if (dbg && threadIdx.x == 0) dbg[(u64)blockIdx.x * 16 + (K)] = wall_clock64()
-    ST_MARK(0);
-    __shared__ long long s_wb[4], s_wa[4], s_wmin[4];
-    __shared__ u32 s_tile, s_ucnt, s_aend;
-    __shared__ long long s_dbase;
-    __shared__ u32 s_val[ST_TILE];             // op values by position
-    __shared__ uint16_t s_A[ST_TILE + 1];      // depth after op i (- tmin) at [i + 1]; [0] = start
-    // sparse min table over the threads' minima: s_sp[j][k] = min of threads (k - 2^j, k]
-    __shared__ uint16_t s_sp[9][ST_TPB];
-    __shared__ uint16_t s_sw[4];               // per wave: minimum of its threads
-    __shared__ uint16_t s_tab[ST_TILE];        // last Push position per relative slot
-    __shared__ u32 s_q[4][ST_ITEMS * 64];      // per wave: Pops answered beyond their thread
-    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
-    if (t == 0) {
-        s_tile = (exp & 1) ? blockIdx.x : atomicAdd(ticket, 1u);  // exp 1: diagnostic only
-        s_ucnt = 0;
-    }
-    __syncthreads();
-    ST_MARK(1);
-    const u32 tile = s_tile;
+// One workgroup per 8192-op tile; lane t of its 256 replays ops [32 t, 32 t + 32) in order.
+//   1. Local pass: every lane keeps its own stack in LDS (row = height, column = lane, so the
+//      64 lanes of a wave never share a bank). A Pop with a non-empty local stack returns its
+//      top; a Pop on an empty local stack is "unmatched" (it reaches below the lane's start).
+//      Nothing here depends on the lane's start depth: the lane leaves `nun` unmatched Pops and
+//      a residual stack of `top` Pushes, i.e. the map (m, e) = (-nun, top - nun).
+//   2. Scan of the lanes' (m, e) (waves, then the 4 wave totals in LDS); the tile's aggregate
+//      is published at once for later tiles' look-back.
+//   3. Look-back (wave 0): lane l composes a run of earlier tiles' aggregates, one wave
+//      composition joins the runs -> the tile's start depth D, hence each lane's start depth
+//      D_t, its lowest level amin_t = max(D_t - nun, 0) and its end aend_t = amin_t + top. The
+//      lane's residual Push i sits at level amin_t + i.
+//   4. The k-th unmatched Pop of lane t (k < min(nun, D_t); the others find the stack empty)
+//      reads level L = D_t - 1 - k, written last by the nearest earlier lane v with
+//      amin_v <= L (every lane in between stays above L): residual entry L - amin_v of lane v.
+//      Each wave lists its unmatched Pops and answers them one per lane per round by greedy
+//      skips over a sparse table of lane minima (256 lanes: 8 levels). With no such lane the
+//      Push is in an earlier tile (or before the chunk): the Pop goes to st_finish_kernel's
+//      list with the slot's pre-chunk content.
+//   5. Table: level L of [tmin, tile end) is last pushed by the LAST lane with amin <= L, so
+//      lane t writes the levels [amin_t, min(aend_t, min of later lanes' amin)) of its
+//      residual stack -- exactly one writer per level.
+// Tile order is blockIdx order: the look-back waits only on lower workgroups, which the
+// in-order dispatcher has already placed (a bounded spin latches ERR_CAPACITY instead of
+// hanging). src: the chunk's records in a caller buffer (nrg_stack_round_async); the kernel
+// then writes the log copy itself (Log::append fused). nullptr: records are in the ring.
+__global__ __launch_bounds__(ST_LANES) void st_tile_kernel(const nrg_stack_op* __restrict__ src, nrg_stack_op* ring,
+                                                          u64 ring_mask, u64 lo, u64 n, DevCtl* ctl, u64* desc,
+                                                          StTiles tl, const u32* __restrict__ stack, u64 cap,
+                                                          u64 resp_lo, u64 resp_hi, int push_resp,
+                                                          u32* __restrict__ resp, uint8_t* __restrict__ some,
+                                                          u64* __restrict__ dbg) {
+    const int t = threadIdx.x, wv = t >> 6, lane = t & 63;
+    const u32 tile = blockIdx.x;
     const u64 tbase = (u64)tile * ST_TILE;
-    const u64 base = tbase + (u64)t * ST_ITEMS;
-    const long long d0 = ctl->depth;  // depth before the chunk (st_commit_kernel updates it)
+    const u64 wbase = tbase + (u64)wv * (64 * SW_OPS);  // the wave's 2048 ops
+    const u64 base = tbase + (u64)t * SW_OPS;           // the lane's 32 ops
+    const bool full = base + SW_OPS <= n;
+#define ST_MARK(K) \
+    if (dbg && t == 0) dbg[(u64)tile * 16 + (K)] = wall_clock64()
+    ST_MARK(0);
+    // per wave: the lane stacks (rows of 64 lanes; row SW_OPS absorbs non-Push writes) followed
+    // by the wave's query list; the first 16 KB also stage the wave's ops on their way in
+    constexpr int W_STK = (SW_OPS + 1) * 64, W_UP = 64 * SW_OPS;
+    static_assert(W_STK + W_UP >= 2 * 64 * SW_OPS, "staging fits");
+    __shared__ __attribute__((aligned(16))) u32 s_wave[ST_WAVES][W_STK + W_UP];
+    __shared__ int s_min[ST_LANES];     // lane minimum level - tile minimum
+    __shared__ int s_sp[8][ST_LANES];   // s_sp[j][v] = min of s_min over lanes (v - 2^j, v]
+    __shared__ int s_suf[ST_LANES];     // inclusive suffix minimum of s_min inside the wave
+    __shared__ int s_wm[ST_WAVES], s_we[ST_WAVES], s_wmin[ST_WAVES];
+    __shared__ u32 s_pre[ST_LANES];     // pre-chunk content of levels T0 + [0, 256)
+    __shared__ long long s_D;
+    __shared__ u32 s_ucnt;
+    u32 (*s_stk)[64] = reinterpret_cast<u32 (*)[64]>(s_wave[wv]);
+    u32* s_up = s_wave[wv] + W_STK;
+    if (t == 0) s_ucnt = 0;
 
-    nrg_stack_op ops[ST_ITEMS];
-    Fn agg = {0, 0};
+    // ---- load the lane's 32 ops (and write the log copy when they come from the caller) ----
+    u32 val[SW_OPS];
+    u32 pm = 0, qm = 0;  // Push / Pop bit per op (padding past n is neither)
+    {
+        const u64 rw0 = (lo + wbase) & ring_mask;
+        const bool ring_run = rw0 + 64 * SW_OPS <= ring_mask + 1 && !(rw0 & 1);  // contiguous, 16-B aligned
+        const nrg_stack_op* wp = src ? src + wbase : ring + rw0;
+        const bool vec = wbase + 64 * SW_OPS <= n && (src ? !((uintptr_t)wp & 15) : ring_run);  // wave-uniform
+        if (vec) {
+            // coalesced: 16-B unit u = 64 i + lane of the wave's ops (two ops), then through LDS
+            // to the lane that replays it (row u / 16, column (u % 16) ^ (row % 16): no conflicts)
+            const uint4* p4 = (const uint4*)wp;
+            uint4 x[SW_OPS / 2];
 #pragma unroll
-    for (int q = 0; q < ST_ITEMS; q++) {
-        const u64 i = base + q;
-        if (i < n) {
-            ops[q] = src ? src[i] : ring[(lo + i) & ring_mask];
-            Fn f;
-            f.b = ops[q].op ? 1 : -1;
-            f.a = ops[q].op ? 1 : 0;
-            agg = fn_then(agg, f);
+            for (int i = 0; i < SW_OPS / 2; i++) x[i] = p4[64 * i + lane];
+            if (src) {
+                if (ring_run) {
+                    uint4* w4 = (uint4*)(ring + rw0);
+#pragma unroll
+                    for (int i = 0; i < SW_OPS / 2; i++) w4[64 * i + lane] = x[i];
+                } else {
+#pragma unroll
+                    for (int i = 0; i < SW_OPS / 2; i++) {
+                        const u64 o = lo + wbase + 2 * (64 * i + lane);
+                        ring[o & ring_mask] = nrg_stack_op{x[i].x, x[i].y};
+                        ring[(o + 1) & ring_mask] = nrg_stack_op{x[i].z, x[i].w};
+                    }
+                }
+            }
+            uint4* s4 = reinterpret_cast<uint4*>(s_wave[wv]);
+#pragma unroll
+            for (int i = 0; i < SW_OPS / 2; i++) {
+                const int u = 64 * i + lane, r = u >> 4;
+                s4[r * 16 + ((u & 15) ^ (r & 15))] = x[i];
+            }
+            wave_sync();
+#pragma unroll
+            for (int j = 0; j < SW_OPS / 2; j++) {
+                const uint4 y = s4[lane * 16 + (j ^ (lane & 15))];
+                val[2 * j] = y.x;
+                val[2 * j + 1] = y.z;
+                pm |= (u32)(y.y != 0) << (2 * j) | (u32)(y.w != 0) << (2 * j + 1);
+                qm |= (u32)(y.y == 0) << (2 * j) | (u32)(y.w == 0) << (2 * j + 1);
+            }
+            wave_sync();  // the staging rows become the lane stacks
         } else {
-            ops[q].op = 2;  // padding
-            ops[q].val = 0;
+            // partial last tile, a ring wrap or an unaligned caller buffer: one op at a time,
+            // staged through the (not yet used) stack rows so that val[] keeps static indices
+            for (int q = 0; q < SW_OPS; q++) {
+                const u64 i = base + q;
+                u32 v = 0;
+                if (i < n) {
+                    const nrg_stack_op o = src ? src[i] : ring[(lo + i) & ring_mask];
+                    if (src) ring[(lo + i) & ring_mask] = o;
+                    v = o.val;
+                    pm |= (u32)(o.op != 0) << q;
+                    qm |= (u32)(o.op == 0) << q;
+                }
+                s_stk[q][lane] = v;
+            }
+#pragma unroll
+            for (int q = 0; q < SW_OPS; q++) val[q] = s_stk[q][lane];
+            wave_sync();
         }
     }
-    if (src) {  // the log copy, lane-contiguous (the loads above are 8 records per thread)
-        for (u32 k = t; k < ST_TILE; k += ST_TPB) {
-            const u64 i = tbase + k;
-            if (i < n) ring[(lo + i) & ring_mask] = src[i];
-        }
+    ST_MARK(1);
+
+    // ---- 1. local pass (branch-free: no per-op lane masks held in SGPRs) ----
+    u32 rt[SW_OPS];  // what each Pop read from the local stack (valid for matched Pops)
+    u32 top = 0, nun = 0, umask = 0, topmax = 0;
+    int hmax = 0;
+#pragma unroll
+    for (int q = 0; q < SW_OPS; q++) {
+        const u32 pu = (pm >> q) & 1u, po = (qm >> q) & 1u;
+        s_stk[SW_OPS + pu * (top - SW_OPS)][lane] = val[q];
+        rt[q] = s_stk[min(top - 1u, (u32)SW_OPS)][lane];
+        const u32 un = (u32)max((int)po - (int)top, 0);  // a Pop on the empty local stack
+        umask |= un << q;
+        nun += un;
+        top = top + pu - po + un;
+        topmax = max(topmax, top);
+        hmax = max(hmax, (int)top - (int)nun);
     }
-    // wave inclusive scan of thread aggregates (order matters)
-    Fn inc = agg;
+    // fold the known responses into rt[] (val[] dies here): Push -> its value if Push answers
+    // Some, matched Pop -> what it read, everything else None (unmatched Pops are patched later)
+    const u32 smask = (push_resp ? pm : 0u) | (qm & ~umask);
+#pragma unroll
+    for (int q = 0; q < SW_OPS; q++) {
+        const u32 pq = (u32)__builtin_amdgcn_sbfe((int)pm, q, 1);
+        rt[q] = ((val[q] & pq) | (rt[q] & ~pq)) & (u32)__builtin_amdgcn_sbfe((int)smask, q, 1);
+    }
+    ST_MARK(2);
+
+    // ---- 2. scan of (m, e): inclusive over the wave, then the wave totals ----
+    int im = -(int)nun, ie = (int)top - (int)nun;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
-        Fn o;
-        o.b = __shfl_up(inc.b, off, 64);
-        o.a = __shfl_up(inc.a, off, 64);
-        if (lane >= off) inc = fn_then(o, inc);
+        const int om = __shfl_up(im, off, 64), oe = __shfl_up(ie, off, 64);
+        if (lane >= off) {
+            int m = om, e = oe;
+            me_then(m, e, im, ie);
+            im = m;
+            ie = e;
+        }
     }
     if (lane == 63) {
-        s_wb[w] = inc.b;
-        s_wa[w] = inc.a;
+        s_wm[wv] = im;
+        s_we[wv] = ie;
     }
-    // exclusive within wave
-    Fn ex;
-    ex.b = __shfl_up(inc.b, 1, 64);
-    ex.a = __shfl_up(inc.a, 1, 64);
-    if (lane == 0) ex = Fn{0, 0};
+    int xm = __shfl_up(im, 1, 64), xe = __shfl_up(ie, 1, 64);  // exclusive within the wave
+    if (lane == 0) xm = xe = 0;
     __syncthreads();
-    Fn wpre = {0, 0};
-    for (int i = 0; i < w; i++) wpre = fn_then(wpre, Fn{s_wb[i], s_wa[i]});
-    ST_MARK(2);
-    const Fn tpre = fn_then(wpre, ex);
-    Fn tagg = {0, 0};
-    for (int i = 0; i < 4; i++) tagg = fn_then(tagg, Fn{s_wb[i], s_wa[i]});
+    int M = 0, E = 0, pmw = 0, pew = 0;  // tile aggregate; prefix of the earlier waves
+#pragma unroll
+    for (int w = 0; w < ST_WAVES; w++) {
+        if (w == wv) {
+            pmw = M;
+            pew = E;
+        }
+        me_then(M, E, s_wm[w], s_we[w]);
+    }
+    me_then(pmw, pew, xm, xe);  // the lane's exclusive prefix within the tile
+    xm = pmw;
+    xe = pew;
+    const Fn tagg = {E, E - M};  // max(a, x + b) form for the look-back
     if (t == 0) __hip_atomic_store(&desc[tile], pack_agg(tagg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
-    // Pass 0 pairs the tile speculatively on the UNCLAMPED walk relative to the tile's start:
-    // Push/Pop pairing depends only on relative depths, and it is the real pairing unless the
-    // stack runs empty inside the tile (a Pop at depth 0 is a no-op). Whether it does needs the
-    // tile's start depth, i.e. the look-back, which therefore runs after pass 0 and finds its
-    // predecessors' aggregates already published. Pass 1 (a stack within 2048 of empty) redoes
-    // the pairing on the clamped walk from the known start depth.
-    long long dstart = tpre.b;
-    bool clamp = false;
-    long long tmin = 0;   // minimum of the walk, start and end included (pass 0: relative)
-    u32 a[ST_ITEMS];      // depth after each of this thread's ops - tmin
-    u32 astart = 0;       // depth before this thread's first op - tmin
-    u32 rv[ST_ITEMS];     // response per op:
-    uint8_t rk[ST_ITEMS]; //   0 none (padding, or queued below), 1 Some(rv), 2 None
-    u32 qe[ST_ITEMS], qv[ST_ITEMS];  // queued Pops this lane resolved: entry and value,
-    bool qx[ST_ITEMS];               //   or outside the tile (qx)
-    u32 qn = 0;                      // wave-uniform queue length
-    for (int pass = 0;; pass++) {
-        long long dd = dstart, dmin = dd;
-#pragma unroll
-        for (int q = 0; q < ST_ITEMS; q++) {
-            if (ops[q].op == 1) dd += 1;
-            else if (ops[q].op == 0 && (!clamp || dd > 0)) dd -= 1;
-            dmin = dd < dmin ? dd : dmin;
-        }
-        tmin = block_min4(dmin, s_wmin, w, lane);
-        ST_MARK(3);
-        u32 amin = ST_INF;
-        dd = dstart;
-#pragma unroll
-        for (int q = 0; q < ST_ITEMS; q++) {
-            if (ops[q].op == 1) dd += 1;
-            else if (ops[q].op == 0 && (!clamp || dd > 0)) dd -= 1;
-            a[q] = (u32)(dd - tmin);
-            amin = a[q] < amin ? a[q] : amin;
-            s_A[t * ST_ITEMS + q + 1] = (uint16_t)a[q];
-            s_val[t * ST_ITEMS + q] = ops[q].val;
-        }
-        astart = (u32)(dstart - tmin);
-        if (t == 0) s_A[0] = (uint16_t)astart;
-        s_sp[0][t] = (uint16_t)amin;
-        // suffix minimum over the threads after this one (exclusive), for the last-Push records
-        u32 sfx = amin;  // inclusive suffix min within the wave
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const u32 o = __shfl_down(sfx, off, 64);
-            if (lane + off < 64) sfx = o < sfx ? o : sfx;
-        }
-        if (lane == 0) s_sw[w] = (uint16_t)sfx;
-        for (int r = t; r < ST_TILE; r += ST_TPB) s_tab[r] = ST_NO_PUSH;
-        __syncthreads();
-        {
-            u32 m = amin;
-#pragma unroll
-            for (int j = 1; j < 9; j++) {
-                const int h = 1 << (j - 1);
-                if (t >= h) {
-                    const u32 o = s_sp[j - 1][t - h];
-                    m = o < m ? o : m;
-                }
-                s_sp[j][t] = (uint16_t)m;
-                __syncthreads();
-            }
-        }
-        ST_MARK(4);
-        u32 after = __shfl_down(sfx, 1, 64);  // min over later threads in the wave
-        if (lane == 63) after = ST_INF;
-        for (int i = w + 1; i < 4; i++) after = s_sw[i] < after ? s_sw[i] : after;
-
-        // Last Push to each slot below the tile's end depth: after the last time the walk is at
-        // (or below) a level it pushes that level, i.e. at i + 1 for every suffix-record low i.
-        {
-            u32 cur = after;
-            const bool lastthr = t == ST_TPB - 1;
-#pragma unroll
-            for (int q = ST_ITEMS - 1; q >= 0; q--) {
-                const bool final = lastthr && q == ST_ITEMS - 1;  // nothing follows position 2047
-                if (!final && a[q] < cur) s_tab[a[q]] = (uint16_t)(t * ST_ITEMS + q + 1);
-                cur = a[q] < cur ? a[q] : cur;
-            }
-            if (t == 0 && astart < cur) s_tab[astart] = 0;
-        }
-
-        // Each Pop returns the Push right after the last earlier position whose depth is <= the
-        // depth the Pop leaves (a previous-smaller-or-equal query over the tile). Pops that the
-        // thread cannot answer from its own ops are queued per wave and answered with all lanes.
-        u32 prv = astart;
-        qn = 0;
-#pragma unroll
-        for (int q = 0; q < ST_ITEMS; q++) {
-            const u32 pos = (u32)(t * ST_ITEMS + q);
-            const bool pop = ops[q].op == 0 && prv > a[q];  // a non-empty Pop (empty: depth stays 0)
-            rk[q] = 0;
-            rv[q] = 0;
-            if (ops[q].op == 0 && !pop) {
-                rk[q] = 2;  // Pop on an empty stack: None
-            } else if (ops[q].op == 1) {
-                rk[q] = push_resp ? 1 : 2;
-                rv[q] = ops[q].val;
-            }
-            bool need = false;
-            if (pop) {
-                const u32 s = a[q];
-                int r = astart <= s ? t * ST_ITEMS - 1 : -2;
-#pragma unroll
-                for (int qq = 0; qq < ST_ITEMS; qq++)
-                    if (qq < q && a[qq] <= s) r = t * ST_ITEMS + qq;
-                if (r != -2) {
-                    rk[q] = 1;
-                    rv[q] = s_val[r + 1];
-                } else {
-                    need = true;
-                }
-            }
-            const u64 m = __ballot(need);
-            if (need) s_q[w][qn + __popcll(m & ((1ull << lane) - 1))] = (a[q] << 11) | pos;
-            qn += (u32)__popcll(m);
-            prv = a[q];
-        }
-        __syncthreads();
-        ST_MARK(5);
-#pragma unroll
-        for (int j = 0; j < ST_ITEMS; j++) {
-            const u32 i = (u32)lane + 64u * j;
-            if (i >= qn) continue;
-            const u32 e = s_q[w][i];
-            const u32 s = e >> 11, pos = e & 2047u;
-            // nearest earlier thread whose minimum is <= s: binary lifting, 9 steps
-            int k = (int)(pos / ST_ITEMS) - 1;
-            int r = -2;
-#pragma unroll
-            for (int jj = 8; jj >= 0; jj--)
-                if (k >= 0 && s_sp[jj][k] > s) k -= 1 << jj;
-            if (k >= 0) {
-                u32 v[ST_ITEMS];
-#pragma unroll
-                for (int qq = 0; qq < ST_ITEMS; qq++) v[qq] = s_A[k * ST_ITEMS + qq + 1];
-#pragma unroll
-                for (int qq = 0; qq < ST_ITEMS; qq++)
-                    if (v[qq] <= s) r = k * ST_ITEMS + qq;
-            } else if (s_A[0] <= s) {
-                r = -1;
-            }
-            qe[j] = e;
-            qx[j] = r == -2;  // the Push is in an earlier tile or before the chunk
-            qv[j] = r == -2 ? 0u : s_val[r + 1];
-        }
-        ST_MARK(6);
-        if (pass == 1) break;
-
-        if (w == 0) {
-            // Wave 0 composes the aggregates of ALL earlier tiles itself (64 per wave
-            // instruction, every load of a group in flight at once) instead of waiting for an
-            // inclusive prefix to ripple down the chain of tiles. Lane l composes the run of
-            // predecessors [r*G, r*G + G), r = 63 - l, in registers (older first); one wave
-            // composition then joins the runs (the highest lane holds the oldest).
-            const int np = (int)tile;
-            const int G = (np + 63) / 64;
-            const int r0 = (63 - lane) * G;
-            Fn acc = FN_ID;
-            constexpr int B = 8;  // descriptor loads in flight per lane
-            for (int g0 = 0; g0 < G; g0 += B) {
-                u64 v[B];
-#pragma unroll
-                for (int q = 0; q < B; q++) {
-                    const int idx = r0 + g0 + q;
-                    v[q] = (g0 + q < G && idx < np)
-                               ? __hip_atomic_load(&desc[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                               : 0ull;
-                }
-#pragma unroll
-                for (int q = 0; q < B; q++) {
-                    const int idx = r0 + g0 + q;
-                    if (g0 + q >= G || idx >= np) continue;
-                    u32 spins = 0;
-                    while (!(v[q] & D_MASK)) {  // not published yet (its tile is still loading)
-                        __builtin_amdgcn_s_sleep(1);
-                        v[q] = __hip_atomic_load(&desc[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        if (++spins == (1u << 26)) {  // bounded: never hang the device
-                            atomicOr(&ctl->err, ERR_CAPACITY);
-                            break;
-                        }
-                    }
-                    acc = fn_then(acc, unpack_agg(v[q]));
-                }
-            }
-            acc = np ? wave_compose(acc) : Fn{0, 0};
-            const long long dbase = fn_apply(acc, d0);
-            if (lane == 0) {
-                const u64 ntiles = (n + ST_TILE - 1) / ST_TILE;
-                if ((u64)tile == ntiles - 1) {
-                    ctl->depth_next = fn_apply(tagg, dbase);
-                    ctl->depth0 = d0;
-                }
-                s_dbase = dbase;
-            }
-        }
-        __syncthreads();
-        ST_MARK(7);
-        const long long D = s_dbase;  // depth before the tile
-        if (D + tmin >= 0) {          // the walk never reaches an empty stack: pass 0 holds
-            tmin += D;
-            break;
-        }
-        dstart = fn_apply(tpre, D);
-        clamp = true;
-    }
-
-    // Responses, the capacity check, cross-tile Pops (with the slot's pre-chunk content: no
-    // tile writes the stack before st_finish_kernel), then the last-Push table.
+    // responses known now, lane-contiguous (unmatched Pops stay None until patched below)
     {
-        bool over = false;
-        u32 prv = astart;
+        const u64 g0 = lo + base;
+        const bool in = full && g0 >= resp_lo && g0 + SW_OPS <= resp_hi;
+        u32* rp = resp + (g0 - resp_lo);
+        uint8_t* sp = some + (g0 - resp_lo);
+        if (in && !((uintptr_t)rp & 15) && !((uintptr_t)sp & 15)) {
 #pragma unroll
-        for (int q = 0; q < ST_ITEMS; q++) {
-            const u64 g = lo + tbase + (u64)(t * ST_ITEMS + q);
-            over |= ops[q].op == 1 && (u64)(tmin + (long long)prv) >= cap;
-            if (rk[q] && g >= resp_lo && g < resp_hi) {
-                resp[g - resp_lo] = rk[q] == 1 ? rv[q] : 0u;
-                some[g - resp_lo] = rk[q] == 1 ? 1 : 0;
+            for (int j = 0; j < SW_OPS / 4; j++)
+                ((uint4*)rp)[j] = uint4{rt[4 * j], rt[4 * j + 1], rt[4 * j + 2], rt[4 * j + 3]};
+#pragma unroll
+            for (int j = 0; j < SW_OPS / 16; j++) {
+                uint4 b;
+                u32* bb = (u32*)&b;
+#pragma unroll
+                for (int k = 0; k < 4; k++) bb[k] = (((smask >> (16 * j + 4 * k)) & 15u) * 0x204081u) & 0x01010101u;
+                ((uint4*)sp)[j] = b;
             }
-            prv = a[q];
-        }
-        if (over) atomicOr(&ctl->err, ERR_CAPACITY);
+        } else if (resp) {
 #pragma unroll
-        for (int j = 0; j < ST_ITEMS; j++) {
-            const u32 i = (u32)lane + 64u * j;
-            if (i >= qn) continue;
-            const u32 e = qe[j];
-            const u64 g = lo + tbase + (e & 2047u);
-            if (qx[j]) {
-                const u32 h = atomicAdd(&s_ucnt, 1u);
-                const long long slot = tmin + (long long)(e >> 11);
-                tl.upop[(u64)tile * ST_TILE + h] = e;
-                tl.uval[(u64)tile * ST_TILE + h] = slot < d0 && (u64)slot < cap ? stack[slot] : 0u;
-            } else if (g >= resp_lo && g < resp_hi) {
-                resp[g - resp_lo] = qv[j];
-                some[g - resp_lo] = 1;
+            for (int q = 0; q < SW_OPS; q++) {
+                const u64 g = g0 + q;
+                if (base + q < n && g >= resp_lo && g < resp_hi) {
+                    resp[g - resp_lo] = rt[q];
+                    some[g - resp_lo] = (smask >> q) & 1;
+                }
             }
         }
     }
-    if (t == ST_TPB - 1) s_aend = a[ST_ITEMS - 1];
+    ST_MARK(3);
+
+    // ---- 3. look-back (wave 0): compose the aggregates of ALL earlier tiles (64 runs in
+    // parallel, 8 loads in flight per lane); the highest lane holds the oldest run ----
+    const long long d0 = ctl->depth;  // depth before the chunk (st_finish_kernel updates it)
+    if (wv == 0) {
+        const int np = (int)tile;
+        const int G = (np + 63) / 64;
+        const int r0 = (63 - lane) * G;
+        Fn acc = FN_ID;
+        constexpr int B = 8;
+        for (int g0 = 0; g0 < G; g0 += B) {
+            u64 v[B];
+#pragma unroll
+            for (int q = 0; q < B; q++) {
+                const int idx = r0 + g0 + q;
+                v[q] = (g0 + q < G && idx < np) ? __hip_atomic_load(&desc[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                                : 0ull;
+            }
+            // predecessors publish right after their local pass: re-poll only what is missing
+            for (u32 spins = 0;; spins++) {
+                bool ok = true;
+#pragma unroll
+                for (int q = 0; q < B; q++) ok &= g0 + q >= G || r0 + g0 + q >= np || (v[q] & D_MASK);
+                if (ok) break;
+                if (spins == (1u << 24)) {  // bounded: never hang the device
+                    atomicOr(&ctl->err, ERR_CAPACITY);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+                for (int q = 0; q < B; q++) {
+                    const int idx = r0 + g0 + q;
+                    if (g0 + q < G && idx < np && !(v[q] & D_MASK))
+                        v[q] = __hip_atomic_load(&desc[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < B; q++)
+                if (g0 + q < G && r0 + g0 + q < np) acc = fn_then(acc, unpack_agg(v[q]));
+        }
+        acc = np ? wave_compose(acc) : Fn{0, 0};
+        if (lane == 0) s_D = fn_apply(acc, d0);
+    }
     __syncthreads();
-    // Levels [tmin, end depth) each have a last Push (suffix records); no other level has one.
-    u32* tab = tl.table + (u64)tile * ST_TILE;
-    for (u32 r = t; r < s_aend; r += ST_TPB) tab[r] = s_val[s_tab[r]];
-    if (t == 0) {
-        tl.tmin[tile] = tmin;
-        tl.tend[tile] = s_aend;
+    ST_MARK(4);
+    const long long D = s_D;
+    const long long T0 = D + M > 0 ? D + M : 0;              // the tile's lowest level
+    const long long Dt = D + xe > xe - xm ? D + xe : xe - xm;  // the lane's start depth
+    const long long aminl = Dt - (long long)nun > 0 ? Dt - (long long)nun : 0;
+    const int amin = (int)(aminl - T0);  // levels relative to T0 from here on
+    const int dt = (int)(Dt - T0);
+    const int aend_r = amin + (int)top;  // the lane's end depth: max(Dt + e, top) - T0
+    if (t == ST_LANES - 1 && tile == (u32)((n + ST_TILE - 1) / ST_TILE) - 1) {
+        ctl->depth_next = T0 + aend_r;
+        ctl->depth0 = d0;
+    }
+    if (Dt + hmax > (long long)cap || (long long)topmax > (long long)cap) atomicOr(&ctl->err, ERR_CAPACITY);
+    {
+        // cross-tile Pops read levels in [T0, D) below the chunk's start depth: fetch the first
+        // 256 of them now, while the query structures are built
+        const long long slot = T0 + t;
+        s_pre[t] = slot < d0 && slot < D && (u64)slot < cap ? stack[slot] : 0u;
+    }
+    s_min[t] = amin;
+    // sparse table: levels 0..6 inside the wave (windows clipped at the wave's first lane; the
+    // part in earlier waves is added below), inclusive suffix minimum inside the wave
+    int spw[7];
+    spw[0] = amin;
+#pragma unroll
+    for (int j = 1; j < 7; j++) {
+        const int o = __shfl_up(spw[j - 1], 1 << (j - 1), 64);
+        spw[j] = lane >= (1 << (j - 1)) && o < spw[j - 1] ? o : spw[j - 1];
+    }
+    int sf = amin;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_down(sf, off, 64);
+        if (lane + off < 64) sf = o < sf ? o : sf;
+    }
+    int later = __shfl_down(sf, 1, 64);
+    if (lane == 63) later = 1 << 30;
+    s_suf[t] = sf;
+    if (lane == 0) s_wmin[wv] = sf;
+    // the wave's query list: lane t's unmatched Pops k < min(nun, D_t) (the rest find it empty)
+    const int uq = (int)(Dt < (long long)nun ? Dt : (long long)nun);
+    int inc = uq;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_up(inc, off, 64);
+        if (lane >= off) inc += o;
+    }
+    const int total = __shfl(inc, 63, 64);
+    {
+        u32 um = umask;
+        for (int k = 0, h = inc - uq; k < uq; k++, h++) {
+            const int q = __builtin_ctz(um);
+            um &= um - 1;
+            s_up[h] = ((u32)(dt - 1 - k) << ST_PB) | ((u32)t * SW_OPS + (u32)q);
+        }
+    }
+    __syncthreads();
+    // complete the windows (t - 2^j, t] that reach into earlier waves: a suffix of the previous
+    // wave (its inclusive suffix minimum) and, for level 7, whole waves before it
+    {
+#pragma unroll
+        for (int j = 0; j < 7; j++) {
+            int m = spw[j];
+            if (wv > 0 && lane < (1 << j) - 1) {
+                const int o = s_suf[t - (1 << j) + 1];
+                m = o < m ? o : m;
+            }
+            s_sp[j][t] = m;
+        }
+        int m7 = spw[6];
+        if (wv > 0) m7 = s_wmin[wv - 1] < m7 ? s_wmin[wv - 1] : m7;
+        if (wv > 1 && lane < 63) m7 = s_suf[t - 127] < m7 ? s_suf[t - 127] : m7;
+        s_sp[7][t] = m7;
+        for (int w = wv + 1; w < ST_WAVES; w++) later = s_wmin[w] < later ? s_wmin[w] : later;
+    }
+    __syncthreads();
+    ST_MARK(5);
+
+    // ---- 4. unmatched Pops: QI queries per lane at a time, their table walks interleaved ----
+    constexpr int QI = 4;
+    for (int h0 = lane; h0 < total; h0 += 64 * QI) {
+        u32 e[QI];
+        int v[QI];
+#pragma unroll
+        for (int i = 0; i < QI; i++) {
+            const int h = h0 + 64 * i;
+            e[i] = h < total ? s_up[h] : 0u;
+            v[i] = h < total ? (int)((e[i] & ST_PMASK) / SW_OPS) - 1 : -1;
+        }
+        // the nearest earlier lane whose minimum is <= the level (greedy skips of 128, ..., 1)
+#pragma unroll
+        for (int j = 7; j >= 0; j--) {
+#pragma unroll
+            for (int i = 0; i < QI; i++)
+                if (v[i] >= 0 && s_sp[j][v[i]] > (int)(e[i] >> ST_PB)) v[i] -= 1 << j;
+        }
+#pragma unroll
+        for (int i = 0; i < QI; i++) {
+            if (h0 + 64 * i >= total) continue;
+            const int Lr = (int)(e[i] >> ST_PB);
+            const u32 pos = e[i] & ST_PMASK;
+            if (v[i] >= 0) {
+                const u64 g = lo + tbase + pos;
+                if (resp && g >= resp_lo && g < resp_hi) {
+                    resp[g - resp_lo] = s_wave[v[i] >> 6][(Lr - s_min[v[i]]) * 64 + (v[i] & 63)];
+                    some[g - resp_lo] = 1;
+                }
+            } else {  // its Push is in an earlier tile or before the chunk
+                const u32 x = atomicAdd(&s_ucnt, 1u);
+                const long long slot = T0 + Lr;
+                tl.upop[(u64)tile * ST_TILE + x] = e[i];
+                tl.uval[(u64)tile * ST_TILE + x] =
+                    slot < d0 && (u64)slot < cap ? (Lr < ST_LANES ? s_pre[Lr] : stack[slot]) : 0u;
+            }
+        }
+    }
+    ST_MARK(6);
+
+    // ---- 5. the tile's last-Push table for levels [T0, tile end) ----
+    {
+        u32* tab = tl.table + (u64)tile * ST_TILE;
+        const int hi = aend_r < later ? aend_r : later;
+        for (int L = amin; L < hi; L++) tab[L] = s_stk[L - amin][lane];
+    }
+    __syncthreads();
+    if (t == ST_LANES - 1) {
+        tl.tmin[tile] = T0;
+        tl.tend[tile] = (u32)aend_r;
         tl.ucnt[tile] = s_ucnt;
     }
-    ST_MARK(8);
+    ST_MARK(7);
 #undef ST_MARK
+}
+
+// The nearest tile k <= from whose minimum is <= s (skipping 8- and 64-tile groups whose
+// minimum is above s), or -1.
+__device__ __forceinline__ int st_walk(const long long* s_tm, const long long* s_g8, const long long* s_gm, int k,
+                                       long long s) {
+    while (k >= 0) {
+        if ((k & 63) == 63 && s_gm[k >> 6] > s) {
+            k -= 64;
+            continue;
+        }
+        if ((k & 7) == 7 && s_g8[k >> 3] > s) {
+            k -= 8;
+            continue;
+        }
+        if (s_tm[k] <= s) break;
+        k--;
+    }
+    return k;
 }
 
 // One block per tile after st_tile_kernel. Every block stages all tile minima in LDS (with the
@@ -457,7 +533,7 @@ __global__ __launch_bounds__(ST_TPB) void st_tile_kernel(const nrg_stack_op* __r
 __global__ __launch_bounds__(256) void st_finish_kernel(u64 lo, u64 n, DevCtl* ctl, StTiles tl,
                                                         u32* __restrict__ stack, u64 cap, u64 resp_lo, u64 resp_hi,
                                                         u32* __restrict__ resp, uint8_t* __restrict__ some,
-                                                        u64* desc, u32* ticket) {
+                                                        u64* desc) {
     extern __shared__ long long s_tm[];  // [tiles] tile minima, [tiles/8 + 1] and [tiles/64 + 1] group minima
     __shared__ long long s_lo[4];
     const u32 tiles = gridDim.x;
@@ -469,7 +545,6 @@ __global__ __launch_bounds__(256) void st_finish_kernel(u64 lo, u64 n, DevCtl* c
     const u32 uv0 = tl.uval[(u64)tile * ST_TILE + t];
     const u32 tend = tl.tend[tile];
     if (t == 0) desc[tile] = 0;  // ready for the next chunk (the tile kernel is done)
-    if (tile == 0 && t == 0) *ticket = 0;
     const u32 ngr = (tiles + 63) / 64;
     long long* s_g8 = s_tm + tiles;
     long long* s_gm = s_g8 + tiles / 8 + 1;
@@ -495,41 +570,44 @@ __global__ __launch_bounds__(256) void st_finish_kernel(u64 lo, u64 n, DevCtl* c
     if (lane == 0) s_lo[w] = later;
     __syncthreads();
     if (tile == 0 && t == 0) ctl->depth = ctl->depth_next;
+    for (int i = 0; i < 4; i++) later = s_lo[i] < later ? s_lo[i] : later;
+    const long long tmin = s_tm[tile];
+    // cross-tile Pops first (their table loads), then the commit, then the answers: the loads of
+    // both are in flight together
+    u32 pval = 0;
+    u64 pg = ~0ull;
+    const bool one = cnt <= 256;  // the common case: one Pop per thread
+    if (one && (u32)t < cnt) {
+        const u64 g = lo + (u64)tile * ST_TILE + (v0 & ST_PMASK);
+        if (g >= resp_lo && g < resp_hi) {
+            const long long s = tmin + (v0 >> ST_PB);
+            const int k = st_walk(s_tm, s_g8, s_gm, (int)tile - 1, s);
+            pval = k >= 0 ? tl.table[(u64)k * ST_TILE + (u64)(s - s_tm[k])] : uv0;
+            pg = g;
+        }
+    }
     {
-        for (int i = 0; i < 4; i++) later = s_lo[i] < later ? s_lo[i] : later;
-        const long long tm = s_tm[tile];
-        long long hi = tm + (long long)tend;
+        long long hi = tmin + (long long)tend;
         hi = hi < later ? hi : later;
         const u32* tab = tl.table + (u64)tile * ST_TILE;
-        for (long long sl = tm + t; sl < hi; sl += 256)
-            if ((u64)sl < cap) stack[sl] = tab[sl - tm];
+        for (long long sl = tmin + t; sl < hi; sl += 256)
+            if ((u64)sl < cap) stack[sl] = tab[sl - tmin];
     }
-    const long long tmin = s_tm[tile];
-    for (u32 j = t; j < cnt; j += 256) {
-        const u32 v = j == (u32)t ? v0 : tl.upop[(u64)tile * ST_TILE + j];
-        const u64 g = lo + (u64)tile * ST_TILE + (v & 2047u);
-        if (g < resp_lo || g >= resp_hi) continue;
-        const long long s = tmin + (v >> 11);
-        int k = (int)tile - 1;
-        while (k >= 0) {
-            if ((k & 63) == 63 && s_gm[k >> 6] > s) {
-                k -= 64;
-                continue;
-            }
-            if ((k & 7) == 7 && s_g8[k >> 3] > s) {
-                k -= 8;
-                continue;
-            }
-            if (s_tm[k] <= s) break;
-            k--;
+    if (pg != ~0ull) {
+        resp[pg - resp_lo] = pval;
+        some[pg - resp_lo] = 1;
+    }
+    if (!one) {
+        for (u32 j = t; j < cnt; j += 256) {
+            const u32 v = j == (u32)t ? v0 : tl.upop[(u64)tile * ST_TILE + j];
+            const u64 g = lo + (u64)tile * ST_TILE + (v & ST_PMASK);
+            if (g < resp_lo || g >= resp_hi) continue;
+            const long long s = tmin + (v >> ST_PB);
+            const int k = st_walk(s_tm, s_g8, s_gm, (int)tile - 1, s);
+            resp[g - resp_lo] = k >= 0 ? tl.table[(u64)k * ST_TILE + (u64)(s - s_tm[k])]
+                                       : (j == (u32)t ? uv0 : tl.uval[(u64)tile * ST_TILE + j]);
+            some[g - resp_lo] = 1;
         }
-        u32 val;
-        if (k >= 0)
-            val = tl.table[(u64)k * ST_TILE + (u64)(s - s_tm[k])];
-        else
-            val = j == (u32)t ? uv0 : tl.uval[(u64)tile * ST_TILE + j];
-        resp[g - resp_lo] = val;
-        some[g - resp_lo] = 1;
     }
 }
 
@@ -540,10 +618,9 @@ hipError_t st_replay_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 resp_hi, 
     const u64 ring_mask = c->log_size - 1;
     nrg_stack_op* ring = (nrg_stack_op*)c->d_ring;
     const u64 tiles = (n + ST_TILE - 1) / ST_TILE;
-    // descriptors: [ticket (64 words of u32 = 32 u64)] [tiles u64]; zero at open, and
-    // st_finish_kernel clears what st_tile_kernel used (no memset launch per chunk)
+    // descriptors: [32 u64 unused] [tiles u64]; zero at open, and st_finish_kernel clears what
+    // st_tile_kernel used (no memset launch per chunk)
     u64* desc = (u64*)c->d_scan_desc + 32;
-    u32* ticket = c->d_scan_desc;
     const u64 mt = (c->cfg.max_batch + ST_TILE - 1) / ST_TILE;
     StTiles tl;
     tl.tmin = (long long*)c->d_st_aux;
@@ -555,13 +632,11 @@ hipError_t st_replay_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 resp_hi, 
     const bool want = d_resp != nullptr && resp_lo < lo + n && resp_hi > lo;
     const u64 rlo = want ? resp_lo : 0, rhi = want ? resp_hi : 0;
     timer_begin(c, "st_replay");
-    st_tile_kernel<<<(unsigned)tiles, ST_TPB, 0, st>>>(src, ring, ring_mask, lo, n, c->d_ctl, desc, ticket, tl,
-                                                      c->d_stack, c->cfg.stack_capacity, rlo, rhi,
-                                                      (int)c->cfg.stack_push_resp, d_resp, d_some, c->exp,
-                                                      (c->exp & 2) ? c->d_dbg : nullptr);
+    st_tile_kernel<<<(unsigned)tiles, ST_LANES, 0, st>>>(src, ring, ring_mask, lo, n, c->d_ctl, desc, tl, c->d_stack,
+                                                         c->cfg.stack_capacity, rlo, rhi, (int)c->cfg.stack_push_resp,
+                                                         d_resp, d_some, (c->exp & 2) ? c->d_dbg : nullptr);
     st_finish_kernel<<<(unsigned)tiles, 256, (tiles + tiles / 8 + tiles / 64 + 2) * 8, st>>>(
-        lo, n, c->d_ctl, tl, c->d_stack, c->cfg.stack_capacity, rlo, rhi,
-        want ? d_resp : nullptr, d_some, desc, ticket);
+        lo, n, c->d_ctl, tl, c->d_stack, c->cfg.stack_capacity, rlo, rhi, want ? d_resp : nullptr, d_some, desc);
     timer_end(c, "st_replay");
     return hipGetLastError();
 }
