@@ -615,7 +615,7 @@ def run_stack(args, env):
     Ng = N * world
     cap = args.stack_init + 4 * Ng + (1 << 16)
     rep = nrgpu.DeviceReplica(L.NRG_DS_STACK, env.local, max_batch=Ng, stack_capacity=cap,
-                              log_bytes=64 * 4 * max(Ng, 8192), replica_id=rank + 1)
+                              log_bytes=64 * 4 * max(Ng, 8192), replica_id=rank + 1, pipeline=args.pipeline)
     rep.use_torch_stream()
     rep.st_init(list(range(args.stack_init)))  # benches/stack.rs:50-63: 0..50000
     P = max(1, min(args.pool, args.steps + args.warmup))
@@ -623,8 +623,11 @@ def run_stack(args, env):
     seed0 = 0x5354434B00000001 + rank * 0x1000193
     for p in range(P):
         rep.gen_stack_ops_device(ops[p], N, seed0 + p)
-    resp = torch.empty(N, dtype=torch.int32, device=dev_t)
-    some = torch.empty(N, dtype=torch.uint8, device=dev_t)
+    # pipeline=1: a round's cross-tile Pops are answered in the next round's launch, so rounds
+    # alternate between two response buffers
+    resps = [torch.empty(N, dtype=torch.int32, device=dev_t) for _ in range(2)]
+    somes = [torch.empty(N, dtype=torch.uint8, device=dev_t) for _ in range(2)]
+    resp, some = resps[0], somes[0]
     torch.cuda.synchronize()
     # distinct slots written per round (S of SURVEY.md §8d): pushes at distinct depths; the
     # depth walk is shift-invariant while it stays above 0 (it starts at 50k)
@@ -650,12 +653,13 @@ def run_stack(args, env):
         group = ReplicatedLog(rep, device=dev_t)
     round_fn, h = rep._lib.nrg_stack_round_async, rep._h
     ptrs = [ops[p].data_ptr() for p in range(P)]
-    r_p, s_p = resp.data_ptr(), some.data_ptr()
+    rps = [(r.data_ptr(), s_.data_ptr()) for r, s_ in zip(resps, somes)]
     gathered = {}
     mode = {"n": 0}
 
     def step(i):
         p = i % P
+        r_p, s_p = rps[i & 1]
         if cgroup is not None:
             cgroup.round_async(ptrs[p], N, r_p, s_p)
         elif group is None:
@@ -667,7 +671,7 @@ def run_stack(args, env):
             g = gathered.pop(i) if i in gathered else group.gather_async(ops[p], stride=N)
             if i + 1 < mode["n"]:
                 gathered[i + 1] = group.gather_async(ops[(i + 1) % P], stride=N)
-            group.replay(g, resp, some)
+            group.replay(g, resps[i & 1], somes[i & 1])
 
     mode["n"] = args.warmup
     for i in range(args.warmup):

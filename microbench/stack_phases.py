@@ -18,24 +18,35 @@ import nrgpu  # noqa: E402
 from nrgpu import _lib as L  # noqa: E402
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
-dev = nrgpu.DeviceReplica(L.NRG_DS_STACK, 0, max_batch=N, stack_capacity=N * 4 + 100_000,
+dev = nrgpu.DeviceReplica(L.NRG_DS_STACK, 0, max_batch=N, stack_capacity=N * 4 + 100_000, pipeline=int(os.environ.get("PIPE", "1")),
                           log_bytes=64 * 4 * max(N, 8192))
 dev.use_torch_stream()
 dev.st_init(list(range(50_000)))
-ops = torch.empty(N, dtype=torch.int64, device="cuda")
-dev.gen_stack_ops_device(ops, N, 12345)
-resp = torch.empty(N, dtype=torch.int32, device="cuda")
-some = torch.empty(N, dtype=torch.uint8, device="cuda")
+# BB=k: k back-to-back rounds over distinct batches before each reading (as bench.py runs them)
+BB = int(os.environ.get("BB", "1"))
+opsl = [torch.empty(N, dtype=torch.int64, device="cuda") for _ in range(BB)]
+for i, o in enumerate(opsl):
+    dev.gen_stack_ops_device(o, N, 12345 + i)
+resps = [torch.empty(N, dtype=torch.int32, device="cuda") for _ in range(2)]
+somes = [torch.empty(N, dtype=torch.uint8, device="cuda") for _ in range(2)]
 tiles = (N + 8191) // 8192
 names = ["loads", "local pass", "scan+responses", "lookback", "query list+sparse table", "queries", "table"]
 acc = np.zeros((tiles, 8))
 R = 20
+fin = []
 for r in range(R + 3):
-    dev.st_round_device(ops, N, 1, resp, some)
+    for i in range(BB):  # pipeline=1: a round's finish rides in the next launch
+        dev.st_round_device(opsl[i], N, 1, resps[i & 1], somes[i & 1])
     torch.cuda.synchronize()
     buf = np.zeros(tiles * 16, np.uint64)
     L.check(L.load().nrg_test_debug_read(dev.handle, buf.ctypes.data_as(C.c_void_p), tiles * 16))
+    full = np.zeros(256 * 16, np.uint64)
+    L.check(L.load().nrg_test_debug_read(dev.handle, full.ctypes.data_as(C.c_void_p), 256 * 16))
+    fb = full.reshape(256, 16)[128:128 + tiles, :2].astype(np.float64)
     t = buf.reshape(tiles, 16)[:, :8].astype(np.float64)
+    if r >= 3 and fb[:, 0].min() > 0:
+        o = min(t[:, 0].min(), fb[:, 0].min())
+        fin.append((fb[:, 0].min() - o, fb[:, 0].max() - o, fb[:, 1].max() - o, t[:, 0].min() - o, t[:, 7].max() - o))
     if r >= 3:
         acc += t - t[:, :1].min()
 acc /= R
@@ -46,3 +57,7 @@ for k, nm in enumerate(names):
     print(f"  {nm:14s} mean {d.mean():7.2f} us  max {d.max():7.2f} us")
 end = acc[:, 7] / 100.0
 print(f"  last tile end {end.max():.2f} us after the first start; mean tile span {(acc[:, 7] - acc[:, 0]).mean() / 100:.2f} us")
+if fin:
+    f = np.array(fin).mean(0) / 100.0
+    print("fused finish of the previous chunk (us from the launch's first workgroup): start %.2f..%.2f, last end %.2f;"
+          " tiles start %.2f, last tile end %.2f" % tuple(f))

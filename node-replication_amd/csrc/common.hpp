@@ -79,8 +79,8 @@ struct __attribute__((aligned(64))) DevCtl {
     long long depth;  // stack: current length
     u64 counter;      // scratch counter (dump compaction)
     u64 nkeys_total;  // hashmap: nkeys + keys created by replay rounds (hm_count)
-    long long depth0;      // stack: length before the chunk being replayed
-    long long depth_next;  // stack: length after it (st_commit_kernel moves it to depth)
+    long long depth0;      // stack: length after the last chunk of buffer parity 0 (stack.hip)
+    long long depth_next;  // stack: ... of parity 1; a chunk starts from the other parity's slot
     u64 pad;
     Slot sp;          // hashmap: side slot of the key EMPTY_KEY (val, stamps; key unused)
 };

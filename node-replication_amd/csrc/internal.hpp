@@ -59,6 +59,16 @@ struct HmDeferred {
     uint8_t* found = nullptr;
 };
 
+// A stack chunk whose finish (cross-tile Pops, commit) has not run yet (stack.hip).
+struct StDeferred {
+    bool valid = false;
+    u64 lo = 0, n = 0;
+    u32 tiles = 0, par = 0;
+    u64 rlo = 0, rhi = 0;
+    uint32_t* resp = nullptr;
+    uint8_t* some = nullptr;
+};
+
 struct HostRun {  // origin tags of appended log ranges (the Entry::replica field)
     u64 first, count;
     u32 origin;
@@ -94,6 +104,8 @@ struct nrg_ctx {
     // pipeline == false they are flushed at the end of every call.
     bool pipeline = false;
     nrg::HmDeferred pend;
+    nrg::StDeferred st_pend;  // stack: the last chunk's finish, if deferred
+    uint32_t st_par = 0;      // stack: buffer parity of the next chunk
     uint64_t* d_created = nullptr;  // [HM_CREATED_SLOTS] keys created by replay rounds
     void* d_bk_ent = nullptr;       // [index tiles][tile] 16-B {id << 32 | i+1, value}
     uint64_t* d_bk_key = nullptr;   // [index tiles][tile] key of each entry
@@ -165,6 +177,7 @@ bool timer_events(nrg_ctx* c, const char* name, hipEvent_t* start, hipEvent_t* s
 int ctx_use_device(nrg_ctx* c);
 // launch the deferred reads of the last hashmap round, if any (hashmap.hip)
 hipError_t hm_flush(nrg_ctx* c);
+hipError_t st_flush(nrg_ctx* c);
 
 // hashmap.hip
 hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool write_ring,

@@ -69,8 +69,13 @@ int use_device(nrg_ctx* c) {
     return NRG_OK;
 }
 
-// the deferred half of the last hashmap round (hashmap.hip), launched now if there is one
-hipError_t hm_flush_if(nrg_ctx* c) { return c->cfg.ds_kind == NRG_DS_HASHMAP ? hm_flush(c) : hipSuccess; }
+// the deferred half of the last hashmap round (hashmap.hip) or the deferred finish of the last
+// stack chunk (stack.hip), launched now if there is one
+hipError_t hm_flush_if(nrg_ctx* c) {
+    if (c->cfg.ds_kind == NRG_DS_HASHMAP) return hm_flush(c);
+    if (c->cfg.ds_kind == NRG_DS_STACK) return st_flush(c);
+    return hipSuccess;
+}
 
 // Log GC boundary: the slowest replica's tail (this replica's ltail), held back to the first
 // record of a deferred hashmap stamp round, whose apply and reads take values from the ring.
@@ -364,6 +369,8 @@ int nrg_open(int dev, const nrg_config* cfg_in, nrg_ctx** out) {
         OPEN_CHK(hipMalloc(&c->d_scan_desc, c->scan_desc_words * 4));
         OPEN_CHK(hipMemsetAsync(c->d_scan_desc, 0, c->scan_desc_words * 4, c->stream));
         OPEN_CHK(hipMalloc(&c->d_st_aux, st_aux_bytes(mb)));
+        c->pipeline = cf.pipeline != 0;
+        if (const char* e = std::getenv("NRG_PIPELINE")) c->pipeline = std::atoi(e) != 0;
         if (const char* e = std::getenv("NRG_EXP")) c->exp = (uint32_t)std::atoi(e);
         if (c->exp & 2) OPEN_CHK(hipMalloc(&c->d_dbg, ((mb + 2047) / 2048) * 16 * sizeof(uint64_t)));
     } else {
@@ -542,6 +549,7 @@ int nrg_log_exec(nrg_ctx* c, uint64_t resp_lo, uint64_t resp_hi, void* resp, uin
         HIPCHK(hipMemsetAsync(ds, 0, w, c->stream));
     }
     if ((r = exec_range(c, resp_lo, resp_hi, dr, ds))) return r;
+    HIPCHK(hm_flush_if(c));  // deferred work writes responses too: complete them before the copy
     if (w) {
         HIPCHK(hipMemcpyAsync(resp, dr, w * resp_elem_bytes(c), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipMemcpyAsync(some, ds, w, hipMemcpyDeviceToHost, c->stream));
@@ -830,9 +838,12 @@ int nrg_stack_init(nrg_ctx* c, const uint32_t* vals, uint64_t n) {
     int r = need(c, NRG_DS_STACK);
     if (r) return r;
     if (n > c->cfg.stack_capacity) return NRG_E_CAPACITY;
+    HIPCHK(hm_flush_if(c));  // a deferred chunk finish commits before the stack is replaced
     if (n) HIPCHK(hipMemcpyAsync(c->d_stack, vals, n * 4, hipMemcpyHostToDevice, c->stream));
     long long d = (long long)n;
     HIPCHK(hipMemcpyAsync(&c->d_ctl->depth, &d, sizeof(d), hipMemcpyHostToDevice, c->stream));
+    // the depth slot the next chunk starts from (stack.hip: chunk of parity p reads slot p ^ 1)
+    HIPCHK(hipMemcpyAsync(&c->d_ctl->depth0 + (c->st_par ^ 1), &d, sizeof(d), hipMemcpyHostToDevice, c->stream));
     HIPCHK(sync_all(c));
     return NRG_OK;
 }
@@ -841,6 +852,7 @@ int nrg_stack_len(nrg_ctx* c, uint64_t* n) {
     int r = need(c, NRG_DS_STACK);
     if (r) return r;
     long long d = 0;
+    HIPCHK(hm_flush_if(c));  // a deferred chunk finish publishes the length
     HIPCHK(hipMemcpyAsync(&d, &c->d_ctl->depth, sizeof(d), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(sync_all(c));
     // an overflowing chunk latches ERR_CAPACITY once but keeps counting: never report (or
@@ -937,6 +949,7 @@ int nrg_memcpy_d2h(nrg_ctx* c, void* h, const void* d, uint64_t bytes) {
     if (!c) return NRG_E_INVAL;
     int r = use_device(c);
     if (r) return r;
+    HIPCHK(hm_flush_if(c));
     HIPCHK(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(sync_all(c));
     return NRG_OK;
@@ -1073,7 +1086,8 @@ extern "C" int nrg_test_debug_read(nrg_ctx* c, uint64_t* out, uint64_t words) {
     if (!c->d_dbg) return NRG_E_INVAL;
     int r = use_device(c);
     if (r) return r;
-    HIPCHK(sync_all(c));
+    // diagnostic timestamps of the launches so far: no flush of deferred work (it would stamp over them)
+    HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipMemcpy(out, c->d_dbg, words * 8, hipMemcpyDeviceToHost));
     return NRG_OK;
 }

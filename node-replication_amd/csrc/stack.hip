@@ -97,6 +97,65 @@ struct StTiles {
     u32* uval;         // [tiles][ST_TILE] their slot's content before the chunk (if below it)
 };
 
+// The nearest tile k <= from whose minimum is <= s (skipping 8- and 64-tile groups whose
+// minimum is above s), or -1.
+__device__ __forceinline__ int st_walk(const long long* s_tm, const long long* s_g8, const long long* s_gm, int k,
+                                       long long s) {
+    while (k >= 0) {
+        if ((k & 63) == 63 && s_gm[k >> 6] > s) {
+            k -= 64;
+            continue;
+        }
+        if ((k & 7) == 7 && s_g8[k >> 3] > s) {
+            k -= 8;
+            continue;
+        }
+        if (s_tm[k] <= s) break;
+        k--;
+    }
+    return k;
+}
+
+// Stage the tile minima of a chunk in LDS (256 threads): s_tm[tiles], then the minimum of
+// every 8-tile group (s_g8) and 64-tile group (s_gm). Returns this thread's minimum over the
+// tiles after `after` (pass ~0u for none).
+__device__ __forceinline__ long long st_stage(const long long* __restrict__ tmin, u32 tiles, long long* s_tm,
+                                              long long* s_g8, long long* s_gm, u32 after) {
+    const int t = threadIdx.x, lane = t & 63;
+    const u32 ngr = (tiles + 63) / 64;
+    long long later = 1ll << 62;
+    for (u32 k = t; k < ngr * 64; k += 256) {
+        const long long v = k < tiles ? tmin[k] : (1ll << 62);
+        if (k < tiles) s_tm[k] = v;
+        if (k > after) later = v < later ? v : later;
+        long long m = v;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const long long x = __shfl_xor(m, off, 64);
+            m = x < m ? x : m;
+            if (off == 4 && (lane & 7) == 0 && (k >> 3) <= tiles / 8) s_g8[k >> 3] = m;
+        }
+        if (lane == 0) s_gm[k >> 6] = m;
+    }
+    return later;
+}
+
+// A replay launch: the tile pass of chunk e (A) and, in the workgroups before it, the finish
+// of chunk e-1 (P): its cross-tile Pops and its commit. Chunks alternate between two sets of
+// per-tile buffers (parity), so the two never touch the same scratch.
+struct StPass {
+    const nrg_stack_op* src;  // chunk records in a caller buffer, or nullptr (ring)
+    nrg_stack_op* ring;
+    u64 ring_mask;
+    u64 lo, n;                // log range
+    u32 tiles, par;           // tiles; parity of the chunk's buffers and depth slot
+    u64* desc;                // look-back descriptors (parity buffer)
+    StTiles tl;
+    u64 rlo, rhi;             // response window (log indices)
+    u32* resp;
+    uint8_t* some;
+};
+
 __device__ __forceinline__ void wave_sync() {  // LDS written by other lanes of this wave
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -137,14 +196,17 @@ __device__ __forceinline__ void me_then(int& m, int& e, int m2, int e2) {
 // in-order dispatcher has already placed (a bounded spin latches ERR_CAPACITY instead of
 // hanging). src: the chunk's records in a caller buffer (nrg_stack_round_async); the kernel
 // then writes the log copy itself (Log::append fused). nullptr: records are in the ring.
-__global__ __launch_bounds__(ST_LANES) void st_tile_kernel(const nrg_stack_op* __restrict__ src, nrg_stack_op* ring,
-                                                          u64 ring_mask, u64 lo, u64 n, DevCtl* ctl, u64* desc,
-                                                          StTiles tl, const u32* __restrict__ stack, u64 cap,
-                                                          u64 resp_lo, u64 resp_hi, int push_resp,
-                                                          u32* __restrict__ resp, uint8_t* __restrict__ some,
-                                                          u64* __restrict__ dbg) {
+__device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u32 tile, DevCtl* ctl,
+                                             const u32* __restrict__ stack, u64 cap, int push_resp,
+                                             u64* __restrict__ dbg) {
+    const nrg_stack_op* __restrict__ src = A.src;
+    nrg_stack_op* ring = A.ring;
+    const u64 ring_mask = A.ring_mask, lo = A.lo, n = A.n, resp_lo = A.rlo, resp_hi = A.rhi;
+    u64* desc = A.desc;
+    const StTiles& tl = A.tl;
+    u32* __restrict__ resp = A.resp;
+    uint8_t* __restrict__ some = A.some;
     const int t = threadIdx.x, wv = t >> 6, lane = t & 63;
-    const u32 tile = blockIdx.x;
     const u64 tbase = (u64)tile * ST_TILE;
     const u64 wbase = tbase + (u64)wv * (64 * SW_OPS);  // the wave's 2048 ops
     const u64 base = tbase + (u64)t * SW_OPS;           // the lane's 32 ops
@@ -161,12 +223,16 @@ __global__ __launch_bounds__(ST_LANES) void st_tile_kernel(const nrg_stack_op* _
     __shared__ int s_sp[8][ST_LANES];   // s_sp[j][v] = min of s_min over lanes (v - 2^j, v]
     __shared__ int s_suf[ST_LANES];     // inclusive suffix minimum of s_min inside the wave
     __shared__ int s_wm[ST_WAVES], s_we[ST_WAVES], s_wmin[ST_WAVES];
-    __shared__ u32 s_pre[ST_LANES];     // pre-chunk content of levels T0 + [0, 256)
     __shared__ long long s_D;
     __shared__ u32 s_ucnt;
     u32 (*s_stk)[64] = reinterpret_cast<u32 (*)[64]>(s_wave[wv]);
     u32* s_up = s_wave[wv] + W_STK;
     if (t == 0) s_ucnt = 0;
+    // the previous chunk's tile minima: a slot it wrote (>= its lowest level) is read from its
+    // owner's table, because that chunk's commit runs in this same launch
+    extern __shared__ long long s_ptm[];
+    long long* s_pg8 = s_ptm + P.tiles;
+    long long* s_pgm = s_pg8 + P.tiles / 8 + 1;
 
     // ---- load the lane's 32 ops (and write the log copy when they come from the caller) ----
     u32 val[SW_OPS];
@@ -279,6 +345,7 @@ __global__ __launch_bounds__(ST_LANES) void st_tile_kernel(const nrg_stack_op* _
     }
     int xm = __shfl_up(im, 1, 64), xe = __shfl_up(ie, 1, 64);  // exclusive within the wave
     if (lane == 0) xm = xe = 0;
+    if (P.tiles) (void)st_stage(P.tl.tmin, P.tiles, s_ptm, s_pg8, s_pgm, ~0u);  // after the op loads
     __syncthreads();
     int M = 0, E = 0, pmw = 0, pew = 0;  // tile aggregate; prefix of the earlier waves
 #pragma unroll
@@ -328,7 +395,8 @@ __global__ __launch_bounds__(ST_LANES) void st_tile_kernel(const nrg_stack_op* _
 
     // ---- 3. look-back (wave 0): compose the aggregates of ALL earlier tiles (64 runs in
     // parallel, 8 loads in flight per lane); the highest lane holds the oldest run ----
-    const long long d0 = ctl->depth;  // depth before the chunk (st_finish_kernel updates it)
+    long long* sdepth = &ctl->depth0;             // depth after the chunk of each parity
+    const long long d0 = sdepth[A.par ^ 1];        // depth before this chunk
     if (wv == 0) {
         const int np = (int)tile;
         const int G = (np + 63) / 64;
@@ -377,17 +445,8 @@ __global__ __launch_bounds__(ST_LANES) void st_tile_kernel(const nrg_stack_op* _
     const int amin = (int)(aminl - T0);  // levels relative to T0 from here on
     const int dt = (int)(Dt - T0);
     const int aend_r = amin + (int)top;  // the lane's end depth: max(Dt + e, top) - T0
-    if (t == ST_LANES - 1 && tile == (u32)((n + ST_TILE - 1) / ST_TILE) - 1) {
-        ctl->depth_next = T0 + aend_r;
-        ctl->depth0 = d0;
-    }
+    if (t == ST_LANES - 1 && tile == A.tiles - 1) sdepth[A.par] = T0 + aend_r;
     if (Dt + hmax > (long long)cap || (long long)topmax > (long long)cap) atomicOr(&ctl->err, ERR_CAPACITY);
-    {
-        // cross-tile Pops read levels in [T0, D) below the chunk's start depth: fetch the first
-        // 256 of them now, while the query structures are built
-        const long long slot = T0 + t;
-        s_pre[t] = slot < d0 && slot < D && (u64)slot < cap ? stack[slot] : 0u;
-    }
     s_min[t] = amin;
     // sparse table: levels 0..6 inside the wave (windows clipped at the wave's first lane; the
     // part in earlier waves is added below), inclusive suffix minimum inside the wave
@@ -477,13 +536,23 @@ __global__ __launch_bounds__(ST_LANES) void st_tile_kernel(const nrg_stack_op* _
                     some[g - resp_lo] = 1;
                 }
             } else {  // its Push is in an earlier tile or before the chunk
-                const u32 x = atomicAdd(&s_ucnt, 1u);
-                const long long slot = T0 + Lr;
-                tl.upop[(u64)tile * ST_TILE + x] = e[i];
-                tl.uval[(u64)tile * ST_TILE + x] =
-                    slot < d0 && (u64)slot < cap ? (Lr < ST_LANES ? s_pre[Lr] : stack[slot]) : 0u;
+                tl.upop[(u64)tile * ST_TILE + atomicAdd(&s_ucnt, 1u)] = e[i];
             }
         }
+    }
+    __syncthreads();
+    // the cross-tile Pops' pre-chunk content, one per thread (all loads in flight together): a
+    // slot the previous chunk wrote comes from its owner's table (that chunk's commit runs in
+    // this launch), any other from the stack
+    const u32 ucnt = s_ucnt;
+    for (u32 h = t; h < ucnt; h += ST_LANES) {
+        const long long slot = T0 + (long long)(tl.upop[(u64)tile * ST_TILE + h] >> ST_PB);
+        u32 pv = 0;
+        if (slot < d0 && (u64)slot < cap) {
+            const int k = P.tiles ? st_walk(s_ptm, s_pg8, s_pgm, (int)P.tiles - 1, slot) : -1;
+            pv = k >= 0 ? P.tl.table[(u64)k * ST_TILE + (u64)(slot - s_ptm[k])] : stack[slot];
+        }
+        tl.uval[(u64)tile * ST_TILE + h] = pv;
     }
     ST_MARK(6);
 
@@ -493,75 +562,41 @@ __global__ __launch_bounds__(ST_LANES) void st_tile_kernel(const nrg_stack_op* _
         const int hi = aend_r < later ? aend_r : later;
         for (int L = amin; L < hi; L++) tab[L] = s_stk[L - amin][lane];
     }
-    __syncthreads();
     if (t == ST_LANES - 1) {
         tl.tmin[tile] = T0;
         tl.tend[tile] = (u32)aend_r;
-        tl.ucnt[tile] = s_ucnt;
+        tl.ucnt[tile] = ucnt;
     }
     ST_MARK(7);
 #undef ST_MARK
 }
 
-// The nearest tile k <= from whose minimum is <= s (skipping 8- and 64-tile groups whose
-// minimum is above s), or -1.
-__device__ __forceinline__ int st_walk(const long long* s_tm, const long long* s_g8, const long long* s_gm, int k,
-                                       long long s) {
-    while (k >= 0) {
-        if ((k & 63) == 63 && s_gm[k >> 6] > s) {
-            k -= 64;
-            continue;
-        }
-        if ((k & 7) == 7 && s_g8[k >> 3] > s) {
-            k -= 8;
-            continue;
-        }
-        if (s_tm[k] <= s) break;
-        k--;
-    }
-    return k;
-}
-
-// One block per tile after st_tile_kernel. Every block stages all tile minima in LDS (with the
-// minimum of every 8- and 64-tile group) and then
+// The finish of chunk P, one workgroup per tile: with all tile minima staged in LDS it
 //   * commits: the tile's levels [tmin, min(end depth, min of every later tile's minimum)) are
 //     the slots whose last Push of the chunk is this tile's, held in its table;
 //   * resolves the tile's Pops whose Push lies in an earlier tile: the nearest earlier tile
 //     whose minimum is <= the slot (a walk that skips 8- and 64-tile groups whose minimum is
-//     above the slot), or the pre-chunk content st_tile_kernel read.
-// Block 0 publishes the new depth.
-__global__ __launch_bounds__(256) void st_finish_kernel(u64 lo, u64 n, DevCtl* ctl, StTiles tl,
-                                                        u32* __restrict__ stack, u64 cap, u64 resp_lo, u64 resp_hi,
-                                                        u32* __restrict__ resp, uint8_t* __restrict__ some,
-                                                        u64* desc) {
+//     above the slot), or the pre-chunk content the tile pass read.
+// Tile 0 publishes the chunk's end depth as the stack's length.
+__device__ __forceinline__ void st_finish_role(const StPass& P, u32 tile, DevCtl* ctl, u32* __restrict__ stack,
+                                               u64 cap) {
     extern __shared__ long long s_tm[];  // [tiles] tile minima, [tiles/8 + 1] and [tiles/64 + 1] group minima
     __shared__ long long s_lo[4];
-    const u32 tiles = gridDim.x;
-    const u32 tile = blockIdx.x;
+    const u32 tiles = P.tiles;
+    const StTiles& tl = P.tl;
+    const u64 lo = P.lo, resp_lo = P.rlo, resp_hi = P.rhi;
+    u32* __restrict__ resp = P.resp;
+    uint8_t* __restrict__ some = P.some;
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     // independent loads first: they overlap the staging below
     const u32 cnt = resp ? tl.ucnt[tile] : 0u;
     const u32 v0 = tl.upop[(u64)tile * ST_TILE + t];
     const u32 uv0 = tl.uval[(u64)tile * ST_TILE + t];
     const u32 tend = tl.tend[tile];
-    if (t == 0) desc[tile] = 0;  // ready for the next chunk (the tile kernel is done)
-    const u32 ngr = (tiles + 63) / 64;
+    if (t == 0) P.desc[tile] = 0;  // ready for the next chunk of this parity
     long long* s_g8 = s_tm + tiles;
     long long* s_gm = s_g8 + tiles / 8 + 1;
-    long long later = 1ll << 62;  // minimum over the tiles after this one
-    for (u32 k = t; k < ngr * 64; k += 256) {
-        const long long v = k < tiles ? tl.tmin[k] : (1ll << 62);
-        if (k < tiles) s_tm[k] = v;
-        if (k > tile) later = v < later ? v : later;
-        long long m = v;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const long long x = __shfl_xor(m, off, 64);
-            m = x < m ? x : m;
-            if (off == 4 && (lane & 7) == 0 && (k >> 3) <= tiles / 8) s_g8[k >> 3] = m;
-        }
-        if (lane == 0) s_gm[k >> 6] = m;
-    }
+    long long later = st_stage(tl.tmin, tiles, s_tm, s_g8, s_gm, tile);  // minimum over the later tiles
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
         const long long x = __shfl_xor(later, off, 64);
@@ -569,7 +604,7 @@ __global__ __launch_bounds__(256) void st_finish_kernel(u64 lo, u64 n, DevCtl* c
     }
     if (lane == 0) s_lo[w] = later;
     __syncthreads();
-    if (tile == 0 && t == 0) ctl->depth = ctl->depth_next;
+    if (tile == 0 && t == 0) ctl->depth = (&ctl->depth0)[P.par];
     for (int i = 0; i < 4; i++) later = s_lo[i] < later ? s_lo[i] : later;
     const long long tmin = s_tm[tile];
     // cross-tile Pops first (their table loads), then the commit, then the answers: the loads of
@@ -611,39 +646,105 @@ __global__ __launch_bounds__(256) void st_finish_kernel(u64 lo, u64 n, DevCtl* c
     }
 }
 
-hipError_t st_replay_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 resp_hi, uint32_t* d_resp, uint8_t* d_some,
-                           const nrg_stack_op* src) {
-    if (n == 0) return hipSuccess;
-    hipStream_t st = c->stream;
-    const u64 ring_mask = c->log_size - 1;
-    nrg_stack_op* ring = (nrg_stack_op*)c->d_ring;
-    const u64 tiles = (n + ST_TILE - 1) / ST_TILE;
-    // descriptors: [32 u64 unused] [tiles u64]; zero at open, and st_finish_kernel clears what
-    // st_tile_kernel used (no memset launch per chunk)
-    u64* desc = (u64*)c->d_scan_desc + 32;
-    const u64 mt = (c->cfg.max_batch + ST_TILE - 1) / ST_TILE;
-    StTiles tl;
-    tl.tmin = (long long*)c->d_st_aux;
-    tl.ucnt = (u32*)(tl.tmin + mt);
-    tl.tend = tl.ucnt + mt;
-    tl.upop = tl.tend + mt;
-    tl.uval = tl.upop + mt * ST_TILE;
-    tl.table = tl.uval + mt * ST_TILE;
-    const bool want = d_resp != nullptr && resp_lo < lo + n && resp_hi > lo;
-    const u64 rlo = want ? resp_lo : 0, rhi = want ? resp_hi : 0;
-    timer_begin(c, "st_replay");
-    st_tile_kernel<<<(unsigned)tiles, ST_LANES, 0, st>>>(src, ring, ring_mask, lo, n, c->d_ctl, desc, tl, c->d_stack,
-                                                         c->cfg.stack_capacity, rlo, rhi, (int)c->cfg.stack_push_resp,
-                                                         d_resp, d_some, (c->exp & 2) ? c->d_dbg : nullptr);
-    st_finish_kernel<<<(unsigned)tiles, 256, (tiles + tiles / 8 + tiles / 64 + 2) * 8, st>>>(
-        lo, n, c->d_ctl, tl, c->d_stack, c->cfg.stack_capacity, rlo, rhi, want ? d_resp : nullptr, d_some, desc);
-    timer_end(c, "st_replay");
+__global__ __launch_bounds__(ST_LANES) void st_round_kernel(StPass A, StPass P, DevCtl* ctl, u32* __restrict__ stack,
+                                                           u64 cap, int push_resp, u64* __restrict__ dbg) {
+    // tile workgroups first: the dispatcher places workgroups in order, and the finish
+    // workgroups (independent of this launch's tiles) fill in behind them
+    if (blockIdx.x < A.tiles) {
+        st_tile_role(A, P, blockIdx.x, ctl, stack, cap, push_resp, dbg);
+    } else {
+        const u32 f = blockIdx.x - A.tiles;
+        // diagnostic (NRG_EXP & 2): finish workgroups' start/end at dbg[(128 + tile) * 16 + {0, 1}]
+        if (dbg && threadIdx.x == 0 && f < 128) dbg[(128 + f) * 16] = wall_clock64();
+        st_finish_role(P, f, ctl, stack, cap);
+        if (dbg && threadIdx.x == 0 && f < 128) dbg[(128 + f) * 16 + 1] = wall_clock64();
+    }
+}
+
+static u64 st_max_tiles(const nrg_ctx* c) { return (c->cfg.max_batch + ST_TILE - 1) / ST_TILE; }
+
+static u64 st_parity_bytes(u64 mt) { return mt * (8 + 4 + 4) + mt * ST_TILE * (4 + 4 + 4); }
+
+// the per-tile buffers and look-back descriptors of parity `par`
+static StPass st_pass(nrg_ctx* c, u32 par) {
+    const u64 mt = st_max_tiles(c);
+    StPass s{};
+    s.par = par;
+    s.ring = (nrg_stack_op*)c->d_ring;
+    s.ring_mask = c->log_size - 1;
+    // descriptors: [32 u64 unused] [parity][max tiles] u64; zero at open, and each chunk's finish
+    // clears what its tile pass used (no memset launch per chunk)
+    s.desc = (u64*)c->d_scan_desc + 32 + par * mt;
+    char* base = (char*)c->d_st_aux + par * st_parity_bytes(mt);
+    s.tl.tmin = (long long*)base;
+    s.tl.ucnt = (u32*)(s.tl.tmin + mt);
+    s.tl.tend = s.tl.ucnt + mt;
+    s.tl.upop = s.tl.tend + mt;
+    s.tl.uval = s.tl.upop + mt * ST_TILE;
+    s.tl.table = s.tl.uval + mt * ST_TILE;
+    return s;
+}
+
+static hipError_t st_launch(nrg_ctx* c, const StPass& A, const StPass& P) {
+    const unsigned grid = A.tiles + P.tiles;
+    const size_t dyn = P.tiles ? (size_t)(P.tiles + P.tiles / 8 + P.tiles / 64 + 2) * 8 : 0;
+    st_round_kernel<<<grid, ST_LANES, dyn, c->stream>>>(A, P, c->d_ctl, c->d_stack, c->cfg.stack_capacity,
+                                                         (int)c->cfg.stack_push_resp, (c->exp & 2) ? c->d_dbg : nullptr);
     return hipGetLastError();
 }
 
-u64 st_aux_bytes(u64 max_batch) {
-    const u64 mt = (max_batch + ST_TILE - 1) / ST_TILE;
-    return mt * (8 + 4 + 4) + mt * ST_TILE * (4 + 4 + 4);
+// The finish of the last replayed chunk (its cross-tile Pops and its commit), if still pending.
+hipError_t st_flush(nrg_ctx* c) {
+    if (!c->st_pend.valid) return hipSuccess;
+    StPass P = st_pass(c, c->st_pend.par);
+    P.lo = c->st_pend.lo;
+    P.n = c->st_pend.n;
+    P.tiles = c->st_pend.tiles;
+    P.rlo = c->st_pend.rlo;
+    P.rhi = c->st_pend.rhi;
+    P.resp = c->st_pend.resp;
+    P.some = c->st_pend.some;
+    c->st_pend.valid = false;
+    StPass A{};
+    return st_launch(c, A, P);
 }
+
+// One chunk: its tile pass, fused with the previous chunk's finish in one launch. The chunk's
+// own finish runs in the next chunk's launch (config.pipeline = 1, until nrg_join or a sync)
+// or right away.
+hipError_t st_replay_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 resp_hi, uint32_t* d_resp, uint8_t* d_some,
+                           const nrg_stack_op* src) {
+    if (n == 0) return hipSuccess;
+    StPass A = st_pass(c, c->st_par);
+    A.src = src;
+    A.lo = lo;
+    A.n = n;
+    A.tiles = (u32)((n + ST_TILE - 1) / ST_TILE);
+    const bool want = d_resp != nullptr && resp_lo < lo + n && resp_hi > lo;
+    A.rlo = want ? resp_lo : 0;
+    A.rhi = want ? resp_hi : 0;
+    A.resp = want ? d_resp : nullptr;
+    A.some = want ? d_some : nullptr;
+    StPass P{};
+    if (c->st_pend.valid) {
+        P = st_pass(c, c->st_pend.par);
+        P.lo = c->st_pend.lo;
+        P.n = c->st_pend.n;
+        P.tiles = c->st_pend.tiles;
+        P.rlo = c->st_pend.rlo;
+        P.rhi = c->st_pend.rhi;
+        P.resp = c->st_pend.resp;
+        P.some = c->st_pend.some;
+    }
+    timer_begin(c, "st_replay");
+    hipError_t e = st_launch(c, A, P);
+    timer_end(c, "st_replay");
+    if (e != hipSuccess) return e;
+    c->st_pend = StDeferred{true, lo, n, A.tiles, A.par, A.rlo, A.rhi, A.resp, A.some};
+    c->st_par ^= 1;
+    return c->pipeline ? hipSuccess : st_flush(c);
+}
+
+u64 st_aux_bytes(u64 max_batch) { return 2 * st_parity_bytes((max_batch + ST_TILE - 1) / ST_TILE); }
 
 }  // namespace nrg

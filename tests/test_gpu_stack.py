@@ -147,3 +147,44 @@ def test_stack_eight_segment_round(nrg, orc, init_n):
         assert dev.st_len() == len(os_.dump())
     np.testing.assert_array_equal(dev.st_dump(), os_.dump())
     dev.close()
+
+
+@pytest.mark.parametrize("init_n,n,rounds", [(50000, 200000, 4), (3, 20000, 3), (0, 8192 * 3 + 77, 3)])
+def test_stack_pipelined_rounds(nrg, orc, init_n, n, rounds):
+    """pipeline=1: a chunk's finish (cross-tile Pops, commit) rides in the next chunk's launch
+    (Replica::combine rounds back to back, nr/src/replica.rs:544-595); every round answers into
+    its own buffers, complete after nrg_join. Then chunked exec (several chunks per call, each
+    fused with the previous chunk's finish) and a final dump, all against the Vec oracle."""
+    import torch
+
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_STACK, 0, max_batch=1 << 18, stack_capacity=1 << 22, pipeline=1,
+                            log_bytes=64 * 4 * (1 << 20))
+    init = np.arange(init_n, dtype=np.uint32)
+    dev.st_init(init)
+    os_ = orc.Stack(init)
+    outs = []
+    for r in range(rounds):
+        vals, ops = orc.gen_stack_ops(n, 301 + r)
+        if init_n == 3:
+            ops[: n // 2] = 0  # pops on an empty stack first
+        d_ops = torch.from_numpy(_ops(vals, ops).view(np.int64).copy()).cuda()
+        resp = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+        some = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+        dev.st_round_device(d_ops, n, 1, resp, some)
+        outs.append((d_ops, resp, some, os_.replay(vals, ops)))
+    dev.join()
+    torch.cuda.synchronize()
+    for r, (_, resp, some, (oresp, osome)) in enumerate(outs):
+        np.testing.assert_array_equal(some.cpu().numpy(), osome, err_msg=f"round {r} some")
+        np.testing.assert_array_equal(resp.cpu().numpy().view(np.uint32), oresp, err_msg=f"round {r} resp")
+    assert dev.st_len() == len(os_)
+    # exec over several max_batch chunks (append + exec, 3 chunks of 2^18)
+    vals, ops = orc.gen_stack_ops(3 * (1 << 18) - 5, 999)
+    first = dev.log_append(_ops(vals, ops), 1)
+    resp, some = dev.log_exec(first, first + len(ops))
+    oresp, osome = os_.replay(vals, ops)
+    np.testing.assert_array_equal(some, osome)
+    np.testing.assert_array_equal(resp, oresp)
+    assert dev.st_peek() == os_.peek()
+    np.testing.assert_array_equal(dev.st_dump(), os_.dump())
+    dev.close()
