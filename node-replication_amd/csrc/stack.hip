@@ -220,11 +220,13 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
     static_assert(W_STK + W_UP >= 2 * 64 * SW_OPS, "staging fits");
     __shared__ __attribute__((aligned(16))) u32 s_wave[ST_WAVES][W_STK + W_UP];
     __shared__ int s_min[ST_LANES];     // lane minimum level - tile minimum
-    __shared__ int s_sp[8][ST_LANES];   // s_sp[j][v] = min of s_min over lanes (v - 2^j, v]
+    __shared__ unsigned short s_sp[8][ST_LANES];  // s_sp[j][v] = min of s_min over lanes (v - 2^j, v]
     __shared__ int s_suf[ST_LANES];     // inclusive suffix minimum of s_min inside the wave
     __shared__ int s_wm[ST_WAVES], s_we[ST_WAVES], s_wmin[ST_WAVES];
     __shared__ long long s_D;
     __shared__ u32 s_ucnt;
+    constexpr u32 ST_XL = 1024;
+    __shared__ u32 s_xl[ST_XL];         // the first cross-tile Pops (the rest re-read from upop)
     u32 (*s_stk)[64] = reinterpret_cast<u32 (*)[64]>(s_wave[wv]);
     u32* s_up = s_wave[wv] + W_STK;
     if (t == 0) s_ucnt = 0;
@@ -495,12 +497,12 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
                 const int o = s_suf[t - (1 << j) + 1];
                 m = o < m ? o : m;
             }
-            s_sp[j][t] = m;
+            s_sp[j][t] = (unsigned short)m;  // levels are < 2 * ST_TILE
         }
         int m7 = spw[6];
         if (wv > 0) m7 = s_wmin[wv - 1] < m7 ? s_wmin[wv - 1] : m7;
         if (wv > 1 && lane < 63) m7 = s_suf[t - 127] < m7 ? s_suf[t - 127] : m7;
-        s_sp[7][t] = m7;
+        s_sp[7][t] = (unsigned short)m7;
         for (int w = wv + 1; w < ST_WAVES; w++) later = s_wmin[w] < later ? s_wmin[w] : later;
     }
     __syncthreads();
@@ -522,7 +524,7 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
         for (int j = 7; j >= 0; j--) {
 #pragma unroll
             for (int i = 0; i < QI; i++)
-                if (v[i] >= 0 && s_sp[j][v[i]] > (int)(e[i] >> ST_PB)) v[i] -= 1 << j;
+                if (v[i] >= 0 && (int)s_sp[j][v[i]] > (int)(e[i] >> ST_PB)) v[i] -= 1 << j;
         }
 #pragma unroll
         for (int i = 0; i < QI; i++) {
@@ -536,7 +538,9 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
                     some[g - resp_lo] = 1;
                 }
             } else {  // its Push is in an earlier tile or before the chunk
-                tl.upop[(u64)tile * ST_TILE + atomicAdd(&s_ucnt, 1u)] = e[i];
+                const u32 x = atomicAdd(&s_ucnt, 1u);
+                tl.upop[(u64)tile * ST_TILE + x] = e[i];
+                if (x < ST_XL) s_xl[x] = e[i];
             }
         }
     }
@@ -546,7 +550,8 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
     // this launch), any other from the stack
     const u32 ucnt = s_ucnt;
     for (u32 h = t; h < ucnt; h += ST_LANES) {
-        const long long slot = T0 + (long long)(tl.upop[(u64)tile * ST_TILE + h] >> ST_PB);
+        const u32 e = h < ST_XL ? s_xl[h] : tl.upop[(u64)tile * ST_TILE + h];
+        const long long slot = T0 + (long long)(e >> ST_PB);
         u32 pv = 0;
         if (slot < d0 && (u64)slot < cap) {
             const int k = P.tiles ? st_walk(s_ptm, s_pg8, s_pgm, (int)P.tiles - 1, slot) : -1;
