@@ -524,7 +524,7 @@ def run_synthetic(args, env):
     N = args.ops_per_gpu
     Ng = N * world
     rep = nrgpu.DeviceReplica(L.NRG_DS_SYNTHETIC, env.local, max_batch=Ng, log_bytes=64 * 4 * max(Ng, 8192),
-                              replica_id=rank + 1)
+                              replica_id=rank + 1, pipeline=args.pipeline)
     rep.use_torch_stream()
     P = max(1, min(args.pool, 8, args.steps + args.warmup))
     gen = torch.Generator(device=dev_t)
@@ -536,8 +536,10 @@ def run_synthetic(args, env):
         ops[p, :, 1] = torch.randint(lo, hi, (N,), generator=gen, device=dev_t)
         ops[p, :, 2] = torch.randint(lo, hi, (N,), generator=gen, device=dev_t)
         ops[p, :, 3] = 1
-    resp = torch.empty(N, dtype=torch.int64, device=dev_t)
-    some = torch.empty(N, dtype=torch.uint8, device=dev_t)
+    # pipeline=1: a round's sums are written in the next round's first launch, so rounds
+    # alternate between two response buffers
+    resps = [torch.empty(N, dtype=torch.int64, device=dev_t) for _ in range(2)]
+    somes = [torch.empty(N, dtype=torch.uint8, device=dev_t) for _ in range(2)]
     torch.cuda.synchronize()
     group = cgroup = None
     if world > 1 and args.backend == "nccl":
@@ -552,12 +554,13 @@ def run_synthetic(args, env):
         group = ReplicatedLog(rep, device=dev_t)
     round_fn, h = rep._lib.nrg_synth_round_async, rep._h
     ptrs = [ops[p].data_ptr() for p in range(P)]
-    r_p, s_p = resp.data_ptr(), some.data_ptr()
+    rps = [(r.data_ptr(), s_.data_ptr()) for r, s_ in zip(resps, somes)]
     gathered = {}
     mode = {"n": 0}
 
     def step(i):
         p = i % P
+        r_p, s_p = rps[i & 1]
         if cgroup is not None:
             cgroup.round_async(ptrs[p], N, r_p, s_p)
         elif group is None:
@@ -569,7 +572,7 @@ def run_synthetic(args, env):
             g = gathered.pop(i) if i in gathered else group.gather_async(ops[p], stride=N)
             if i + 1 < mode["n"]:
                 gathered[i + 1] = group.gather_async(ops[(i + 1) % P], stride=N)
-            group.replay(g, resp, some)
+            group.replay(g, resps[i & 1], somes[i & 1])
 
     mode["n"] = args.warmup
     for i in range(args.warmup):

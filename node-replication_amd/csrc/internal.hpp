@@ -69,6 +69,17 @@ struct StDeferred {
     uint8_t* some = nullptr;
 };
 
+// A synthetic chunk whose per-op sums and hot-word fold have not run yet (synthetic.hip).
+struct SyDeferred {
+    bool valid = false;
+    u32 par = 0;
+    u64 lo = 0, n = 0;
+    u32 ntiles = 0, want = 0, t0 = 0, t1 = 1;
+    u64 rlo = 0, rhi = 0;
+    u64* resp = nullptr;
+    uint8_t* some = nullptr;
+};
+
 struct HostRun {  // origin tags of appended log ranges (the Entry::replica field)
     u64 first, count;
     u32 origin;
@@ -106,6 +117,8 @@ struct nrg_ctx {
     nrg::HmDeferred pend;
     nrg::StDeferred st_pend;  // stack: the last chunk's finish, if deferred
     uint32_t st_par = 0;      // stack: buffer parity of the next chunk
+    nrg::SyDeferred sy_pend;  // synthetic: the last chunk's sums, if deferred
+    uint32_t sy_par = 0;      // synthetic: buffer parity of the next chunk
     uint64_t* d_created = nullptr;  // [HM_CREATED_SLOTS] keys created by replay rounds
     void* d_bk_ent = nullptr;       // [index tiles][tile] 16-B {id << 32 | i+1, value}
     uint64_t* d_bk_key = nullptr;   // [index tiles][tile] key of each entry
@@ -178,6 +191,7 @@ int ctx_use_device(nrg_ctx* c);
 // launch the deferred reads of the last hashmap round, if any (hashmap.hip)
 hipError_t hm_flush(nrg_ctx* c);
 hipError_t st_flush(nrg_ctx* c);
+hipError_t sy_flush(nrg_ctx* c);
 
 // hashmap.hip
 hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool write_ring,

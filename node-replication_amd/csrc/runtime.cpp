@@ -69,12 +69,13 @@ int use_device(nrg_ctx* c) {
     return NRG_OK;
 }
 
-// the deferred half of the last hashmap round (hashmap.hip) or the deferred finish of the last
-// stack chunk (stack.hip), launched now if there is one
+// the deferred half of the last hashmap round (hashmap.hip), the deferred finish of the last
+// stack chunk (stack.hip) or the deferred sums of the last synthetic chunk (synthetic.hip),
+// launched now if there is one
 hipError_t hm_flush_if(nrg_ctx* c) {
     if (c->cfg.ds_kind == NRG_DS_HASHMAP) return hm_flush(c);
     if (c->cfg.ds_kind == NRG_DS_STACK) return st_flush(c);
-    return hipSuccess;
+    return sy_flush(c);
 }
 
 // Log GC boundary: the slowest replica's tail (this replica's ltail), held back to the first
@@ -392,6 +393,8 @@ int nrg_open(int dev, const nrg_config* cfg_in, nrg_ctx** out) {
         const char* force_sort = std::getenv("NRG_SY_SORT");
         if (sy_bucket_eligible(cf) && !(force_sort && std::atoi(force_sort)))
             OPEN_CHK(hipMalloc(&c->d_sy_aux, sy_bucket_aux_bytes(cf)));
+        c->pipeline = cf.pipeline != 0;
+        if (const char* e = std::getenv("NRG_PIPELINE")) c->pipeline = std::atoi(e) != 0;
         if (const char* e = std::getenv("NRG_EXP")) c->exp = (uint32_t)std::atoi(e);
         if (c->exp & 2) OPEN_CHK(hipMalloc(&c->d_dbg, 1024 * 16 * sizeof(uint64_t)));  // <= 1024 buckets
         OPEN_CHK(sy_init(c));
@@ -916,6 +919,7 @@ int nrg_synth_dump(nrg_ctx* c, uint64_t* words, uint64_t cap, uint64_t* n) {
     if (r) return r;
     *n = c->cfg.synth_n;
     if (*n > cap) return NRG_E_CAPACITY;
+    HIPCHK(hm_flush_if(c));  // deferred sums fold the hot words
     HIPCHK(hipMemcpyAsync(words, c->d_words, *n * 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(sync_all(c));
     return check_err(c);

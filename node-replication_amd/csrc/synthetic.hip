@@ -309,27 +309,66 @@ __device__ __forceinline__ u32 wave_rank(bool on, u32 key, int lane, u64* mask, 
     return c0 + (u32)__popcll(peers & ((1ull << lane) - 1));
 }
 
+// Arguments of the partition pass of chunk e and of the sums of chunk e-1, which share a launch.
+struct SyPartArgs {
+    const nrg_synth_op* src;  // the chunk's ops in a caller buffer, or nullptr (ring)
+    nrg_synth_op* ring;
+    u64 ring_mask, lo, n, span, span_m;
+    u32 HR;
+    u64 hr_m;
+    u32 HW, NB, W;
+    u64 wm;
+    u32 ntiles;
+    u32* E;
+    u32* cnt_bt;
+    SyHot* hot;
+};
+struct SySumArgs {
+    u32 blocks;  // workgroups of the sum role (0: none)
+    const u32* E;
+    const u64* V;
+    u64 n, lo, resp_lo, resp_hi;
+    u64* resp;
+    uint8_t* some;
+    u32 tile0, want;
+    const SyHot* hot;
+    u32 ntiles, HR, CW;
+    u64* words;
+};
+
+// LDS of a partition workgroup: ranking tables and staged words, then (same bytes) the tile's
+// touches grouped by bucket; the sum role reuses the same bytes for its per-op sums
 template <int CW>
-// src: the chunk's ops in a caller buffer (nrg_synth_round_async); the kernel then writes the
-// log copy itself (lane-contiguous). nullptr: the ops are in the ring.
-__global__ __launch_bounds__(SYA_TPB) void sy_part_kernel(const nrg_synth_op* __restrict__ src, nrg_synth_op* ring,
-                                                          u64 ring_mask, u64 lo,
-                                                          u64 n, u64 span, u64 span_m, u32 HR, u64 hr_m, u32 HW, u32 NB, u32 W, u64 wm,
-                                                          u32 ntiles, u32* __restrict__ E, u32* __restrict__ cnt_bt,
-                                                          SyHot* __restrict__ hot) {
-    __shared__ unsigned short s_wcnt[SYA_WAVES][SY_MAX_NB];
-    // ranking tables and staged words, then (same bytes) the tile's touches grouped by bucket
-    __shared__ union {
+struct SyPartLds {
+    unsigned short wcnt[SYA_WAVES][SY_MAX_NB];
+    union {
         struct {
             u64 mask[SYA_WAVES][SY_MAX_NB];
             u32 words[SYA_WAVES][64 * CW];
         } r;
         u32 stage[SYA_OPS * CW];
-    } s_u;
-    __shared__ SyHot s_hot[SYA_WAVES][SY_MAX_HOT];
-    __shared__ u32 s_part[SYA_WAVES];
+        u64 sum[SYA_OPS];
+    } u;
+    SyHot hot[SYA_WAVES][SY_MAX_HOT];
+    u32 part[SYA_WAVES];
+};
+
+// src: the chunk's ops in a caller buffer (nrg_synth_round_async); the role then writes the
+// log copy itself (lane-contiguous). nullptr: the ops are in the ring.
+template <int CW>
+__device__ __forceinline__ void sy_part_role(const SyPartArgs& A, u32 tile, SyPartLds<CW>& L) {
+    const nrg_synth_op* __restrict__ src = A.src;
+    nrg_synth_op* ring = A.ring;
+    const u64 ring_mask = A.ring_mask, lo = A.lo, n = A.n, span = A.span, span_m = A.span_m, hr_m = A.hr_m, wm = A.wm;
+    const u32 HR = A.HR, HW = A.HW, NB = A.NB, W = A.W, ntiles = A.ntiles;
+    u32* __restrict__ E = A.E;
+    u32* __restrict__ cnt_bt = A.cnt_bt;
+    SyHot* __restrict__ hot = A.hot;
+    auto& s_wcnt = L.wcnt;
+    auto& s_u = L.u;
+    auto& s_hot = L.hot;
+    auto& s_part = L.part;
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    const u32 tile = blockIdx.x;
     const u64 op0 = (u64)tile * SYA_OPS;
     for (u32 i = tid; i < SYA_WAVES * SY_MAX_NB / 2; i += SYA_TPB) ((u32*)&s_wcnt[0][0])[i] = 0;
     for (u32 i = tid; i < SYA_WAVES * SY_MAX_NB; i += SYA_TPB) (&s_u.r.mask[0][0])[i] = 0;
@@ -669,15 +708,20 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
 #undef SY_ACC
 }
 
-__global__ __launch_bounds__(SYC_TPB) void sy_sum_kernel(const u32* __restrict__ E, const u64* __restrict__ V, u32 CW,
-                                                         u64 n, u64 lo, u64 resp_lo, u64 resp_hi,
-                                                         u64* __restrict__ resp, uint8_t* __restrict__ some, u32 tile0,
-                                                         u32 want, const SyHot* __restrict__ hot, u32 ntiles, u32 HR,
-                                                         u64* __restrict__ words) {
-    __shared__ u64 s_sum[SYA_OPS];
+// Per-op sums of chunk S (one workgroup per 2048-op tile of the response window), then, in
+// workgroup 0, the ordered fold of the tiles' hot-word summaries into the hot words.
+__device__ __forceinline__ void sy_sum_role(const SySumArgs& S, u32 blk, u64* s_sum) {
+    const u32* __restrict__ E = S.E;
+    const u64* __restrict__ V = S.V;
+    const u64 n = S.n, lo = S.lo, resp_lo = S.resp_lo, resp_hi = S.resp_hi;
+    u64* __restrict__ resp = S.resp;
+    uint8_t* __restrict__ some = S.some;
+    const u32 tile0 = S.tile0, want = S.want, ntiles = S.ntiles, HR = S.HR, CW = S.CW;
+    const SyHot* __restrict__ hot = S.hot;
+    u64* __restrict__ words = S.words;
     const int tid = threadIdx.x;
     if (want) {
-        const u64 tile = tile0 + blockIdx.x;
+        const u64 tile = tile0 + blk;
         const u64 op0 = tile * SYA_OPS;
         const u32 nops = (u32)(n - op0 < SYA_OPS ? n - op0 : SYA_OPS);
         for (u32 i = tid; i < SYA_OPS; i += SYC_TPB) s_sum[i] = 0;
@@ -696,7 +740,7 @@ __global__ __launch_bounds__(SYC_TPB) void sy_sum_kernel(const u32* __restrict__
             }
         }
     }
-    if (blockIdx.x != 0) return;
+    if (blk != 0) return;
     // hot words: ordered fold of the tiles' summaries
     __syncthreads();
     SyHot* s_h = (SyHot*)s_sum;  // SYC_TPB entries
@@ -721,19 +765,99 @@ __global__ __launch_bounds__(SYC_TPB) void sy_sum_kernel(const u32* __restrict__
     }
 }
 
+// One launch: the partition of chunk e in workgroups [0, A.ntiles) (on the critical path: the
+// bucket pass waits for it) and the sums of chunk e-1 in the workgroups behind them.
+template <int CW>
+__global__ __launch_bounds__(SYA_TPB) void sy_part_kernel(SyPartArgs A, SySumArgs S) {
+    __shared__ SyPartLds<CW> L;
+    if (blockIdx.x < A.ntiles)
+        sy_part_role<CW>(A, blockIdx.x, L);
+    else
+        sy_sum_role(S, blockIdx.x - A.ntiles, L.u.sum);
+}
+
 bool sy_bucket_eligible(const nrg_config& cf) {
     const u64 span = cf.synth_n - cf.synth_hot_reads;
     return cf.synth_cold_writes >= 1 && cf.synth_cold_writes <= SY_MAX_CW && cf.synth_hot_reads <= SY_MAX_HOT &&
            span <= 1 + (u64)(SY_MAX_NB - 1) * SYB_WORDS && cf.max_batch <= (u64)SY_MAX_TILES * SYA_OPS;
 }
 
-u64 sy_bucket_aux_bytes(const nrg_config& cf) {
+// scratch: V (seen values, u64 per touch), then per buffer parity: E (touch entries), the
+// [bucket][tile] counts and the hot summaries; a chunk's sums may run in the next chunk's
+// partition launch, so E and the hot summaries alternate between two parities
+struct SyAux {
+    u64* V;
+    u32* E[2];
+    u32* cnt;
+    SyHot* hot[2];
+};
+static u64 sy_nb(const nrg_config& cf) {
     const u64 span = cf.synth_n - cf.synth_hot_reads;
     const u64 W = span > 1 ? (span - 1 + SY_MAX_NB - 2) / (SY_MAX_NB - 1) : 1;
-    const u64 NB = 1 + (span - 1 + W - 1) / W;
+    return 1 + (span - 1 + W - 1) / W;
+}
+static SyAux sy_aux(void* base, const nrg_config& cf) {
     const u64 tiles = (cf.max_batch + SYA_OPS - 1) / SYA_OPS;
-    return tiles * SYA_OPS * cf.synth_cold_writes * 12 + NB * tiles * 4 + tiles * cf.synth_hot_reads * sizeof(SyHot) +
-           256;
+    const u64 te = tiles * SYA_OPS * cf.synth_cold_writes;
+    SyAux x;
+    x.V = (u64*)base;
+    x.E[0] = (u32*)(x.V + te);
+    x.E[1] = x.E[0] + te;
+    x.cnt = x.E[1] + te;
+    x.hot[0] = (SyHot*)(((uintptr_t)(x.cnt + sy_nb(cf) * tiles) + 15) & ~(uintptr_t)15);
+    x.hot[1] = x.hot[0] + tiles * cf.synth_hot_reads;
+    return x;
+}
+
+u64 sy_bucket_aux_bytes(const nrg_config& cf) {
+    const u64 tiles = (cf.max_batch + SYA_OPS - 1) / SYA_OPS;
+    const u64 te = tiles * SYA_OPS * cf.synth_cold_writes;
+    return te * (8 + 4 + 4) + sy_nb(cf) * tiles * 4 + 2 * tiles * cf.synth_hot_reads * sizeof(SyHot) + 256;
+}
+
+static SySumArgs sy_sum_args(nrg_ctx* c, const SyDeferred& d) {
+    const nrg_config& cf = c->cfg;
+    SyAux x = sy_aux(c->d_sy_aux, cf);
+    SySumArgs S{};
+    S.blocks = d.t1 - d.t0;
+    S.E = x.E[d.par];
+    S.V = x.V;
+    S.n = d.n;
+    S.lo = d.lo;
+    S.resp_lo = d.rlo;
+    S.resp_hi = d.rhi;
+    S.resp = d.resp;
+    S.some = d.some;
+    S.tile0 = d.t0;
+    S.want = d.want;
+    S.hot = x.hot[d.par];
+    S.ntiles = d.ntiles;
+    S.HR = cf.synth_hot_reads;
+    S.CW = cf.synth_cold_writes;
+    S.words = c->d_words;
+    return S;
+}
+
+static hipError_t sy_launch_part(nrg_ctx* c, const SyPartArgs& A, const SySumArgs& S) {
+    const unsigned grid = A.ntiles + S.blocks;
+    hipStream_t st = c->stream;
+#define SY_PART(CWV) \
+    case CWV: sy_part_kernel<CWV><<<grid, SYA_TPB, 0, st>>>(A, S); break
+    switch (c->cfg.synth_cold_writes) {
+        SY_PART(1); SY_PART(2); SY_PART(3); SY_PART(4); SY_PART(5); SY_PART(6); SY_PART(7); SY_PART(8);
+        default: return hipErrorInvalidValue;
+    }
+#undef SY_PART
+    return hipGetLastError();
+}
+
+// The sums (and hot-word fold) of the last replayed chunk, if still pending.
+hipError_t sy_flush(nrg_ctx* c) {
+    if (!c->sy_pend.valid) return hipSuccess;
+    const SySumArgs S = sy_sum_args(c, c->sy_pend);
+    c->sy_pend.valid = false;
+    SyPartArgs A{};
+    return sy_launch_part(c, A, S);
 }
 
 static hipError_t sy_bucket_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 resp_hi, u64* d_resp, uint8_t* d_some,
@@ -745,42 +869,61 @@ static hipError_t sy_bucket_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 re
     // bucket 0: cold word 0 alone; buckets 1..: W words each (<= 512, sy_bucket_eligible)
     const u32 W = span > 1 ? (u32)((span - 1 + SY_MAX_NB - 2) / (SY_MAX_NB - 1)) : 1u;
     const u32 NB = 1 + (u32)((span - 1 + W - 1) / W);
-    const u64 wm = ((1ull << 40) + W - 1) / W;
-    const u64 span_m = ~0ull / span, hr_m = ~0ull / HR;
     const u32 ntiles = (u32)((n + SYA_OPS - 1) / SYA_OPS);
-    const u64 max_tiles = (cf.max_batch + SYA_OPS - 1) / SYA_OPS;
-    const u64 ring_mask = c->log_size - 1;
-    nrg_synth_op* ring = (nrg_synth_op*)c->d_ring;
-    u64* V = (u64*)c->d_sy_aux;
-    u32* E = (u32*)(V + max_tiles * SYA_OPS * CW);
-    u32* cnt = E + max_tiles * SYA_OPS * CW;
-    SyHot* hot = (SyHot*)(((uintptr_t)(cnt + (u64)NB * max_tiles) + 15) & ~(uintptr_t)15);
+    SyAux x = sy_aux(c->d_sy_aux, cf);
+    const u32 par = c->sy_par;
+    SyPartArgs A;
+    A.src = src;
+    A.ring = (nrg_synth_op*)c->d_ring;
+    A.ring_mask = c->log_size - 1;
+    A.lo = lo;
+    A.n = n;
+    A.span = span;
+    A.span_m = ~0ull / span;
+    A.HR = HR;
+    A.hr_m = ~0ull / HR;
+    A.HW = HW;
+    A.NB = NB;
+    A.W = W;
+    A.wm = ((1ull << 40) + W - 1) / W;
+    A.ntiles = ntiles;
+    A.E = x.E[par];
+    A.cnt_bt = x.cnt;
+    A.hot = x.hot[par];
+    SySumArgs S{};
+    if (c->sy_pend.valid) S = sy_sum_args(c, c->sy_pend);
+    c->sy_pend.valid = false;
     timer_begin(c, "sy_replay");
-#define SY_PART(CWV)                                                                                               \
-    case CWV:                                                                                                      \
-        sy_part_kernel<CWV><<<ntiles, SYA_TPB, 0, st>>>(src, ring, ring_mask, lo, n, span, span_m, HR, hr_m, HW, NB, W, wm, \
-                                                        ntiles, E, cnt, hot);                                              \
-        break
-    switch (CW) {
-        SY_PART(1); SY_PART(2); SY_PART(3); SY_PART(4); SY_PART(5); SY_PART(6); SY_PART(7); SY_PART(8);
-        default: return hipErrorInvalidValue;
-    }
-#undef SY_PART
+    hipError_t e = sy_launch_part(c, A, S);
+    if (e != hipSuccess) return e;
     const size_t dyn = (size_t)(ntiles + 1) * 4 + (size_t)ntiles * 2;
-    sy_bucket_kernel<<<NB, SYB_TPB, dyn, st>>>(E, cnt, ntiles, SYA_OPS * CW, V, c->d_words, cf.synth_n, HR, W, ring,
-                                               ring_mask, lo, (c->exp & 2) ? c->d_dbg : nullptr);
-    const bool want = d_resp != nullptr && resp_lo < lo + n && resp_hi > lo;
-    u32 t0 = 0, t1 = 1;
-    if (want) {
+    sy_bucket_kernel<<<NB, SYB_TPB, dyn, st>>>(x.E[par], x.cnt, ntiles, SYA_OPS * CW, x.V, c->d_words, cf.synth_n, HR,
+                                               W, A.ring, A.ring_mask, lo, (c->exp & 2) ? c->d_dbg : nullptr);
+    timer_end(c, "sy_replay");
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    // this chunk's sums: in the next chunk's partition launch (pipeline = 1) or now
+    SyDeferred d;
+    d.valid = true;
+    d.par = par;
+    d.lo = lo;
+    d.n = n;
+    d.ntiles = ntiles;
+    d.want = d_resp != nullptr && resp_lo < lo + n && resp_hi > lo;
+    d.t0 = 0;
+    d.t1 = 1;
+    if (d.want) {
         const u64 a = resp_lo > lo ? resp_lo - lo : 0;
         const u64 z = resp_hi < lo + n ? resp_hi - lo : n;
-        t0 = (u32)(a / SYA_OPS);
-        t1 = (u32)((z + SYA_OPS - 1) / SYA_OPS);
+        d.t0 = (u32)(a / SYA_OPS);
+        d.t1 = (u32)((z + SYA_OPS - 1) / SYA_OPS);
     }
-    sy_sum_kernel<<<t1 - t0, SYC_TPB, 0, st>>>(E, V, CW, n, lo, resp_lo, resp_hi, d_resp, d_some, t0, want ? 1u : 0u,
-                                               hot, ntiles, HR, c->d_words);
-    timer_end(c, "sy_replay");
-    return hipGetLastError();
+    d.rlo = resp_lo;
+    d.rhi = resp_hi;
+    d.resp = d.want ? d_resp : nullptr;
+    d.some = d.want ? d_some : nullptr;
+    c->sy_pend = d;
+    c->sy_par ^= 1;
+    return c->pipeline ? hipSuccess : sy_flush(c);
 }
 
 hipError_t sy_init(nrg_ctx* c) {
@@ -850,6 +993,8 @@ hipError_t sy_maxscan(nrg_ctx* c, const u32* sk, const u32* sv, u64 n, u32* M) {
 
 hipError_t sy_read(nrg_ctx* c, const nrg_synth_rd* d_ops, u64 n, u64* d_sums) {
     if (n == 0) return hipSuccess;
+    hipError_t e = sy_flush(c);  // reads see the hot words of every replayed chunk
+    if (e != hipSuccess) return e;
     const nrg_config& cf = c->cfg;
     sy_read_kernel<<<(unsigned)((n + 255) / 256), 256, 0, c->stream>>>(
         d_ops, n, c->d_words, cf.synth_n, cf.synth_hot_reads, cf.synth_hot_writes, cf.synth_cold_reads, d_sums);

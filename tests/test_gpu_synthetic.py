@@ -158,3 +158,34 @@ def test_synth_heavy_buckets(nrg, orc, monkeypatch, wo):
     dev = nrg.DeviceReplica(nrg._lib.NRG_DS_SYNTHETIC, 0, max_batch=1 << 18)
     _check_rounds(nrg, orc, dev, orc.Synthetic(), 4, 200_000, 0x4EA + wo, list(range(64)), wo, tweak)
     dev.close()
+
+
+def test_synth_pipelined_rounds(nrg, orc):
+    """pipeline=1: a chunk's per-op sums and hot-word fold ride in the next chunk's partition
+    launch; every round answers into its own buffers, complete after nrg_join. Then reads
+    (ReadOnly, which see the folded hot words), a multi-chunk exec and the final storage, all
+    against the oracle (benches/synthetic.rs:112-195)."""
+    import torch
+
+    n = 100_000
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_SYNTHETIC, 0, max_batch=1 << 17, log_bytes=64 * 4 * (1 << 19), pipeline=1)
+    os_ = orc.Synthetic()
+    outs = []
+    for r in range(4):
+        ops = _ops(orc, n, 1200 + r, list(range(64)), 10 if r == 2 else 0)
+        d_ops = torch.from_numpy(ops.view(np.int64).reshape(n, -1).copy()).cuda()
+        resp = torch.zeros(n, dtype=torch.int64, device="cuda")
+        some = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        dev.sy_round_device(d_ops, n, 1, resp, some)
+        outs.append((d_ops, resp, some, os_.replay(np.stack([ops["tid"], ops["r1"], ops["r2"], ops["op"]], axis=1))))
+    dev.join()
+    torch.cuda.synchronize()
+    for r, (_, resp, some, oresp) in enumerate(outs):
+        np.testing.assert_array_equal(resp.cpu().numpy().view(np.uint64), oresp, err_msg=f"round {r}")
+        assert np.all(some.cpu().numpy() == 1)
+    rd = np.zeros(500, nrg.SYNTH_RD_DTYPE)
+    raw = orc.gen_raw(1500, 77)
+    rd["tid"], rd["r1"], rd["r2"] = raw[0::3] % 8, raw[1::3], raw[2::3]
+    np.testing.assert_array_equal(dev.sy_read(rd), os_.read(np.stack([rd["tid"], rd["r1"], rd["r2"]], axis=1)))
+    _check_rounds(nrg, orc, dev, os_, 1, 3 * (1 << 17) - 11, 1300, [0, 3, 63], 5)
+    dev.close()
