@@ -116,13 +116,16 @@ typedef struct {
     uint32_t stack_push_resp; /* 0: Push -> None (benches/stack.rs:77-80, nr/examples/stack.rs:70-73)
                                  1: Push -> Some(v) (nr/tests/stack.rs:89-92)               */
     uint32_t replica_id;      /* this replica's id (Log::register, ids start at 1)         */
-    uint32_t pipeline;        /* hashmap, opt-in (default 0). 0: every output of an *_async call
-                                 is ordered on the context's stream. 1: the reads of an async
-                                 round run on an internal side stream, overlapping the next
-                                 round's index pass; their outputs (and their key buffer) are
-                                 ordered on the context's stream only after nrg_join(), the
-                                 next call that replays writes on this context, or nrg_sync(). Synchronous
-                                 calls are unaffected (their outputs are complete on return). */
+    uint32_t pipeline;        /* opt-in (default 0). 0: every output of an *_async call is
+                                 ordered on the context's stream. 1: the tail of a replay round
+                                 rides in the next round's launch -- hashmap: the apply + reads;
+                                 stack: the Pops answered from earlier tiles and the commit;
+                                 synthetic: the per-op sums and the hot-word fold. Those outputs
+                                 (and the buffers they read) are complete only after nrg_join(),
+                                 the next call that replays writes on this context, or
+                                 nrg_sync(); give back-to-back rounds distinct response buffers.
+                                 Synchronous calls are unaffected (their outputs are complete on
+                                 return). */
 } nrg_config;
 
 /* Fill `cfg` with the defaults of the reference benches for `ds_kind`. */

@@ -76,12 +76,12 @@ def main():
         tk = json.loads(txt[-1])["roofline"].get("traffic_key")
     except (NameError, ValueError, KeyError, IndexError):
         pass
-    # the timed unit: one hm_round launch, or one stack chunk (st_tile + st_finish kernels)
-    # (stack: st_tile + st_finish kernels; synthetic: sy_part + sy_bucket + sy_sum kernels)
+    # the timed unit: one hm_round launch, one stack round (st_round: tile pass of chunk e +
+    # finish of chunk e-1) or one synthetic round (sy_part with the previous sums + sy_bucket)
     if tk and tk.startswith("stack"):
-        parts = ["st_tile_kernel", "st_finish_kernel"]
+        parts = ["st_round_kernel"]
     elif tk and tk.startswith("synthetic"):
-        parts = ["sy_part_kernel", "sy_bucket_kernel", "sy_sum_kernel"]
+        parts = ["sy_part_kernel", "sy_bucket_kernel"]
     else:
         parts = ["hm_round_kernel"]
 
