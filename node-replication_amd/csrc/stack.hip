@@ -282,23 +282,33 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
             }
             wave_sync();  // the staging rows become the lane stacks
         } else {
-            // partial last tile, a ring wrap or an unaligned caller buffer: one op at a time,
-            // staged through the (not yet used) stack rows so that val[] keeps static indices
-            for (int q = 0; q < SW_OPS; q++) {
-                const u64 i = base + q;
-                u32 v = 0;
-                if (i < n) {
-                    const nrg_stack_op o = src ? src[i] : ring[(lo + i) & ring_mask];
-                    if (src) ring[(lo + i) & ring_mask] = o;
-                    v = o.val;
-                    pm |= (u32)(o.op != 0) << q;
-                    qm |= (u32)(o.op == 0) << q;
+            // partial last wave, a ring wrap or an unaligned caller buffer: 8-B op loads, still
+            // coalesced and all in flight (op u = 64 i + lane of the wave), then through LDS
+            // (row u / 32, column (u % 32) ^ (row % 32)) to the lane that replays it
+            const u64 nw = n > wbase ? (n - wbase < 64 * SW_OPS ? n - wbase : 64 * SW_OPS) : 0;
+            uint2* s2 = reinterpret_cast<uint2*>(s_wave[wv]);
+#pragma unroll 8
+            for (int i = 0; i < SW_OPS; i++) {
+                const u32 u = 64 * i + lane;
+                nrg_stack_op o{0, 0};  // past the chunk: masked out below
+                if (u < nw) {
+                    const u64 r = (lo + wbase + u) & ring_mask;
+                    o = src ? src[wbase + u] : ring[r];
+                    if (src) ring[r] = o;
                 }
-                s_stk[q][lane] = v;
+                const u32 row = u >> 5;
+                s2[row * 32 + ((u & 31) ^ (row & 31))] = uint2{o.val, o.op};
             }
-#pragma unroll
-            for (int q = 0; q < SW_OPS; q++) val[q] = s_stk[q][lane];
             wave_sync();
+#pragma unroll
+            for (int q = 0; q < SW_OPS; q++) {
+                const uint2 y = s2[lane * 32 + (q ^ (lane & 31))];
+                const bool in = (u32)(lane * SW_OPS + q) < nw;
+                val[q] = y.x;
+                pm |= (u32)(in && y.y != 0) << q;
+                qm |= (u32)(in && y.y == 0) << q;
+            }
+            wave_sync();  // the staging rows become the lane stacks
         }
     }
     ST_MARK(1);

@@ -117,14 +117,17 @@ def test_group_join_one_rank_hashmap(nrg, orc):
     dev.close()
 
 
-def test_group_stack_rounds(nrg, orc):
-    """A stack replica group: pop responses for the member's own segment, final stack equal."""
+@pytest.mark.parametrize("pipeline", [0, 1])
+def test_group_stack_rounds(nrg, orc, pipeline):
+    """A stack replica group: pop responses for the member's own segment, final stack equal;
+    with pipeline = 1 each round's finish rides in the next round's launch (nrg_group_sync
+    completes the last one)."""
     import torch
 
     L = nrg._lib
     lib = L.load()
     cfg = L.default_config(L.NRG_DS_STACK)
-    cfg.max_batch, cfg.stack_capacity = 1 << 16, 1 << 20
+    cfg.max_batch, cfg.stack_capacity, cfg.pipeline = 1 << 16, 1 << 20, pipeline
     g = C.c_void_p()
     L.check(lib.nrg_group_open((C.c_int * 1)(0), 1, C.byref(cfg), C.byref(g)), "nrg_group_open")
     ctx = lib.nrg_group_replica(g, 0)
@@ -154,4 +157,44 @@ def test_group_stack_rounds(nrg, orc):
     m = C.c_uint64()
     L.check(lib.nrg_stack_dump(ctx, out.ctypes.data_as(C.c_void_p), n.value, C.byref(m)))
     np.testing.assert_array_equal(out[:m.value], st.dump())
+    L.check(lib.nrg_group_close(g))
+
+
+@pytest.mark.parametrize("pipeline", [0, 1])
+def test_group_synth_rounds(nrg, orc, pipeline):
+    """A synthetic replica group (benches/synthetic.rs:112-195): per-op sums for the member's
+    own segment and the final storage equal to the oracle; with pipeline = 1 each round's sums
+    ride in the next round's partition launch."""
+    import torch
+
+    L = nrg._lib
+    lib = L.load()
+    cfg = L.default_config(L.NRG_DS_SYNTHETIC)
+    cfg.max_batch, cfg.pipeline = 1 << 16, pipeline
+    g = C.c_void_p()
+    L.check(lib.nrg_group_open((C.c_int * 1)(0), 1, C.byref(cfg), C.byref(g)), "nrg_group_open")
+    ctx = lib.nrg_group_replica(g, 0)
+    os_ = orc.Synthetic()
+    outs = []
+    for r in range(4):
+        n = 20000 + 3000 * r
+        raw = orc.gen_raw(4 * n, 700 + r)
+        recs = np.zeros(n, nrg.SYNTH_OP_DTYPE)
+        recs["tid"], recs["r1"], recs["r2"] = raw[0::4] % 64, raw[1::4], raw[2::4]
+        recs["op"] = (raw[3::4] % 100 >= 5).astype(np.uint64)
+        d_ops = torch.from_numpy(recs.view(np.int64).reshape(n, -1).copy()).cuda()
+        resp = torch.full((n,), -1, dtype=torch.int64, device="cuda")
+        some = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+        rd = L.Round()
+        rd.recs, rd.n, rd.resp, rd.some = d_ops.data_ptr(), n, resp.data_ptr(), some.data_ptr()
+        L.check(lib.nrg_group_round_async(g, C.byref(rd), None))
+        outs.append((d_ops, resp, some, os_.replay(np.stack([recs["tid"], recs["r1"], recs["r2"], recs["op"]], axis=1))))
+    L.check(lib.nrg_group_sync(g))
+    for r, (_, resp, some, oresp) in enumerate(outs):
+        np.testing.assert_array_equal(resp.cpu().numpy().view(np.uint64), oresp, err_msg=f"round {r}")
+        assert np.all(some.cpu().numpy() == 1)
+    words = np.zeros(cfg.synth_n, np.uint64)
+    m = C.c_uint64()
+    L.check(lib.nrg_synth_dump(ctx, words.ctypes.data_as(C.c_void_p), cfg.synth_n, C.byref(m)))
+    np.testing.assert_array_equal(words[:m.value], os_.dump())
     L.check(lib.nrg_group_close(g))

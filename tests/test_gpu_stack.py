@@ -188,3 +188,35 @@ def test_stack_pipelined_rounds(nrg, orc, init_n, n, rounds):
     assert dev.st_peek() == os_.peek()
     np.testing.assert_array_equal(dev.st_dump(), os_.dump())
     dev.close()
+
+
+def test_stack_op_words_and_load_paths(nrg, orc):
+    """Any nonzero op word is a Push (the oracle's `if ops[i]`); rounds through both load paths of
+    the tile pass: whole 16-B-aligned waves (coalesced 16-B loads) and partial or misaligned
+    waves (8-B loads) -- odd round sizes shift the ring position off 16-B alignment and wrap it."""
+    import torch
+
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_STACK, 0, max_batch=1 << 16, stack_capacity=1 << 20,
+                            log_bytes=64 * 32768)
+    init = np.arange(20, dtype=np.uint32)
+    dev.st_init(init)
+    os_ = orc.Stack(init)
+    rng = np.random.default_rng(5)
+    for r, n in enumerate([4096, 3001, 8192 + 5, 2048 * 5 + 1, 6000]):
+        vals = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+        ops = rng.choice(np.array([0, 0, 1, 2, 0xFFFFFFFF], np.uint32), n)
+        if r % 2:
+            first = dev.log_append(_ops(vals, ops), 1)
+            resp, some = dev.log_exec(first, first + n)
+        else:
+            d_ops = torch.from_numpy(_ops(vals, ops).view(np.int64).copy()).cuda()
+            rt = torch.zeros(n, dtype=torch.int32, device="cuda")
+            st = torch.zeros(n, dtype=torch.uint8, device="cuda")
+            dev.st_round_device(d_ops, n, 1, rt, st)
+            torch.cuda.synchronize()
+            resp, some = rt.cpu().numpy().view(np.uint32), st.cpu().numpy()
+        oresp, osome = os_.replay(vals, ops)
+        np.testing.assert_array_equal(some, osome, err_msg=f"round {r}")
+        np.testing.assert_array_equal(resp, oresp, err_msg=f"round {r}")
+    np.testing.assert_array_equal(dev.st_dump(), os_.dump())
+    dev.close()
