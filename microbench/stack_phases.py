@@ -31,9 +31,10 @@ resps = [torch.empty(N, dtype=torch.int32, device="cuda") for _ in range(2)]
 somes = [torch.empty(N, dtype=torch.uint8, device="cuda") for _ in range(2)]
 tiles = (N + 8191) // 8192
 names = ["loads", "local pass", "scan+responses", "lookback", "query list+sparse table", "queries", "table"]
-acc = np.zeros((tiles, 8))
+acc = np.zeros((tiles, 9))
 R = 20
 fin = []
+q8 = []
 for r in range(R + 3):
     for i in range(BB):  # pipeline=1: a round's finish rides in the next launch
         dev.st_round_device(opsl[i], N, 1, resps[i & 1], somes[i & 1])
@@ -43,10 +44,12 @@ for r in range(R + 3):
     full = np.zeros(256 * 16, np.uint64)
     L.check(L.load().nrg_test_debug_read(dev.handle, full.ctypes.data_as(C.c_void_p), 256 * 16))
     fb = full.reshape(256, 16)[128:128 + tiles, :2].astype(np.float64)
-    t = buf.reshape(tiles, 16)[:, :8].astype(np.float64)
+    t = buf.reshape(tiles, 16)[:, :9].astype(np.float64)
     if r >= 3 and fb[:, 0].min() > 0:
         o = min(t[:, 0].min(), fb[:, 0].min())
         fin.append((fb[:, 0].min() - o, fb[:, 0].max() - o, fb[:, 1].max() - o, t[:, 0].min() - o, t[:, 7].max() - o))
+    if r >= 3:
+        q8.append((t[:, 8] - t[:, 5]).mean() / 100.0)
     if r >= 3:
         acc += t - t[:, :1].min()
 acc /= R
@@ -61,3 +64,5 @@ if fin:
     f = np.array(fin).mean(0) / 100.0
     print("fused finish of the previous chunk (us from the launch's first workgroup): start %.2f..%.2f, last end %.2f;"
           " tiles start %.2f, last tile end %.2f" % tuple(f))
+if q8:
+    print("  of the unmatched-Pop phase, the intra-tile queries: mean %.2f us" % np.mean(q8))

@@ -558,6 +558,7 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
     // the cross-tile Pops' pre-chunk content, one per thread (all loads in flight together): a
     // slot the previous chunk wrote comes from its owner's table (that chunk's commit runs in
     // this launch), any other from the stack
+    ST_MARK(8);  // queries done (stored after the phases 0..7)
     const u32 ucnt = s_ucnt;
     for (u32 h = t; h < ucnt; h += ST_LANES) {
         const u32 e = h < ST_XL ? s_xl[h] : tl.upop[(u64)tile * ST_TILE + h];
