@@ -220,7 +220,8 @@ hipError_t copy_segments(nrg_ctx* c, const void* d_base, u32 nseg, u64 seg_strid
 // stack.hip
 hipError_t st_replay_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 resp_hi, uint32_t* d_resp,
                            uint8_t* d_some, const nrg_stack_op* src = nullptr);
-u64 st_aux_bytes(u64 max_batch);  // size of nrg_ctx::d_st_aux
+u64 st_aux_bytes(u64 max_batch);   // size of nrg_ctx::d_st_aux
+u64 st_desc_words(u64 max_batch);  // u32 words of look-back descriptors the stack needs
 
 // synthetic.hip
 hipError_t sy_init(nrg_ctx* c);

@@ -366,14 +366,17 @@ int nrg_open(int dev, const nrg_config* cfg_in, nrg_ctx** out) {
             return NRG_E_INVAL;
         }
         OPEN_CHK(hipMalloc(&c->d_stack, cf.stack_capacity * sizeof(uint32_t)));
-        c->scan_desc_words = 2 * (32 + (mb + 2047) / 2048);
+        // look-back descriptors of both tile parities (stack.hip st_pass), and at least what
+        // nrg_test_maxscan's 2048-key tiles use
+        c->scan_desc_words = std::max<uint64_t>(st_desc_words(mb), 2 * (32 + (mb + 2047) / 2048));
         OPEN_CHK(hipMalloc(&c->d_scan_desc, c->scan_desc_words * 4));
         OPEN_CHK(hipMemsetAsync(c->d_scan_desc, 0, c->scan_desc_words * 4, c->stream));
         OPEN_CHK(hipMalloc(&c->d_st_aux, st_aux_bytes(mb)));
         c->pipeline = cf.pipeline != 0;
         if (const char* e = std::getenv("NRG_PIPELINE")) c->pipeline = std::atoi(e) != 0;
         if (const char* e = std::getenv("NRG_EXP")) c->exp = (uint32_t)std::atoi(e);
-        if (c->exp & 2) OPEN_CHK(hipMalloc(&c->d_dbg, ((mb + 2047) / 2048) * 16 * sizeof(uint64_t)));
+        // diagnostic stamps: tile t at [t * 16], the fused finish workgroups at [(128 + f) * 16]
+        if (c->exp & 2) OPEN_CHK(hipMalloc(&c->d_dbg, std::max<uint64_t>(256, (mb + 2047) / 2048) * 16 * sizeof(uint64_t)));
     } else {
         const uint64_t T = cf.synth_hot_writes + cf.synth_cold_writes;
         if (!cf.synth_n || cf.synth_hot_reads == 0 || cf.synth_n <= cf.synth_hot_reads || T == 0 || T > 64 ||

@@ -1,41 +1,39 @@
 // stack.hip — Stack replica replay on gfx950 (benches/stack.rs:36-84, nr/tests/stack.rs:31-96).
 //
 // Vec<u32>::push/pop in log order, with pop on an empty stack returning None and leaving
-// the depth at 0. Each op is the function f(x) = max(a, x + b) of the depth before it
-// (Push: b=+1, a=1; Pop: b=-1, a=0); these compose associatively
-//      (f then g) = (b_f + b_g, max(a_g, a_f + b_g)),
-// so the depth before every op is an exclusive scan (one pass, decoupled look-back).
+// the depth at 0. A run of ops maps the depth x before it to max(x + e, e - m), where m <= 0 is
+// the unclamped minimum of its ±1 walk and e its end; these compose associatively, so every
+// lane's start depth is an exclusive scan (one pass, decoupled look-back over tiles).
 //
 // A Push at depth d writes slot d; a Pop at depth d > 0 reads slot d-1. Because the depth
-// moves by ±1, the touches of one slot (crossings of the edge (s, s+1)) alternate Push/Pop in
-// log order. No global sort is needed to pair them:
-//   * inside a tile of 2048 ops, sorting the tile's touches by (slot, position) in LDS puts
-//     every Pop right after the Push it returns, unless the Pop heads its slot's group;
-//   * a Pop that heads its group started its tile above the slot, so its Push is the last
-//     Push to that slot in the NEAREST EARLIER TILE WHOSE MINIMUM DEPTH IS <= the slot (every
-//     tile in between stayed above the slot and so never touched it; that tile went at or below
-//     the slot and ended above it, so its last op on the slot was a Push) — or, with no such
-//     tile, the slot's content before the chunk.
-// Each tile publishes its minimum depth and a table "last Push to slot tmin + r" (u16
-// positions), so the cross-tile Pops (a few percent for random ops) walk back over tile minima
-// only. The chunk's final content of a slot s below the final depth is its last Push, which
-// lies in the LAST tile whose minimum depth is <= s (the walk never comes back down to s after
-// it); that tile's table already holds it, so st_finish_kernel commits, per tile, the levels
-// [tmin, min(tile end depth, minimum depth of every later tile)).
-//
-// Kernels: st_tile_kernel (scan + in-tile pairing + tables), st_finish_kernel (cross-tile
-// Pops, last Pushes -> stack, depth update).
+// moves by ±1, the touches of one slot alternate Push/Pop in log order, so no sort is needed
+// to pair them:
+//   * each lane replays its own ops against a stack of its own in LDS;
+//   * a Pop below the lane's start reads the level's last Push in the nearest earlier lane
+//     whose lowest level is <= it (every lane in between stays above it);
+//   * with no such lane in the tile, the nearest earlier TILE whose minimum depth is <= the
+//     slot holds it (its table "last Push to slot tmin + r"), or else the slot's content
+//     before the chunk;
+//   * the chunk's final content of a slot s below the final depth is its last Push, in the
+//     LAST tile whose minimum depth is <= s: that tile commits the levels
+//     [tmin, min(tile end depth, minimum depth of every later tile)).
+// One kernel, st_round_kernel: the tile pass of chunk e and the finish (cross-tile Pops,
+// commit) of chunk e-1 in one launch.
 #include "internal.hpp"
 
 namespace nrg {
 
-constexpr int SW_OPS = 32;                  // ops per lane, replayed in order by that lane
+#ifndef NRG_ST_OPS
+#define NRG_ST_OPS 16  // measured at 1M-op rounds: 8 -> 21.5 us, 16 -> 20.6 us, 32 -> 22.7 us
+#endif
+constexpr int SW_OPS = NRG_ST_OPS;          // ops per lane, replayed in order by that lane (<= 32)
 constexpr int ST_WAVES = 4;                 // a tile is one workgroup of 4 waves
 constexpr int ST_LANES = 64 * ST_WAVES;     // 256 lanes
-constexpr int ST_TILE = ST_LANES * SW_OPS;  // 8192 ops
-constexpr int ST_PB = 13;                   // bits of a position in the tile
+constexpr int ST_TILE = ST_LANES * SW_OPS;  // 4096 ops
+constexpr int ST_PB = SW_OPS == 32 ? 13 : SW_OPS == 16 ? 12 : 11;  // bits of a position in the tile
 constexpr u32 ST_PMASK = (1u << ST_PB) - 1;
 static_assert(ST_TILE == 1 << ST_PB, "positions");
+static_assert(SW_OPS == 8 || SW_OPS == 16 || SW_OPS == 32, "ops per lane");
 
 struct Fn {
     long long b;
@@ -170,7 +168,7 @@ __device__ __forceinline__ void me_then(int& m, int& e, int m2, int e2) {
     e += e2;
 }
 
-// One workgroup per 8192-op tile; lane t of its 256 replays ops [32 t, 32 t + 32) in order.
+// One workgroup per tile of 256 * SW_OPS ops; lane t replays ops [SW_OPS t, SW_OPS (t + 1)) in order.
 //   1. Local pass: every lane keeps its own stack in LDS (row = height, column = lane, so the
 //      64 lanes of a wave never share a bank). A Pop with a non-empty local stack returns its
 //      top; a Pop on an empty local stack is "unmatched" (it reaches below the lane's start).
@@ -208,8 +206,8 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
     uint8_t* __restrict__ some = A.some;
     const int t = threadIdx.x, wv = t >> 6, lane = t & 63;
     const u64 tbase = (u64)tile * ST_TILE;
-    const u64 wbase = tbase + (u64)wv * (64 * SW_OPS);  // the wave's 2048 ops
-    const u64 base = tbase + (u64)t * SW_OPS;           // the lane's 32 ops
+    const u64 wbase = tbase + (u64)wv * (64 * SW_OPS);  // the wave's ops
+    const u64 base = tbase + (u64)t * SW_OPS;           // the lane's ops
     const bool full = base + SW_OPS <= n;
 #define ST_MARK(K) \
     if (dbg && t == 0) dbg[(u64)tile * 16 + (K)] = wall_clock64()
@@ -236,7 +234,7 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
     long long* s_pg8 = s_ptm + P.tiles;
     long long* s_pgm = s_pg8 + P.tiles / 8 + 1;
 
-    // ---- load the lane's 32 ops (and write the log copy when they come from the caller) ----
+    // ---- load the lane's ops (and write the log copy when they come from the caller) ----
     u32 val[SW_OPS];
     u32 pm = 0, qm = 0;  // Push / Pop bit per op (padding past n is neither)
     {
@@ -266,15 +264,16 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
                 }
             }
             uint4* s4 = reinterpret_cast<uint4*>(s_wave[wv]);
+            constexpr int UPR = SW_OPS / 2;  // 16-B units per lane
 #pragma unroll
             for (int i = 0; i < SW_OPS / 2; i++) {
-                const int u = 64 * i + lane, r = u >> 4;
-                s4[r * 16 + ((u & 15) ^ (r & 15))] = x[i];
+                const int u = 64 * i + lane, r = u / UPR;
+                s4[r * UPR + ((u % UPR) ^ (r % UPR))] = x[i];
             }
             wave_sync();
 #pragma unroll
             for (int j = 0; j < SW_OPS / 2; j++) {
-                const uint4 y = s4[lane * 16 + (j ^ (lane & 15))];
+                const uint4 y = s4[lane * UPR + (j ^ (lane % UPR))];
                 val[2 * j] = y.x;
                 val[2 * j + 1] = y.z;
                 pm |= (u32)(y.y != 0) << (2 * j) | (u32)(y.w != 0) << (2 * j + 1);
@@ -296,13 +295,13 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
                     o = src ? src[wbase + u] : ring[r];
                     if (src) ring[r] = o;
                 }
-                const u32 row = u >> 5;
-                s2[row * 32 + ((u & 31) ^ (row & 31))] = uint2{o.val, o.op};
+                const u32 row = u / SW_OPS;
+                s2[row * SW_OPS + ((u % SW_OPS) ^ (row % SW_OPS))] = uint2{o.val, o.op};
             }
             wave_sync();
 #pragma unroll
             for (int q = 0; q < SW_OPS; q++) {
-                const uint2 y = s2[lane * 32 + (q ^ (lane & 31))];
+                const uint2 y = s2[lane * SW_OPS + (q ^ (lane % SW_OPS))];
                 const bool in = (u32)(lane * SW_OPS + q) < nw;
                 val[q] = y.x;
                 pm |= (u32)(in && y.y != 0) << q;
@@ -380,17 +379,22 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
         const bool in = full && g0 >= resp_lo && g0 + SW_OPS <= resp_hi;
         u32* rp = resp + (g0 - resp_lo);
         uint8_t* sp = some + (g0 - resp_lo);
-        if (in && !((uintptr_t)rp & 15) && !((uintptr_t)sp & 15)) {
+        if (in && !((uintptr_t)rp & 15) && !((uintptr_t)sp & (SW_OPS >= 16 ? 15 : 7))) {
 #pragma unroll
             for (int j = 0; j < SW_OPS / 4; j++)
                 ((uint4*)rp)[j] = uint4{rt[4 * j], rt[4 * j + 1], rt[4 * j + 2], rt[4 * j + 3]};
+            if constexpr (SW_OPS >= 16) {
 #pragma unroll
-            for (int j = 0; j < SW_OPS / 16; j++) {
-                uint4 b;
-                u32* bb = (u32*)&b;
+                for (int j = 0; j < SW_OPS / 16; j++) {
+                    uint4 b;
+                    u32* bb = (u32*)&b;
 #pragma unroll
-                for (int k = 0; k < 4; k++) bb[k] = (((smask >> (16 * j + 4 * k)) & 15u) * 0x204081u) & 0x01010101u;
-                ((uint4*)sp)[j] = b;
+                    for (int k = 0; k < 4; k++) bb[k] = (((smask >> (16 * j + 4 * k)) & 15u) * 0x204081u) & 0x01010101u;
+                    ((uint4*)sp)[j] = b;
+                }
+            } else {  // 8 ops per lane: one 8-B store
+                *(uint2*)sp = uint2{((smask & 15u) * 0x204081u) & 0x01010101u,
+                                    (((smask >> 4) & 15u) * 0x204081u) & 0x01010101u};
             }
         } else if (resp) {
 #pragma unroll
@@ -760,6 +764,9 @@ hipError_t st_replay_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 resp_hi, 
     c->st_par ^= 1;
     return c->pipeline ? hipSuccess : st_flush(c);
 }
+
+// [32 u64 unused] [parity][max tiles] u64 (st_pass)
+u64 st_desc_words(u64 max_batch) { return 2 * (32 + 2 * ((max_batch + ST_TILE - 1) / ST_TILE)); }
 
 u64 st_aux_bytes(u64 max_batch) { return 2 * st_parity_bytes((max_batch + ST_TILE - 1) / ST_TILE); }
 
