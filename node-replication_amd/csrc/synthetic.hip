@@ -314,6 +314,7 @@ struct SyPartArgs {
     const nrg_synth_op* src;  // the chunk's ops in a caller buffer, or nullptr (ring)
     nrg_synth_op* ring;
     u64 ring_mask, lo, n, span, span_m;
+    u32 w64;  // 2^64 mod span
     u32 HR;
     u64 hr_m;
     u32 HW, NB, W;
@@ -360,6 +361,7 @@ __device__ __forceinline__ void sy_part_role(const SyPartArgs& A, u32 tile, SyPa
     const nrg_synth_op* __restrict__ src = A.src;
     nrg_synth_op* ring = A.ring;
     const u64 ring_mask = A.ring_mask, lo = A.lo, n = A.n, span = A.span, span_m = A.span_m, hr_m = A.hr_m, wm = A.wm;
+    const u32 w64 = A.w64;
     const u32 HR = A.HR, HW = A.HW, NB = A.NB, W = A.W, ntiles = A.ntiles;
     u32* __restrict__ E = A.E;
     u32* __restrict__ cnt_bt = A.cnt_bt;
@@ -394,8 +396,9 @@ __device__ __forceinline__ void sy_part_role(const SyPartArgs& A, u32 tile, SyPa
         for (u32 h = 0; h < HR; h++) {
             int ls = -1;
             u32 js = 0, tot = 0;
-            for (u32 j = 0; j < HW; j++) {
-                const bool on = hot_ok && (h0 + j) % HR == h;
+            // (h0 + j) % HR, stepped (no integer division per hot touch)
+            for (u32 j = 0, hj = h0; j < HW; j++, hj = hj + 1 == HR ? 0u : hj + 1) {
+                const bool on = hot_ok && hj == h;
                 const u64 m = __ballot(on);
                 const u64 sm = __ballot(on && set);
                 tot += (u32)__popcll(m);
@@ -413,8 +416,8 @@ __device__ __forceinline__ void sy_part_role(const SyPartArgs& A, u32 tile, SyPa
             if (ls >= 0) {
                 after = 0;
                 const u64 gt = ls == 63 ? 0ull : (~0ull << (ls + 1));
-                for (u32 j = 0; j < HW; j++) {
-                    const u64 m = __ballot(hot_ok && (h0 + j) % HR == h);
+                for (u32 j = 0, hj = h0; j < HW; j++, hj = hj + 1 == HR ? 0u : hj + 1) {
+                    const u64 m = __ballot(hot_ok && hj == h);
                     after += (u32)__popcll(m & gt) + ((j > js && ((m >> ls) & 1ull)) ? 1u : 0u);
                 }
                 base = shfl_u64(o.tid, ls);
@@ -425,12 +428,21 @@ __device__ __forceinline__ void sy_part_role(const SyPartArgs& A, u32 tile, SyPa
             }
         }
         // cold touches: this lane's CW words, then rank them in log order (op-major) per bucket
+        // word k is (r1·tid + k·r2) mod 2^64 mod span: two reciprocal reductions per op, then
+        // stepped in 32 bits -- x += r2 mod span, less 2^64 mod span when the u64 sum wraps
         u64 begin = o.r1 * o.tid;
+        u32 xm = (u32)mod_recip(begin, span, span_m);
+        const u32 r2m = (u32)mod_recip(o.r2, span, span_m), sp32 = (u32)span;
 #pragma unroll
         for (int k = 0; k < CW; k++) {
-            const u32 x = (u32)mod_recip(begin, span, span_m) + HR;
-            begin += o.r2;
-            s_u.r.words[w][lane * CW + k] = valid ? (x | (set ? SETBIT : 0u)) : NOTOUCH;
+            s_u.r.words[w][lane * CW + k] = valid ? ((xm + HR) | (set ? SETBIT : 0u)) : NOTOUCH;
+            const u64 nb = begin + o.r2;
+            const bool wrap = nb < begin;
+            begin = nb;
+            u32 t = xm + r2m;  // < 2 span < 2^32
+            t = t >= sp32 ? t - sp32 : t;
+            if (wrap) t = t >= w64 ? t - w64 : t + (sp32 - w64);
+            xm = t;
         }
         wave_lds_sync();
 #pragma unroll
@@ -880,6 +892,7 @@ static hipError_t sy_bucket_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 re
     A.n = n;
     A.span = span;
     A.span_m = ~0ull / span;
+    A.w64 = (u32)((~0ull % span + 1) % span);
     A.HR = HR;
     A.hr_m = ~0ull / HR;
     A.HW = HW;
