@@ -410,22 +410,98 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
     ST_MARK(3);
 
     // ---- 3. look-back (wave 0): compose the aggregates of ALL earlier tiles (64 runs in
-    // parallel, 8 loads in flight per lane); the highest lane holds the oldest run ----
+    // parallel, 8 loads in flight per lane; the highest lane holds the oldest run). The loads of
+    // the first 8 per lane are issued now and land while the query structures are built: those
+    // need the tile's start depth only when the stack empties inside the tile, so they are
+    // built for the unclamped walk and rebuilt in that (rare) case. ----
     long long* sdepth = &ctl->depth0;             // depth after the chunk of each parity
     const long long d0 = sdepth[A.par ^ 1];        // depth before this chunk
+    const int np = (int)tile;
+    const int G = (np + 63) / 64;
+    const int r0 = (63 - lane) * G;
+    constexpr int B = 8;
+    u64 v0[B];
     if (wv == 0) {
-        const int np = (int)tile;
-        const int G = (np + 63) / 64;
-        const int r0 = (63 - lane) * G;
+#pragma unroll
+        for (int q = 0; q < B; q++) {
+            const int idx = r0 + q;
+            v0[q] = (q < G && idx < np) ? __hip_atomic_load(&desc[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+        }
+    }
+
+    // Query structures for lane levels relative to the tile's lowest level: lane minimum amin_,
+    // start dt_, and uq_ unmatched Pops that find an element. Outputs: s_min, the sparse table
+    // s_sp, `later` (minimum over the later lanes) and the wave's query list s_up[0, total).
+    int later = 0, total = 0;
+    auto build = [&](int amin_, int dt_, int uq_) {
+        s_min[t] = amin_;
+        // sparse table: levels 0..6 inside the wave (windows clipped at the wave's first lane;
+        // the part in earlier waves is added below), inclusive suffix minimum inside the wave
+        int spw[7];
+        spw[0] = amin_;
+#pragma unroll
+        for (int j = 1; j < 7; j++) {
+            const int o = __shfl_up(spw[j - 1], 1 << (j - 1), 64);
+            spw[j] = lane >= (1 << (j - 1)) && o < spw[j - 1] ? o : spw[j - 1];
+        }
+        int sf = amin_;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int o = __shfl_down(sf, off, 64);
+            if (lane + off < 64) sf = o < sf ? o : sf;
+        }
+        later = __shfl_down(sf, 1, 64);
+        if (lane == 63) later = 1 << 30;
+        s_suf[t] = sf;
+        if (lane == 0) s_wmin[wv] = sf;
+        // the wave's query list: lane t's unmatched Pops k < uq_
+        int inc = uq_;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int o = __shfl_up(inc, off, 64);
+            if (lane >= off) inc += o;
+        }
+        total = __shfl(inc, 63, 64);
+        {
+            u32 um = umask;
+            for (int k = 0, h = inc - uq_; k < uq_; k++, h++) {
+                const int q = __builtin_ctz(um);
+                um &= um - 1;
+                s_up[h] = ((u32)(dt_ - 1 - k) << ST_PB) | ((u32)t * SW_OPS + (u32)q);
+            }
+        }
+        __syncthreads();
+        // complete the windows (t - 2^j, t] that reach into earlier waves: a suffix of the
+        // previous wave (its inclusive suffix minimum) and, for level 7, whole waves before it
+#pragma unroll
+        for (int j = 0; j < 7; j++) {
+            int m = spw[j];
+            if (wv > 0 && lane < (1 << j) - 1) {
+                const int o = s_suf[t - (1 << j) + 1];
+                m = o < m ? o : m;
+            }
+            s_sp[j][t] = (unsigned short)m;  // levels are < 2 * ST_TILE
+        }
+        int m7 = spw[6];
+        if (wv > 0) m7 = s_wmin[wv - 1] < m7 ? s_wmin[wv - 1] : m7;
+        if (wv > 1 && lane < 63) m7 = s_suf[t - 127] < m7 ? s_suf[t - 127] : m7;
+        s_sp[7][t] = (unsigned short)m7;
+        for (int w = wv + 1; w < ST_WAVES; w++) later = s_wmin[w] < later ? s_wmin[w] : later;
+    };
+    // unclamped walk (D + M >= 0): amin = xe - nun - M, start xe - M, every unmatched Pop reads
+    build(xe - (int)nun - M, xe - M, (int)nun);
+
+    if (wv == 0) {
         Fn acc = FN_ID;
-        constexpr int B = 8;
         for (int g0 = 0; g0 < G; g0 += B) {
             u64 v[B];
 #pragma unroll
             for (int q = 0; q < B; q++) {
                 const int idx = r0 + g0 + q;
-                v[q] = (g0 + q < G && idx < np) ? __hip_atomic_load(&desc[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                                : 0ull;
+                v[q] = g0 == 0 ? v0[q]
+                               : ((g0 + q < G && idx < np)
+                                      ? __hip_atomic_load(&desc[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                      : 0ull);
             }
             // predecessors publish right after their local pass: re-poll only what is missing
             for (u32 spins = 0;; spins++) {
@@ -463,62 +539,8 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
     const int aend_r = amin + (int)top;  // the lane's end depth: max(Dt + e, top) - T0
     if (t == ST_LANES - 1 && tile == A.tiles - 1) sdepth[A.par] = T0 + aend_r;
     if (Dt + hmax > (long long)cap || (long long)topmax > (long long)cap) atomicOr(&ctl->err, ERR_CAPACITY);
-    s_min[t] = amin;
-    // sparse table: levels 0..6 inside the wave (windows clipped at the wave's first lane; the
-    // part in earlier waves is added below), inclusive suffix minimum inside the wave
-    int spw[7];
-    spw[0] = amin;
-#pragma unroll
-    for (int j = 1; j < 7; j++) {
-        const int o = __shfl_up(spw[j - 1], 1 << (j - 1), 64);
-        spw[j] = lane >= (1 << (j - 1)) && o < spw[j - 1] ? o : spw[j - 1];
-    }
-    int sf = amin;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const int o = __shfl_down(sf, off, 64);
-        if (lane + off < 64) sf = o < sf ? o : sf;
-    }
-    int later = __shfl_down(sf, 1, 64);
-    if (lane == 63) later = 1 << 30;
-    s_suf[t] = sf;
-    if (lane == 0) s_wmin[wv] = sf;
-    // the wave's query list: lane t's unmatched Pops k < min(nun, D_t) (the rest find it empty)
-    const int uq = (int)(Dt < (long long)nun ? Dt : (long long)nun);
-    int inc = uq;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const int o = __shfl_up(inc, off, 64);
-        if (lane >= off) inc += o;
-    }
-    const int total = __shfl(inc, 63, 64);
-    {
-        u32 um = umask;
-        for (int k = 0, h = inc - uq; k < uq; k++, h++) {
-            const int q = __builtin_ctz(um);
-            um &= um - 1;
-            s_up[h] = ((u32)(dt - 1 - k) << ST_PB) | ((u32)t * SW_OPS + (u32)q);
-        }
-    }
-    __syncthreads();
-    // complete the windows (t - 2^j, t] that reach into earlier waves: a suffix of the previous
-    // wave (its inclusive suffix minimum) and, for level 7, whole waves before it
-    {
-#pragma unroll
-        for (int j = 0; j < 7; j++) {
-            int m = spw[j];
-            if (wv > 0 && lane < (1 << j) - 1) {
-                const int o = s_suf[t - (1 << j) + 1];
-                m = o < m ? o : m;
-            }
-            s_sp[j][t] = (unsigned short)m;  // levels are < 2 * ST_TILE
-        }
-        int m7 = spw[6];
-        if (wv > 0) m7 = s_wmin[wv - 1] < m7 ? s_wmin[wv - 1] : m7;
-        if (wv > 1 && lane < 63) m7 = s_suf[t - 127] < m7 ? s_suf[t - 127] : m7;
-        s_sp[7][t] = (unsigned short)m7;
-        for (int w = wv + 1; w < ST_WAVES; w++) later = s_wmin[w] < later ? s_wmin[w] : later;
-    }
+    // the stack empties inside the tile: Pops at depth 0 are no-ops, levels shift (block-uniform)
+    if (D + M < 0) build(amin, dt, (int)(Dt < (long long)nun ? Dt : (long long)nun));
     __syncthreads();
     ST_MARK(5);
 
