@@ -360,7 +360,7 @@ int nrg_open(int dev, const nrg_config* cfg_in, nrg_ctx** out) {
         c->pipeline = cf.pipeline != 0;
         if (const char* e = std::getenv("NRG_PIPELINE")) c->pipeline = std::atoi(e) != 0;
     } else if (cf.ds_kind == NRG_DS_STACK) {
-        // max_batch <= 2^24: st_cross_kernel stages one minimum per 2048-op tile in LDS
+        // max_batch <= 2^24: the finish stages one minimum per tile in LDS (stack.hip)
         if (!cf.stack_capacity || cf.stack_capacity >= (1ull << 31) || mb > (1ull << 24)) {
             nrg_close(c);
             return NRG_E_INVAL;

@@ -84,7 +84,7 @@ __device__ __forceinline__ Fn unpack_agg(u64 v) {
     return f;
 }
 
-// Per-tile results of st_tile_kernel, read by st_cross_kernel.
+// Per-tile results of the tile pass, read by the chunk's finish (st_round_kernel).
 struct StTiles {
     long long* tmin;   // [tiles] minimum depth reached in the tile (start and end included)
     u32* tend;         // [tiles] end depth of the tile - tmin
@@ -185,7 +185,7 @@ __device__ __forceinline__ void me_then(int& m, int& e, int m2, int e2) {
 //      amin_v <= L (every lane in between stays above L): residual entry L - amin_v of lane v.
 //      Each wave lists its unmatched Pops and answers them one per lane per round by greedy
 //      skips over a sparse table of lane minima (256 lanes: 8 levels). With no such lane the
-//      Push is in an earlier tile (or before the chunk): the Pop goes to st_finish_kernel's
+//      Push is in an earlier tile (or before the chunk): the Pop goes to the finish's
 //      list with the slot's pre-chunk content.
 //   5. Table: level L of [tmin, tile end) is last pushed by the LAST lane with amin <= L, so
 //      lane t writes the levels [amin_t, min(aend_t, min of later lanes' amin)) of its
