@@ -242,6 +242,29 @@ int nrg_hashmap_dump(nrg_ctx* ctx, uint64_t* keys, uint64_t* vals, uint64_t cap,
 /* Order-independent digest of the contents: count, sum and xor of mix64(k ^ mix64(v)). */
 int nrg_hashmap_digest(nrg_ctx* ctx, uint64_t out[3]);
 
+/* ---- Flat combining on the host (NrHashMap) --------------------------------------------- */
+/* Replica's flat combiner for many client threads (nr/src/context.rs:88-194,
+ * nr/src/replica.rs:345-356, 414-433, 508-595): each registered thread posts up to 32 ops
+ * (MAX_PENDING_OPS) at a time; whichever posting thread takes the combiner lock collects every
+ * thread's posted ops into ONE GPU round of `ctx` (all Puts appended and replayed, then all
+ * Gets answered against the post-round state) and hands every thread its responses. Calls on
+ * one token are synchronous and must come from one thread at a time; while a combiner is open,
+ * `ctx` is driven only through it. Needs max_threads * 32 <= max_batch and <= max_reads. */
+typedef struct nrg_combiner nrg_combiner;
+int nrg_combiner_open(nrg_ctx* ctx, uint32_t max_threads, nrg_combiner** out);
+int nrg_combiner_close(nrg_combiner* comb);
+/* Replica::register: a token 0..max_threads-1, or NRG_E_CAPACITY. */
+int nrg_combiner_register(nrg_combiner* comb, uint32_t* token);
+/* Replica::execute_mut(Put(keys[i], vals[i])), n <= 32: prev[i]/some[i] = HashMap::insert's
+ * previous value. */
+int nrg_combiner_put(nrg_combiner* comb, uint32_t token, const uint64_t* keys, const uint64_t* vals, uint32_t n,
+                     uint64_t* prev, uint8_t* some);
+/* Replica::execute(Get(keys[i])), n <= 32: vals[i]/found[i]. */
+int nrg_combiner_get(nrg_combiner* comb, uint32_t token, const uint64_t* keys, uint32_t n, uint64_t* vals,
+                     uint8_t* found);
+/* GPU rounds combined so far and the ops they carried. */
+int nrg_combiner_stats(nrg_combiner* comb, uint64_t* rounds, uint64_t* ops);
+
 /* ---- Stack --------------------------------------------------------------------------- */
 /* Stack::default(): storage = vals[0..n) (bottom first). */
 int nrg_stack_init(nrg_ctx* ctx, const uint32_t* vals, uint64_t n);

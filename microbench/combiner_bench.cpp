@@ -1,0 +1,91 @@
+// Native client threads against the flat combiner (nrg_combiner_*), B1's table and stream.
+//
+// T std::threads each loop on synchronous calls of B ops for a fixed time: one call in ten a
+// Put batch (Replica::execute_mut), the others Get batches (Replica::execute), keys uniform over
+// 10M on a 2^26-slot table prefilled with [0, 2^23) -> k+1 (benches/hashmap.rs:77-122 with
+// nr/src/replica.rs's synchronous per-thread API). Prints ops/s, GPU rounds and ops per round.
+// Build: g++ -O2 -std=c++17 -pthread microbench/combiner_bench.cpp -o microbench/combiner_bench \
+//            -Lnode-replication_amd/lib -lnrgpu -Wl,-rpath,$ORIGIN/../node-replication_amd/lib
+// Run:   ./microbench/combiner_bench [seconds]
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <thread>
+#include <vector>
+
+#include "../include/nrgpu.h"
+
+static uint64_t sm64(uint64_t& s) {  // splitmix64
+    uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+static int run(int threads, int batch, double secs) {
+    nrg_config cfg;
+    nrg_config_default(&cfg, NRG_DS_HASHMAP);
+    cfg.log2_slots = 26;
+    cfg.max_batch = cfg.max_reads = 1u << 16;
+    nrg_ctx* ctx = nullptr;
+    if (int r = nrg_open(0, &cfg, &ctx)) return r;
+    if (int r = nrg_hashmap_prefill_range(ctx, 1ull << 23, 1)) return r;
+    nrg_combiner* comb = nullptr;
+    if (int r = nrg_combiner_open(ctx, (uint32_t)threads, &comb)) return r;
+    std::atomic<bool> stop{false};
+    std::atomic<int> err{0};
+    std::vector<uint64_t> done(threads, 0);
+    std::vector<std::thread> th;
+    for (int i = 0; i < threads; i++)
+        th.emplace_back([&, i] {
+            uint32_t tok = 0;
+            if (nrg_combiner_register(comb, &tok)) {
+                err = 1;
+                return;
+            }
+            uint64_t s = 1000 + i, k[32], v[32], out[32];
+            uint8_t f[32];
+            uint64_t calls = 0, n = 0;
+            while (!stop.load(std::memory_order_relaxed)) {
+                for (int j = 0; j < batch; j++) {
+                    k[j] = sm64(s) % 10000000ull;
+                    v[j] = k[j] + 7;
+                }
+                const int r = calls++ % 10 == 0 ? nrg_combiner_put(comb, tok, k, v, batch, out, f)
+                                                : nrg_combiner_get(comb, tok, k, batch, out, f);
+                if (r) {
+                    err = r;
+                    return;
+                }
+                n += batch;
+            }
+            done[i] = n;
+        });
+    const auto t0 = std::chrono::steady_clock::now();
+    std::this_thread::sleep_for(std::chrono::duration<double>(secs));
+    stop = true;
+    for (auto& x : th) x.join();
+    const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    uint64_t rounds = 0, ops = 0, tot = 0;
+    nrg_combiner_stats(comb, &rounds, &ops);
+    for (uint64_t d : done) tot += d;
+    std::printf("threads %4d ops/call %3d: %9.3f Mops/s  rounds %7llu  ops/round %7.1f  round rate %6.1f k/s%s\n",
+                threads, batch, tot / dt / 1e6, (unsigned long long)rounds, rounds ? (double)ops / rounds : 0.0,
+                rounds / dt / 1e3, err ? "  ERROR" : "");
+    std::fflush(stdout);
+    nrg_combiner_close(comb);
+    nrg_close(ctx);
+    return err.load();
+}
+
+int main(int argc, char** argv) {
+    const double secs = argc > 1 ? std::atof(argv[1]) : 2.0;
+    const int cases[][2] = {{8, 1}, {8, 32}, {64, 1}, {64, 32}, {128, 32}, {256, 32}};
+    for (auto& c : cases)
+        if (int r = run(c[0], c[1], secs)) {
+            std::printf("error %d (%s)\n", r, nrg_strerror(r));
+            return 1;
+        }
+    return 0;
+}

@@ -5,6 +5,7 @@ include/nrgpu.h). This package mirrors the reference `nr` crate's API on top of 
 """
 from . import _lib
 from ._lib import NrgError, load
+from .combiner import Combiner
 from .replica import (
     PUT_DTYPE,
     STACK_OP_DTYPE,
@@ -28,7 +29,7 @@ from .replica import (
 )
 
 __all__ = [
-    "_lib", "NrgError", "load", "PUT_DTYPE", "STACK_OP_DTYPE", "SYNTH_OP_DTYPE", "SYNTH_RD_DTYPE",
+    "_lib", "NrgError", "load", "Combiner", "PUT_DTYPE", "STACK_OP_DTYPE", "SYNTH_OP_DTYPE", "SYNTH_RD_DTYPE",
     "AbstractDataStructure", "DeviceReplica", "Get", "Log", "NrHashMap", "Peek", "Pop", "Push", "Put",
     "ReadOnly", "ReadWrite", "Replica", "ReplicaToken", "Stack", "WriteOnly",
 ]

@@ -160,6 +160,12 @@ SIGNATURES = {
     "nrg_group_set_input_stream": (C.c_int, [vp, C.c_int, vp]),
     "nrg_group_round_async": (C.c_int, [vp, C.POINTER(Round), u64p]),
     "nrg_group_sync": (C.c_int, [vp]),
+    "nrg_combiner_open": (C.c_int, [vp, u32, C.POINTER(vp)]),
+    "nrg_combiner_close": (C.c_int, [vp]),
+    "nrg_combiner_register": (C.c_int, [vp, C.POINTER(u32)]),
+    "nrg_combiner_put": (C.c_int, [vp, u32, vp, vp, u32, vp, vp]),
+    "nrg_combiner_get": (C.c_int, [vp, u32, vp, u32, vp, vp]),
+    "nrg_combiner_stats": (C.c_int, [vp, u64p, u64p]),
     "nrg_key_owner": (C.c_uint32, [u64, C.c_uint32]),
     "nrg_hashmap_partition_async": (C.c_int, [vp, vp, u64, vp, u64, C.c_uint32, vp, vp, vp, vp, vp]),
     "nrg_route_back_async": (C.c_int, [vp, vp, vp, vp, u64, vp, vp]),
