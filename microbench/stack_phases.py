@@ -33,6 +33,7 @@ TILE = int(os.environ.get("ST_TILE", "4096"))  # ops per tile of the build (256 
 tiles = (N + TILE - 1) // TILE
 names = ["loads", "local pass", "scan+responses", "lookback", "query list+sparse table", "queries", "table"]
 acc = np.zeros((tiles, 9))
+w0 = []
 R = 20
 fin = []
 q8 = []
@@ -51,6 +52,8 @@ for r in range(R + 3):
         fin.append((fb[:, 0].min() - o, fb[:, 0].max() - o, fb[:, 1].max() - o, t[:, 0].min() - o, t[:, 7].max() - o))
     if r >= 3:
         q8.append((t[:, 8] - t[:, 5]).mean() / 100.0)
+        t9 = buf.reshape(tiles, 16)[:, 9:11].astype(np.float64)
+        w0.append(((t9[:, 0] - t[:, 5]).mean() / 100.0, t9[:, 1].mean(), ((t[:, 6] - t[:, 8]).mean() / 100.0)))
     if r >= 3:
         acc += t - t[:, :1].min()
 acc /= R
@@ -67,3 +70,4 @@ if fin:
           " tiles start %.2f, last tile end %.2f" % tuple(f))
 if q8:
     print("  of the unmatched-Pop phase, the intra-tile queries: mean %.2f us" % np.mean(q8))
+    print("  wave 0's own queries %.2f us over a list of %.0f; pre-chunk pass %.2f us" % tuple(np.mean(w0, 0)))

@@ -218,7 +218,9 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
     static_assert(W_STK + W_UP >= 2 * 64 * SW_OPS, "staging fits");
     __shared__ __attribute__((aligned(16))) u32 s_wave[ST_WAVES][W_STK + W_UP];
     __shared__ int s_min[ST_LANES];     // lane minimum level - tile minimum
-    __shared__ unsigned short s_sp[8][ST_LANES];  // s_sp[j][v] = min of s_min over lanes (v - 2^j, v]
+    // s_sp[j][v + 1] = min of s_min over lanes (v - 2^j, v]; column 0 (lane -1) holds 0, below
+    // every level, so a walk that has left the tile stops there without a branch
+    __shared__ unsigned short s_sp[8][ST_LANES + 1];
     __shared__ int s_suf[ST_LANES];     // inclusive suffix minimum of s_min inside the wave
     __shared__ int s_wm[ST_WAVES], s_we[ST_WAVES], s_wmin[ST_WAVES];
     __shared__ long long s_D;
@@ -237,32 +239,23 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
     // ---- load the lane's ops (and write the log copy when they come from the caller) ----
     u32 val[SW_OPS];
     u32 pm = 0, qm = 0;  // Push / Pop bit per op (padding past n is neither)
+    // the wave's records as loaded (16-B unit 64 i + lane): with a caller buffer their log copy
+    // is written after the tile's aggregate is published, so the copy's HBM writes do not slow
+    // the loads every later tile's look-back waits on
+    uint4 x[SW_OPS / 2];
+    const u64 rw0 = (lo + wbase) & ring_mask;
+    const bool ring_run = rw0 + 64 * SW_OPS <= ring_mask + 1 && !(rw0 & 1);  // contiguous, 16-B aligned
+    bool copy_later = false;
     {
-        const u64 rw0 = (lo + wbase) & ring_mask;
-        const bool ring_run = rw0 + 64 * SW_OPS <= ring_mask + 1 && !(rw0 & 1);  // contiguous, 16-B aligned
         const nrg_stack_op* wp = src ? src + wbase : ring + rw0;
         const bool vec = wbase + 64 * SW_OPS <= n && (src ? !((uintptr_t)wp & 15) : ring_run);  // wave-uniform
         if (vec) {
             // coalesced: 16-B unit u = 64 i + lane of the wave's ops (two ops), then through LDS
             // to the lane that replays it (row u / 16, column (u % 16) ^ (row % 16): no conflicts)
             const uint4* p4 = (const uint4*)wp;
-            uint4 x[SW_OPS / 2];
 #pragma unroll
             for (int i = 0; i < SW_OPS / 2; i++) x[i] = p4[64 * i + lane];
-            if (src) {
-                if (ring_run) {
-                    uint4* w4 = (uint4*)(ring + rw0);
-#pragma unroll
-                    for (int i = 0; i < SW_OPS / 2; i++) w4[64 * i + lane] = x[i];
-                } else {
-#pragma unroll
-                    for (int i = 0; i < SW_OPS / 2; i++) {
-                        const u64 o = lo + wbase + 2 * (64 * i + lane);
-                        ring[o & ring_mask] = nrg_stack_op{x[i].x, x[i].y};
-                        ring[(o + 1) & ring_mask] = nrg_stack_op{x[i].z, x[i].w};
-                    }
-                }
-            }
+            copy_later = src != nullptr;
             uint4* s4 = reinterpret_cast<uint4*>(s_wave[wv]);
             constexpr int UPR = SW_OPS / 2;  // 16-B units per lane
 #pragma unroll
@@ -356,7 +349,6 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
     }
     int xm = __shfl_up(im, 1, 64), xe = __shfl_up(ie, 1, 64);  // exclusive within the wave
     if (lane == 0) xm = xe = 0;
-    if (P.tiles) (void)st_stage(P.tl.tmin, P.tiles, s_ptm, s_pg8, s_pgm, ~0u);  // after the op loads
     __syncthreads();
     int M = 0, E = 0, pmw = 0, pew = 0;  // tile aggregate; prefix of the earlier waves
 #pragma unroll
@@ -372,6 +364,20 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
     xe = pew;
     const Fn tagg = {E, E - M};  // max(a, x + b) form for the look-back
     if (t == 0) __hip_atomic_store(&desc[tile], pack_agg(tagg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (copy_later) {  // Log::append's copy of the wave's records
+        if (ring_run) {
+            uint4* w4 = (uint4*)(ring + rw0);
+#pragma unroll
+            for (int i = 0; i < SW_OPS / 2; i++) w4[64 * i + lane] = x[i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < SW_OPS / 2; i++) {
+                const u64 o = lo + wbase + 2 * (64 * i + lane);
+                ring[o & ring_mask] = nrg_stack_op{x[i].x, x[i].y};
+                ring[(o + 1) & ring_mask] = nrg_stack_op{x[i].z, x[i].w};
+            }
+        }
+    }
 
     // responses known now, lane-contiguous (unmatched Pops stay None until patched below)
     {
@@ -428,6 +434,9 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
             v0[q] = (q < G && idx < np) ? __hip_atomic_load(&desc[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
         }
     }
+    // the previous chunk's tile minima (read only by the pre-chunk pass, after the queries): staged
+    // here, after the aggregate is published, so their load is off the look-back's critical path
+    if (P.tiles) (void)st_stage(P.tl.tmin, P.tiles, s_ptm, s_pg8, s_pgm, ~0u);
 
     // Query structures for lane levels relative to the tile's lowest level: lane minimum amin_,
     // start dt_, and uq_ unmatched Pops that find an element. Outputs: s_min, the sparse table
@@ -480,12 +489,13 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
                 const int o = s_suf[t - (1 << j) + 1];
                 m = o < m ? o : m;
             }
-            s_sp[j][t] = (unsigned short)m;  // levels are < 2 * ST_TILE
+            s_sp[j][t + 1] = (unsigned short)m;  // levels are < 2 * ST_TILE
         }
         int m7 = spw[6];
         if (wv > 0) m7 = s_wmin[wv - 1] < m7 ? s_wmin[wv - 1] : m7;
         if (wv > 1 && lane < 63) m7 = s_suf[t - 127] < m7 ? s_suf[t - 127] : m7;
-        s_sp[7][t] = (unsigned short)m7;
+        s_sp[7][t + 1] = (unsigned short)m7;
+        if (t < 8) s_sp[t][0] = 0;
         for (int w = wv + 1; w < ST_WAVES; w++) later = s_wmin[w] < later ? s_wmin[w] : later;
     };
     // unclamped walk (D + M >= 0): amin = xe - nun - M, start xe - M, every unmatched Pop reads
@@ -555,12 +565,19 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
             e[i] = h < total ? s_up[h] : 0u;
             v[i] = h < total ? (int)((e[i] & ST_PMASK) / SW_OPS) - 1 : -1;
         }
-        // the nearest earlier lane whose minimum is <= the level (greedy skips of 128, ..., 1)
+        // the nearest earlier lane whose minimum is <= the level (greedy skips of 128, ..., 1);
+        // branch-free, so each level's QI table reads are in flight together (predicated reads
+        // compiled to one LDS round trip per query and level: 2.5 us for a 4096-op tile)
 #pragma unroll
         for (int j = 7; j >= 0; j--) {
+            int m[QI];
 #pragma unroll
-            for (int i = 0; i < QI; i++)
-                if (v[i] >= 0 && (int)s_sp[j][v[i]] > (int)(e[i] >> ST_PB)) v[i] -= 1 << j;
+            for (int i = 0; i < QI; i++) m[i] = (int)s_sp[j][v[i] + 1];
+#pragma unroll
+            for (int i = 0; i < QI; i++) {
+                const int w = v[i] - (m[i] > (int)(e[i] >> ST_PB) ? 1 << j : 0);
+                v[i] = w > -1 ? w : -1;
+            }
         }
 #pragma unroll
         for (int i = 0; i < QI; i++) {
@@ -580,6 +597,8 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
             }
         }
     }
+    ST_MARK(9);  // wave 0's own queries done
+    if (dbg && t == 0) dbg[(u64)tile * 16 + 10] = (u64)total;
     __syncthreads();
     // the cross-tile Pops' pre-chunk content, one per thread (all loads in flight together): a
     // slot the previous chunk wrote comes from its owner's table (that chunk's commit runs in
