@@ -114,6 +114,43 @@ __device__ __forceinline__ int st_walk(const long long* s_tm, const long long* s
     return k;
 }
 
+// The last tile of [0, tiles) whose minimum is <= s, or -1: the last 64-tile group with a
+// minimum <= s, then its last such 8-tile group, then its last such tile, each level's eight
+// reads in flight together (three or four LDS round trips instead of a walk's dependent steps).
+__device__ __forceinline__ int st_find(const long long* s_tm, const long long* s_g8, const long long* s_gm, int tiles,
+                                       long long s) {
+    constexpr long long INF = 1ll << 62;
+    int g = (tiles - 1) >> 6;
+    for (;;) {  // 64-tile groups from the last, four at a time
+        if (g < 0) return -1;
+        long long m[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) m[i] = g - i >= 0 ? s_gm[g - i] : INF;
+        int hit = -1;
+#pragma unroll
+        for (int i = 3; i >= 0; i--) hit = m[i] <= s ? i : hit;
+        if (hit >= 0) {
+            g -= hit;
+            break;
+        }
+        g -= 4;
+    }
+    const int n8 = (tiles - 1) / 8;  // last valid 8-tile group
+    long long m8[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) m8[i] = g * 8 + i <= n8 ? s_g8[g * 8 + i] : INF;
+    int b = g * 8;
+#pragma unroll
+    for (int i = 0; i < 8; i++) b = m8[i] <= s ? g * 8 + i : b;
+    long long m1[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) m1[i] = b * 8 + i < tiles ? s_tm[b * 8 + i] : INF;
+    int k = -1;
+#pragma unroll
+    for (int i = 0; i < 8; i++) k = m1[i] <= s ? b * 8 + i : k;
+    return k;
+}
+
 // Stage the tile minima of a chunk in LDS (256 threads): s_tm[tiles], then the minimum of
 // every 8-tile group (s_g8) and 64-tile group (s_gm). Returns this thread's minimum over the
 // tiles after `after` (pass ~0u for none).
@@ -223,10 +260,11 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
     __shared__ unsigned short s_sp[8][ST_LANES + 1];
     __shared__ int s_suf[ST_LANES];     // inclusive suffix minimum of s_min inside the wave
     __shared__ int s_wm[ST_WAVES], s_we[ST_WAVES], s_wmin[ST_WAVES];
-    __shared__ long long s_D;
+    __shared__ long long s_D, s_d0;
     __shared__ u32 s_ucnt;
     constexpr u32 ST_XL = 1024;
     __shared__ u32 s_xl[ST_XL];         // the first cross-tile Pops (the rest re-read from upop)
+    __shared__ u32 s_pre[ST_LANES];     // pre-chunk content of levels T0 .. T0 + 255
     u32 (*s_stk)[64] = reinterpret_cast<u32 (*)[64]>(s_wave[wv]);
     u32* s_up = s_wave[wv] + W_STK;
     if (t == 0) s_ucnt = 0;
@@ -421,7 +459,9 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
     // need the tile's start depth only when the stack empties inside the tile, so they are
     // built for the unclamped walk and rebuilt in that (rare) case. ----
     long long* sdepth = &ctl->depth0;             // depth after the chunk of each parity
-    const long long d0 = sdepth[A.par ^ 1];        // depth before this chunk
+    // depth before this chunk: loaded by wave 0 alone and passed on through LDS, so no other
+    // wave waits on it (a vector load's wait would also wait for every store issued before it)
+    const long long d0g = wv == 0 ? sdepth[A.par ^ 1] : 0;
     const int np = (int)tile;
     const int G = (np + 63) / 64;
     const int r0 = (63 - lane) * G;
@@ -536,11 +576,14 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
                 if (g0 + q < G && r0 + g0 + q < np) acc = fn_then(acc, unpack_agg(v[q]));
         }
         acc = np ? wave_compose(acc) : Fn{0, 0};
-        if (lane == 0) s_D = fn_apply(acc, d0);
+        if (lane == 0) {
+            s_D = fn_apply(acc, d0g);
+            s_d0 = d0g;
+        }
     }
     __syncthreads();
     ST_MARK(4);
-    const long long D = s_D;
+    const long long D = s_D, d0 = s_d0;
     const long long T0 = D + M > 0 ? D + M : 0;              // the tile's lowest level
     const long long Dt = D + xe > xe - xm ? D + xe : xe - xm;  // the lane's start depth
     const long long aminl = Dt - (long long)nun > 0 ? Dt - (long long)nun : 0;
@@ -551,8 +594,18 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
     if (Dt + hmax > (long long)cap || (long long)topmax > (long long)cap) atomicOr(&ctl->err, ERR_CAPACITY);
     // the stack empties inside the tile: Pops at depth 0 are no-ops, levels shift (block-uniform)
     if (D + M < 0) build(amin, dt, (int)(Dt < (long long)nun ? Dt : (long long)nun));
+    // The cross-tile Pops read exactly the levels [T0, D), each on the tile's first descent below
+    // it. Their pre-chunk content: a slot the previous chunk wrote comes from its owner's table
+    // (that chunk's commit runs in this launch), any other from the stack. Fetched now for the
+    // first 256 levels, one per thread, so the loads land while the queries run.
+    auto pre_content = [&](long long slot) -> u32 {
+        if (slot >= d0 || (u64)slot >= cap) return 0u;
+        const int k = P.tiles ? st_find(s_ptm, s_pg8, s_pgm, (int)P.tiles, slot) : -1;
+        return k >= 0 ? P.tl.table[(u64)k * ST_TILE + (u64)(slot - s_ptm[k])] : stack[slot];
+    };
     __syncthreads();
     ST_MARK(5);
+    const u32 pre = t < D - T0 ? pre_content(T0 + t) : 0u;  // after the barrier: its fence would wait
 
     // ---- 4. unmatched Pops: QI queries per lane at a time, their table walks interleaved ----
     constexpr int QI = 4;
@@ -579,15 +632,24 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
                 v[i] = w > -1 ? w : -1;
             }
         }
+        // the found lanes' residual entries, read together (lane 0's column for the others)
+        int mn[QI];
+        u32 rv[QI];
+#pragma unroll
+        for (int i = 0; i < QI; i++) mn[i] = s_min[v[i] > 0 ? v[i] : 0];
+#pragma unroll
+        for (int i = 0; i < QI; i++) {
+            const int vv = v[i] > 0 ? v[i] : 0;
+            rv[i] = s_wave[vv >> 6][v[i] >= 0 ? ((int)(e[i] >> ST_PB) - mn[i]) * 64 + (vv & 63) : 0];
+        }
 #pragma unroll
         for (int i = 0; i < QI; i++) {
             if (h0 + 64 * i >= total) continue;
-            const int Lr = (int)(e[i] >> ST_PB);
             const u32 pos = e[i] & ST_PMASK;
             if (v[i] >= 0) {
                 const u64 g = lo + tbase + pos;
                 if (resp && g >= resp_lo && g < resp_hi) {
-                    resp[g - resp_lo] = s_wave[v[i] >> 6][(Lr - s_min[v[i]]) * 64 + (v[i] & 63)];
+                    resp[g - resp_lo] = rv[i];
                     some[g - resp_lo] = 1;
                 }
             } else {  // its Push is in an earlier tile or before the chunk
@@ -599,21 +661,15 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
     }
     ST_MARK(9);  // wave 0's own queries done
     if (dbg && t == 0) dbg[(u64)tile * 16 + 10] = (u64)total;
+    s_pre[t] = pre;
     __syncthreads();
-    // the cross-tile Pops' pre-chunk content, one per thread (all loads in flight together): a
-    // slot the previous chunk wrote comes from its owner's table (that chunk's commit runs in
-    // this launch), any other from the stack
+    // the cross-tile Pops' pre-chunk content (prefetched for the first 256 levels)
     ST_MARK(8);  // queries done (stored after the phases 0..7)
     const u32 ucnt = s_ucnt;
     for (u32 h = t; h < ucnt; h += ST_LANES) {
         const u32 e = h < ST_XL ? s_xl[h] : tl.upop[(u64)tile * ST_TILE + h];
-        const long long slot = T0 + (long long)(e >> ST_PB);
-        u32 pv = 0;
-        if (slot < d0 && (u64)slot < cap) {
-            const int k = P.tiles ? st_walk(s_ptm, s_pg8, s_pgm, (int)P.tiles - 1, slot) : -1;
-            pv = k >= 0 ? P.tl.table[(u64)k * ST_TILE + (u64)(slot - s_ptm[k])] : stack[slot];
-        }
-        tl.uval[(u64)tile * ST_TILE + h] = pv;
+        const u32 lr = e >> ST_PB;
+        tl.uval[(u64)tile * ST_TILE + h] = lr < (u32)ST_LANES ? s_pre[lr] : pre_content(T0 + (long long)lr);
     }
     ST_MARK(6);
 
