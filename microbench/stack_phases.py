@@ -68,6 +68,16 @@ if fin:
     f = np.array(fin).mean(0) / 100.0
     print("fused finish of the previous chunk (us from the launch's first workgroup): start %.2f..%.2f, last end %.2f;"
           " tiles start %.2f, last tile end %.2f" % tuple(f))
+hw = buf.reshape(tiles, 16)[:, 11]
+cu = [(int(h) >> 32 & 15, int(h) >> 13 & 3, int(h) >> 12 & 1, int(h) >> 8 & 15) for h in hw]  # xcc, se, sh, cu
+from collections import Counter
+cnt = Counter(cu)
+share = np.array([cnt[c] for c in cu])
+ld = (acc[:, 1] - acc[:, 0]) / 100.0
+print("  placement (last round): %d tiles on %d CUs; tiles sharing a CU: %d; load mean %.2f us alone, %.2f us shared"
+      % (tiles, len(cnt), int((share > 1).sum()), ld[share == 1].mean() if (share == 1).any() else 0, ld[share > 1].mean() if (share > 1).any() else 0))
+slow = np.argsort(-ld)[:8]
+print("  slowest loads: " + ", ".join("tile %d %.2f us (xcc %d se %d cu %d, %d on CU)" % (k, ld[k], cu[k][0], cu[k][1], cu[k][3], share[k]) for k in slow))
 if q8:
     print("  of the unmatched-Pop phase, the intra-tile queries: mean %.2f us" % np.mean(q8))
     print("  wave 0's own queries %.2f us over a list of %.0f; pre-chunk pass %.2f us" % tuple(np.mean(w0, 0)))

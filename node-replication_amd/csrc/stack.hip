@@ -249,6 +249,9 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
 #define ST_MARK(K) \
     if (dbg && t == 0) dbg[(u64)tile * 16 + (K)] = wall_clock64()
     ST_MARK(0);
+    if (dbg && t == 0)  // placement: HW_ID (CU, SH, SE) and XCC_ID
+        dbg[(u64)tile * 16 + 11] = (u64)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+                                   (u64)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32;
     // per wave: the lane stacks (rows of 64 lanes; row SW_OPS absorbs non-Push writes) followed
     // by the wave's query list; the first 16 KB also stage the wave's ops on their way in
     constexpr int W_STK = (SW_OPS + 1) * 64, W_UP = 64 * SW_OPS;
