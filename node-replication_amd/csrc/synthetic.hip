@@ -445,15 +445,19 @@ __device__ __forceinline__ void sy_part_role(const SyPartArgs& A, u32 tile, SyPa
             xm = t;
         }
         wave_lds_sync();
+        // all CW words read back (one LDS round trip) and bucketed before the rankings, which
+        // then cost one round trip each
+        u32 vw[CW], bw[CW];
+#pragma unroll
+        for (int r = 0; r < CW; r++) vw[r] = s_u.r.words[w][r * 64 + lane];
+#pragma unroll
+        for (int r = 0; r < CW; r++) bw[r] = vw[r] != NOTOUCH ? bucket_of((vw[r] & ~SETBIT) - HR, wm) : 0u;
 #pragma unroll
         for (int r = 0; r < CW; r++) {
-            const u32 v = s_u.r.words[w][r * 64 + lane];
-            const bool tv = v != NOTOUCH;
-            const u32 b = tv ? bucket_of((v & ~SETBIT) - HR, wm) : 0u;
             u64 peers;
-            const u32 rank = wave_rank(tv, b, lane, s_u.r.mask[w], s_wcnt[w], &peers);
-            xs[orr * CW + r] = v;
-            pk[orr * CW + r] = (b << 16) | rank;
+            const u32 rank = wave_rank(vw[r] != NOTOUCH, bw[r], lane, s_u.r.mask[w], s_wcnt[w], &peers);
+            xs[orr * CW + r] = vw[r];
+            pk[orr * CW + r] = (bw[r] << 16) | rank;
         }
     }
     __syncthreads();
