@@ -29,7 +29,7 @@ for i, o in enumerate(opsl):
     dev.gen_stack_ops_device(o, N, 12345 + i)
 resps = [torch.empty(N, dtype=torch.int32, device="cuda") for _ in range(2)]
 somes = [torch.empty(N, dtype=torch.uint8, device="cuda") for _ in range(2)]
-TILE = int(os.environ.get("ST_TILE", "4096"))  # ops per tile of the build (256 lanes x NRG_ST_OPS)
+TILE = int(os.environ.get("ST_TILE", "2048"))  # ops per tile of the build (256 lanes x NRG_ST_OPS)
 tiles = (N + TILE - 1) // TILE
 names = ["loads", "local pass", "scan+responses", "lookback", "query list+sparse table", "queries", "table"]
 acc = np.zeros((tiles, 9))

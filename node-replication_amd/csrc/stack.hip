@@ -24,12 +24,14 @@
 namespace nrg {
 
 #ifndef NRG_ST_OPS
-#define NRG_ST_OPS 16  // measured at 1M-op rounds: 8 -> 21.5 us, 16 -> 20.6 us, 32 -> 22.7 us
+// ops per lane, measured at 1M-op rounds (bench.py --workload stack): 8 -> 17.4 us, 16 -> 18.8 us,
+// 32 -> 21.2 us (session 7, before the branch-free query walk: 21.5 / 20.6 / 22.7 us)
+#define NRG_ST_OPS 8
 #endif
 constexpr int SW_OPS = NRG_ST_OPS;          // ops per lane, replayed in order by that lane (<= 32)
 constexpr int ST_WAVES = 4;                 // a tile is one workgroup of 4 waves
 constexpr int ST_LANES = 64 * ST_WAVES;     // 256 lanes
-constexpr int ST_TILE = ST_LANES * SW_OPS;  // 4096 ops
+constexpr int ST_TILE = ST_LANES * SW_OPS;  // 2048 ops
 constexpr int ST_PB = SW_OPS == 32 ? 13 : SW_OPS == 16 ? 12 : 11;  // bits of a position in the tile
 constexpr u32 ST_PMASK = (1u << ST_PB) - 1;
 static_assert(ST_TILE == 1 << ST_PB, "positions");
