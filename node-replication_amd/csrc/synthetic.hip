@@ -227,7 +227,10 @@ constexpr u32 SYB_WORDS = 1u << SYB_SHIFT;  // LDS words per bucket (a bucket ho
 constexpr int SYA_TPB = 512, SYA_WAVES = SYA_TPB / 64, SYA_OROUNDS = 4;
 constexpr u32 SYA_OPS = SYA_WAVES * SYA_OROUNDS * 64;  // ops per tile (11 bits)
 constexpr u32 SY_MAX_NB = 512, SY_MAX_HOT = 16, SY_MAX_TILES = 4096, SY_MAX_CW = 8;
-constexpr int SYB_TPB = 512, SYB_WAVES = SYB_TPB / 64, SYB_PER = 8;
+#ifndef NRG_SYB_PER
+#define NRG_SYB_PER 8  // 1M-op rounds: 4 -> 63.2 us, 8 -> 62.4 us, 12 -> 100.5 us (VGPR cap)
+#endif
+constexpr int SYB_TPB = 512, SYB_WAVES = SYB_TPB / 64, SYB_PER = NRG_SYB_PER;
 constexpr u32 SYB_PASS = SYB_TPB * SYB_PER;  // touches per pass of a bucket workgroup
 constexpr int SYC_TPB = 512;
 constexpr u32 NOTOUCH = 0xFFFFFFFFu;
