@@ -756,14 +756,15 @@ def main():
     ap.add_argument("--share-gpu", action="store_true", help="all ranks on cuda:0 (gloo rehearsal on a 1-GPU box)")
     ap.add_argument("--csv", default=None, help="append scaleout_benchmarks.csv rows (reference format)")
     ap.add_argument("--timing-every", type=int, default=0,
-                    help="event-stamp every n-th launch of the timed kernel (0: max(1, min(8, steps // 10)), "
-                         "so the roofline averages >= 10 launches)")
+                    help="event-stamp every n-th launch of the timed kernel (0: max(1, min(32, steps // 10)), "
+                         "so the roofline averages >= 10 launches; a stamped launch costs wall time, "
+                         "profiles/r02_s8_timing_sampling.txt)")
     ap.add_argument("--pipeline", type=int, default=1,
                     help="1: a round's apply+reads ride in the next round's launch (nrg_config.pipeline); "
                          "0: every round call completes its own reads")
     args = ap.parse_args()
     if args.timing_every <= 0:
-        args.timing_every = max(1, min(8, args.steps // 10))
+        args.timing_every = max(1, min(32, args.steps // 10))
     env = Env(args)
     runner = {"stack": run_stack, "synthetic": run_synthetic}.get(args.workload, run_hashmap)
     res = runner(args, env)
