@@ -246,6 +246,12 @@ class Env:
             self.dist.destroy_process_group()
 
 
+def apply_knobs(rep, args):
+    for kv in args.knob:
+        name, _, v = kv.partition("=")
+        rep.set_knob(name.strip().upper(), int(v, 0))
+
+
 def common_fields(args, env, value, ms_per_step, metric, dtype, config):
     return {
         "metric": metric,
@@ -296,6 +302,7 @@ def run_hashmap(args, env):
     Wg = W * world
     rep = nrgpu.DeviceReplica(L.NRG_DS_HASHMAP, env.local, log2_slots=args.log2_slots, max_batch=max(Wg, 1),
                               log_bytes=64 * 4 * max(Wg, 8192), replica_id=rank + 1, pipeline=args.pipeline)
+    apply_knobs(rep, args)
     rep.use_torch_stream()
     if args.partitioned:  # cnr-style: this rank holds only the keys it owns
         rep.hm_prefill_partition(args.prefill, 1, rank, world)
@@ -525,6 +532,7 @@ def run_synthetic(args, env):
     Ng = N * world
     rep = nrgpu.DeviceReplica(L.NRG_DS_SYNTHETIC, env.local, max_batch=Ng, log_bytes=64 * 4 * max(Ng, 8192),
                               replica_id=rank + 1, pipeline=args.pipeline)
+    apply_knobs(rep, args)
     rep.use_torch_stream()
     P = max(1, min(args.pool, 8, args.steps + args.warmup))
     gen = torch.Generator(device=dev_t)
@@ -619,6 +627,7 @@ def run_stack(args, env):
     cap = args.stack_init + 4 * Ng + (1 << 16)
     rep = nrgpu.DeviceReplica(L.NRG_DS_STACK, env.local, max_batch=Ng, stack_capacity=cap,
                               log_bytes=64 * 4 * max(Ng, 8192), replica_id=rank + 1, pipeline=args.pipeline)
+    apply_knobs(rep, args)
     rep.use_torch_stream()
     rep.st_init(list(range(args.stack_init)))  # benches/stack.rs:50-63: 0..50000
     P = max(1, min(args.pool, args.steps + args.warmup))
@@ -759,6 +768,9 @@ def main():
                     help="event-stamp every n-th launch of the timed kernel (0: max(1, min(32, steps // 10)), "
                          "so the roofline averages >= 10 launches; a stamped launch costs wall time, "
                          "profiles/r02_s8_timing_sampling.txt)")
+    ap.add_argument("--knob", action="append", default=[], metavar="NAME=VALUE",
+                    help="diagnostic/tuning knob of the replica (nrg_test_set_knob, include/nrgpu_testing.h), "
+                         "e.g. K1=2; never needed for the headline")
     ap.add_argument("--pipeline", type=int, default=1,
                     help="1: a round's apply+reads ride in the next round's launch (nrg_config.pipeline); "
                          "0: every round call completes its own reads")

@@ -103,7 +103,8 @@ typedef struct {
 /* ---- configuration ------------------------------------------------------------------ */
 typedef struct {
     uint32_t ds_kind;         /* NRG_DS_*                                                  */
-    uint32_t log2_slots;      /* hashmap: table has 2^log2_slots 64-B slots (default 26)    */
+    uint32_t log2_slots;      /* hashmap: table has 2^log2_slots 32-B slots {key, value, two
+                                 round stamps} (default 26: 2 GiB of HBM; < 2^30 slots)       */
     uint64_t log_bytes;       /* Log::new(bytes): ring entries = bytes/64 rounded as in the
                                  reference (min 2*GC_FROM_HEAD, power of two). 0 = 32 MiB   */
     uint64_t max_batch;       /* largest number of log records replayed per kernel pass;

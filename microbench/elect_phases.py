@@ -1,9 +1,9 @@
 """Phase timings of hm_elect_kernel<true> on B1 rounds with previous values (diagnostic; GPU box).
 
 Opens the B1 replica (2^26 slots, prefill 2^23, keys over 10M), replays rounds of 100k Puts +
-900k Gets asking for previous values, with NRG_EXP=65536 (elector timestamps, wall_clock64 at
+900k Gets asking for previous values, with knob EXP=65536 (elector timestamps, wall_clock64 at
 100 MHz), and prints per phase the mean and max over buckets.
-Usage: NRG_EXP=65536 python microbench/elect_phases.py
+Usage: python microbench/elect_phases.py
 """
 import ctypes as C
 import os
@@ -18,7 +18,7 @@ import nrgpu  # noqa: E402
 from nrgpu import _lib as L  # noqa: E402
 
 W, R = 100_000, 900_000
-dev = nrgpu.DeviceReplica(L.NRG_DS_HASHMAP, 0, log2_slots=26, max_batch=W, log_bytes=64 * 4 * W)
+dev = nrgpu.DeviceReplica(L.NRG_DS_HASHMAP, 0, knobs={"EXP": 0x10000}, log2_slots=26, max_batch=W, log_bytes=64 * 4 * W)
 dev.use_torch_stream()
 dev.hm_prefill_range(1 << 23, 1)
 P = 8

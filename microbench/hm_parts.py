@@ -17,7 +17,7 @@ from nrgpu import _lib as L  # noqa: E402
 def main():
     W, R, steps = 100_000, 900_000, 200
     rep = nrgpu.DeviceReplica(L.NRG_DS_HASHMAP, 0, log2_slots=26, max_batch=W, log_bytes=64 * 4 * W,
-                              pipeline=int(os.environ.get("NRG_PIPELINE", "0")))
+                              pipeline=int(os.environ.get("PIPE", "0")))
     rep.use_torch_stream()
     rep.hm_prefill_range(1 << 23, 1)
     P = 32
@@ -55,7 +55,6 @@ def main():
         rep.kernel_timing(False)
         print(f"{name:28s} {el:8.2f} us/step  kernels(avg us): {parts}", flush=True)
 
-    print(f"NRG_K1_ITEMS={os.environ.get('NRG_K1_ITEMS', 'default')}")
     run("gets only (900k)", lambda i: rep.hm_get_device(gk[i % P], R, gv, gf))
     run("puts only (100k)", lambda i: rep.hm_round_device(puts[i % P], W, 1, None, 0, None, None))
     run("round 100k put + 900k get", lambda i: rep.hm_round_device(puts[i % P], W, 1, gk[i % P], R, gv, gf))

@@ -1,9 +1,9 @@
 """Phase timings of st_tile_kernel (diagnostic; run on the GPU box).
 
-Opens a stack replica with NRG_EXP=2 (timestamps), replays rounds of N ops over a
+Opens a stack replica with knob EXP=2 (timestamps), replays rounds of N ops over a
 50,000-element stack and prints, per phase, the mean and max over tiles of the time since the
 tile's start (wall_clock64, 100 MHz), plus the spread of tile start times.
-Usage: NRG_EXP=2 python microbench/stack_phases.py [N]
+Usage: python microbench/stack_phases.py [N]
 """
 import ctypes as C
 import os
@@ -18,7 +18,7 @@ import nrgpu  # noqa: E402
 from nrgpu import _lib as L  # noqa: E402
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
-dev = nrgpu.DeviceReplica(L.NRG_DS_STACK, 0, max_batch=N, stack_capacity=N * 4 + 100_000, pipeline=int(os.environ.get("PIPE", "1")),
+dev = nrgpu.DeviceReplica(L.NRG_DS_STACK, 0, knobs={"EXP": 2}, max_batch=N, stack_capacity=N * 4 + 100_000, pipeline=int(os.environ.get("PIPE", "1")),
                           log_bytes=64 * 4 * max(N, 8192))
 dev.use_torch_stream()
 dev.st_init(list(range(50_000)))

@@ -1,8 +1,8 @@
 """Phase timings of sy_bucket_kernel (diagnostic; run on the GPU box).
 
 Opens a synthetic replica as bench.py does (200,000 words, 1 hot + 5 cold touches per ReadWrite)
-with NRG_EXP=2 (timestamps), replays rounds of N ops and prints, per phase, the mean and max over
-buckets (wall_clock64, 100 MHz). Usage: NRG_EXP=2 python microbench/synth_phases.py [N]
+with knob EXP=2 (timestamps), replays rounds of N ops and prints, per phase, the mean and max over
+buckets (wall_clock64, 100 MHz). Usage: python microbench/synth_phases.py [N]
 """
 import ctypes as C
 import os
@@ -17,7 +17,7 @@ import nrgpu  # noqa: E402
 from nrgpu import _lib as L  # noqa: E402
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
-dev = nrgpu.DeviceReplica(L.NRG_DS_SYNTHETIC, 0, max_batch=N, log_bytes=64 * 4 * max(N, 8192))
+dev = nrgpu.DeviceReplica(L.NRG_DS_SYNTHETIC, 0, knobs={"EXP": 2}, max_batch=N, log_bytes=64 * 4 * max(N, 8192))
 dev.use_torch_stream()
 g = torch.Generator(device="cuda")
 g.manual_seed(7)

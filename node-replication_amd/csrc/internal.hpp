@@ -107,9 +107,10 @@ struct nrg_ctx {
     uint64_t slots = 0;
     nrg::Slot* d_table = nullptr;
     uint64_t rounds = 0;             // replay rounds launched (statistics)
-    uint32_t k1_items = 0;           // Puts per index thread (0: by round size; NRG_K1 overrides)
-    uint32_t bk_ent = 0;             // target entries per elector bucket (0: default; NRG_BK_ENT)
-    uint32_t exp = 0;                // diagnostic knobs (NRG_EXP; see hashmap.hip IndexJob/ElectJob)
+    // tuning and diagnostic knobs: set only through nrg_test_set_knob (include/nrgpu_testing.h)
+    uint32_t k1_items = 0;           // Puts per index thread (0: by round size; NRG_KNOB_K1)
+    uint32_t bk_ent = 0;             // target entries per elector bucket (0: default; NRG_KNOB_BK_ENT)
+    uint32_t exp = 0;                // diagnostic bits (NRG_KNOB_EXP; see hashmap.hip IndexJob/ElectJob)
     // Reads of the last replayed round: answered in the next launch beside the next round's
     // index pass, or by nrg_join / nrg_sync / any call that reads the table. With
     // pipeline == false they are flushed at the end of every call.
@@ -125,8 +126,9 @@ struct nrg_ctx {
     uint32_t* d_bk_cnt = nullptr;   // [bucket][index tiles] offset << 16 | count
     // Stamp rounds (<= stamp_max Puts, no previous values): per-Put slot ids by epoch parity.
     uint64_t stamp_max = 0;
+    uint64_t stamp_alloc = 0;  // Puts the put_slot arrays hold (stamp_max <= stamp_alloc)
     uint32_t epoch = 1;  // epoch of the last replay round (1: prefill / before any round)
-    uint32_t epoch_limit = 0xFFFFFFF0u;  // renormalise stamps here (NRG_EPOCH_LIMIT for tests)
+    uint32_t epoch_limit = 0xFFFFFFF0u;  // renormalise stamps here (NRG_KNOB_EPOCH_LIMIT for tests)
     uint32_t* d_put_slot[2] = {nullptr, nullptr};
     // Key skew (hm_dup_sample_kernel): Puts combined inside their index block, sampled every
     // dup_every rounds into mapped host memory; a skewed stream takes the bucket rounds.
@@ -159,7 +161,8 @@ struct nrg_ctx {
     uint64_t scan_desc_words = 0;
 
     nrg::Staging stg[4];
-    uint64_t* d_dbg = nullptr;  // diagnostic phase timestamps (NRG_EXP & 2), [tiles][16]
+    uint64_t* d_dbg = nullptr;  // diagnostic phase timestamps (NRG_KNOB_EXP), [tiles][16]
+    uint64_t dbg_words = 0;     // u64 words d_dbg holds
 
     // ---- timing ----
     bool timing = false;

@@ -11,7 +11,6 @@
 
 #include <algorithm>
 #include <cstdio>
-#include <cstdlib>
 #include <cstring>
 #include <new>
 
@@ -348,17 +347,9 @@ int nrg_open(int dev, const nrg_config* cfg_in, nrg_ctx** out) {
         // stream is skewed (hashmap.hip skew_sample); skewed and previous-value rounds take the
         // bucket elector
         c->stamp_max = HM_MAX_BATCH;  // every size; skewed streams switch to bucket rounds
-        if (const char* e = std::getenv("NRG_STAMP_MAX")) c->stamp_max = (uint64_t)std::atoll(e);
-        if (const char* e = std::getenv("NRG_SKEW_EVERY")) c->dup_every = (uint32_t)std::max(1, std::atoi(e));
-        if (const char* e = std::getenv("NRG_EPOCH_LIMIT")) c->epoch_limit = (uint32_t)std::atoll(e);
-        OPEN_CHK(hm_alloc(c, mb));
-        // tuning knobs: Puts per index thread, target entries per elector bucket
-        if (const char* e = std::getenv("NRG_K1")) c->k1_items = (uint32_t)std::atoi(e);
-        if (const char* e = std::getenv("NRG_BK_ENT")) c->bk_ent = (uint32_t)std::atoi(e);
-        if (const char* e = std::getenv("NRG_EXP")) c->exp = (uint32_t)std::atoi(e);
-        if (c->exp & 0x10000) OPEN_CHK(hipMalloc(&c->d_dbg, HM_BK_MAX * 16 * sizeof(uint64_t)));
+        OPEN_CHK(hm_alloc(c, mb));       // clamps stamp_max to max_batch (the put_slot arrays' size)
+        c->stamp_alloc = c->stamp_max;
         c->pipeline = cf.pipeline != 0;
-        if (const char* e = std::getenv("NRG_PIPELINE")) c->pipeline = std::atoi(e) != 0;
     } else if (cf.ds_kind == NRG_DS_STACK) {
         // max_batch <= 2^24: the finish stages one minimum per tile in LDS (stack.hip)
         if (!cf.stack_capacity || cf.stack_capacity >= (1ull << 31) || mb > (1ull << 24)) {
@@ -373,10 +364,6 @@ int nrg_open(int dev, const nrg_config* cfg_in, nrg_ctx** out) {
         OPEN_CHK(hipMemsetAsync(c->d_scan_desc, 0, c->scan_desc_words * 4, c->stream));
         OPEN_CHK(hipMalloc(&c->d_st_aux, st_aux_bytes(mb)));
         c->pipeline = cf.pipeline != 0;
-        if (const char* e = std::getenv("NRG_PIPELINE")) c->pipeline = std::atoi(e) != 0;
-        if (const char* e = std::getenv("NRG_EXP")) c->exp = (uint32_t)std::atoi(e);
-        // diagnostic stamps: tile t at [t * 16], the fused finish workgroups at [(128 + f) * 16]
-        if (c->exp & 2) OPEN_CHK(hipMalloc(&c->d_dbg, std::max<uint64_t>(256, (mb + 2047) / 2048) * 16 * sizeof(uint64_t)));
     } else {
         const uint64_t T = cf.synth_hot_writes + cf.synth_cold_writes;
         if (!cf.synth_n || cf.synth_hot_reads == 0 || cf.synth_n <= cf.synth_hot_reads || T == 0 || T > 64 ||
@@ -392,14 +379,10 @@ int nrg_open(int dev, const nrg_config* cfg_in, nrg_ctx** out) {
         c->scan_desc_words = 2 * (32 + (mb * T + 2047) / 2048);
         OPEN_CHK(hipMalloc(&c->d_scan_desc, c->scan_desc_words * 4));
         if (sort_alloc(c->sort, mb * T) != NRG_OK) { nrg_close(c); return NRG_E_NOMEM; }
-        // sort-free bucket replay where the config allows it; NRG_SY_SORT=1 keeps the sort path
-        const char* force_sort = std::getenv("NRG_SY_SORT");
-        if (sy_bucket_eligible(cf) && !(force_sort && std::atoi(force_sort)))
-            OPEN_CHK(hipMalloc(&c->d_sy_aux, sy_bucket_aux_bytes(cf)));
+        // sort-free bucket replay where the config allows it (the sort path stays for the rest;
+        // nrg_test_set_knob(NRG_KNOB_SY_SORT) forces it for tests)
+        if (sy_bucket_eligible(cf)) OPEN_CHK(hipMalloc(&c->d_sy_aux, sy_bucket_aux_bytes(cf)));
         c->pipeline = cf.pipeline != 0;
-        if (const char* e = std::getenv("NRG_PIPELINE")) c->pipeline = std::atoi(e) != 0;
-        if (const char* e = std::getenv("NRG_EXP")) c->exp = (uint32_t)std::atoi(e);
-        if (c->exp & 2) OPEN_CHK(hipMalloc(&c->d_dbg, 1024 * 16 * sizeof(uint64_t)));  // <= 1024 buckets
         OPEN_CHK(sy_init(c));
     }
     OPEN_CHK(hipStreamSynchronize(c->stream));
@@ -1090,11 +1073,76 @@ extern "C" int nrg_test_hm_skewed(nrg_ctx* c, int* out) {
 
 extern "C" int nrg_test_debug_read(nrg_ctx* c, uint64_t* out, uint64_t words) {
     if (!c || !out) return NRG_E_INVAL;
-    if (!c->d_dbg) return NRG_E_INVAL;
+    if (!c->d_dbg || words > c->dbg_words) return NRG_E_INVAL;
     int r = use_device(c);
     if (r) return r;
     // diagnostic timestamps of the launches so far: no flush of deferred work (it would stamp over them)
     HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipMemcpy(out, c->d_dbg, words * 8, hipMemcpyDeviceToHost));
     return NRG_OK;
+}
+
+// Tuning and diagnostic knobs (include/nrgpu_testing.h): the only way to change them.
+extern "C" int nrg_test_set_knob(nrg_ctx* c, int knob, uint64_t v) {
+    if (!c) return NRG_E_INVAL;
+    int r = use_device(c);
+    if (r) return r;
+    HIPCHK(sync_all(c));  // deferred work of the old setting completes first
+    const bool hm = c->cfg.ds_kind == NRG_DS_HASHMAP, sy = c->cfg.ds_kind == NRG_DS_SYNTHETIC;
+    switch (knob) {
+        case NRG_KNOB_STAMP_MAX:
+            if (!hm) return NRG_E_INVAL;
+            c->stamp_max = std::min<uint64_t>(v, c->stamp_alloc);
+            return NRG_OK;
+        case NRG_KNOB_SKEW_EVERY:
+            if (!hm || v < 1 || v > (1u << 30)) return NRG_E_INVAL;
+            c->dup_every = (uint32_t)v;
+            return NRG_OK;
+        case NRG_KNOB_EPOCH_LIMIT:
+            if (!hm || v < 2 || v > 0xFFFFFFF0ull) return NRG_E_INVAL;
+            c->epoch_limit = (uint32_t)v;
+            return NRG_OK;
+        case NRG_KNOB_K1:
+            if (!hm || v > 4) return NRG_E_INVAL;
+            c->k1_items = (uint32_t)v;
+            return NRG_OK;
+        case NRG_KNOB_BK_ENT:
+            if (!hm || v > (1u << 20)) return NRG_E_INVAL;
+            c->bk_ent = (uint32_t)v;
+            return NRG_OK;
+        case NRG_KNOB_EXP: {
+            if (v > 0xFFFFFFFFull) return NRG_E_INVAL;
+            c->exp = (uint32_t)v;
+            // timestamp buffer: hashmap elector blocks, stack tiles (+ finish workgroups at 128..),
+            // synthetic buckets (<= 1024); 16 words each
+            uint64_t words = 0;
+            if (hm && (c->exp & 0x10000)) words = (uint64_t)HM_BK_MAX * 16;
+            if (c->cfg.ds_kind == NRG_DS_STACK && (c->exp & 2))
+                words = std::max<uint64_t>(256, (c->cfg.max_batch + 2047) / 2048) * 16;
+            if (sy && (c->exp & 2)) words = 1024 * 16;
+            if (words > c->dbg_words) {
+                if (c->d_dbg) HIPCHK(hipFree(c->d_dbg));
+                c->d_dbg = nullptr;
+                c->dbg_words = 0;
+                HIPCHK(hipMalloc(&c->d_dbg, words * sizeof(uint64_t)));
+                HIPCHK(hipMemsetAsync(c->d_dbg, 0, words * sizeof(uint64_t), c->stream));
+                c->dbg_words = words;
+            }
+            return NRG_OK;
+        }
+        case NRG_KNOB_SY_SORT:
+            if (!sy || v > 1) return NRG_E_INVAL;
+            if (v && c->d_sy_aux) {  // sort path: the bucket scratch goes away
+                HIPCHK(hipFree(c->d_sy_aux));
+                c->d_sy_aux = nullptr;
+            } else if (!v && !c->d_sy_aux && sy_bucket_eligible(c->cfg)) {
+                HIPCHK(hipMalloc(&c->d_sy_aux, sy_bucket_aux_bytes(c->cfg)));
+            }
+            return NRG_OK;
+        case NRG_KNOB_PIPELINE:
+            if (v > 1) return NRG_E_INVAL;
+            c->pipeline = v != 0;
+            return NRG_OK;
+        default: return NRG_E_INVAL;
+    }
 }

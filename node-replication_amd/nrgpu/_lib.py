@@ -180,7 +180,12 @@ TEST_SIGNATURES = {
     "nrg_test_ring_read": (C.c_int, [vp, u64, vp]),
     "nrg_test_debug_read": (C.c_int, [vp, vp, u64]),
     "nrg_test_hm_skewed": (C.c_int, [vp, vp]),
+    "nrg_test_set_knob": (C.c_int, [vp, C.c_int, u64]),
 }
+
+# nrg_test_set_knob knobs (include/nrgpu_testing.h): tuning and diagnostics of an open context
+KNOBS = {"STAMP_MAX": 1, "SKEW_EVERY": 2, "EPOCH_LIMIT": 3, "K1": 4, "BK_ENT": 5, "EXP": 6, "SY_SORT": 7,
+         "PIPELINE": 8}
 
 _lib = None
 

@@ -50,7 +50,9 @@ def _dptr(t) -> C.c_void_p:
 class DeviceReplica:
     """Thin owner of one nrg_ctx (one replica in one GPU's HBM)."""
 
-    def __init__(self, kind: int, device: int = 0, **cfg):
+    def __init__(self, kind: int, device: int = 0, knobs: Optional[dict] = None, **cfg):
+        """`cfg`: nrg_config fields; `knobs`: {name: value} of nrg_test_set_knob (tuning and
+        diagnostics, include/nrgpu_testing.h), applied right after nrg_open."""
         lib = L.load()
         self.kind = kind
         self.device = device
@@ -64,6 +66,12 @@ class DeviceReplica:
         L.check(lib.nrg_open(device, C.byref(c), C.byref(h)), "nrg_open")
         self._h = h
         self._lib = lib
+        for k, v in (knobs or {}).items():
+            self.set_knob(k, v)
+
+    def set_knob(self, name: str, value: int):
+        """nrg_test_set_knob: a tuning/diagnostic knob by name (L.KNOBS) on this open context."""
+        L.check(self._lib.nrg_test_set_knob(self._h, L.KNOBS[name], int(value)), f"knob {name}")
 
     # -- lifetime ------------------------------------------------------------------
     def close(self):

@@ -137,17 +137,16 @@ def test_fused_round_device(nrg, orc):
 
 
 @pytest.mark.parametrize("path", ["stamp", "bucket"])
-def test_pipelined_rounds_back_to_back(nrg, orc, monkeypatch, path):
+def test_pipelined_rounds_back_to_back(nrg, orc, path):
     """config.pipeline = 1: rounds enqueued back to back, no host sync in between. Each round's
     reads run in the next round's launch, beside its index pass (and, for stamp rounds, beside
     the apply of their own round's writes), and must see exactly their own round's state (keys
     created by later rounds invisible, values overwritten later not yet there).
-    NRG_STAMP_MAX=0 sends every round through the bucket elector instead."""
+    Knob STAMP_MAX = 0 sends every round through the bucket elector instead."""
     import torch
 
-    if path == "bucket":
-        monkeypatch.setenv("NRG_STAMP_MAX", "0")
-    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=17, max_batch=1 << 14, pipeline=1)
+    knobs = {"STAMP_MAX": 0} if path == "bucket" else {}
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, knobs=knobs, log2_slots=17, max_batch=1 << 14, pipeline=1)
     dev.use_torch_stream()
     om = orc.HashMap()
     dev.hm_prefill_range(3000, 1)
@@ -406,22 +405,21 @@ def test_b1_full_size_rounds(nrg, orc):
     assert dev.hm_digest() == om.digest()
 
 
-def test_epoch_renormalisation(nrg, orc, monkeypatch):
+def test_epoch_renormalisation(nrg, orc):
     """Replay epochs are 32-bit; before they wrap every stamp is renormalised to epoch 1. A limit
-    of 6 (NRG_EPOCH_LIMIT) renormalises every few rounds: pipelined stamp and bucket rounds with
+    of 6 (knob EPOCH_LIMIT) renormalises every few rounds: pipelined stamp and bucket rounds with
     new keys, overwrites and side-slot keys across several renormalisations, against the oracle."""
     import torch
 
-    monkeypatch.setenv("NRG_EPOCH_LIMIT", "6")
-    monkeypatch.setenv("NRG_STAMP_MAX", "5000")
-    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=16, max_batch=8192, pipeline=1)
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, knobs={"EPOCH_LIMIT": 6, "STAMP_MAX": 5000}, log2_slots=16,
+                            max_batch=8192, pipeline=1)
     dev.use_torch_stream()
     om = orc.HashMap()
     dev.hm_prefill_range(500, 1)
     om.prefill_range(500, 1)
     outs, want = [], []
     for r in range(17):
-        W = 3000 if r % 3 else 7000  # 7000 > NRG_STAMP_MAX: bucket rounds in between
+        W = 3000 if r % 3 else 7000  # 7000 > STAMP_MAX: bucket rounds in between
         keys = orc.gen_uniform(W, 900 + r, 4000 + 150 * r)
         keys[::113] = EMPTY
         vals = orc.gen_raw(W, 950 + r)
@@ -444,7 +442,7 @@ def test_epoch_renormalisation(nrg, orc, monkeypatch):
     _check_state(dev, om)
 
 
-def test_skew_switches_round_kind(nrg, orc, monkeypatch):
+def test_skew_switches_round_kind(nrg, orc):
     """Stamp rounds (one launch, one stamp atomic per distinct key per block) are faster for
     uniform keys, bucket rounds (no atomics per Put) for skewed ones; the replica switches from
     the sampled share of Puts combined inside their block (every 2 rounds here). Uniform rounds,
@@ -454,8 +452,8 @@ def test_skew_switches_round_kind(nrg, orc, monkeypatch):
 
     import torch
 
-    monkeypatch.setenv("NRG_SKEW_EVERY", "2")
-    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=19, max_batch=1 << 15, pipeline=1)
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, knobs={"SKEW_EVERY": 2}, log2_slots=19, max_batch=1 << 15,
+                            pipeline=1)
     dev.use_torch_stream()
     om = orc.HashMap()
     dev.hm_prefill_range(5000, 1)

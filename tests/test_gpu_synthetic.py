@@ -1,7 +1,7 @@
 """AbstractDataStructure parity (benches/synthetic.rs): HIP replay vs oracle.
 
 Both replay paths are covered: the default sort-free bucket replay and the sort-based one
-(NRG_SY_SORT=1, kept for configurations the bucket path does not take).
+(knob NRG_KNOB_SY_SORT = 1, kept for configurations the bucket path does not take).
 
 The bench uses ReadWrite only with tid = core id (:296-335); WriteOnly and ReadOnly are
 part of the data structure's Dispatch (:177-195) and are covered too, including the
@@ -26,12 +26,9 @@ def _ops(orc, n, seed, tids, wo_frac):
 
 
 @pytest.fixture(params=["bucket", "sort"])
-def path(request, monkeypatch):
-    if request.param == "sort":
-        monkeypatch.setenv("NRG_SY_SORT", "1")
-    else:
-        monkeypatch.delenv("NRG_SY_SORT", raising=False)
-    return request.param
+def path(request):
+    """the replay path's knobs (nrg_test_set_knob)"""
+    return {"SY_SORT": 1} if request.param == "sort" else {}
 
 
 def _check_rounds(nrg, orc, dev, os_, rounds, n, seed, tids, wo, tweak=None):
@@ -50,7 +47,7 @@ def _check_rounds(nrg, orc, dev, os_, rounds, n, seed, tids, wo, tweak=None):
 @pytest.mark.parametrize("n,wo,tids", [(1000, 0, [0]), (20000, 0, [0, 1, 5, 63]), (20000, 30, [3, 7]),
                                        (5000, 100, [1, 2])])
 def test_synth_rounds(nrg, orc, path, n, wo, tids):
-    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_SYNTHETIC, 0, max_batch=1 << 15)
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_SYNTHETIC, 0, knobs=path, max_batch=1 << 15)
     os_ = orc.Synthetic()
     for r in range(3):
         ops = _ops(orc, n, 900 + r, tids, wo)
@@ -72,7 +69,7 @@ def test_synth_rounds(nrg, orc, path, n, wo, tids):
 
 def test_synth_large_rounds(nrg, orc, path):
     """Many 2048-op tiles and all 391 buckets: the bench's op kind (ReadWrite, tid < 64)."""
-    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_SYNTHETIC, 0, max_batch=1 << 19)
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_SYNTHETIC, 0, knobs=path, max_batch=1 << 19)
     _check_rounds(nrg, orc, dev, orc.Synthetic(), 3, 300_000, 4242, list(range(64)), 0)
     dev.close()
 
@@ -85,7 +82,7 @@ def test_synth_one_word(nrg, orc, path, wo):
         ops["r2"][:] = 0
         ops["tid"][::7] = 0
 
-    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_SYNTHETIC, 0, max_batch=1 << 16)
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_SYNTHETIC, 0, knobs=path, max_batch=1 << 16)
     _check_rounds(nrg, orc, dev, orc.Synthetic(), 2, 40_000, 77, [0], wo, tweak)
     dev.close()
 
@@ -96,7 +93,7 @@ def test_synth_partial_tiles_mixed(nrg, orc, path):
         ops["op"][1000:1300] = 0
         ops["r2"][::37] = 0xFFFFFFFFFFFFFFFF
 
-    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_SYNTHETIC, 0, max_batch=1 << 15)
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_SYNTHETIC, 0, knobs=path, max_batch=1 << 15)
     os_ = orc.Synthetic()
     for n, seed in ((1, 5), (63, 6), (2049, 7), (4095, 8), (12345, 9)):
         _check_rounds(nrg, orc, dev, os_, 1, n, seed, [0, 2, 9, 31, 63], 5, tweak if n > 1300 else None)
@@ -109,7 +106,7 @@ def test_synth_round_fused(nrg, orc, path, n, wo, tids):
     several rounds whose ring positions wrap (small log)."""
     import torch
 
-    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_SYNTHETIC, 0, max_batch=1 << 15, log_bytes=64 * 65536)
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_SYNTHETIC, 0, knobs=path, max_batch=1 << 15, log_bytes=64 * 65536)
     os_ = orc.Synthetic()
     resp = torch.zeros(n, dtype=torch.int64, device="cuda")
     some = torch.zeros(n, dtype=torch.uint8, device="cuda")
@@ -145,12 +142,10 @@ def test_synth_bench_size_rounds(nrg, orc):
 
 
 @pytest.mark.parametrize("wo", [0, 40])
-def test_synth_heavy_buckets(nrg, orc, monkeypatch, wo):
+def test_synth_heavy_buckets(nrg, orc, wo):
     """Skewed rounds: tid 0 (whose cold touches start at word hot_reads) on 30 % of the ops and
     r2 = 0 (all of an op's cold touches on one word) on 5 %, so a few buckets carry several times
     the mean and take many passes; WriteOnly ops make the values depend on each word's last SET."""
-    monkeypatch.delenv("NRG_SY_SORT", raising=False)
-
     def tweak(ops):
         ops["tid"][::3] = 0
         ops["r2"][::20] = 0

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Kernel-trace a bench.py run on the GPU box and print the per-kernel stats (rocprofv3).
 # Usage (from the repo root, through gpurun): tools/ktrace.sh TAG [bench.py args...]
-# Environment knobs (NRG_K1, NRG_BK_ENT, ...) are taken from the caller's environment.
+# Tuning knobs go through bench.py --knob NAME=VALUE (nrg_test_set_knob), e.g. --knob K1=2.
 # Output: gpurun_out/kt_<TAG>/ (trace CSVs, bench JSON line) and a summary on stdout.
 set -o pipefail
 TAG=$1; shift
