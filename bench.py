@@ -270,6 +270,25 @@ def common_fields(args, env, value, ms_per_step, metric, dtype, config):
     }
 
 
+ROOF_ROUNDS = 64  # rounds of the roofline region (at least --steps)
+
+
+def roofline_region(args, rep, run, names):
+    """Kernel durations for the roofline, measured right after the timed region on the same
+    stream and workload: max(steps, ROOF_ROUNDS) more rounds with every timing_every-th launch
+    of the named kernels bracketed by HIP events stamped from their own dispatch. The timed
+    region itself carries no events (a bracketed launch costs wall time,
+    profiles/r02_s8_event_bracketing.txt), so `value` is the unperturbed rate.
+    Returns {name: (launches, total_ms)}."""
+    if args.no_kernel_timing:
+        return {n: (0, 0.0) for n in names}
+    rep.kernel_timing(True, only=",".join(names), every=args.timing_every)
+    run(max(args.steps, ROOF_ROUNDS))
+    out = {n: rep.kernel_time(n) for n in names}
+    rep.kernel_timing(False)
+    return out
+
+
 def roofline(kernel, k_bytes, k_n, k_ms, args, traffic):
     k_avg_s = (k_ms / 1e3 / k_n) if k_n else float("nan")
     achieved = k_bytes / k_avg_s / 1e9 if k_n else None
@@ -284,6 +303,8 @@ def roofline(kernel, k_bytes, k_n, k_ms, args, traffic):
         "traffic_source": traffic.get("source") if traffic else None,
         "bytes_per_launch": int(k_bytes),
         "sampled_every": args.timing_every,
+        "region": "%d rounds after the timed region, every %d-th launch event-bracketed" % (
+            max(args.steps, ROOF_ROUNDS), args.timing_every),
         "traffic_key": traffic_key(args),
         "avg_launch_us": round(k_avg_s * 1e6, 3) if k_n else None,
         "launches": k_n,
@@ -406,19 +427,17 @@ def run_hashmap(args, env):
     rep.sync()
     log(f"rank {rank}: warmup {args.warmup} rounds done")
 
-    # timed region. The dominant (and only per-round) kernel, hm_round, is timed with HIP events
-    # stamped from its own dispatch packets (hipExtLaunchKernelGGL start/stop events on the
-    # stream it runs on). An event-stamped dispatch costs ~5 us of command-processor time, so
-    # only every TIMING_EVERY-th launch is stamped (steady-state launches: round e's index plus
-    # round e-1's apply and reads, i.e. one round of work each).
+    # timed region: no HIP events. The dominant (and only per-round) kernel, hm_round, is then
+    # timed in the roofline region with events stamped from its own dispatch packets
+    # (hipExtLaunchKernelGGL start/stop events on the stream it runs on) on every timing_every-th
+    # launch (steady-state launches: round e's index plus round e-1's apply and reads, i.e. one
+    # round of work each).
     host_s = [0.0]
-    rep.kernel_timing(not args.no_kernel_timing, only="hm_round,hm_elect", every=args.timing_every)
-    elapsed = run(args.steps, host_s=host_s)
-    k_n, k_ms = rep.kernel_time("hm_round")
-    e_n, e_ms = rep.kernel_time("hm_elect")
+    elapsed = run(args.steps, host_s=host_s)  # no events in the timed region
+    kt = roofline_region(args, rep, run, ["hm_round", "hm_elect"])
+    (k_n, k_ms), (e_n, e_ms) = kt["hm_round"], kt["hm_elect"]
     if e_n and k_n:  # bucket-elected rounds: the round's kernels are hm_round + hm_elect
         k_ms = k_ms + e_ms * k_n / e_n
-    rep.kernel_timing(False)
     rep.sync()
     value = world * args.ops_per_gpu * args.steps / elapsed / 1e6
 
@@ -586,11 +605,12 @@ def run_synthetic(args, env):
     for i in range(args.warmup):
         step(i)
     rep.sync()
-    rep.kernel_timing(not args.no_kernel_timing, only="sy_replay", every=args.timing_every)
-    mode["n"] = args.steps
-    elapsed = env.timed(args.steps, step, rep)
-    k_n, k_ms = rep.kernel_time("sy_replay")
-    rep.kernel_timing(False)
+    def run(n):
+        mode["n"] = n
+        return env.timed(n, step, rep)
+
+    elapsed = run(args.steps)  # no events in the timed region
+    k_n, k_ms = roofline_region(args, rep, run, ["sy_replay"])["sy_replay"]
     rep.sync()
     value = world * N * args.steps / elapsed / 1e6
     if rank != 0:
@@ -689,11 +709,12 @@ def run_stack(args, env):
     for i in range(args.warmup):
         step(i)
     rep.sync()
-    rep.kernel_timing(not args.no_kernel_timing, only="st_replay", every=args.timing_every)
-    mode["n"] = args.steps
-    elapsed = env.timed(args.steps, step, rep)
-    k_n, k_ms = rep.kernel_time("st_replay")
-    rep.kernel_timing(False)
+    def run(n):
+        mode["n"] = n
+        return env.timed(n, step, rep)
+
+    elapsed = run(args.steps)  # no events in the timed region
+    k_n, k_ms = roofline_region(args, rep, run, ["st_replay"])["st_replay"]
     rep.sync()
     value = world * N * args.steps / elapsed / 1e6
     if rank != 0:
@@ -764,10 +785,9 @@ def main():
                     help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo: CPU rehearsal)")
     ap.add_argument("--share-gpu", action="store_true", help="all ranks on cuda:0 (gloo rehearsal on a 1-GPU box)")
     ap.add_argument("--csv", default=None, help="append scaleout_benchmarks.csv rows (reference format)")
-    ap.add_argument("--timing-every", type=int, default=0,
-                    help="event-stamp every n-th launch of the timed kernel (0: max(1, min(32, steps // 10)), "
-                         "so the roofline averages >= 10 launches; a stamped launch costs wall time, "
-                         "profiles/r02_s8_timing_sampling.txt)")
+    ap.add_argument("--timing-every", type=int, default=4,
+                    help="roofline region: event-stamp every n-th launch of the dominant kernel (>= 16 samples "
+                         "over its 64+ rounds; the timed region itself is never stamped)")
     ap.add_argument("--knob", action="append", default=[], metavar="NAME=VALUE",
                     help="diagnostic/tuning knob of the replica (nrg_test_set_knob, include/nrgpu_testing.h), "
                          "e.g. K1=2; never needed for the headline")
@@ -775,8 +795,7 @@ def main():
                     help="1: a round's apply+reads ride in the next round's launch (nrg_config.pipeline); "
                          "0: every round call completes its own reads")
     args = ap.parse_args()
-    if args.timing_every <= 0:
-        args.timing_every = max(1, min(32, args.steps // 10))
+    args.timing_every = max(1, args.timing_every)
     env = Env(args)
     runner = {"stack": run_stack, "synthetic": run_synthetic}.get(args.workload, run_hashmap)
     res = runner(args, env)

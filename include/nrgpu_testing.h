@@ -40,6 +40,15 @@ int nrg_test_debug_read(nrg_ctx* ctx, uint64_t* out, uint64_t words);
 #define NRG_KNOB_SY_SORT 7     /* synthetic: 1 = sort-based replay instead of the bucket path      */
 #define NRG_KNOB_PIPELINE 8    /* overrides nrg_config.pipeline                                    */
 int nrg_test_set_knob(nrg_ctx* ctx, int knob, uint64_t value);
+
+/* Replica groups created after nrg_test_loopback_collectives(1) (nrg_group_open,
+ * nrg_group_unique_id / nrg_group_join) use an in-process stand-in for RCCL instead of RCCL:
+ * all-gathers and send/recv pairs become device copies on the members' streams, ordered with
+ * events exactly where RCCL orders them. With it, nrg_group_open(devices = {0, 0, ...}) runs a
+ * G-member group on one GPU -- the multi-rank code of nrg_group_round_async and
+ * nrg_group_partitioned_round -- so tests check it against the oracle. One process must drive
+ * every member (nrg_group_join: groups of one). 0 switches back to RCCL for later groups. */
+int nrg_test_loopback_collectives(int on);
 // Hashmap: 1 when the sampled key skew sends rounds to the bucket elector (hashmap.hip
 // skew_sample), 0 when they take the one-launch stamp rounds.
 int nrg_test_hm_skewed(nrg_ctx* ctx, int* out);

@@ -18,26 +18,20 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <mutex>
 #include <new>
 #include <vector>
 
+#include "collectives.hpp"
 #include "internal.hpp"
+#include "../../include/nrgpu_testing.h"
 
 namespace {
 
-struct Rccl {
-    decltype(&ncclGetUniqueId) get_unique_id = nullptr;
-    decltype(&ncclCommInitRank) init_rank = nullptr;
-    decltype(&ncclCommInitAll) init_all = nullptr;
-    decltype(&ncclAllGather) all_gather = nullptr;
-    decltype(&ncclGroupStart) group_start = nullptr;
-    decltype(&ncclGroupEnd) group_end = nullptr;
-    decltype(&ncclCommDestroy) destroy = nullptr;
-    decltype(&ncclSend) send = nullptr;  // partitioned rounds only
-    decltype(&ncclRecv) recv = nullptr;
-};
+using Rccl = nrg::Collectives;
 
 std::mutex g_rccl_mu;
 bool g_rccl_tried = false;
@@ -70,6 +64,12 @@ const Rccl* rccl() {
     return g_rccl_ok ? &g_rccl : nullptr;
 }
 
+// nrg_test_loopback_collectives: groups created from now on use loopback.cpp instead of RCCL
+std::atomic<int> g_loopback{0};
+
+// the collectives a new group binds to (kept by the group for its lifetime)
+const Rccl* backend() { return g_loopback.load() ? nrg::loopback_collectives() : rccl(); }
+
 constexpr int NBUF = 3;  // gathered-log buffers in rotation per member
 
 // A device buffer grown on demand; a reallocation first drains the streams that may use it.
@@ -80,7 +80,9 @@ struct DBuf {
 
 // Partitioned rounds (nrg_group_partitioned_round): buffers of one member.
 enum PtBuf { PB_POUT, PB_PPOS, PB_KOUT, PB_GPOS, PB_CNT, PB_ALLCNT, PB_RPUT, PB_RKEY, PB_RVAL, PB_RFOUND, PB_RPREV,
-             PB_RPREVF, PB_AVAL, PB_AFOUND, PB_APREV, PB_APREVF, PB_N };
+             PB_RPREVF, PB_AVAL, PB_AFOUND, PB_APREV, PB_APREVF, PB_ST, PB_ALLST, PB_N };
+
+constexpr uint64_t GC_FROM_HEAD = 32 * 256;  // nr/src/log.rs:36 (the ring keeps this much free)
 
 struct Member {
     nrg_ctx* ctx = nullptr;
@@ -98,7 +100,8 @@ struct Member {
     void* sbuf = nullptr;  // padded send copy when a segment is shorter than the stride
     uint64_t sbytes = 0;
     DBuf pt[PB_N];               // partitioned rounds
-    std::vector<uint64_t> hcnt;  // [nranks][2 * nranks + 1] counts (and previous-value flags)
+    std::vector<uint64_t> hcnt;  // [nranks][2 * nranks + XW_N] counts, capacities, flags
+    uint64_t xwords[8] = {};     // this rank's host words of the exchange
     hipEvent_t pt_ev = nullptr;
 };
 
@@ -145,6 +148,7 @@ void member_free(Member& m, const Rccl* R) {
 }  // namespace
 
 struct nrg_group {
+    const Rccl* R = nullptr;  // RCCL, or the test loopback (fixed at creation)
     int nranks = 0;
     int rank0 = 0;
     bool owns = false;  // replicas opened by nrg_group_open
@@ -154,9 +158,14 @@ struct nrg_group {
 
 extern "C" {
 
+int nrg_test_loopback_collectives(int on) {
+    g_loopback.store(on ? 1 : 0);
+    return NRG_OK;
+}
+
 int nrg_group_unique_id(uint8_t id[NRG_GROUP_ID_BYTES]) {
     if (!id) return NRG_E_INVAL;
-    const Rccl* R = rccl();
+    const Rccl* R = backend();
     if (!R) return NRG_E_COMM;
     ncclUniqueId u;
     if (R->get_unique_id(&u) != ncclSuccess) return NRG_E_COMM;
@@ -168,10 +177,11 @@ int nrg_group_unique_id(uint8_t id[NRG_GROUP_ID_BYTES]) {
 int nrg_group_join(nrg_ctx* replica, const uint8_t id[NRG_GROUP_ID_BYTES], int nranks, int rank, nrg_group** out) {
     if (!replica || !id || !out || nranks < 1 || rank < 0 || rank >= nranks || nranks > 64) return NRG_E_INVAL;
     *out = nullptr;
-    const Rccl* R = rccl();
+    const Rccl* R = backend();
     if (!R) return NRG_E_COMM;
     nrg_group* g = new (std::nothrow) nrg_group();
     if (!g) return NRG_E_NOMEM;
+    g->R = R;
     g->nranks = nranks;
     g->rank0 = rank;
     g->m.resize(1);
@@ -194,10 +204,11 @@ int nrg_group_join(nrg_ctx* replica, const uint8_t id[NRG_GROUP_ID_BYTES], int n
 int nrg_group_open(const int* devices, int n, const nrg_config* cfg, nrg_group** out) {
     if (!devices || n < 1 || n > 64 || !cfg || !out) return NRG_E_INVAL;
     *out = nullptr;
-    const Rccl* R = rccl();
+    const Rccl* R = backend();
     if (!R) return NRG_E_COMM;
     nrg_group* g = new (std::nothrow) nrg_group();
     if (!g) return NRG_E_NOMEM;
+    g->R = R;
     g->nranks = n;
     g->rank0 = 0;
     g->owns = true;
@@ -226,7 +237,7 @@ int nrg_group_open(const int* devices, int n, const nrg_config* cfg, nrg_group**
 
 int nrg_group_close(nrg_group* g) {
     if (!g) return NRG_E_INVAL;
-    const Rccl* R = rccl();
+    const Rccl* R = g->R;
     for (Member& m : g->m) {
         nrg_ctx* c = m.ctx;
         member_free(m, R);
@@ -258,7 +269,7 @@ int nrg_group_set_input_stream(nrg_group* g, int member, void* s) {
 
 int nrg_group_round_async(nrg_group* g, const nrg_round* rounds, const uint64_t* seg_lens) {
     if (!g || !rounds) return NRG_E_INVAL;
-    const Rccl* R = rccl();
+    const Rccl* R = g->R;
     if (!R) return NRG_E_COMM;
     const int nl = (int)g->m.size();
     const uint32_t kind = g->m[0].ctx->cfg.ds_kind;
@@ -389,44 +400,64 @@ static int order(Member& m, hipStream_t from, hipStream_t to) {
         if (_r != NRG_OK) return _r;              \
     } while (0)
 
+// Exchange words per rank (u64): [0, G) Puts per owner, [G, 2G) Gets per owner, then
+enum : uint64_t {
+    XW_PREV = 0,    // 1 when this rank wants its Puts' previous values
+    XW_RP_CAP = 1,  // received Puts its buffers hold now
+    XW_RK_CAP = 2,  // received Get keys its buffers hold now
+    XW_ERR = 3,     // -NRG_E_* of a local failure before the exchange, else 0
+    XW_N = 4,
+};
+
 int nrg_group_partitioned_round(nrg_group* g, const nrg_round* rounds) {
     if (!g || !rounds) return NRG_E_INVAL;
-    const Rccl* R = rccl();
+    const Rccl* R = g->R;
     if (!R || !R->send || !R->recv) return NRG_E_COMM;
     const int G = g->nranks, nl = (int)g->m.size();
     if (G > NRG_MAX_PARTS) return NRG_E_INVAL;
-    const uint64_t CW = 2 * (uint64_t)G + 1;  // per rank: Puts per owner, Gets per owner, wants previous values
-    for (int i = 0; i < nl; i++) {
-        const nrg_round& x = rounds[i];
-        if (g->m[i].ctx->cfg.ds_kind != NRG_DS_HASHMAP || (x.n && !x.recs) ||
-            (x.n_gets && (!x.get_keys || !x.get_vals || !x.get_found)))
-            return NRG_E_INVAL;
-        if (x.n >= (1ull << 32) || x.n_gets >= (1ull << 32)) return NRG_E_CAPACITY;
-    }
-    // 1. partition each member's Puts and Gets by owner (its stream, after its inputs)
+    const uint64_t CW = 2 * (uint64_t)G + XW_N;
+    // Every failure from here to the send/recv plan is agreed on by all ranks before anyone
+    // posts a send or receive: a rank that returned alone would leave its peers waiting in RCCL.
+    // Local failures before the count exchange travel in its XW_ERR word; buffer growth after it
+    // is known to every rank from the exchanged capacities and confirmed by a status all-gather.
     for (int i = 0; i < nl; i++) {
         Member& m = g->m[i];
         const nrg_round& x = rounds[i];
+        int err = NRG_OK;
+        if (m.ctx->cfg.ds_kind != NRG_DS_HASHMAP || (x.n && !x.recs) ||
+            (x.n_gets && (!x.get_keys || !x.get_vals || !x.get_found)))
+            err = NRG_E_INVAL;
+        else if (x.n >= (1ull << 32) || x.n_gets >= (1ull << 32))
+            err = NRG_E_CAPACITY;
         nrg_ctx* c = m.ctx;
         RCHK(nrg::ctx_use_device(c));
-        RCHK(grow(m, PB_POUT, x.n * 16));
-        RCHK(grow(m, PB_PPOS, x.n * 4));
-        RCHK(grow(m, PB_KOUT, x.n_gets * 8));
-        RCHK(grow(m, PB_GPOS, x.n_gets * 4));
+        // exchange buffers first: without them this rank cannot take part at all
         RCHK(grow(m, PB_CNT, CW * 8));
         RCHK(grow(m, PB_ALLCNT, (uint64_t)G * CW * 8));
+        RCHK(grow(m, PB_ST, 8));
+        RCHK(grow(m, PB_ALLST, (uint64_t)G * 8));
+        if (err == NRG_OK) {
+            const PtBuf local[] = {PB_POUT, PB_PPOS, PB_KOUT, PB_GPOS, PB_AVAL, PB_AFOUND, PB_APREV, PB_APREVF};
+            const uint64_t bytes[] = {x.n * 16, x.n * 4, x.n_gets * 8, x.n_gets * 4,
+                                      x.n_gets * 8, x.n_gets, x.n * 8, x.n};
+            for (int k = 0; k < 8 && err == NRG_OK; k++) err = grow(m, local[k], bytes[k]);
+        }
         if (m.in_set && m.in_stream != c->stream) RCHK(order(m, m.in_stream, c->stream));
-        RCHK(nrg_hashmap_partition_async(c, (const nrg_put*)x.recs, x.n, x.get_keys, x.n_gets, (uint32_t)G,
-                                         (nrg_put*)m.pt[PB_POUT].p, (uint32_t*)m.pt[PB_PPOS].p,
-                                         (uint64_t*)m.pt[PB_KOUT].p, (uint32_t*)m.pt[PB_GPOS].p,
-                                         (uint64_t*)m.pt[PB_CNT].p));
-        // word 2G: 1 when this rank wants its Puts' previous values (little-endian u64)
-        void* flag = (uint64_t*)m.pt[PB_CNT].p + 2 * G;
-        GCHK(hipMemsetAsync(flag, 0, 8, c->stream));
-        if (x.resp && x.some) GCHK(hipMemsetAsync(flag, 1, 1, c->stream));
+        if (err == NRG_OK)
+            err = nrg_hashmap_partition_async(c, (const nrg_put*)x.recs, x.n, x.get_keys, x.n_gets, (uint32_t)G,
+                                              (nrg_put*)m.pt[PB_POUT].p, (uint32_t*)m.pt[PB_PPOS].p,
+                                              (uint64_t*)m.pt[PB_KOUT].p, (uint32_t*)m.pt[PB_GPOS].p,
+                                              (uint64_t*)m.pt[PB_CNT].p);
+        uint64_t* w = m.xwords;
+        w[XW_PREV] = (x.resp && x.some) ? 1 : 0;
+        w[XW_RP_CAP] = std::min(std::min(m.pt[PB_RPUT].bytes / 16, m.pt[PB_RPREV].bytes / 8), m.pt[PB_RPREVF].bytes);
+        w[XW_RK_CAP] = std::min(std::min(m.pt[PB_RKEY].bytes / 8, m.pt[PB_RVAL].bytes / 8), m.pt[PB_RFOUND].bytes);
+        w[XW_ERR] = (uint64_t)(-err);
+        // host words of the exchange (pageable source: copied before hipMemcpyAsync returns)
+        GCHK(hipMemcpyAsync((uint64_t*)m.pt[PB_CNT].p + 2 * G, w, XW_N * 8, hipMemcpyHostToDevice, c->stream));
         RCHK(order(m, c->stream, m.cstream));
     }
-    // 2. every rank's counts to every rank; the host needs them to size the exchanges
+    // 2. every rank's counts, capacities and status to every rank (one host round trip)
     if (R->group_start() != ncclSuccess) return NRG_E_COMM;
     ncclResult_t res = ncclSuccess;
     for (int i = 0; i < nl && res == ncclSuccess; i++)
@@ -439,8 +470,20 @@ int nrg_group_partitioned_round(nrg_group* g, const nrg_round* rounds) {
         GCHK(hipMemcpyAsync(m.hcnt.data(), m.pt[PB_ALLCNT].p, (uint64_t)G * CW * 8, hipMemcpyDeviceToHost, m.cstream));
         GCHK(hipStreamSynchronize(m.cstream));
     }
-    bool any_prev = false;
-    for (int s = 0; s < G; s++) any_prev |= g->m[0].hcnt[(size_t)s * CW + 2 * G] != 0;
+    const std::vector<uint64_t>& H = g->m[0].hcnt;  // identical on every rank
+    auto word = [&](int s, uint64_t k) { return H[(size_t)s * CW + 2 * G + k]; };
+    for (int s = 0; s < G; s++)
+        if (word(s, XW_ERR)) return -(int)word(s, XW_ERR);  // the same answer on every rank
+    bool any_prev = false, any_grow = false;
+    for (int s = 0; s < G; s++) {
+        any_prev |= word(s, XW_PREV) != 0;
+        uint64_t rp = 0, rk = 0;  // what rank s receives
+        for (int o = 0; o < G; o++) {
+            rp += H[(size_t)o * CW + s];
+            rk += H[(size_t)o * CW + G + s];
+        }
+        any_grow |= rp > word(s, XW_RP_CAP) || rk > word(s, XW_RK_CAP);
+    }
     // 3. Puts and Get keys to their owners: member rank r sends its owner-o group to o and receives
     //    rank s's group for r at offset sum_{s' < s} (rank order = the global log order)
     struct Plan {
@@ -448,6 +491,7 @@ int nrg_group_partitioned_round(nrg_group* g, const nrg_round* rounds) {
         uint64_t rp = 0, rk = 0;
     };
     std::vector<Plan> plan(nl);
+    std::vector<int> grow_err(nl, NRG_OK);
     for (int i = 0; i < nl; i++) {
         Member& m = g->m[i];
         Plan& P = plan[i];
@@ -466,20 +510,40 @@ int nrg_group_partitioned_round(nrg_group* g, const nrg_round* rounds) {
             P.pfrom_off[o] = cq, cq += P.pfrom[o];
             P.gfrom_off[o] = d, d += P.gfrom[o];
         }
-        if (a != rounds[i].n || b != rounds[i].n_gets) return NRG_E_HIP;  // counts disagree with the inputs
+        if (a != rounds[i].n || b != rounds[i].n_gets) grow_err[i] = NRG_E_HIP;  // partition kernel disagrees
         P.rp = cq;
         P.rk = d;
-        const nrg_round& x = rounds[i];
-        RCHK(grow(m, PB_RPUT, P.rp * 16));
-        RCHK(grow(m, PB_RKEY, P.rk * 8));
-        RCHK(grow(m, PB_RVAL, P.rk * 8));
-        RCHK(grow(m, PB_RFOUND, P.rk));
-        RCHK(grow(m, PB_RPREV, P.rp * 8));
-        RCHK(grow(m, PB_RPREVF, P.rp));
-        RCHK(grow(m, PB_AVAL, x.n_gets * 8));
-        RCHK(grow(m, PB_AFOUND, x.n_gets));
-        RCHK(grow(m, PB_APREV, x.n * 8));
-        RCHK(grow(m, PB_APREVF, x.n));
+        if (any_grow && grow_err[i] == NRG_OK) {
+            RCHK(nrg::ctx_use_device(m.ctx));
+            const PtBuf recv[] = {PB_RPUT, PB_RPREV, PB_RPREVF, PB_RKEY, PB_RVAL, PB_RFOUND};
+            const uint64_t bytes[] = {P.rp * 16, P.rp * 8, P.rp, P.rk * 8, P.rk * 8, P.rk};
+            for (int k = 0; k < 6 && grow_err[i] == NRG_OK; k++) grow_err[i] = grow(m, recv[k], bytes[k]);
+        }
+    }
+    if (any_grow) {  // every rank knows a rank had to grow: all confirm before any send/recv
+        for (int i = 0; i < nl; i++) {
+            Member& m = g->m[i];
+            RCHK(nrg::ctx_use_device(m.ctx));
+            m.xwords[0] = (uint64_t)(-grow_err[i]);
+            GCHK(hipMemcpyAsync(m.pt[PB_ST].p, m.xwords, 8, hipMemcpyHostToDevice, m.cstream));
+        }
+        if (R->group_start() != ncclSuccess) return NRG_E_COMM;
+        for (int i = 0; i < nl && res == ncclSuccess; i++)
+            res = R->all_gather(g->m[i].pt[PB_ST].p, g->m[i].pt[PB_ALLST].p, 1, ncclUint64, g->m[i].comm,
+                                g->m[i].cstream);
+        if (R->group_end() != ncclSuccess || res != ncclSuccess) return NRG_E_COMM;
+        std::vector<uint64_t> st(G);
+        for (int i = 0; i < nl; i++) {
+            Member& m = g->m[i];
+            RCHK(nrg::ctx_use_device(m.ctx));
+            GCHK(hipMemcpyAsync(st.data(), m.pt[PB_ALLST].p, (uint64_t)G * 8, hipMemcpyDeviceToHost, m.cstream));
+            GCHK(hipStreamSynchronize(m.cstream));
+        }
+        for (int s = 0; s < G; s++)
+            if (st[s]) return -(int)st[s];
+    } else {
+        for (int i = 0; i < nl; i++)
+            if (grow_err[i]) return grow_err[i];  // cannot happen: the counts come from the same kernel
     }
     auto at = [](const DBuf& d, uint64_t off) { return (void*)((char*)d.p + off); };
     if (R->group_start() != ncclSuccess) return NRG_E_COMM;
@@ -497,18 +561,32 @@ int nrg_group_partitioned_round(nrg_group* g, const nrg_round* rounds) {
         }
     }
     if (R->group_end() != ncclSuccess || res != ncclSuccess) return NRG_E_COMM;
-    // 4. each owner replays the Puts it received (rank order) and answers the Gets it received
+    // 4. each owner replays the Puts it received (rank order) and answers the Gets it received. A
+    //    skewed round can hand one owner more Puts than its max_batch (or ring) takes in one
+    //    replay: consecutive rounds of at most that many, the Gets answered after the last.
     for (int i = 0; i < nl; i++) {
         Member& m = g->m[i];
         const Plan& P = plan[i];
         nrg_ctx* c = m.ctx;
         RCHK(nrg::ctx_use_device(c));
         RCHK(order(m, m.cstream, c->stream));
-        if (P.rp || P.rk)
-            RCHK(nrg_hashmap_round_async(c, (const nrg_put*)m.pt[PB_RPUT].p, P.rp, (uint32_t)m.rank + 1,
-                                         (const uint64_t*)m.pt[PB_RKEY].p, P.rk, (uint64_t*)m.pt[PB_RVAL].p,
-                                         (uint8_t*)m.pt[PB_RFOUND].p, any_prev ? (uint64_t*)m.pt[PB_RPREV].p : nullptr,
-                                         any_prev ? (uint8_t*)m.pt[PB_RPREVF].p : nullptr));
+        const uint64_t ring_room = c->log_size > 2 * GC_FROM_HEAD ? c->log_size - GC_FROM_HEAD : GC_FROM_HEAD;
+        const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(c->cfg.max_batch, ring_room));
+        const nrg_put* rput = (const nrg_put*)m.pt[PB_RPUT].p;
+        uint64_t* rprev = any_prev ? (uint64_t*)m.pt[PB_RPREV].p : nullptr;
+        uint8_t* rprevf = any_prev ? (uint8_t*)m.pt[PB_RPREVF].p : nullptr;
+        uint64_t off = 0;
+        do {
+            const uint64_t n = std::min(chunk, P.rp - off);
+            const bool last = off + n == P.rp;
+            if (n || (last && P.rk))
+                RCHK(nrg_hashmap_round_async(c, rput + off, n, (uint32_t)m.rank + 1,
+                                             last ? (const uint64_t*)m.pt[PB_RKEY].p : nullptr, last ? P.rk : 0,
+                                             last ? (uint64_t*)m.pt[PB_RVAL].p : nullptr,
+                                             last ? (uint8_t*)m.pt[PB_RFOUND].p : nullptr,
+                                             rprev ? rprev + off : nullptr, rprevf ? rprevf + off : nullptr));
+            off += n;
+        } while (off < P.rp);
         RCHK(nrg_join(c));
         RCHK(order(m, c->stream, m.cstream));
     }
@@ -519,7 +597,7 @@ int nrg_group_partitioned_round(nrg_group* g, const nrg_round* rounds) {
         const Plan& P = plan[i];
         const bool mine = rounds[i].resp && rounds[i].some;
         for (int o = 0; o < G && res == ncclSuccess; o++) {
-            const bool theirs = m.hcnt[(size_t)o * CW + 2 * G] != 0;
+            const bool theirs = word(o, XW_PREV) != 0;
             if (P.gfrom[o]) {
                 res = R->send(at(m.pt[PB_RVAL], P.gfrom_off[o] * 8), P.gfrom[o], ncclUint64, o, m.comm, m.cstream);
                 if (res == ncclSuccess)

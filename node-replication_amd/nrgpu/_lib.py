@@ -181,6 +181,7 @@ TEST_SIGNATURES = {
     "nrg_test_debug_read": (C.c_int, [vp, vp, u64]),
     "nrg_test_hm_skewed": (C.c_int, [vp, vp]),
     "nrg_test_set_knob": (C.c_int, [vp, C.c_int, u64]),
+    "nrg_test_loopback_collectives": (C.c_int, [C.c_int]),
 }
 
 # nrg_test_set_knob knobs (include/nrgpu_testing.h): tuning and diagnostics of an open context
