@@ -243,24 +243,35 @@ int nrg_hashmap_dump(nrg_ctx* ctx, uint64_t* keys, uint64_t* vals, uint64_t cap,
 /* Order-independent digest of the contents: count, sum and xor of mix64(k ^ mix64(v)). */
 int nrg_hashmap_digest(nrg_ctx* ctx, uint64_t out[3]);
 
-/* ---- Flat combining on the host (NrHashMap) --------------------------------------------- */
+/* ---- Flat combining on the host ---------------------------------------------------------- */
 /* Replica's flat combiner for many client threads (nr/src/context.rs:88-194,
- * nr/src/replica.rs:345-356, 414-433, 508-595): each registered thread posts up to 32 ops
- * (MAX_PENDING_OPS) at a time; whichever posting thread takes the combiner lock collects every
- * thread's posted ops into ONE GPU round of `ctx` (all Puts appended and replayed, then all
- * Gets answered against the post-round state) and hands every thread its responses. Calls on
- * one token are synchronous and must come from one thread at a time; while a combiner is open,
- * `ctx` is driven only through it. Needs max_threads * 32 <= max_batch and <= max_reads. */
+ * nr/src/replica.rs:345-356, 404-433, 483-497, 508-595), for any of the three data structures:
+ * each registered thread posts up to 32 ops (MAX_PENDING_OPS) per call into the open batch;
+ * whichever waiting thread takes the combiner lock turns the batch into ONE GPU round of `ctx`
+ * (its writes appended and replayed in batch order, then its reads answered against the
+ * post-round state) without waiting for the GPU, so the next batch fills while a round runs.
+ * Batches live in mapped pinned host memory that the round's kernels read and write directly.
+ * Calls on one token are synchronous and must come from one thread at a time; while a combiner
+ * is open, `ctx` is driven only through it, and no thread may be inside a call when it is closed.
+ * Needs max_threads * 32 <= max_batch (and <= max_reads for the hashmap). */
 typedef struct nrg_combiner nrg_combiner;
 int nrg_combiner_open(nrg_ctx* ctx, uint32_t max_threads, nrg_combiner** out);
 int nrg_combiner_close(nrg_combiner* comb);
 /* Replica::register: a token 0..max_threads-1, or NRG_E_CAPACITY. */
 int nrg_combiner_register(nrg_combiner* comb, uint32_t* token);
-/* Replica::execute_mut(Put(keys[i], vals[i])), n <= 32: prev[i]/some[i] = HashMap::insert's
- * previous value. */
+/* Replica::execute_mut for n <= 32 log records of the replica's kind (nrg_put / nrg_stack_op /
+ * nrg_synth_op): resp[i] / some[i] as nrg_log_exec gives them (u64 previous value, u32 popped
+ * value, u64 sum). */
+int nrg_combiner_execute_mut(nrg_combiner* comb, uint32_t token, const void* recs, uint32_t n, void* resp,
+                             uint8_t* some);
+/* Replica::execute for n <= 32 reads: hashmap Get (u64 keys -> u64 value, found), stack Peek
+ * (`reads` unused -> u32 top, some), synthetic ReadOnly (nrg_synth_rd -> u64 sum, some = 1). */
+int nrg_combiner_execute(nrg_combiner* comb, uint32_t token, const void* reads, uint32_t n, void* resp,
+                         uint8_t* some);
+/* NrHashMap conveniences: Put(keys[i], vals[i]) -> prev[i]/some[i] = HashMap::insert's previous
+ * value; Get(keys[i]) -> vals[i]/found[i]. */
 int nrg_combiner_put(nrg_combiner* comb, uint32_t token, const uint64_t* keys, const uint64_t* vals, uint32_t n,
                      uint64_t* prev, uint8_t* some);
-/* Replica::execute(Get(keys[i])), n <= 32: vals[i]/found[i]. */
 int nrg_combiner_get(nrg_combiner* comb, uint32_t token, const uint64_t* keys, uint32_t n, uint64_t* vals,
                      uint8_t* found);
 /* GPU rounds combined so far and the ops they carried. */

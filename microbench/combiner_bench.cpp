@@ -4,6 +4,7 @@
 // Put batch (Replica::execute_mut), the others Get batches (Replica::execute), keys uniform over
 // 10M on a 2^26-slot table prefilled with [0, 2^23) -> k+1 (benches/hashmap.rs:77-122 with
 // nr/src/replica.rs's synchronous per-thread API). Prints ops/s, GPU rounds and ops per round.
+// The stack cases (benches/stack.rs: 50/50 push/pop, 50,000 initial elements) follow.
 // Build: g++ -O2 -std=c++17 -pthread microbench/combiner_bench.cpp -o microbench/combiner_bench \
 //            -Lnode-replication_amd/lib -lnrgpu -Wl,-rpath,$ORIGIN/../node-replication_amd/lib
 // Run:   ./microbench/combiner_bench [seconds]
@@ -23,14 +24,21 @@ static uint64_t sm64(uint64_t& s) {  // splitmix64
     return z ^ (z >> 31);
 }
 
-static int run(int threads, int batch, double secs) {
+static int run(int threads, int batch, double secs, bool stack) {
     nrg_config cfg;
-    nrg_config_default(&cfg, NRG_DS_HASHMAP);
+    nrg_config_default(&cfg, stack ? NRG_DS_STACK : NRG_DS_HASHMAP);
     cfg.log2_slots = 26;
     cfg.max_batch = cfg.max_reads = 1u << 16;
+    cfg.stack_capacity = 1u << 26;
     nrg_ctx* ctx = nullptr;
     if (int r = nrg_open(0, &cfg, &ctx)) return r;
-    if (int r = nrg_hashmap_prefill_range(ctx, 1ull << 23, 1)) return r;
+    if (stack) {
+        std::vector<uint32_t> init(50000);
+        for (uint32_t i = 0; i < 50000; i++) init[i] = i;
+        if (int r = nrg_stack_init(ctx, init.data(), init.size())) return r;
+    } else if (int r = nrg_hashmap_prefill_range(ctx, 1ull << 23, 1)) {
+        return r;
+    }
     nrg_combiner* comb = nullptr;
     if (int r = nrg_combiner_open(ctx, (uint32_t)threads, &comb)) return r;
     std::atomic<bool> stop{false};
@@ -46,14 +54,24 @@ static int run(int threads, int batch, double secs) {
             }
             uint64_t s = 1000 + i, k[32], v[32], out[32];
             uint8_t f[32];
+            nrg_stack_op so[32];
             uint64_t calls = 0, n = 0;
             while (!stop.load(std::memory_order_relaxed)) {
-                for (int j = 0; j < batch; j++) {
-                    k[j] = sm64(s) % 10000000ull;
-                    v[j] = k[j] + 7;
+                int r;
+                if (stack) {  // benches/stack.rs:87-102: push or pop with equal odds
+                    for (int j = 0; j < batch; j++) {
+                        const uint64_t x = sm64(s);
+                        so[j] = nrg_stack_op{(uint32_t)(x >> 32), (uint32_t)(x & 1)};
+                    }
+                    r = nrg_combiner_execute_mut(comb, tok, so, batch, out, f);
+                } else {
+                    for (int j = 0; j < batch; j++) {
+                        k[j] = sm64(s) % 10000000ull;
+                        v[j] = k[j] + 7;
+                    }
+                    r = calls++ % 10 == 0 ? nrg_combiner_put(comb, tok, k, v, batch, out, f)
+                                          : nrg_combiner_get(comb, tok, k, batch, out, f);
                 }
-                const int r = calls++ % 10 == 0 ? nrg_combiner_put(comb, tok, k, v, batch, out, f)
-                                                : nrg_combiner_get(comb, tok, k, batch, out, f);
                 if (r) {
                     err = r;
                     return;
@@ -70,8 +88,8 @@ static int run(int threads, int batch, double secs) {
     uint64_t rounds = 0, ops = 0, tot = 0;
     nrg_combiner_stats(comb, &rounds, &ops);
     for (uint64_t d : done) tot += d;
-    std::printf("threads %4d ops/call %3d: %9.3f Mops/s  rounds %7llu  ops/round %7.1f  round rate %6.1f k/s%s\n",
-                threads, batch, tot / dt / 1e6, (unsigned long long)rounds, rounds ? (double)ops / rounds : 0.0,
+    std::printf("%s threads %4d ops/call %3d: %9.3f Mops/s  rounds %7llu  ops/round %7.1f  round rate %6.1f k/s%s\n",
+                stack ? "stack  " : "hashmap", threads, batch, tot / dt / 1e6, (unsigned long long)rounds, rounds ? (double)ops / rounds : 0.0,
                 rounds / dt / 1e3, err ? "  ERROR" : "");
     std::fflush(stdout);
     nrg_combiner_close(comb);
@@ -81,9 +99,10 @@ static int run(int threads, int batch, double secs) {
 
 int main(int argc, char** argv) {
     const double secs = argc > 1 ? std::atof(argv[1]) : 2.0;
-    const int cases[][2] = {{8, 1}, {8, 32}, {64, 1}, {64, 32}, {128, 32}, {256, 32}};
+    const int cases[][3] = {{8, 1, 0},   {8, 32, 0},  {64, 1, 0}, {64, 32, 0},
+                            {128, 32, 0}, {256, 32, 0}, {64, 32, 1}, {256, 32, 1}};
     for (auto& c : cases)
-        if (int r = run(c[0], c[1], secs)) {
+        if (int r = run(c[0], c[1], secs, c[2] != 0)) {
             std::printf("error %d (%s)\n", r, nrg_strerror(r));
             return 1;
         }

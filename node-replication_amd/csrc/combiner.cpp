@@ -1,255 +1,381 @@
-// combiner.cpp — the Replica's flat combining on the host, native.
+// combiner.cpp — the Replica's flat combining on the host, native, pipelined.
 //
 // Reference: nr/src/context.rs:88-194 (a per-thread context of at most MAX_PENDING_OPS = 32
-// pending ops and their responses) and nr/src/replica.rs:345-356 (register), :414-433
-// (execute_mut: enqueue, then try to combine until the response is there), :508-595
-// (try_combine / combine: whoever takes the combiner lock collects every thread's pending ops,
-// appends them as ONE batch, replays the log and hands each thread its responses).
+// pending ops and their responses), nr/src/replica.rs:345-356 (register), :404-433 (execute /
+// execute_mut: post, then try to combine until the response is there), :483-497 (reads after
+// sync-to-tail), :508-595 (try_combine / combine: whoever takes the combiner lock appends every
+// thread's pending ops as ONE batch, replays the log and hands each thread its responses).
 //
-// Here the batch is one GPU round of the replica: every posted Put of every thread is appended
-// and replayed (HashMap::insert, previous-value responses), then every posted Get is answered
-// against the post-round state (Replica::read_only after sync-to-tail). Gets posted beside
-// Puts are linearised after the round's Puts: all of them are concurrent with it.
+// A batch is one GPU round of the replica. Batches live in NB slots of mapped, coherent pinned
+// host memory that the round's kernels read and write directly, so a round costs no copies:
+//   post   : a client thread reserves room in the OPEN batch with an atomic add (as Log::append
+//            reserves log entries with a CAS on tail, nr/src/log.rs:391-399), copies its ops in
+//            and waits;
+//   combine: whoever takes the combiner lock seals the open batch, opens the next slot and
+//            enqueues the round on the replica's stream -- Log::append + Log::exec of the batch's
+//            writes, then its reads against the post-round state -- followed by an event; it
+//            does NOT wait for the GPU, so batch k+1 fills while round k is in flight
+//            (at most DEPTH rounds in flight);
+//   retire : a waiting thread that takes the poll lock queries the oldest in-flight round's
+//            event; a completed round's responses are already in host memory, and each client
+//            copies its own out of the batch.
+// Reads ride in the round that collects them, after its writes: they see every write completed
+// before they were posted (sync-to-tail) and never wait behind a later write round. Clients
+// spin briefly, then yield: a round takes tens of microseconds, and the host cores are better
+// left to the threads that combine.
 //
-// A client thread that finds the lock taken waits on its own context (a short spin, then 10-µs
-// sleeps: a round takes tens of microseconds, and the host cores are better left to the
-// combining thread) until the combiner has filled in its responses, or the lock frees up while
-// its ops are still pending, in which case it combines. The combiner owns pinned host staging and device buffers for max_threads * 32
-// ops, so a round is two copies in, one round launch, copies out and one stream sync.
+// Generic over the three data structures (nr's Replica<D> is generic over Dispatch,
+// nr/src/replica.rs:72-115): hashmap Put/Get, stack Push-Pop/Peek, synthetic writes/ReadOnly.
 #include <hip/hip_runtime.h>
+#include <immintrin.h>
+#include <sched.h>
 
 #include <atomic>
-#include <chrono>
 #include <cstring>
 #include <mutex>
 #include <new>
-#include <thread>
-#include <vector>
 
 #include "internal.hpp"
 
 namespace {
 
 constexpr uint32_t MAX_PENDING = 32;  // nr/src/context.rs:12 MAX_PENDING_OPS
+constexpr int NB = 4;                 // batch slots
+constexpr uint64_t DEPTH = 2;         // rounds in flight (NB >= DEPTH + 2: a slot's clients read
+                                      // their responses while two later rounds run)
 
-enum : uint32_t { EMPTY = 0, POSTED = 1, DONE = 2 };
+enum : uint32_t { FREE = 0, OPEN = 1, SEALED = 2, DONE = 3 };
 
-struct alignas(64) Ctx {  // one registered thread's context
-    std::atomic<uint32_t> state{EMPTY};
-    uint32_t n = 0;
-    bool put = false;
-    const uint64_t* keys = nullptr;  // the caller's ops (valid while POSTED)
-    const uint64_t* vals = nullptr;
-    uint64_t* out = nullptr;  // the caller's responses: previous value / value
-    uint8_t* flag = nullptr;  //   Some / found
-    int rc = NRG_OK;
+// A test-and-test-and-set lock: waiters look before they try, so hundreds of polling clients do
+// not bounce its cache line.
+struct alignas(64) SpinFlag {
+    std::atomic<bool> held{false};
+    bool try_lock() { return !held.load(std::memory_order_relaxed) && !held.exchange(true, std::memory_order_acquire); }
+    void lock() {
+        while (!try_lock()) _mm_pause();
+    }
+    void unlock() { held.store(false, std::memory_order_release); }
 };
+
+struct alignas(64) Batch {
+    std::atomic<uint32_t> state{FREE};
+    std::atomic<uint64_t> round{~0ull};  // round number while OPEN/SEALED/DONE
+    alignas(64) std::atomic<uint32_t> writers{0};  // clients copying ops in
+    std::atomic<uint32_t> readers{0};              // clients yet to copy their responses out
+    std::atomic<uint32_t> nw{0}, nr{0};            // write records / reads reserved
+    int rc = NRG_OK;                               // launch or device error of the round
+    // host buffers (mapped, coherent; device addresses equal the host ones under UVA)
+    char* recs = nullptr;   // cap write records
+    char* reads = nullptr;  // cap read records
+    char* wresp = nullptr;  // cap write responses
+    uint8_t* wsome = nullptr;
+    char* rresp = nullptr;  // cap read responses
+    uint8_t* rsome = nullptr;
+    uint32_t* err = nullptr;  // the replica's error latch after the round
+    hipEvent_t done = nullptr;
+};
+
+// device: the error latch of the replica, copied to host memory and cleared after a round
+__global__ void comb_err_kernel(nrg::DevCtl* ctl, uint32_t* out) {
+    if (threadIdx.x == 0) out[0] = atomicExch(&ctl->err, 0u);
+}
+
+// device: n Peeks of the stack after the round (nr/tests/stack.rs:26-29, benches/stack.rs)
+__global__ void comb_peek_kernel(const nrg::DevCtl* ctl, const uint32_t* stack, uint64_t cap, uint32_t n,
+                                 uint32_t* out, uint8_t* some) {
+    const long long d = ctl->depth;
+    const bool has = d > 0 && (uint64_t)d <= cap;
+    const uint32_t top = has ? stack[d - 1] : 0u;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        out[i] = top;
+        some[i] = has;
+    }
+}
+
+int err_code(uint32_t e) {
+    if (!e) return NRG_OK;
+    if (e & nrg::ERR_TABLE_FULL) return NRG_E_TABLE_FULL;
+    if (e & nrg::ERR_CAPACITY) return NRG_E_CAPACITY;
+    return NRG_E_HIP;
+}
 
 }  // namespace
 
 struct nrg_combiner {
     nrg_ctx* ctx = nullptr;
+    uint32_t kind = 0;
     uint32_t max_threads = 0;
-    std::atomic<uint32_t> next{0};
-    Ctx* ctxs = nullptr;
-    std::mutex lock;
-    uint64_t cap = 0;  // ops per round: max_threads * MAX_PENDING
-    // pinned host staging
-    nrg_put* h_puts = nullptr;
-    uint64_t* h_keys = nullptr;
-    uint64_t* h_prev = nullptr;
-    uint8_t* h_prevf = nullptr;
-    uint64_t* h_vals = nullptr;
-    uint8_t* h_found = nullptr;
-    // device buffers
-    nrg_put* d_puts = nullptr;
-    uint64_t* d_keys = nullptr;
-    uint64_t* d_prev = nullptr;
-    uint8_t* d_prevf = nullptr;
-    uint64_t* d_vals = nullptr;
-    uint8_t* d_found = nullptr;
-    std::vector<uint32_t> batch;  // contexts collected by the current combine
-    uint64_t rounds = 0, ops = 0;
+    uint64_t cap = 0;  // ops of each kind per batch: max_threads * MAX_PENDING
+    uint32_t rec_b = 0, rd_b = 0, wr_b = 0, rr_b = 0;  // write record / read record / responses
+    bool saved_pipeline = false;
+    std::atomic<uint32_t> next_tok{0};
+    Batch b[NB];
+    alignas(64) std::atomic<uint64_t> open{0};       // round number of the OPEN batch
+    alignas(64) std::atomic<uint64_t> completed{0};  // rounds < completed are done
+    std::atomic<uint64_t> launched{0};               // rounds < launched are enqueued (combiner lock)
+    SpinFlag comb;                                   // the combiner lock
+    SpinFlag poll;                                   // retiring rounds (event queries)
+    std::atomic<uint64_t> rounds{0}, ops{0};
 };
 
-static void comb_free(nrg_combiner* m) {
+namespace {
+
+void* host_alloc(uint64_t bytes) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, bytes ? bytes : 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return nullptr;
+    return p;
+}
+
+void comb_free(nrg_combiner* m) {
     if (!m) return;
-    (void)hipHostFree(m->h_puts);
-    (void)hipHostFree(m->h_keys);
-    (void)hipHostFree(m->h_prev);
-    (void)hipHostFree(m->h_prevf);
-    (void)hipHostFree(m->h_vals);
-    (void)hipHostFree(m->h_found);
-    (void)hipFree(m->d_puts);
-    (void)hipFree(m->d_keys);
-    (void)hipFree(m->d_prev);
-    (void)hipFree(m->d_prevf);
-    (void)hipFree(m->d_vals);
-    (void)hipFree(m->d_found);
-    delete[] m->ctxs;
+    for (Batch& x : m->b) {
+        void* ps[] = {x.recs, x.reads, x.wresp, x.wsome, x.rresp, x.rsome, x.err};
+        for (void* p : ps)
+            if (p) (void)hipHostFree(p);
+        if (x.done) (void)hipEventDestroy(x.done);
+    }
     delete m;
 }
 
-extern "C" int nrg_combiner_open(nrg_ctx* ctx, uint32_t max_threads, nrg_combiner** out) {
-    if (!ctx || !out || !max_threads || max_threads > 4096 || ctx->cfg.ds_kind != NRG_DS_HASHMAP)
+// Retire completed rounds in order (poll lock held).
+void retire(nrg_combiner* m) {
+    uint64_t k = m->completed.load(std::memory_order_relaxed);
+    while (k < m->launched.load(std::memory_order_acquire)) {
+        Batch& x = m->b[k % NB];
+        const hipError_t q = hipEventQuery(x.done);
+        if (q == hipErrorNotReady) break;
+        if (q != hipSuccess && x.rc == NRG_OK) x.rc = NRG_E_HIP;
+        if (x.rc == NRG_OK) x.rc = err_code(*(volatile uint32_t*)x.err);
+        x.state.store(DONE, std::memory_order_release);
+        m->completed.store(++k, std::memory_order_release);
+    }
+}
+
+// Enqueue the round of sealed batch x (combiner lock held): the replica's writes, then its reads.
+int launch(nrg_combiner* m, Batch& x, uint32_t W, uint32_t R) {
+    nrg_ctx* c = m->ctx;
+    int rc = nrg::ctx_use_device(c);
+    if (rc) return rc;
+    hipStream_t st = (hipStream_t)nrg_get_stream(c);
+    const uint32_t origin = c->cfg.replica_id;
+    switch (m->kind) {
+        case NRG_DS_HASHMAP:  // Put -> HashMap::insert's previous value (nr/examples/hashmap.rs:46-50)
+            rc = nrg_hashmap_round_async(c, (const nrg_put*)x.recs, W, origin, (const uint64_t*)x.reads, R,
+                                         (uint64_t*)x.rresp, x.rsome, (uint64_t*)x.wresp, x.wsome);
+            break;
+        case NRG_DS_STACK:
+            if (W) rc = nrg_stack_round_async(c, (const nrg_stack_op*)x.recs, W, origin, (uint32_t*)x.wresp, x.wsome);
+            if (!rc && R) {
+                comb_peek_kernel<<<1, 256, 0, st>>>(c->d_ctl, c->d_stack, c->cfg.stack_capacity, R,
+                                                    (uint32_t*)x.rresp, x.rsome);
+                if (hipGetLastError() != hipSuccess) rc = NRG_E_HIP;
+            }
+            break;
+        default:  // synthetic: ReadWrite/WriteOnly sums, then ReadOnly sums
+            if (W) rc = nrg_synth_round_async(c, (const nrg_synth_op*)x.recs, W, origin, (uint64_t*)x.wresp, x.wsome);
+            if (!rc && R) {
+                std::memset(x.rsome, 1, R);
+                rc = nrg_synth_read_async(c, (const nrg_synth_rd*)x.reads, R, (uint64_t*)x.rresp);
+            }
+            break;
+    }
+    if (!rc && nrg_join(c)) rc = NRG_E_HIP;  // a deferred round tail would write responses later
+    if (!rc) {
+        comb_err_kernel<<<1, 64, 0, st>>>(c->d_ctl, x.err);
+        if (hipGetLastError() != hipSuccess) rc = NRG_E_HIP;
+    }
+    return rc;
+}
+
+// Combiner lock held: retire what has finished; seal the open batch and enqueue its round if it
+// holds ops and fewer than DEPTH rounds are in flight.
+void advance(nrg_combiner* m) {
+    m->poll.lock();
+    retire(m);
+    m->poll.unlock();
+    const uint64_t k = m->open.load(std::memory_order_relaxed);
+    Batch& x = m->b[k % NB];
+    if (m->launched.load(std::memory_order_relaxed) - m->completed.load(std::memory_order_acquire) >= DEPTH) return;
+    if (!x.nw.load(std::memory_order_relaxed) && !x.nr.load(std::memory_order_relaxed)) return;
+    x.state.store(SEALED, std::memory_order_seq_cst);
+    while (x.writers.load(std::memory_order_seq_cst)) _mm_pause();
+    const uint32_t W = x.nw.load(std::memory_order_relaxed), R = x.nr.load(std::memory_order_relaxed);
+    // open round k+1 in the next slot: its previous round (k+1-NB) is complete (DEPTH < NB - 1);
+    // wait for that round's clients to copy their responses out
+    Batch& y = m->b[(k + 1) % NB];
+    while (y.readers.load(std::memory_order_acquire)) _mm_pause();
+    y.nw.store(0, std::memory_order_relaxed);
+    y.nr.store(0, std::memory_order_relaxed);
+    y.rc = NRG_OK;
+    y.round.store(k + 1, std::memory_order_relaxed);
+    y.state.store(OPEN, std::memory_order_seq_cst);
+    m->open.store(k + 1, std::memory_order_release);
+    x.rc = launch(m, x, W, R);
+    hipStream_t st = (hipStream_t)nrg_get_stream(m->ctx);
+    if (hipEventRecord(x.done, st) != hipSuccess && x.rc == NRG_OK) x.rc = NRG_E_HIP;
+    m->launched.store(k + 1, std::memory_order_release);
+    m->rounds.fetch_add(1, std::memory_order_relaxed);
+    m->ops.fetch_add(W + R, std::memory_order_relaxed);
+}
+
+// Post n ops of one thread, then combine or wait until their round is done (nr/src/replica.rs:414-433).
+int post_and_wait(nrg_combiner* m, uint32_t token, bool write, const void* ops, uint32_t n, void* out,
+                  uint8_t* some) {
+    if (!m || token >= m->max_threads || (n && (!out || !some || (!ops && (write || m->kind != NRG_DS_STACK)))))
         return NRG_E_INVAL;
+    if (n > MAX_PENDING) return NRG_E_CAPACITY;
+    if (!n) return NRG_OK;
+    const uint32_t in_b = write ? m->rec_b : m->rd_b, out_b = write ? m->wr_b : m->rr_b;
+    uint64_t k;
+    Batch* x;
+    uint32_t off;
+    for (uint32_t spins = 0;; spins++) {  // reserve room in the open batch (Context::enqueue)
+        k = m->open.load(std::memory_order_acquire);
+        x = &m->b[k % NB];
+        x->writers.fetch_add(1, std::memory_order_seq_cst);
+        if (x->state.load(std::memory_order_seq_cst) == OPEN && x->round.load(std::memory_order_relaxed) == k) {
+            off = (write ? x->nw : x->nr).fetch_add(n, std::memory_order_relaxed);
+            x->readers.fetch_add(1, std::memory_order_relaxed);
+            if (in_b && ops) std::memcpy((write ? x->recs : x->reads) + (uint64_t)off * in_b, ops, (size_t)n * in_b);
+            x->writers.fetch_sub(1, std::memory_order_release);
+            break;
+        }
+        x->writers.fetch_sub(1, std::memory_order_relaxed);
+        if (spins > 64) sched_yield();
+        else _mm_pause();
+    }
+    for (uint32_t spins = 0; m->completed.load(std::memory_order_acquire) <= k; spins++) {
+        if (m->comb.try_lock()) {
+            advance(m);
+            m->comb.unlock();
+        } else if (m->poll.try_lock()) {
+            retire(m);
+            m->poll.unlock();
+        }
+        if (m->completed.load(std::memory_order_acquire) > k) break;
+        if (spins > 32) sched_yield();
+        else
+            for (int i = 0; i < 16; i++) _mm_pause();
+    }
+    std::memcpy(out, (write ? x->wresp : x->rresp) + (uint64_t)off * out_b, (size_t)n * out_b);
+    std::memcpy(some, (write ? x->wsome : x->rsome) + off, n);
+    const int rc = x->rc;
+    x->readers.fetch_sub(1, std::memory_order_release);
+    return rc;
+}
+
+}  // namespace
+
+extern "C" int nrg_combiner_open(nrg_ctx* ctx, uint32_t max_threads, nrg_combiner** out) {
+    if (!ctx || !out || !max_threads || max_threads > 4096) return NRG_E_INVAL;
+    const uint32_t kind = ctx->cfg.ds_kind;
+    if (kind != NRG_DS_HASHMAP && kind != NRG_DS_STACK && kind != NRG_DS_SYNTHETIC) return NRG_E_INVAL;
     const uint64_t cap = (uint64_t)max_threads * MAX_PENDING;
-    if (cap > ctx->cfg.max_batch || cap > ctx->cfg.max_reads) return NRG_E_CAPACITY;
+    if (cap > ctx->cfg.max_batch || (kind == NRG_DS_HASHMAP && cap > ctx->cfg.max_reads)) return NRG_E_CAPACITY;
     int r = nrg::ctx_use_device(ctx);
     if (r) return r;
+    // the replica's queued work completes first; rounds then complete within their own launch
+    // sequence (no deferred tail), so an event after a round covers all of its responses
+    if ((r = nrg_sync(ctx))) return r;
     nrg_combiner* m = new (std::nothrow) nrg_combiner();
     if (!m) return NRG_E_NOMEM;
     m->ctx = ctx;
+    m->kind = kind;
     m->max_threads = max_threads;
     m->cap = cap;
-    m->ctxs = new (std::nothrow) Ctx[max_threads];
-    m->batch.reserve(max_threads);
-    bool ok = m->ctxs != nullptr;
-    ok = ok && hipHostMalloc(&m->h_puts, cap * sizeof(nrg_put)) == hipSuccess;
-    ok = ok && hipHostMalloc(&m->h_keys, cap * 8) == hipSuccess;
-    ok = ok && hipHostMalloc(&m->h_prev, cap * 8) == hipSuccess;
-    ok = ok && hipHostMalloc(&m->h_prevf, cap) == hipSuccess;
-    ok = ok && hipHostMalloc(&m->h_vals, cap * 8) == hipSuccess;
-    ok = ok && hipHostMalloc(&m->h_found, cap) == hipSuccess;
-    ok = ok && hipMalloc(&m->d_puts, cap * sizeof(nrg_put)) == hipSuccess;
-    ok = ok && hipMalloc(&m->d_keys, cap * 8) == hipSuccess;
-    ok = ok && hipMalloc(&m->d_prev, cap * 8) == hipSuccess;
-    ok = ok && hipMalloc(&m->d_prevf, cap) == hipSuccess;
-    ok = ok && hipMalloc(&m->d_vals, cap * 8) == hipSuccess;
-    ok = ok && hipMalloc(&m->d_found, cap) == hipSuccess;
+    m->rec_b = ctx->rec_bytes;
+    switch (kind) {
+        case NRG_DS_HASHMAP: m->rd_b = 8, m->wr_b = 8, m->rr_b = 8; break;            // key; previous value; value
+        case NRG_DS_STACK: m->rd_b = 0, m->wr_b = 4, m->rr_b = 4; break;              // Peek; popped; top
+        default: m->rd_b = sizeof(nrg_synth_rd), m->wr_b = 8, m->rr_b = 8; break;  // sums
+    }
+    bool ok = true;
+    for (Batch& x : m->b) {
+        ok = ok && (x.recs = (char*)host_alloc(cap * m->rec_b));
+        ok = ok && (x.reads = (char*)host_alloc(cap * (m->rd_b ? m->rd_b : 1)));
+        ok = ok && (x.wresp = (char*)host_alloc(cap * m->wr_b));
+        ok = ok && (x.wsome = (uint8_t*)host_alloc(cap));
+        ok = ok && (x.rresp = (char*)host_alloc(cap * m->rr_b));
+        ok = ok && (x.rsome = (uint8_t*)host_alloc(cap));
+        ok = ok && (x.err = (uint32_t*)host_alloc(64));
+        ok = ok && hipEventCreateWithFlags(&x.done, hipEventDisableTiming) == hipSuccess;
+        if (ok) *x.err = 0;
+    }
     if (!ok) {
         comb_free(m);
         return NRG_E_NOMEM;
     }
+    m->saved_pipeline = ctx->pipeline;
+    ctx->pipeline = false;
+    m->b[0].round.store(0);
+    m->b[0].state.store(OPEN);
     *out = m;
     return NRG_OK;
 }
 
+// No thread may be inside nrg_combiner_put/get/execute* when the combiner is closed.
 extern "C" int nrg_combiner_close(nrg_combiner* m) {
     if (!m) return NRG_E_INVAL;
-    std::lock_guard<std::mutex> g(m->lock);
-    (void)nrg::ctx_use_device(m->ctx);
-    (void)hipStreamSynchronize((hipStream_t)nrg_get_stream(m->ctx));
-    comb_free(m);
-    return NRG_OK;
+    int rc = NRG_OK;
+    {
+        m->comb.lock();
+        m->poll.lock();
+        (void)nrg::ctx_use_device(m->ctx);
+        if (hipStreamSynchronize((hipStream_t)nrg_get_stream(m->ctx)) != hipSuccess) rc = NRG_E_HIP;
+        retire(m);
+        m->ctx->pipeline = m->saved_pipeline;
+        m->poll.unlock();
+        m->comb.unlock();
+    }
+    comb_free(m);  // after both locks are released: nothing of m is touched afterwards
+    return rc;
 }
 
-// Replica::register (nr/src/replica.rs:345-356): a context for the calling thread.
+// Replica::register (nr/src/replica.rs:279-298): a context for the calling thread.
 extern "C" int nrg_combiner_register(nrg_combiner* m, uint32_t* token) {
     if (!m || !token) return NRG_E_INVAL;
-    uint32_t t = m->next.load(std::memory_order_relaxed);
+    uint32_t t = m->next_tok.load(std::memory_order_relaxed);
     do {
         if (t >= m->max_threads) return NRG_E_CAPACITY;
-    } while (!m->next.compare_exchange_weak(t, t + 1, std::memory_order_relaxed));
+    } while (!m->next_tok.compare_exchange_weak(t, t + 1, std::memory_order_relaxed));
     *token = t;
     return NRG_OK;
 }
 
-// Replica::combine (nr/src/replica.rs:544-595), under the combiner lock: one GPU round of
-// every posted op, responses scattered back to their contexts.
-static void combine(nrg_combiner* m) {
-    nrg_ctx* c = m->ctx;
-    m->batch.clear();
-    uint64_t W = 0, R = 0;
-    for (uint32_t i = 0; i < m->max_threads; i++) {
-        Ctx& x = m->ctxs[i];
-        if (x.state.load(std::memory_order_acquire) != POSTED) continue;
-        m->batch.push_back(i);
-        if (x.put) {
-            for (uint32_t k = 0; k < x.n; k++) m->h_puts[W + k] = nrg_put{x.keys[k], x.vals[k]};
-            W += x.n;
-        } else {
-            std::memcpy(m->h_keys + R, x.keys, x.n * 8);
-            R += x.n;
-        }
-    }
-    if (m->batch.empty()) return;
-    int rc = nrg::ctx_use_device(c);
-    hipStream_t st = (hipStream_t)nrg_get_stream(c);
-    if (!rc && W && hipMemcpyAsync(m->d_puts, m->h_puts, W * sizeof(nrg_put), hipMemcpyHostToDevice, st))
-        rc = NRG_E_HIP;
-    if (!rc && R && hipMemcpyAsync(m->d_keys, m->h_keys, R * 8, hipMemcpyHostToDevice, st)) rc = NRG_E_HIP;
-    if (!rc)
-        rc = nrg_hashmap_round_async(c, m->d_puts, W, c->cfg.replica_id, m->d_keys, R, m->d_vals, m->d_found,
-                                     m->d_prev, m->d_prevf);
-    // responses are complete once the round's deferred half (config.pipeline) has run
-    if (!rc && nrg_join(c)) rc = NRG_E_HIP;
-    if (!rc && W &&
-        (hipMemcpyAsync(m->h_prev, m->d_prev, W * 8, hipMemcpyDeviceToHost, st) ||
-         hipMemcpyAsync(m->h_prevf, m->d_prevf, W, hipMemcpyDeviceToHost, st)))
-        rc = NRG_E_HIP;
-    if (!rc && R &&
-        (hipMemcpyAsync(m->h_vals, m->d_vals, R * 8, hipMemcpyDeviceToHost, st) ||
-         hipMemcpyAsync(m->h_found, m->d_found, R, hipMemcpyDeviceToHost, st)))
-        rc = NRG_E_HIP;
-    if (!rc) rc = nrg_sync(c);  // waits for the copies and reports latched device errors
-    W = R = 0;
-    for (uint32_t i : m->batch) {
-        Ctx& x = m->ctxs[i];
-        if (!rc) {
-            if (x.put) {
-                std::memcpy(x.out, m->h_prev + W, x.n * 8);
-                std::memcpy(x.flag, m->h_prevf + W, x.n);
-                W += x.n;
-            } else {
-                std::memcpy(x.out, m->h_vals + R, x.n * 8);
-                std::memcpy(x.flag, m->h_found + R, x.n);
-                R += x.n;
-            }
-        }
-        x.rc = rc;
-        x.state.store(DONE, std::memory_order_release);
-    }
-    m->rounds++;
-    m->ops += W + R;
+// Replica::execute_mut for up to 32 write ops (log records of the replica's kind).
+extern "C" int nrg_combiner_execute_mut(nrg_combiner* m, uint32_t token, const void* recs, uint32_t n, void* resp,
+                                        uint8_t* some) {
+    return post_and_wait(m, token, true, recs, n, resp, some);
 }
 
-// Post n ops in the calling thread's context, then combine or wait (nr/src/replica.rs:414-433).
-static int post_and_wait(nrg_combiner* m, uint32_t token, bool put, const uint64_t* keys, const uint64_t* vals,
-                         uint32_t n, uint64_t* out, uint8_t* flag) {
-    if (!m || token >= m->max_threads || (n && (!keys || !out || !flag || (put && !vals)))) return NRG_E_INVAL;
-    if (n > MAX_PENDING) return NRG_E_CAPACITY;
-    if (!n) return NRG_OK;
-    Ctx& x = m->ctxs[token];
-    x.n = n;
-    x.put = put;
-    x.keys = keys;
-    x.vals = vals;
-    x.out = out;
-    x.flag = flag;
-    x.state.store(POSTED, std::memory_order_release);
-    for (uint32_t spins = 0; x.state.load(std::memory_order_acquire) != DONE; spins++) {
-        if (m->lock.try_lock()) {
-            if (x.state.load(std::memory_order_acquire) != DONE) combine(m);
-            m->lock.unlock();
-        } else if (spins > 64) {
-            // a round is tens of microseconds: waiting threads sleep instead of competing with
-            // the combining thread for the host cores
-            std::this_thread::sleep_for(std::chrono::microseconds(10));
-        }
-    }
-    x.state.store(EMPTY, std::memory_order_relaxed);
-    return x.rc;
+// Replica::execute for up to 32 read ops.
+extern "C" int nrg_combiner_execute(nrg_combiner* m, uint32_t token, const void* reads, uint32_t n, void* resp,
+                                    uint8_t* some) {
+    return post_and_wait(m, token, false, reads, n, resp, some);
 }
 
 // Replica::execute_mut(Put(k, v)) for up to 32 ops of one thread: prev[i] / some[i] =
 // HashMap::insert's previous value (nr/examples/hashmap.rs:46-50).
 extern "C" int nrg_combiner_put(nrg_combiner* m, uint32_t token, const uint64_t* keys, const uint64_t* vals,
                                 uint32_t n, uint64_t* prev, uint8_t* some) {
-    return post_and_wait(m, token, true, keys, vals, n, prev, some);
+    if (!m || m->kind != NRG_DS_HASHMAP || (n && (!keys || !vals))) return NRG_E_INVAL;
+    if (n > MAX_PENDING) return NRG_E_CAPACITY;
+    nrg_put recs[MAX_PENDING];
+    for (uint32_t i = 0; i < n; i++) recs[i] = nrg_put{keys[i], vals[i]};
+    return post_and_wait(m, token, true, recs, n, prev, some);
 }
 
 // Replica::execute(Get(k)) for up to 32 ops of one thread: vals[i] / found[i].
 extern "C" int nrg_combiner_get(nrg_combiner* m, uint32_t token, const uint64_t* keys, uint32_t n, uint64_t* vals,
                                 uint8_t* found) {
-    return post_and_wait(m, token, false, keys, nullptr, n, vals, found);
+    if (!m || m->kind != NRG_DS_HASHMAP) return NRG_E_INVAL;
+    return post_and_wait(m, token, false, keys, n, vals, found);
 }
 
 // GPU rounds combined so far and the ops they carried.
 extern "C" int nrg_combiner_stats(nrg_combiner* m, uint64_t* rounds, uint64_t* ops) {
     if (!m || !rounds || !ops) return NRG_E_INVAL;
-    std::lock_guard<std::mutex> g(m->lock);
-    *rounds = m->rounds;
-    *ops = m->ops;
+    *rounds = m->rounds.load(std::memory_order_relaxed);
+    *ops = m->ops.load(std::memory_order_relaxed);
     return NRG_OK;
 }

@@ -164,6 +164,8 @@ SIGNATURES = {
     "nrg_combiner_close": (C.c_int, [vp]),
     "nrg_combiner_register": (C.c_int, [vp, C.POINTER(u32)]),
     "nrg_combiner_put": (C.c_int, [vp, u32, vp, vp, u32, vp, vp]),
+    "nrg_combiner_execute_mut": (C.c_int, [vp, u32, vp, u32, vp, vp]),
+    "nrg_combiner_execute": (C.c_int, [vp, u32, vp, u32, vp, vp]),
     "nrg_combiner_get": (C.c_int, [vp, u32, vp, u32, vp, vp]),
     "nrg_combiner_stats": (C.c_int, [vp, u64p, u64p]),
     "nrg_key_owner": (C.c_uint32, [u64, C.c_uint32]),

@@ -491,6 +491,12 @@ class Log:
     process the copies are filled directly; across processes/GPUs the write segments are
     all-gathered, see parallel.py). `tail` is the shared logical tail, `ctail` the max tail any
     replica has replayed (nr/src/log.rs:522), used by reads to sync.
+
+    The host keeps the appended batches of the live window [head, tail) (head = the slowest
+    replica's ltail, advanced when the log nears full as Log::append's GC does,
+    nr/src/log.rs:364-387, :536-580), so that a replica registered after appends can be given the
+    entries it has not seen and catch up through exec from its ltail = 0 (nr/src/log.rs:272-292,
+    :473-524; nr/src/replica.rs:469-479).
     """
 
     def __init__(self, nbytes: int = DEFAULT_LOG_BYTES):
@@ -507,17 +513,25 @@ class Log:
         self.ctail = 0
         self._next = 1
         self._replicas: List["Replica"] = []
+        self._live: list = []  # (first log index, records, origin) of the batches in [head, tail)
         self.lock = threading.RLock()
 
     def register(self, replica: "Replica") -> Optional[int]:
-        """Log::register (nr/src/log.rs:272-292): ids 1.., None at MAX_REPLICAS."""
+        """Log::register (nr/src/log.rs:272-292): ids 1.., None at MAX_REPLICAS. A replica
+        registered after appends starts at ltail 0 like the reference's; its copy of the log is
+        filled with the live entries, which it replays on its next combine or sync. If GC has
+        already moved head past entry 0 the reference's exec would panic ("Local tail not within
+        the shared log", nr/src/log.rs:486-488): here registration fails with RuntimeError."""
         with self.lock:
             if self._next >= MAX_REPLICAS:
                 return None
-            # each replica's copy of the log starts empty: a late replica could not catch up on
-            # entries appended before it (checked before any state changes)
-            if self.tail != 0:
-                raise RuntimeError("register replicas before appending to the log")
+            if self.head > 0:
+                raise RuntimeError(f"cannot register a replica: the log was garbage-collected up to {self.head}, "
+                                   "so entries a new replica must replay from index 0 are gone")
+            for first, recs, origin in self._live:  # catch-up copy, same logical indices
+                got = replica.dev.log_append(recs, origin)
+                if got != first:
+                    raise RuntimeError("log copies diverged")
             idx = self._next
             self._next += 1
             self._replicas.append(replica)
@@ -557,6 +571,11 @@ class Log:
                 elif f != first:
                     raise RuntimeError("log copies diverged")
             self.tail = first + len(recs)
+            self._live.append((first, np.array(recs, copy=True), idx))
+            if self.tail - self.head > self.size - GC_FROM_HEAD:  # nearly full: GC (nr/src/log.rs:364-387)
+                self.advance_head()
+            while self._live and self._live[0][0] + len(self._live[0][1]) <= self.head:
+                self._live.pop(0)
             return first
 
 

@@ -1,4 +1,7 @@
-"""Native flat combining (nrg_combiner_*): many client threads, one GPU round per combine.
+"""Native flat combining (nrg_combiner_*): many client threads, one GPU round per combine,
+for the hashmap (per-thread models), the stack and the synthetic structure (the replica's own
+log, read back, replayed by the oracle: every call's responses equal the oracle's at the call's
+log positions).
 
 Mirrors the reference's multi-threaded replica use (nr/src/replica.rs:345-356 register,
 :414-433 execute_mut, :508-595 combine; nr/tests/stack.rs:170-262 threads against one replica):
@@ -82,11 +85,175 @@ def test_combiner_limits(nrg):
     assert (a, b) == (0, 1)
     with pytest.raises(nrg.NrgError):  # past max_threads
         comb.register()
-    with pytest.raises(nrg.NrgError):  # more than MAX_PENDING_OPS per call
+    with pytest.raises(ValueError):  # more than MAX_PENDING_OPS per call
         comb.put(a, np.arange(33), np.arange(33))
+    with pytest.raises(ValueError):  # keys and values of different lengths
+        comb.put(a, np.arange(3), np.arange(2))
+    recs = np.zeros(33, nrg.PUT_DTYPE)
+    with pytest.raises(nrg.NrgError):  # the C ABI refuses it too
+        comb.execute_mut(a, recs)
     prev, some = comb.put(a, [7, 7], [1, 2])
     assert list(some) == [0, 1] and int(prev[1]) == 1
     vals, found = comb.get(b, [7, 8])
     assert list(found) == [1, 0] and int(vals[0]) == 2
     comb.close()
+    dev.close()
+
+
+def _read_log(nrg, dev, dtype):
+    """The replica's log [head, tail) as records (nrgpu_testing.h nrg_test_ring_read)."""
+    import ctypes as C
+
+    lib = nrg._lib.load()
+    st = dev.log_state()
+    out = np.zeros(st["tail"] - st["head"], dtype)
+    rec = np.zeros(1, dtype)
+    for i in range(st["head"], st["tail"]):
+        nrg._lib.check(lib.nrg_test_ring_read(dev.handle, i & (st["size"] - 1), C.c_void_p(rec.ctypes.data)))
+        out[i - st["head"]] = rec[0]
+    return out
+
+
+def _run_threads(T, fn):
+    errors = []
+
+    def wrap(i):
+        try:
+            fn(i)
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    th = [threading.Thread(target=wrap, args=(i,)) for i in range(T)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors[0]
+
+
+def test_combiner_stack_threads(nrg, orc):
+    """Stack replica behind the combiner (configs[4]'s data structure, nr/tests/stack.rs):
+    phase 1, T threads push and pop concurrently in calls of 1..32 mixed ops; every call's pop
+    values equal the oracle's replay of the replica's log at the call's positions. Phase 2
+    (parallel_push_sequential_pop, nr/tests/stack.rs:282-343): threads push increasing values,
+    then one thread pops everything and each pusher's values come out decreasing (VerifyStack)."""
+    T, CALLS = 8, 30
+    L = nrg._lib
+    dev = nrg.DeviceReplica(L.NRG_DS_STACK, 0, max_batch=1 << 12, stack_capacity=1 << 20, log_bytes=64 * (1 << 17))
+    init = np.arange(100, dtype=np.uint32)
+    dev.st_init(init)
+    comb = nrg.Combiner(dev, T)
+    calls = {}
+
+    def client(i):
+        tok = comb.register()
+        rng = np.random.default_rng(500 + i)
+        mine = []
+        for c in range(CALLS):
+            n = int(rng.integers(1, 33))
+            recs = np.zeros(n, nrg.STACK_OP_DTYPE)
+            recs["op"] = rng.integers(0, 2, n)
+            recs["op"][0] = L.NRG_STACK_PUSH  # every call starts with a unique Push: finds it in the log
+            recs["val"] = ((tok + 1) << 24) | (c << 8) | np.arange(n)
+            resp, some = comb.execute_mut(tok, recs)
+            mine.append((recs, resp, some))
+            if c % 7 == 3:
+                top, has = comb.execute(tok, n=4)  # Peek
+                assert np.all(has == has[0]) and np.all(top == top[0])
+        calls[tok] = mine
+
+    _run_threads(T, client)
+    log = _read_log(nrg, dev, nrg.STACK_OP_DTYPE)
+    ost = orc.Stack(init)
+    oresp, osome = ost.replay(log["val"], log["op"])
+    pos = {int(v): i for i, (v, o) in enumerate(zip(log["val"], log["op"])) if o == L.NRG_STACK_PUSH}
+    for tok, mine in calls.items():
+        for recs, resp, some in mine:
+            p = pos[int(recs["val"][0])]
+            n = len(recs)
+            np.testing.assert_array_equal(log[p:p + n], recs)  # a call's ops are contiguous in the log
+            np.testing.assert_array_equal(some, osome[p:p + n])
+            np.testing.assert_array_equal(resp, oresp[p:p + n])
+    rounds, ops = comb.stats()
+    assert ops == len(log) + sum(4 for m in calls.values() for c in range(CALLS) if c % 7 == 3)
+
+    # phase 2: parallel pushes, then sequential pops (VerifyStack's invariant)
+    base = len(ost.dump())
+
+    def pusher(i):
+        tok = i  # tokens 0..T-1 are taken; pushes carry the pusher id in the low byte
+        for c in range(20):
+            recs = np.zeros(8, nrg.STACK_OP_DTYPE)
+            recs["op"] = L.NRG_STACK_PUSH
+            recs["val"] = ((c * 8 + np.arange(8)) << 8) | (0x80 | tok)
+            comb.execute_mut(tok, recs)
+
+    _run_threads(T, pusher)
+    last = {}
+    popped = 0
+    while True:
+        recs = np.zeros(32, nrg.STACK_OP_DTYPE)  # Pops
+        resp, some = comb.execute_mut(0, recs)
+        for v, s_ in zip(resp, some):
+            if not s_:
+                continue
+            if (int(v) & 0x80) and popped < 20 * 8 * T:
+                tid, seq = int(v) & 0x7F, int(v) >> 8
+                assert seq < last.get(tid, 1 << 30), "a pusher's values come out decreasing"
+                last[tid] = seq
+                popped += 1
+        if not np.all(some):
+            break
+    assert popped == 20 * 8 * T and len(last) == T
+    assert base > 0
+    comb.close()
+    assert dev.st_len() == 0
+    dev.close()
+
+
+def test_combiner_synthetic_threads(nrg, orc):
+    """AbstractDataStructure behind the combiner: concurrent ReadWrite/WriteOnly calls whose
+    sums equal the oracle's replay of the replica's log, then ReadOnly reads against the final
+    storage, which equals the oracle's."""
+    T, CALLS = 8, 25
+    L = nrg._lib
+    dev = nrg.DeviceReplica(L.NRG_DS_SYNTHETIC, 0, max_batch=1 << 12, log_bytes=64 * (1 << 17))
+    comb = nrg.Combiner(dev, T)
+    calls = {}
+
+    def client(i):
+        tok = comb.register()
+        rng = np.random.default_rng(900 + i)
+        mine = []
+        for c in range(CALLS):
+            n = int(rng.integers(1, 33))
+            recs = np.zeros(n, nrg.SYNTH_OP_DTYPE)
+            recs["tid"] = tok
+            recs["r1"] = rng.integers(0, 2**63, n, dtype=np.uint64)
+            recs["r2"] = rng.integers(0, 2**63, n, dtype=np.uint64)
+            recs["op"] = (rng.integers(0, 10, n) > 0).astype(np.uint64)
+            resp, some = comb.execute_mut(tok, recs)
+            assert np.all(some == 1)
+            mine.append((recs, resp))
+        calls[tok] = mine
+
+    _run_threads(T, client)
+    log = _read_log(nrg, dev, nrg.SYNTH_OP_DTYPE)
+    os_ = orc.Synthetic()
+    oresp = os_.replay(np.stack([log["tid"], log["r1"], log["r2"], log["op"]], axis=1))
+    pos = {int(r): i for i, r in enumerate(log["r1"])}
+    for tok, mine in calls.items():
+        for recs, resp in mine:
+            p = pos[int(recs["r1"][0])]
+            n = len(recs)
+            np.testing.assert_array_equal(log[p:p + n], recs)
+            np.testing.assert_array_equal(resp, oresp[p:p + n])
+    rd = np.zeros(20, nrg.SYNTH_RD_DTYPE)
+    raw = orc.gen_raw(60, 5)
+    rd["tid"], rd["r1"], rd["r2"] = raw[0::3] % 8, raw[1::3], raw[2::3]
+    got, some = comb.execute(0, rd)
+    np.testing.assert_array_equal(got, os_.read(np.stack([rd["tid"], rd["r1"], rd["r2"]], axis=1)))
+    assert np.all(some == 1)
+    comb.close()
+    np.testing.assert_array_equal(dev.sy_dump(), os_.dump())
     dev.close()

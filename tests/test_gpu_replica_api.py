@@ -99,3 +99,67 @@ def test_replicas_are_equal(nrg, ds):
     assert states[0] == states[1], "Data-structures don't match."
     for rep in reps:
         rep.dev.close()
+
+
+@pytest.mark.parametrize("ds", ["stack", "hashmap"])
+def test_late_replica_catches_up(nrg, ds):
+    """A replica registered after three rounds of writes (nr/src/log.rs:272-292: register at any
+    time; the new replica's ltail is 0) replays the live log on its first read (sync to ctail,
+    nr/src/replica.rs:469-479, :483-497) and ends equal to the first replica and the model."""
+    rng = random.Random(0x1A7E)
+    log = nrg.Log(1 << 20)
+    mk = (lambda: nrg.Replica(log, nrg.Stack, 0)) if ds == "stack" else (
+        lambda: nrg.Replica(log, nrg.NrHashMap, 0, log2_slots=14))
+    a = mk()
+    ta = a.register()
+    model = [] if ds == "stack" else {}
+    for _ in range(3):
+        if ds == "stack":
+            ops = [nrg.Push(rng.getrandbits(32)) if rng.random() < 0.7 else nrg.Pop() for _ in range(150)]
+        else:
+            ops = [nrg.Put(rng.randrange(400), rng.getrandbits(64)) for _ in range(150)]
+        a.execute_mut_batch(ops, ta)
+        for op in ops:
+            if ds == "stack":
+                if isinstance(op, nrg.Push):
+                    model.append(op.val)
+                elif model:
+                    model.pop()
+            else:
+                model[op.key] = op.val
+    b = mk()  # registered after 450 appended entries
+    assert b.idx == 2 and b.dev.log_state()["ltail"] == 0
+    tb = b.register()
+    if ds == "stack":
+        assert b.execute(nrg.Peek(), tb) == (model[-1] if model else None)
+    else:
+        for k in range(0, 400, 7):
+            assert b.execute(nrg.Get(k), tb) == model.get(k)
+    # both keep going on the shared log
+    more = [nrg.Push(5), nrg.Pop()] if ds == "stack" else [nrg.Put(1, 2), nrg.Put(3, 4)]
+    b.execute_mut_batch(more, tb)
+    if ds == "stack":
+        model.append(5)
+        model.pop()
+    else:
+        model[1], model[3] = 2, 4
+    states = []
+    for r in (a, b):
+        r.verify(lambda d: states.append(d))
+    assert states[0] == states[1] == model
+    for r in (a, b):
+        r.dev.close()
+
+
+def test_late_replica_after_gc_is_refused(nrg):
+    """Once GC has moved head past entry 0 a late replica cannot replay from its ltail 0 (the
+    reference panics, nr/src/log.rs:486-488): registration fails with a clear error."""
+    log = nrg.Log(2 * 64 * 8192)  # the smallest log: 16384 entries, GC within 8192 of full
+    a = nrg.Replica(log, nrg.NrHashMap, 0, log2_slots=16, max_batch=4096, log_bytes=log.bytes)
+    ta = a.register()
+    for r in range(4):
+        a.execute_mut_batch([nrg.Put(k, r) for k in range(3000)], ta)
+    assert log.head > 0
+    with pytest.raises(RuntimeError, match="garbage-collected"):
+        nrg.Replica(log, nrg.NrHashMap, 0, log2_slots=16, max_batch=4096)
+    a.dev.close()
