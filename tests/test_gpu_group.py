@@ -5,8 +5,10 @@ tests run the whole group path -- RCCL communicator, library-owned all-gather st
 gathered buffers, replay of the gathered log, reads and origin-only responses -- with nranks = 1,
 through both constructors (nrg_group_open: one process drives its GPUs; nrg_group_join: one
 process per GPU), against the sequential oracle. The rank-order concatenation of several
-segments is covered by tests/test_parallel.py (gloo, world 2 and 3) and by
-nrg_hashmap_round_segments_async's tests; the driver's 8-GPU runs exercise N > 1 over xGMI.
+segments is covered by tests/test_gpu_group_multi.py (G = 2, 3 and 8 members on this GPU over
+the loopback collectives of nrgpu_testing.h), tests/test_parallel.py (gloo, world 2 and 3) and
+nrg_hashmap_round_segments_async's tests. RCCL itself with N > 1 runs only on a multi-GPU node
+(the driver's scaling runs); no such run has been recorded yet.
 Reference: nr/src/log.rs:494-511 (every replica replays every entry of the shared log).
 """
 import ctypes as C
