@@ -39,6 +39,8 @@ int nrg_test_debug_read(nrg_ctx* ctx, uint64_t* out, uint64_t words);
                                   0xFF, 0xFF00; synthetic 1, 4, ...) -- measurement only            */
 #define NRG_KNOB_SY_SORT 7     /* synthetic: 1 = sort-based replay instead of the bucket path      */
 #define NRG_KNOB_PIPELINE 8    /* overrides nrg_config.pipeline                                    */
+#define NRG_KNOB_SORT_MIN 9    /* hashmap: rounds of at least this many Puts on an unskewed stream
+                                  replay as sorted rounds (0: never)                              */
 int nrg_test_set_knob(nrg_ctx* ctx, int knob, uint64_t value);
 
 /* Replica groups created after nrg_test_loopback_collectives(1) (nrg_group_open,

@@ -10,52 +10,60 @@
 // host memory that the round's kernels read and write directly, so a round costs no copies:
 //   post   : a client thread reserves room in the OPEN batch with an atomic add (as Log::append
 //            reserves log entries with a CAS on tail, nr/src/log.rs:391-399), copies its ops in
-//            and waits;
-//   combine: whoever takes the combiner lock seals the open batch, opens the next slot and
-//            enqueues the round on the replica's stream -- Log::append + Log::exec of the batch's
-//            writes, then its reads against the post-round state -- followed by an event; it
-//            does NOT wait for the GPU, so batch k+1 fills while round k is in flight
-//            (at most DEPTH rounds in flight);
-//   retire : a waiting thread that takes the poll lock queries the oldest in-flight round's
-//            event; a completed round's responses are already in host memory, and each client
-//            copies its own out of the batch.
+//            and waits for its round;
+//   combine: the combiner seals the open batch, opens the next slot and enqueues the round on the
+//            replica's stream -- Log::append + Log::exec of the batch's writes, then its reads
+//            against the post-round state -- followed by an event, without waiting for the GPU:
+//            batch k+1 fills while round k runs (at most DEPTH rounds in flight);
+//   retire : the combiner queries the in-flight rounds' events in order; a completed round's
+//            responses are already in host memory, its clients are woken and copy theirs out.
+// The combining role belongs to the library's combiner thread rather than to whichever client
+// takes a lock (nr/src/replica.rs:508-540): a round completes asynchronously on the GPU and needs a
+// host thread polling it, and with hundreds of clients on a few cores a client that holds the
+// role is descheduled while everyone waits. Clients spin briefly (longer while there are fewer
+// clients than cores) and then park on a futex of their batch; the combiner thread parks when
+// there is nothing to do and the first post wakes it.
 // Reads ride in the round that collects them, after its writes: they see every write completed
-// before they were posted (sync-to-tail) and never wait behind a later write round. Clients
-// spin briefly, then yield: a round takes tens of microseconds, and the host cores are better
-// left to the threads that combine.
+// before they were posted (sync-to-tail) and never wait behind a later write round.
 //
 // Generic over the three data structures (nr's Replica<D> is generic over Dispatch,
 // nr/src/replica.rs:72-115): hashmap Put/Get, stack Push-Pop/Peek, synthetic writes/ReadOnly.
 #include <hip/hip_runtime.h>
 #include <immintrin.h>
-#include <sched.h>
+#include <linux/futex.h>
+#include <sys/syscall.h>
+#include <time.h>
+#include <unistd.h>
 
 #include <atomic>
 #include <cstring>
-#include <mutex>
 #include <new>
+#include <thread>
 
 #include "internal.hpp"
 
 namespace {
 
 constexpr uint32_t MAX_PENDING = 32;  // nr/src/context.rs:12 MAX_PENDING_OPS
-constexpr int NB = 4;                 // batch slots
-constexpr uint64_t DEPTH = 2;         // rounds in flight (NB >= DEPTH + 2: a slot's clients read
-                                      // their responses while two later rounds run)
+constexpr int NB = 6;                 // batch slots
+constexpr uint64_t DEPTH = 2;         // rounds in flight (NB >= DEPTH + 2: a slot's clients copy
+                                      // their responses out while later rounds run)
 
 enum : uint32_t { FREE = 0, OPEN = 1, SEALED = 2, DONE = 3 };
 
-// A test-and-test-and-set lock: waiters look before they try, so hundreds of polling clients do
-// not bounce its cache line.
-struct alignas(64) SpinFlag {
-    std::atomic<bool> held{false};
-    bool try_lock() { return !held.load(std::memory_order_relaxed) && !held.exchange(true, std::memory_order_acquire); }
-    void lock() {
-        while (!try_lock()) _mm_pause();
-    }
-    void unlock() { held.store(false, std::memory_order_release); }
-};
+void futex_wait(std::atomic<uint32_t>* w, uint32_t seen) {
+    const timespec ts{0, 2000000};  // a lost wake-up costs at most 2 ms
+    syscall(SYS_futex, (uint32_t*)w, FUTEX_WAIT_PRIVATE, seen, &ts, nullptr, 0);
+}
+void futex_wake_all(std::atomic<uint32_t>* w) { syscall(SYS_futex, (uint32_t*)w, FUTEX_WAKE_PRIVATE, INT32_MAX, nullptr, nullptr, 0); }
+
+// CPUs this process may run on (the GPU box gives a job a share of a larger host)
+uint32_t cpus_allowed() {
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) return (uint32_t)CPU_COUNT(&set);
+    const unsigned n = std::thread::hardware_concurrency();
+    return n ? n : 1;
+}
 
 struct alignas(64) Batch {
     std::atomic<uint32_t> state{FREE};
@@ -63,6 +71,8 @@ struct alignas(64) Batch {
     alignas(64) std::atomic<uint32_t> writers{0};  // clients copying ops in
     std::atomic<uint32_t> readers{0};              // clients yet to copy their responses out
     std::atomic<uint32_t> nw{0}, nr{0};            // write records / reads reserved
+    alignas(64) std::atomic<uint32_t> wake{0};     // futex word: bumped when the round completes
+    std::atomic<uint32_t> sleepers{0};             // clients parked on it
     int rc = NRG_OK;                               // launch or device error of the round
     // host buffers (mapped, coherent; device addresses equal the host ones under UVA)
     char* recs = nullptr;   // cap write records
@@ -112,10 +122,14 @@ struct nrg_combiner {
     Batch b[NB];
     alignas(64) std::atomic<uint64_t> open{0};       // round number of the OPEN batch
     alignas(64) std::atomic<uint64_t> completed{0};  // rounds < completed are done
-    std::atomic<uint64_t> launched{0};               // rounds < launched are enqueued (combiner lock)
-    SpinFlag comb;                                   // the combiner lock
-    SpinFlag poll;                                   // retiring rounds (event queries)
+    std::atomic<uint64_t> launched{0};               // rounds < launched are enqueued (combiner thread)
     std::atomic<uint64_t> rounds{0}, ops{0};
+    uint32_t cpus = 1;                               // clients spin longer while fewer than this
+    // the combiner thread
+    std::thread worker;
+    std::atomic<bool> stop{false};
+    alignas(64) std::atomic<uint32_t> work{0};       // futex word: bumped by a post that finds it parked
+    std::atomic<uint32_t> parked{0};
 };
 
 namespace {
@@ -137,7 +151,7 @@ void comb_free(nrg_combiner* m) {
     delete m;
 }
 
-// Retire completed rounds in order (poll lock held).
+// Retire completed rounds in order and wake their clients (combiner thread).
 void retire(nrg_combiner* m) {
     uint64_t k = m->completed.load(std::memory_order_relaxed);
     while (k < m->launched.load(std::memory_order_acquire)) {
@@ -147,11 +161,13 @@ void retire(nrg_combiner* m) {
         if (q != hipSuccess && x.rc == NRG_OK) x.rc = NRG_E_HIP;
         if (x.rc == NRG_OK) x.rc = err_code(*(volatile uint32_t*)x.err);
         x.state.store(DONE, std::memory_order_release);
-        m->completed.store(++k, std::memory_order_release);
+        m->completed.store(++k, std::memory_order_seq_cst);
+        x.wake.fetch_add(1, std::memory_order_seq_cst);
+        if (x.sleepers.load(std::memory_order_seq_cst)) futex_wake_all(&x.wake);
     }
 }
 
-// Enqueue the round of sealed batch x (combiner lock held): the replica's writes, then its reads.
+// Enqueue the round of sealed batch x (combiner thread): the replica's writes, then its reads.
 int launch(nrg_combiner* m, Batch& x, uint32_t W, uint32_t R) {
     nrg_ctx* c = m->ctx;
     int rc = nrg::ctx_use_device(c);
@@ -187,16 +203,13 @@ int launch(nrg_combiner* m, Batch& x, uint32_t W, uint32_t R) {
     return rc;
 }
 
-// Combiner lock held: retire what has finished; seal the open batch and enqueue its round if it
-// holds ops and fewer than DEPTH rounds are in flight.
-void advance(nrg_combiner* m) {
-    m->poll.lock();
-    retire(m);
-    m->poll.unlock();
+// Combiner thread: seal the open batch and enqueue its round if it holds ops and fewer than
+// DEPTH rounds are in flight; true if it did.
+bool advance(nrg_combiner* m) {
     const uint64_t k = m->open.load(std::memory_order_relaxed);
     Batch& x = m->b[k % NB];
-    if (m->launched.load(std::memory_order_relaxed) - m->completed.load(std::memory_order_acquire) >= DEPTH) return;
-    if (!x.nw.load(std::memory_order_relaxed) && !x.nr.load(std::memory_order_relaxed)) return;
+    if (m->launched.load(std::memory_order_relaxed) - m->completed.load(std::memory_order_acquire) >= DEPTH) return false;
+    if (!x.nw.load(std::memory_order_seq_cst) && !x.nr.load(std::memory_order_seq_cst)) return false;
     x.state.store(SEALED, std::memory_order_seq_cst);
     while (x.writers.load(std::memory_order_seq_cst)) _mm_pause();
     const uint32_t W = x.nw.load(std::memory_order_relaxed), R = x.nr.load(std::memory_order_relaxed);
@@ -216,6 +229,31 @@ void advance(nrg_combiner* m) {
     m->launched.store(k + 1, std::memory_order_release);
     m->rounds.fetch_add(1, std::memory_order_relaxed);
     m->ops.fetch_add(W + R, std::memory_order_relaxed);
+    return true;
+}
+
+// The combiner thread: seal and launch, retire, park when idle.
+void combiner_main(nrg_combiner* m) {
+    (void)nrg::ctx_use_device(m->ctx);
+    while (!m->stop.load(std::memory_order_acquire)) {
+        const uint64_t done0 = m->completed.load(std::memory_order_relaxed);
+        retire(m);
+        const bool launched = advance(m);
+        if (launched || m->completed.load(std::memory_order_relaxed) != done0) continue;
+        const bool busy = m->launched.load(std::memory_order_relaxed) != m->completed.load(std::memory_order_relaxed);
+        if (busy) {  // a round is in flight: poll again shortly
+            for (int i = 0; i < 16; i++) _mm_pause();
+            continue;
+        }
+        // idle: park until a post (or close) bumps `work`
+        const uint32_t seen = m->work.load(std::memory_order_seq_cst);
+        m->parked.store(1, std::memory_order_seq_cst);
+        const Batch& o = m->b[m->open.load(std::memory_order_seq_cst) % NB];
+        if (!o.nw.load(std::memory_order_seq_cst) && !o.nr.load(std::memory_order_seq_cst) &&
+            !m->stop.load(std::memory_order_seq_cst))
+            futex_wait(&m->work, seen);
+        m->parked.store(0, std::memory_order_seq_cst);
+    }
 }
 
 // Post n ops of one thread, then combine or wait until their round is done (nr/src/replica.rs:414-433).
@@ -229,33 +267,36 @@ int post_and_wait(nrg_combiner* m, uint32_t token, bool write, const void* ops, 
     uint64_t k;
     Batch* x;
     uint32_t off;
-    for (uint32_t spins = 0;; spins++) {  // reserve room in the open batch (Context::enqueue)
+    for (;;) {  // reserve room in the open batch (Context::enqueue)
         k = m->open.load(std::memory_order_acquire);
         x = &m->b[k % NB];
         x->writers.fetch_add(1, std::memory_order_seq_cst);
         if (x->state.load(std::memory_order_seq_cst) == OPEN && x->round.load(std::memory_order_relaxed) == k) {
-            off = (write ? x->nw : x->nr).fetch_add(n, std::memory_order_relaxed);
+            off = (write ? x->nw : x->nr).fetch_add(n, std::memory_order_seq_cst);
             x->readers.fetch_add(1, std::memory_order_relaxed);
             if (in_b && ops) std::memcpy((write ? x->recs : x->reads) + (uint64_t)off * in_b, ops, (size_t)n * in_b);
             x->writers.fetch_sub(1, std::memory_order_release);
             break;
         }
         x->writers.fetch_sub(1, std::memory_order_relaxed);
-        if (spins > 64) sched_yield();
-        else _mm_pause();
+        _mm_pause();
     }
+    if (m->parked.load(std::memory_order_seq_cst)) {  // wake the combiner thread
+        m->work.fetch_add(1, std::memory_order_seq_cst);
+        syscall(SYS_futex, (uint32_t*)&m->work, FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
+    }
+    // spin, then park on the batch's futex: spin long (about a round) while the clients fit the
+    // cores, briefly when they do not
+    const uint32_t spin_rounds = m->next_tok.load(std::memory_order_relaxed) < m->cpus ? 2048 : 32;
     for (uint32_t spins = 0; m->completed.load(std::memory_order_acquire) <= k; spins++) {
-        if (m->comb.try_lock()) {
-            advance(m);
-            m->comb.unlock();
-        } else if (m->poll.try_lock()) {
-            retire(m);
-            m->poll.unlock();
+        if (spins < spin_rounds) {
+            for (int i = 0; i < 8; i++) _mm_pause();
+            continue;
         }
-        if (m->completed.load(std::memory_order_acquire) > k) break;
-        if (spins > 32) sched_yield();
-        else
-            for (int i = 0; i < 16; i++) _mm_pause();
+        const uint32_t seen = x->wake.load(std::memory_order_seq_cst);
+        x->sleepers.fetch_add(1, std::memory_order_seq_cst);
+        if (m->completed.load(std::memory_order_seq_cst) <= k) futex_wait(&x->wake, seen);
+        x->sleepers.fetch_sub(1, std::memory_order_seq_cst);
     }
     std::memcpy(out, (write ? x->wresp : x->rresp) + (uint64_t)off * out_b, (size_t)n * out_b);
     std::memcpy(some, (write ? x->wsome : x->rsome) + off, n);
@@ -307,8 +348,16 @@ extern "C" int nrg_combiner_open(nrg_ctx* ctx, uint32_t max_threads, nrg_combine
     }
     m->saved_pipeline = ctx->pipeline;
     ctx->pipeline = false;
+    m->cpus = cpus_allowed();
     m->b[0].round.store(0);
     m->b[0].state.store(OPEN);
+    try {
+        m->worker = std::thread(combiner_main, m);
+    } catch (...) {
+        ctx->pipeline = m->saved_pipeline;
+        comb_free(m);
+        return NRG_E_NOMEM;
+    }
     *out = m;
     return NRG_OK;
 }
@@ -317,17 +366,14 @@ extern "C" int nrg_combiner_open(nrg_ctx* ctx, uint32_t max_threads, nrg_combine
 extern "C" int nrg_combiner_close(nrg_combiner* m) {
     if (!m) return NRG_E_INVAL;
     int rc = NRG_OK;
-    {
-        m->comb.lock();
-        m->poll.lock();
-        (void)nrg::ctx_use_device(m->ctx);
-        if (hipStreamSynchronize((hipStream_t)nrg_get_stream(m->ctx)) != hipSuccess) rc = NRG_E_HIP;
-        retire(m);
-        m->ctx->pipeline = m->saved_pipeline;
-        m->poll.unlock();
-        m->comb.unlock();
-    }
-    comb_free(m);  // after both locks are released: nothing of m is touched afterwards
+    m->stop.store(true, std::memory_order_seq_cst);
+    m->work.fetch_add(1, std::memory_order_seq_cst);
+    syscall(SYS_futex, (uint32_t*)&m->work, FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
+    if (m->worker.joinable()) m->worker.join();  // the combiner thread touches nothing after this
+    (void)nrg::ctx_use_device(m->ctx);
+    if (hipStreamSynchronize((hipStream_t)nrg_get_stream(m->ctx)) != hipSuccess) rc = NRG_E_HIP;
+    m->ctx->pipeline = m->saved_pipeline;
+    comb_free(m);
     return rc;
 }
 

@@ -904,6 +904,149 @@ __global__ __launch_bounds__(TPB) void hm_elect_kernel(ElectJob j) {
 #undef EL_MARK
 }
 
+// ---- sorted rounds: large uniform write rounds -------------------------------
+// A stable radix sort of the round's Puts by the top 32 bits of mix64(key) -- whose leading bits
+// are the home slot, so the sorted order sweeps the table -- puts every key's Puts next to each
+// other in log order (two distinct keys share a sort key with probability ~2^-32; the scans below
+// compare full keys). Then, per Put, O(1) neighbour checks:
+//   last of its key  -> it alone finds or claims the key's slot and stores its value (no atomics
+//                       per Put, one table line per distinct key, visited in table order);
+//   previous value   -> the value of the key's preceding Put, or for its first Put the table's
+//                       value before the round (read by hm_sr_prev_kernel before any store).
+// Per Put: 16 B of records (+ the log copy), a 4-B sort key and 8 B per sort pass of streaming
+// traffic, one gather of its record in sorted order; per distinct key one table line.
+struct SortedJob {
+    RecSrc rec;
+    const u32* sk;  // sorted keys (top half of mix64(key))
+    const u32* sv;  // round offsets of the Puts in sorted order
+    u64 n;
+    Slot* table;
+    u32 shift;
+    u64 tmask;
+    DevCtl* ctl;
+    u64* created_acc;
+    u64* dup_acc;   // Puts with a later Put of their key in the same 512-Put tile (key skew)
+    u64 lo, resp_lo, resp_hi;
+    u64* prev;
+    uint8_t* prevf;
+};
+
+// the key pass: sort keys, the log copy, and the sort's four digit histograms in one read
+__global__ __launch_bounds__(TPB) void hm_sr_keys_kernel(RecSrc rec, nrg_put* ring_out, u64 n, u32* keys, u32* hist) {
+    __shared__ u32 sh[4 * 256];
+    for (int q = threadIdx.x; q < 4 * 256; q += TPB) sh[q] = 0;
+    __syncthreads();
+    for (u64 i = blockIdx.x * (u64)TPB + threadIdx.x; i < n; i += (u64)gridDim.x * TPB) {
+        const nrg_put r = rec.at(i);
+        if (ring_out) ring_out[(rec.lo + i) & rec.mask] = r;
+        const u32 k = (u32)(mix64(r.key) >> 32);
+        keys[i] = k;
+#pragma unroll
+        for (int p = 0; p < 4; p++) atomicAdd(&sh[p * 256 + ((k >> (8 * p)) & 255u)], 1u);
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < 4 * 256; q += TPB)
+        if (sh[q]) atomicAdd(&hist[q], sh[q]);
+}
+
+// value of key k before the round (read-only probe); false: absent
+__device__ __forceinline__ bool sr_table_value(const SortedJob& j, u64 k, u64* v) {
+    if (k == EMPTY_KEY) {
+        if (!j.ctl->sp_claim) return false;
+        *v = j.ctl->sp.val;
+        return true;
+    }
+    u64 s = table_home(k, j.shift);
+    for (u64 pr = 0; pr <= j.tmask; pr++) {
+        const u64x2 w = *(const u64x2*)&j.table[s];
+        if (w.x == k) {
+            *v = w.y;
+            return true;
+        }
+        if (w.x == EMPTY_KEY) return false;
+        s = (s + 1) & j.tmask;
+    }
+    return false;
+}
+
+// previous values (HashMap::insert's return, nr/examples/hashmap.rs:46-50), before any store
+__global__ __launch_bounds__(TPB) void hm_sr_prev_kernel(SortedJob j) {
+    const u64 p = blockIdx.x * (u64)TPB + threadIdx.x;
+    if (p >= j.n) return;
+    const u32 i = j.sv[p];
+    const u64 g = j.lo + i;
+    if (g < j.resp_lo || g >= j.resp_hi) return;
+    const u32 hk = j.sk[p];
+    const u64 k = j.rec.at(i).key;
+    u64 v = 0;
+    bool f = false, found_pred = false;
+    for (u64 q = p; q-- > 0 && j.sk[q] == hk;) {  // the key's preceding Put (same sort key, log order)
+        const nrg_put r = j.rec.at(j.sv[q]);
+        if (r.key == k) {
+            v = r.val;
+            f = found_pred = true;
+            break;
+        }
+    }
+    if (!found_pred) f = sr_table_value(j, k, &v);
+    j.prev[g - j.resp_lo] = f ? v : 0;
+    j.prevf[g - j.resp_lo] = f ? 1 : 0;
+}
+
+// the last Put of every key stores its value (claiming a slot for a new key)
+__global__ __launch_bounds__(TPB) void hm_sr_apply_kernel(SortedJob j) {
+    __shared__ u32 s_created, s_dup;
+    if (threadIdx.x == 0) s_created = s_dup = 0;
+    __syncthreads();
+    const u64 p = blockIdx.x * (u64)TPB + threadIdx.x;
+    u32 created = 0, dup = 0;
+    if (p < j.n) {
+        const u32 i = j.sv[p];
+        const u32 hk = j.sk[p];
+        const nrg_put r = j.rec.at(i);
+        bool last = true;
+        for (u64 q = p + 1; q < j.n && j.sk[q] == hk; q++) {
+            const u32 iq = j.sv[q];
+            if (j.rec.at(iq).key == r.key) {
+                last = false;
+                dup = (iq >> 9) == (i >> 9);  // the skew statistic of the index rounds: same 512-Put tile
+                break;
+            }
+        }
+        if (last) {
+            if (r.key == EMPTY_KEY) {  // one last Put per key: a plain store claims the side slot
+                if (!j.ctl->sp_claim) {
+                    j.ctl->sp_claim = 1;
+                    j.ctl->sp.st[0] = j.ctl->sp.st[1] = STAMP_PRESENT;
+                    created = 1;
+                }
+                j.ctl->sp.val = r.val;
+            } else {
+                bool fresh = false;
+                const long long sl = claim_slot(j.table, r.key, table_home(r.key, j.shift), j.tmask, &fresh);
+                if (sl < 0) {
+                    atomicOr(&j.ctl->err, ERR_TABLE_FULL);
+                } else {
+                    j.table[sl].val = r.val;
+                    if (fresh) {
+                        u64x2 z;
+                        z.x = z.y = STAMP_PRESENT;
+                        *(u64x2*)&j.table[sl].st[0] = z;
+                        created = 1;
+                    }
+                }
+            }
+        }
+    }
+    if (created) atomicAdd(&s_created, created);
+    if (dup) atomicAdd(&s_dup, dup);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (s_created) atomicAdd(&j.created_acc[blockIdx.x % HM_CREATED_SLOTS], (u64)s_created);
+        if (s_dup && j.dup_acc) atomicAdd(&j.dup_acc[blockIdx.x % HM_DUP_SLOTS], (u64)s_dup);
+    }
+}
+
 __global__ __launch_bounds__(TPB) void hm_init_table_kernel(Slot* table, u64 slots) {
     for (u64 s = blockIdx.x * (u64)TPB + threadIdx.x; s < slots; s += (u64)gridDim.x * TPB) {
         u64x2 z;
@@ -1261,6 +1404,52 @@ static hipError_t next_epoch(nrg_ctx* c, u32* e) {
     return hipSuccess;
 }
 
+// Sorted round (hm_sr_*): key pass with the log copy and the digit histograms, the 4-pass radix
+// sort, previous values if wanted, the last writers' stores. The round's reads ride in the next
+// launch like a bucket round's. The previous round completes first (its apply and reads).
+static hipError_t sorted_round(nrg_ctx* c, const nrg_put* src, u64 lo, u64 n, bool write_ring, const nrg_put* keep,
+                               u64 resp_lo, u64 resp_hi, u64* d_prev, uint8_t* d_prev_found, bool want_prev) {
+    hipError_t e = hm_flush(c);
+    if (e != hipSuccess) return e;
+    if (c->sort.cap < c->cfg.max_batch) {  // scratch on first use: sort pairs + sort keys
+        if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return e;
+        sort_free(c->sort);
+        if (c->d_sr_keys) (void)hipFree(c->d_sr_keys);
+        c->d_sr_keys = nullptr;
+        if (sort_alloc(c->sort, c->cfg.max_batch) != NRG_OK) return hipErrorOutOfMemory;
+        if ((e = hipMalloc(&c->d_sr_keys, c->cfg.max_batch * sizeof(u32))) != hipSuccess) return e;
+    }
+    u32* hist = nullptr;
+    if ((e = sort_prepare(c->sort, n, 32, c->stream, &hist)) != hipSuccess) return e;
+    timer_begin(c, "hm_sorted");
+    hm_sr_keys_kernel<<<grid_for(n, 2048), TPB, 0, c->stream>>>(ring_src(c, src, lo),
+                                                                write_ring ? (nrg_put*)c->d_ring : nullptr, n,
+                                                                c->d_sr_keys, hist);
+    u32 *sk = nullptr, *sv = nullptr;
+    if ((e = sort_run(c->sort, c->d_sr_keys, nullptr, n, 32, c->stream, &sk, &sv)) != hipSuccess) return e;
+    SortedJob j;
+    j.rec = ring_src(c, keep, lo);  // the log copy written by the key pass, or the caller's records
+    j.sk = sk;
+    j.sv = sv;
+    j.n = n;
+    j.table = c->d_table;
+    j.shift = c->slot_shift;
+    j.tmask = c->slots - 1;
+    j.ctl = c->d_ctl;
+    j.created_acc = c->d_created;
+    j.dup_acc = c->d_dup;
+    j.lo = lo;
+    j.resp_lo = resp_lo;
+    j.resp_hi = resp_hi;
+    j.prev = d_prev;
+    j.prevf = d_prev_found;
+    const unsigned g = (unsigned)((n + TPB - 1) / TPB);
+    if (want_prev) hm_sr_prev_kernel<<<g, TPB, 0, c->stream>>>(j);
+    hm_sr_apply_kernel<<<g, TPB, 0, c->stream>>>(j);
+    timer_end(c, "hm_sorted");
+    return hipGetLastError();
+}
+
 // Replay the records [lo, lo+n) (from `src_recs` if given, else from the ring; writing the
 // ring copy if write_ring) and answer R reads against the state after them.
 hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool write_ring, const u64* d_get_keys,
@@ -1276,8 +1465,14 @@ hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool
     u32 epoch;
     if ((e = next_epoch(c, &epoch)) != hipSuccess) return e;
     Launch L;
-    const bool stamp = !want_prev && c->stamp_max && n <= c->stamp_max && !c->skewed;
-    if (stamp) {
+    const bool sorted = !c->skewed && c->sort_min && n >= c->sort_min;
+    const bool stamp = !sorted && !want_prev && c->stamp_max && n <= c->stamp_max && !c->skewed;
+    if (sorted) {
+        // ---- sorted round: sort by key hash, last writers store (large uniform rounds) ----
+        if ((e = sorted_round(c, src, lo, n, write_ring, keep, resp_lo, resp_hi, d_prev, d_prev_found, want_prev)) !=
+            hipSuccess)
+            return e;
+    } else if (stamp) {
         // ---- stamp round: one launch {index(e) | apply(e-1) | reads(e-1)} ----
         const u32 K1 = stamp_k1_for(c);
         const u32 tile = TPB * K1;

@@ -30,6 +30,12 @@ void sort_free(SortScratch& s);
 // values are 0..n-1. Result pointers are returned (inside the scratch).
 hipError_t sort_pairs(SortScratch& s, const u32* keys_in, const u32* vals_in, u64 n, int key_bits,
                       hipStream_t st, u32** out_k, u32** out_v);
+// The same in two steps, for a caller that builds the digit histograms itself (fused into the
+// pass that produces the keys): sort_prepare clears the control words and returns the
+// [4][256] histogram array to add into; sort_run runs the digit passes.
+hipError_t sort_prepare(SortScratch& s, u64 n, int key_bits, hipStream_t st, u32** hist);
+hipError_t sort_run(SortScratch& s, const u32* keys_in, const u32* vals_in, u64 n, int key_bits, hipStream_t st,
+                    u32** out_k, u32** out_v);
 
 struct KTimer {
     std::vector<hipEvent_t> ev;  // pairs
@@ -127,6 +133,10 @@ struct nrg_ctx {
     // Stamp rounds (<= stamp_max Puts, no previous values): per-Put slot ids by epoch parity.
     uint64_t stamp_max = 0;
     uint64_t stamp_alloc = 0;  // Puts the put_slot arrays hold (stamp_max <= stamp_alloc)
+    // Sorted rounds (hm_sr_*): rounds of at least sort_min Puts (0: never) on a stream that is not
+    // skewed sort their Puts by key hash instead of stamping or bucketing them.
+    uint64_t sort_min = 1ull << 19;
+    uint32_t* d_sr_keys = nullptr;  // [max_batch] sort keys
     uint32_t epoch = 1;  // epoch of the last replay round (1: prefill / before any round)
     uint32_t epoch_limit = 0xFFFFFFF0u;  // renormalise stamps here (NRG_KNOB_EPOCH_LIMIT for tests)
     uint32_t* d_put_slot[2] = {nullptr, nullptr};

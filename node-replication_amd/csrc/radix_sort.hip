@@ -223,31 +223,29 @@ void sort_free(SortScratch& s) {
     s.ctlmem = nullptr;
 }
 
-hipError_t sort_pairs(SortScratch& s, const u32* keys_in, const u32* vals_in, u64 n, int key_bits,
-                      hipStream_t st, u32** out_k, u32** out_v) {
-    if (n == 0) {
-        *out_k = s.k[0];
-        *out_v = s.v[0];
-        return hipSuccess;
-    }
-    if (n > s.cap || n >= (1ull << 30)) return hipErrorInvalidValue;
+static int sort_passes(int key_bits) {
     int passes = (key_bits + 7) / 8;
-    if (passes < 1) passes = 1;
-    if (passes > 4) passes = 4;
+    return passes < 1 ? 1 : passes > 4 ? 4 : passes;
+}
+
+hipError_t sort_prepare(SortScratch& s, u64 n, int key_bits, hipStream_t st, u32** hist) {
+    if (n > s.cap || n >= (1ull << 30)) return hipErrorInvalidValue;
+    const u64 tile_keys = (u64)RS_TPB * rs_items_for(n);
+    const u64 tiles = (n + tile_keys - 1) / tile_keys;
+    const u64 words = RS_HIST_WORDS + RS_TICKET_WORDS + (u64)sort_passes(key_bits) * tiles * 256;
+    *hist = s.ctlmem;
+    return hipMemsetAsync(s.ctlmem, 0, words * 4, st);
+}
+
+hipError_t sort_run(SortScratch& s, const u32* keys_in, const u32* vals_in, u64 n, int key_bits, hipStream_t st,
+                    u32** out_k, u32** out_v) {
+    const int passes = sort_passes(key_bits);
     const int items = rs_items_for(n);
     const u64 tile_keys = (u64)RS_TPB * items;
     const u64 tiles = (n + tile_keys - 1) / tile_keys;
-    const u64 words = RS_HIST_WORDS + RS_TICKET_WORDS + (u64)passes * tiles * 256;
-    hipError_t e = hipMemsetAsync(s.ctlmem, 0, words * 4, st);
-    if (e != hipSuccess) return e;
     u32* hist = s.ctlmem;
     u32* tickets = s.ctlmem + RS_HIST_WORDS;
     u32* desc = s.ctlmem + RS_HIST_WORDS + RS_TICKET_WORDS;
-
-    // The histogram pass needs keys; with vals_in == nullptr the first pass generates 0..n-1.
-    u64 hb = (n + 256 * 8 - 1) / (256 * 8);  // 64 keys per thread measured 2.3x slower
-    if (hb > 1024) hb = 1024;
-    rs_hist_kernel<<<(unsigned)hb, 256, 0, st>>>(keys_in, n, passes, hist);
     const u32* kin = keys_in;
     const u32* vin = vals_in;
     for (int p = 0; p < passes; p++) {
@@ -269,6 +267,23 @@ hipError_t sort_pairs(SortScratch& s, const u32* keys_in, const u32* vals_in, u6
     *out_k = (u32*)kin;
     *out_v = (u32*)vin;
     return hipGetLastError();
+}
+
+hipError_t sort_pairs(SortScratch& s, const u32* keys_in, const u32* vals_in, u64 n, int key_bits,
+                      hipStream_t st, u32** out_k, u32** out_v) {
+    if (n == 0) {
+        *out_k = s.k[0];
+        *out_v = s.v[0];
+        return hipSuccess;
+    }
+    u32* hist = nullptr;
+    hipError_t e = sort_prepare(s, n, key_bits, st, &hist);
+    if (e != hipSuccess) return e;
+    // the histogram pass needs keys; with vals_in == nullptr the first pass generates 0..n-1
+    u64 hb = (n + 256 * 8 - 1) / (256 * 8);  // 64 keys per thread measured 2.3x slower
+    if (hb > 1024) hb = 1024;
+    rs_hist_kernel<<<(unsigned)hb, 256, 0, st>>>(keys_in, n, sort_passes(key_bits), hist);
+    return sort_run(s, keys_in, vals_in, n, key_bits, st, out_k, out_v);
 }
 
 }  // namespace nrg

@@ -399,7 +399,8 @@ int nrg_close(nrg_ctx* c) {
     if (c->stream && c->stream != c->own_stream) (void)hipStreamSynchronize(c->stream);
     void* ptrs[] = {c->d_ring,    c->d_ctl,      c->d_table,    c->d_stack,  c->d_words,
                     c->d_sort_aux, c->d_tmp_u64, c->d_scan_desc, c->d_created, c->d_st_aux,
-                    c->d_sy_aux,  c->d_bk_ent,   c->d_bk_key,   c->d_bk_cnt, c->d_dbg,     c->d_pt};
+                    c->d_sy_aux,  c->d_bk_ent,   c->d_bk_key,   c->d_bk_cnt, c->d_dbg,     c->d_pt,
+                    c->d_sr_keys};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     sort_free(c->sort);
@@ -1138,6 +1139,10 @@ extern "C" int nrg_test_set_knob(nrg_ctx* c, int knob, uint64_t v) {
             } else if (!v && !c->d_sy_aux && sy_bucket_eligible(c->cfg)) {
                 HIPCHK(hipMalloc(&c->d_sy_aux, sy_bucket_aux_bytes(c->cfg)));
             }
+            return NRG_OK;
+        case NRG_KNOB_SORT_MIN:
+            if (!hm) return NRG_E_INVAL;
+            c->sort_min = v;
             return NRG_OK;
         case NRG_KNOB_PIPELINE:
             if (v > 1) return NRG_E_INVAL;

@@ -33,9 +33,14 @@ def _check_state(dev, om):
     assert dev.hm_digest() == om.digest()
 
 
+# knobs of the replay paths: default selection, and sorted rounds forced for every size
+PATHS = {"default": {}, "sorted": {"SORT_MIN": 1}}
+
+
+@pytest.mark.parametrize("path", list(PATHS))
 @pytest.mark.parametrize("span,W,R,rounds", [(64, 300, 500, 6), (5000, 2000, 3000, 5), (1 << 40, 4000, 4000, 3)])
-def test_rounds_prev_and_gets(nrg, orc, span, W, R, rounds):
-    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=16, max_batch=8192)
+def test_rounds_prev_and_gets(nrg, orc, span, W, R, rounds, path):
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, knobs=PATHS[path], log2_slots=16, max_batch=8192)
     om = orc.HashMap()
     dev.hm_prefill_range(min(span, 1000), 1)
     om.prefill_range(min(span, 1000), 1)
@@ -59,9 +64,10 @@ def test_rounds_prev_and_gets(nrg, orc, span, W, R, rounds):
     dev.close()
 
 
-def test_exec_without_responses_matches(nrg, orc):
+@pytest.mark.parametrize("path", list(PATHS))
+def test_exec_without_responses_matches(nrg, orc, path):
     """benches/hashmap.rs:114-119 returns Ok(None): no previous-value pipeline."""
-    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=16, max_batch=4096)
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, knobs=PATHS[path], log2_slots=16, max_batch=4096)
     om = orc.HashMap()
     for r in range(4):
         keys = orc.gen_uniform(3000, 7 + r, 700)
@@ -72,9 +78,10 @@ def test_exec_without_responses_matches(nrg, orc):
     _check_state(dev, om)
 
 
-def test_exec_chunks_longer_than_max_batch(nrg, orc):
+@pytest.mark.parametrize("path", list(PATHS))
+def test_exec_chunks_longer_than_max_batch(nrg, orc, path):
     """An exec range longer than max_batch is replayed in order, chunk by chunk."""
-    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=15, max_batch=1000)
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, knobs=PATHS[path], log2_slots=15, max_batch=1000)
     om = orc.HashMap()
     keys = orc.gen_uniform(4500, 5, 300)  # heavy duplication across chunk boundaries
     vals = orc.gen_raw(4500, 6)
@@ -86,9 +93,11 @@ def test_exec_chunks_longer_than_max_batch(nrg, orc):
     _check_state(dev, om)
 
 
-def test_zipf_conflicts(nrg, orc):
-    """Zipf 0.99 stream: hot keys stress last-writer-wins ordering and CAS contention."""
-    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=20, max_batch=1 << 17)
+@pytest.mark.parametrize("path", list(PATHS))
+def test_zipf_conflicts(nrg, orc, path):
+    """Zipf 0.99 stream: hot keys stress last-writer-wins ordering and CAS contention (sorted
+    rounds: long runs of one key next to each other)."""
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, knobs=PATHS[path], log2_slots=20, max_batch=1 << 17)
     om = orc.HashMap()
     dev.hm_prefill_range(10000, 1)
     om.prefill_range(10000, 1)
@@ -136,7 +145,7 @@ def test_fused_round_device(nrg, orc):
     _check_state(dev, om)
 
 
-@pytest.mark.parametrize("path", ["stamp", "bucket"])
+@pytest.mark.parametrize("path", ["stamp", "bucket", "sorted"])
 def test_pipelined_rounds_back_to_back(nrg, orc, path):
     """config.pipeline = 1: rounds enqueued back to back, no host sync in between. Each round's
     reads run in the next round's launch, beside its index pass (and, for stamp rounds, beside
@@ -145,7 +154,7 @@ def test_pipelined_rounds_back_to_back(nrg, orc, path):
     Knob STAMP_MAX = 0 sends every round through the bucket elector instead."""
     import torch
 
-    knobs = {"STAMP_MAX": 0} if path == "bucket" else {}
+    knobs = {"STAMP_MAX": 0} if path == "bucket" else PATHS["sorted"] if path == "sorted" else {}
     dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, knobs=knobs, log2_slots=17, max_batch=1 << 14, pipeline=1)
     dev.use_torch_stream()
     om = orc.HashMap()
@@ -411,15 +420,15 @@ def test_epoch_renormalisation(nrg, orc):
     new keys, overwrites and side-slot keys across several renormalisations, against the oracle."""
     import torch
 
-    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, knobs={"EPOCH_LIMIT": 6, "STAMP_MAX": 5000}, log2_slots=16,
-                            max_batch=8192, pipeline=1)
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, knobs={"EPOCH_LIMIT": 6, "STAMP_MAX": 5000, "SORT_MIN": 6500},
+                            log2_slots=16, max_batch=8192, pipeline=1)
     dev.use_torch_stream()
     om = orc.HashMap()
     dev.hm_prefill_range(500, 1)
     om.prefill_range(500, 1)
     outs, want = [], []
     for r in range(17):
-        W = 3000 if r % 3 else 7000  # 7000 > STAMP_MAX: bucket rounds in between
+        W = 3000 if r % 3 else (7000 if r % 2 else 6000)  # 7000: a sorted round, 6000: a bucket round
         keys = orc.gen_uniform(W, 900 + r, 4000 + 150 * r)
         keys[::113] = EMPTY
         vals = orc.gen_raw(W, 950 + r)
