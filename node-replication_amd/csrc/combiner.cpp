@@ -176,6 +176,7 @@ int launch(nrg_combiner* m, Batch& x, uint32_t W, uint32_t R) {
     const uint32_t origin = c->cfg.replica_id;
     switch (m->kind) {
         case NRG_DS_HASHMAP:  // Put -> HashMap::insert's previous value (nr/examples/hashmap.rs:46-50)
+            c->err_out = x.err;  // the round's last launch copies the error latch (no extra kernel)
             rc = nrg_hashmap_round_async(c, (const nrg_put*)x.recs, W, origin, (const uint64_t*)x.reads, R,
                                          (uint64_t*)x.rresp, x.rsome, (uint64_t*)x.wresp, x.wsome);
             break;
@@ -196,10 +197,12 @@ int launch(nrg_combiner* m, Batch& x, uint32_t W, uint32_t R) {
             break;
     }
     if (!rc && nrg_join(c)) rc = NRG_E_HIP;  // a deferred round tail would write responses later
-    if (!rc) {
+    if (!rc && (m->kind != NRG_DS_HASHMAP || c->err_out)) {  // no launch took the error copy
+        c->err_out = nullptr;
         comb_err_kernel<<<1, 64, 0, st>>>(c->d_ctl, x.err);
         if (hipGetLastError() != hipSuccess) rc = NRG_E_HIP;
     }
+    c->err_out = nullptr;
     return rc;
 }
 

@@ -74,6 +74,13 @@ struct ReadJob {
     u32 epoch;    // the reads see the state after round `epoch`
     bool use_rec; // that round's apply may run in the same launch: take its winners' records
     RecSrc rec;
+    // key-skew sample riding in this launch (skew_sample): the launch's last block moves the
+    // duplicate counters to mapped host memory as {seq, dups}; seq 0 = none
+    u64* s_acc;
+    volatile u64* s_host;
+    u64 s_seq;
+    // the replica's error latch, copied to (mapped) e_out and cleared by the same block (nrg_combiner)
+    u32* e_out;
 };
 
 __device__ __forceinline__ u32 bucket_of_id(u32 id, u32 bk_shift) { return id == SIDE_ID ? 0u : (id & ID_MASK) >> bk_shift; }
@@ -506,6 +513,21 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_num_sgpr(80))) void hm_r
                                                        Slot* table, u32 shift, u64 tmask, DevCtl* ctl) {
     extern __shared__ __attribute__((aligned(16))) char s_lds[];
     u32 b = blockIdx.x;
+    if ((rj.s_seq || rj.e_out) && b == gridDim.x - 1) {  // the tail block
+        if (rj.e_out && threadIdx.x == 0) *rj.e_out = atomicExch(&ctl->err, 0u);
+        // the skew sample (counters read and cleared atomically)
+        if (rj.s_seq && threadIdx.x < HM_DUP_SLOTS) {
+            u64 v = atomicExch((unsigned long long*)&rj.s_acc[threadIdx.x], 0ull);
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+            if (threadIdx.x == 0) {
+                rj.s_host[1] = v;
+                __threadfence_system();
+                rj.s_host[0] = rj.s_seq;
+            }
+        }
+        return;
+    }
     const u32 nix = IX == IX_STAMP ? sj.nblocks : ij.nblocks;
     if (b < nix) {
         if constexpr (IX == IX_STAMP) stamp_index_role<K1>(sj, b, table, shift, tmask, ctl, s_lds);
@@ -1101,20 +1123,6 @@ __global__ __launch_bounds__(TPB) void hm_prefill_range_kernel(Slot* table, u64 
     if (threadIdx.x == 0 && s_ins) atomicAdd(&ctl->nkeys, (u64)s_ins);
 }
 
-// Key-skew sample: the duplicate count of the rounds since the last sample goes to mapped host
-// memory ({seq, dups}: dups first, then the sequence number that publishes it); slots cleared.
-__global__ __launch_bounds__(64) void hm_dup_sample_kernel(u64* acc, volatile u64* host, u64 seq) {
-    u64 v = acc[threadIdx.x];
-    acc[threadIdx.x] = 0;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    if (threadIdx.x == 0) {
-        host[1] = v;
-        __threadfence_system();
-        host[0] = seq;
-    }
-}
-
 // number of keys = direct inserts (ctl->nkeys) + keys created by replay rounds
 __global__ __launch_bounds__(TPB) void hm_count_kernel(const u64* __restrict__ acc, u64 n, DevCtl* ctl) {
     __shared__ u64 s_w[TPB / 64];
@@ -1289,8 +1297,20 @@ static void launch_round(nrg_ctx* c, const Launch& L, u32 blocks, unsigned lds) 
 static hipError_t launch(nrg_ctx* c, Launch& L) {
     L.rj.nblocks = (u32)((L.rj.R + TPB - 1) / TPB);
     const u32 nix = L.ix == IX_STAMP ? L.sj.nblocks : L.ij.nblocks;
-    const u32 blocks = nix + L.aj.nblocks + L.rj.nblocks;
+    u32 blocks = nix + L.aj.nblocks + L.rj.nblocks;
     if (blocks == 0) return hipSuccess;
+    // a pending skew sample, or the error copy of a launch that ends a round (no index role:
+    // earlier kernels of the round, the elector's claims included, have latched their errors)
+    const bool err_here = c->err_out && nix == 0;
+    if (c->sample_seq || err_here) {  // the launch's last block
+        L.rj.s_acc = c->d_dup;
+        L.rj.s_host = c->h_dup_dev;
+        L.rj.s_seq = c->sample_seq;
+        L.rj.e_out = err_here ? c->err_out : nullptr;
+        c->sample_seq = 0;
+        if (err_here) c->err_out = nullptr;
+        blocks++;
+    }
     unsigned lds = 0;
     if (nix && L.ix == IX_STAMP) {
         lds = L.K1 == 4 ? StampLds<4>::BYTES : L.K1 == 2 ? StampLds<2>::BYTES : StampLds<1>::BYTES;
@@ -1379,11 +1399,11 @@ void hm_free(nrg_ctx* c) {
 static hipError_t skew_sample(nrg_ctx* c) {
     if (c->dup_seq && c->h_dup[0] == c->dup_seq && c->dup_puts_sampled)
         c->skewed = c->h_dup[1] * 64 > c->dup_puts_sampled;
-    hm_dup_sample_kernel<<<1, 64, 0, c->stream>>>(c->d_dup, c->h_dup_dev, ++c->dup_seq);
+    c->sample_seq = ++c->dup_seq;  // taken by the next hm_round launch (its last block)
     c->dup_puts_sampled = c->dup_puts;
     c->dup_puts = 0;
     c->dup_rounds = 0;
-    return hipGetLastError();
+    return hipSuccess;
 }
 
 hipError_t hm_init(nrg_ctx* c) {

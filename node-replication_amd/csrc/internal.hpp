@@ -148,6 +148,8 @@ struct nrg_ctx {
     volatile uint64_t* h_dup = nullptr;   // {seq, dups}, mapped pinned host memory
     uint64_t* h_dup_dev = nullptr;        // its device address
     uint64_t dup_seq = 0, dup_puts = 0, dup_puts_sampled = 0;
+    uint64_t sample_seq = 0;  // a sample the next hm_round launch takes (0: none pending)
+    uint32_t* err_out = nullptr;  // the next hm_round launch copies (and clears) the error latch here
     uint32_t dup_rounds = 0, dup_every = 16;
     bool skewed = false;
     // Zipf generator cache: zeta(zipf_n, zipf_theta)

@@ -264,7 +264,7 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
     // every level, so a walk that has left the tile stops there without a branch
     __shared__ unsigned short s_sp[8][ST_LANES + 1];
     __shared__ int s_suf[ST_LANES];     // inclusive suffix minimum of s_min inside the wave
-    __shared__ int s_wm[ST_WAVES], s_we[ST_WAVES], s_wmin[ST_WAVES];
+    __shared__ int s_wm[ST_WAVES], s_we[ST_WAVES], s_wmin[ST_WAVES], s_tot[ST_WAVES];
     __shared__ long long s_D, s_d0;
     __shared__ u32 s_ucnt;
     constexpr u32 ST_XL = 1024;
@@ -516,6 +516,7 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
             if (lane >= off) inc += o;
         }
         total = __shfl(inc, 63, 64);
+        if (lane == 0) s_tot[wv] = total;
         {
             u32 um = umask;
             for (int k = 0, h = inc - uq_; k < uq_; k++, h++) {
@@ -545,6 +546,66 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
     };
     // unclamped walk (D + M >= 0): amin = xe - nun - M, start xe - M, every unmatched Pop reads
     build(xe - (int)nun - M, xe - M, (int)nun);
+
+    // ---- 4. unmatched Pops: QI queries per lane at a time, their table walks interleaved. The
+    // queries of wave `lw`'s list, entries h = slot*64*QI + lane + k*64*QI*nslots (a wave answers
+    // its own list, or a share of another wave's). Everything here is relative to the tile's
+    // lowest level: with the unclamped structures nothing depends on the start depth D. ----
+    constexpr int QI = 4;
+    auto queries = [&](int lw, int slot, int nslots) {
+        const u32* up = s_wave[lw] + W_STK;
+        const int tot = s_tot[lw];
+        for (int h0 = slot * 64 * QI + lane; h0 < tot; h0 += 64 * QI * nslots) {
+            u32 e[QI];
+            int v[QI];
+#pragma unroll
+            for (int i = 0; i < QI; i++) {
+                const int h = h0 + 64 * i;
+                e[i] = h < tot ? up[h] : 0u;
+                v[i] = h < tot ? (int)((e[i] & ST_PMASK) / SW_OPS) - 1 : -1;
+            }
+            // the nearest earlier lane whose minimum is <= the level (greedy skips of 128, ..., 1);
+            // branch-free, so each level's QI table reads are in flight together (predicated reads
+            // compiled to one LDS round trip per query and level: 2.5 us for a 4096-op tile)
+#pragma unroll
+            for (int j = 7; j >= 0; j--) {
+                int m[QI];
+#pragma unroll
+                for (int i = 0; i < QI; i++) m[i] = (int)s_sp[j][v[i] + 1];
+#pragma unroll
+                for (int i = 0; i < QI; i++) {
+                    const int w = v[i] - (m[i] > (int)(e[i] >> ST_PB) ? 1 << j : 0);
+                    v[i] = w > -1 ? w : -1;
+                }
+            }
+            // the found lanes' residual entries, read together (lane 0's column for the others)
+            int mn[QI];
+            u32 rv[QI];
+#pragma unroll
+            for (int i = 0; i < QI; i++) mn[i] = s_min[v[i] > 0 ? v[i] : 0];
+#pragma unroll
+            for (int i = 0; i < QI; i++) {
+                const int vv = v[i] > 0 ? v[i] : 0;
+                rv[i] = s_wave[vv >> 6][v[i] >= 0 ? ((int)(e[i] >> ST_PB) - mn[i]) * 64 + (vv & 63) : 0];
+            }
+#pragma unroll
+            for (int i = 0; i < QI; i++) {
+                if (h0 + 64 * i >= tot) continue;
+                const u32 pos = e[i] & ST_PMASK;
+                if (v[i] >= 0) {
+                    const u64 g = lo + tbase + pos;
+                    if (resp && g >= resp_lo && g < resp_hi) {
+                        resp[g - resp_lo] = rv[i];
+                        some[g - resp_lo] = 1;
+                    }
+                } else {  // its Push is in an earlier tile or before the chunk
+                    const u32 x = atomicAdd(&s_ucnt, 1u);
+                    tl.upop[(u64)tile * ST_TILE + x] = e[i];
+                    if (x < ST_XL) s_xl[x] = e[i];
+                }
+            }
+        }
+    };
 
     if (wv == 0) {
         Fn acc = FN_ID;
@@ -585,6 +646,11 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
             s_D = fn_apply(acc, d0g);
             s_d0 = d0g;
         }
+    } else {
+        // while wave 0 waits on the look-back the other waves answer every wave's unmatched Pops
+        // for the unclamped walk -- their own lists, then a share of wave 0's
+        queries(wv, 0, 1);
+        queries(0, wv - 1, ST_WAVES - 1);
     }
     __syncthreads();
     ST_MARK(4);
@@ -597,8 +663,24 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
     const int aend_r = amin + (int)top;  // the lane's end depth: max(Dt + e, top) - T0
     if (t == ST_LANES - 1 && tile == A.tiles - 1) sdepth[A.par] = T0 + aend_r;
     if (Dt + hmax > (long long)cap || (long long)topmax > (long long)cap) atomicOr(&ctl->err, ERR_CAPACITY);
-    // the stack empties inside the tile: Pops at depth 0 are no-ops, levels shift (block-uniform)
-    if (D + M < 0) build(amin, dt, (int)(Dt < (long long)nun ? Dt : (long long)nun));
+    // the stack empties inside the tile (block-uniform, rare): Pops at depth 0 are no-ops and
+    // levels shift, so the speculative answers are withdrawn -- every unmatched Pop back to None,
+    // the cross-tile list emptied -- and the queries run again on the clamped structures
+    const bool clamped = D + M < 0;
+    if (clamped) {
+        const u64 g0 = lo + base;
+        for (u32 um = umask; um; um &= um - 1) {
+            const u64 g = g0 + (u64)__builtin_ctz(um);
+            if (resp && g >= resp_lo && g < resp_hi) {
+                resp[g - resp_lo] = 0;
+                some[g - resp_lo] = 0;
+            }
+        }
+        if (t == 0) s_ucnt = 0;
+        __syncthreads();
+        build(amin, dt, (int)(Dt < (long long)nun ? Dt : (long long)nun));
+        queries(wv, 0, 1);
+    }
     // The cross-tile Pops read exactly the levels [T0, D), each on the tile's first descent below
     // it. Their pre-chunk content: a slot the previous chunk wrote comes from its owner's table
     // (that chunk's commit runs in this launch), any other from the stack. Fetched now for the
@@ -611,60 +693,8 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
     __syncthreads();
     ST_MARK(5);
     const u32 pre = t < D - T0 ? pre_content(T0 + t) : 0u;  // after the barrier: its fence would wait
+    ST_MARK(9);
 
-    // ---- 4. unmatched Pops: QI queries per lane at a time, their table walks interleaved ----
-    constexpr int QI = 4;
-    for (int h0 = lane; h0 < total; h0 += 64 * QI) {
-        u32 e[QI];
-        int v[QI];
-#pragma unroll
-        for (int i = 0; i < QI; i++) {
-            const int h = h0 + 64 * i;
-            e[i] = h < total ? s_up[h] : 0u;
-            v[i] = h < total ? (int)((e[i] & ST_PMASK) / SW_OPS) - 1 : -1;
-        }
-        // the nearest earlier lane whose minimum is <= the level (greedy skips of 128, ..., 1);
-        // branch-free, so each level's QI table reads are in flight together (predicated reads
-        // compiled to one LDS round trip per query and level: 2.5 us for a 4096-op tile)
-#pragma unroll
-        for (int j = 7; j >= 0; j--) {
-            int m[QI];
-#pragma unroll
-            for (int i = 0; i < QI; i++) m[i] = (int)s_sp[j][v[i] + 1];
-#pragma unroll
-            for (int i = 0; i < QI; i++) {
-                const int w = v[i] - (m[i] > (int)(e[i] >> ST_PB) ? 1 << j : 0);
-                v[i] = w > -1 ? w : -1;
-            }
-        }
-        // the found lanes' residual entries, read together (lane 0's column for the others)
-        int mn[QI];
-        u32 rv[QI];
-#pragma unroll
-        for (int i = 0; i < QI; i++) mn[i] = s_min[v[i] > 0 ? v[i] : 0];
-#pragma unroll
-        for (int i = 0; i < QI; i++) {
-            const int vv = v[i] > 0 ? v[i] : 0;
-            rv[i] = s_wave[vv >> 6][v[i] >= 0 ? ((int)(e[i] >> ST_PB) - mn[i]) * 64 + (vv & 63) : 0];
-        }
-#pragma unroll
-        for (int i = 0; i < QI; i++) {
-            if (h0 + 64 * i >= total) continue;
-            const u32 pos = e[i] & ST_PMASK;
-            if (v[i] >= 0) {
-                const u64 g = lo + tbase + pos;
-                if (resp && g >= resp_lo && g < resp_hi) {
-                    resp[g - resp_lo] = rv[i];
-                    some[g - resp_lo] = 1;
-                }
-            } else {  // its Push is in an earlier tile or before the chunk
-                const u32 x = atomicAdd(&s_ucnt, 1u);
-                tl.upop[(u64)tile * ST_TILE + x] = e[i];
-                if (x < ST_XL) s_xl[x] = e[i];
-            }
-        }
-    }
-    ST_MARK(9);  // wave 0's own queries done
     if (dbg && t == 0) dbg[(u64)tile * 16 + 10] = (u64)total;
     s_pre[t] = pre;
     __syncthreads();

@@ -288,26 +288,24 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Stable ranking of one wave round in a wave-private (mask, count) table: every lane with a
-// key ORs its bit into mask[key]; the mask read back is the set of lanes with that key
-// (cheaper than matching the key bit by bit with ballots). Returns count[key] + the number
-// of lower lanes with the same key; the highest such lane advances count and clears mask.
-template <typename CNT>
-__device__ __forceinline__ u32 wave_rank(bool on, u32 key, int lane, u64* mask, CNT* count, u64* peers_out) {
-    if (on) atomicOr((unsigned long long*)&mask[key], 1ull << lane);
-    wave_lds_sync();
-    u64 peers = 0;
-    u32 c0 = 0;
-    if (on) {
-        peers = mask[key];
-        c0 = count[key];
+// Stable ranking by ballots: the lanes holding the same BITS-bit key are found by matching the
+// key bit by bit (BITS ballots and no LDS round trip), then one read of the wave-private
+// count[key] and one write by the highest such lane (one wave's LDS accesses stay in order).
+// Returns count[key] + the number of lower lanes with the key; *peers_out = those lanes.
+template <int BITS, typename CNT>
+__device__ __forceinline__ u32 wave_rank_bits(bool on, u32 key, int lane, CNT* count, u64* peers_out) {
+    u64 peers = __ballot(on);
+#pragma unroll
+    for (int b = 0; b < BITS; b++) {
+        const bool bit = (key >> b) & 1u;
+        const u64 bal = __ballot(bit);
+        peers &= bit ? bal : ~bal;
     }
-    wave_lds_sync();
-    if (on && 63 - __clzll(peers) == lane) {
-        mask[key] = 0;
-        count[key] = (CNT)(c0 + (u32)__popcll(peers));
-    }
-    wave_lds_sync();
+    if (!on) peers = 0;
+    const u32 c0 = on ? (u32)count[key] : 0u;
+    __builtin_amdgcn_wave_barrier();
+    if (on && 63 - __clzll(peers) == lane) count[key] = (CNT)(c0 + (u32)__popcll(peers));
+    __builtin_amdgcn_wave_barrier();
     *peers_out = peers;
     return c0 + (u32)__popcll(peers & ((1ull << lane) - 1));
 }
@@ -347,7 +345,6 @@ struct SyPartLds {
     unsigned short wcnt[SYA_WAVES][SY_MAX_NB];
     union {
         struct {
-            u64 mask[SYA_WAVES][SY_MAX_NB];
             u32 words[SYA_WAVES][64 * CW];
         } r;
         u32 stage[SYA_OPS * CW];
@@ -376,7 +373,6 @@ __device__ __forceinline__ void sy_part_role(const SyPartArgs& A, u32 tile, SyPa
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const u64 op0 = (u64)tile * SYA_OPS;
     for (u32 i = tid; i < SYA_WAVES * SY_MAX_NB / 2; i += SYA_TPB) ((u32*)&s_wcnt[0][0])[i] = 0;
-    for (u32 i = tid; i < SYA_WAVES * SY_MAX_NB; i += SYA_TPB) (&s_u.r.mask[0][0])[i] = 0;
     if (lane < SY_MAX_HOT) s_hot[w][lane] = SyHot{0, 0, 0};
     __syncthreads();
     u32 xs[SYA_OROUNDS * CW];
@@ -458,7 +454,7 @@ __device__ __forceinline__ void sy_part_role(const SyPartArgs& A, u32 tile, SyPa
 #pragma unroll
         for (int r = 0; r < CW; r++) {
             u64 peers;
-            const u32 rank = wave_rank(vw[r] != NOTOUCH, bw[r], lane, s_u.r.mask[w], s_wcnt[w], &peers);
+            const u32 rank = wave_rank_bits<9>(vw[r] != NOTOUCH, bw[r], lane, s_wcnt[w], &peers);
             xs[orr * CW + r] = vw[r];
             pk[orr * CW + r] = (bw[r] << 16) | rank;
         }
@@ -538,7 +534,6 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
     extern __shared__ u32 s_dyn[];  // s_pre[ntiles + 1], s_off[ntiles] (u16)
     __shared__ u64 s_cur[SYB_WORDS];
     __shared__ u32 s_wc[SYB_WAVES][SYB_WORDS];
-    __shared__ u64 s_mk[SYB_WAVES][SYB_WORDS];
     __shared__ unsigned short s_tile[2][SYB_PASS];  // tile of every touch of a pass (double buffered)
     __shared__ u32 s_part[SYB_WAVES];
     u32* s_pre = s_dyn;
@@ -553,10 +548,7 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
         s_pre[t] = p & 0xFFFFu;
     }
     for (u32 i = tid; i < SYB_WORDS; i += SYB_TPB) s_cur[i] = i < nw && w0 + i < N ? words[w0 + i] : 0ull;
-    for (u32 i = tid; i < SYB_WAVES * SYB_WORDS; i += SYB_TPB) {
-        (&s_wc[0][0])[i] = 0;
-        (&s_mk[0][0])[i] = 0;
-    }
+    for (u32 i = tid; i < SYB_WAVES * SYB_WORDS; i += SYB_TPB) (&s_wc[0][0])[i] = 0;
     __syncthreads();
     SY_MARK(1);
     // exclusive scan of the per-tile counts: thread owns tiles [tid*K, tid*K + K)
@@ -645,7 +637,7 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
                 for (int q = 0; q < SYB_PER; q++) {
                     const u32 i = base + (u32)w * (SYB_PER * 64) + q * 64 + lane;
                     u64 peers;
-                    sv[q] = wave_rank(i < total, ent_word(ent[q]), lane, s_mk[w], s_wc[w], &peers);
+                    sv[q] = wave_rank_bits<SYB_SHIFT>(i < total, ent_word(ent[q]), lane, s_wc[w], &peers);
                 }
             }
             __syncthreads();
@@ -686,7 +678,7 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
                         const u32 xl = ent_word(ent[q]);
                         const bool isset = valid && ent_set(ent[q]);
                         u64 peers;
-                        (void)wave_rank(valid, xl, lane, s_mk[w], s_wc[w], &peers);
+                        (void)wave_rank_bits<SYB_SHIFT>(valid, xl, lane, s_wc[w], &peers);
                         const u64 P = peers & ((1ull << lane) - 1);
                         const u64 S = __ballot(isset) & P;
                         const int sl = S ? 63 - __clzll(S) : lane;
