@@ -121,6 +121,8 @@ struct nrg_combiner {
     std::atomic<uint32_t> next_tok{0};
     Batch b[NB];
     alignas(64) std::atomic<uint64_t> open{0};       // round number of the OPEN batch
+    std::atomic<uint32_t> opened{0};                 // futex word: bumped when a batch opens
+    std::atomic<uint32_t> open_sleepers{0};          // clients parked until one does
     alignas(64) std::atomic<uint64_t> completed{0};  // rounds < completed are done
     std::atomic<uint64_t> launched{0};               // rounds < launched are enqueued (combiner thread)
     std::atomic<uint64_t> rounds{0}, ops{0};
@@ -225,7 +227,9 @@ bool advance(nrg_combiner* m) {
     y.rc = NRG_OK;
     y.round.store(k + 1, std::memory_order_relaxed);
     y.state.store(OPEN, std::memory_order_seq_cst);
-    m->open.store(k + 1, std::memory_order_release);
+    m->open.store(k + 1, std::memory_order_seq_cst);
+    m->opened.fetch_add(1, std::memory_order_seq_cst);
+    if (m->open_sleepers.load(std::memory_order_seq_cst)) futex_wake_all(&m->opened);
     x.rc = launch(m, x, W, R);
     hipStream_t st = (hipStream_t)nrg_get_stream(m->ctx);
     if (hipEventRecord(x.done, st) != hipSuccess && x.rc == NRG_OK) x.rc = NRG_E_HIP;
@@ -270,8 +274,9 @@ int post_and_wait(nrg_combiner* m, uint32_t token, bool write, const void* ops, 
     uint64_t k;
     Batch* x;
     uint32_t off;
-    for (;;) {  // reserve room in the open batch (Context::enqueue)
-        k = m->open.load(std::memory_order_acquire);
+    for (uint32_t spins = 0;; spins++) {  // reserve room in the open batch (Context::enqueue)
+        const uint32_t seen = m->opened.load(std::memory_order_seq_cst);
+        k = m->open.load(std::memory_order_seq_cst);
         x = &m->b[k % NB];
         x->writers.fetch_add(1, std::memory_order_seq_cst);
         if (x->state.load(std::memory_order_seq_cst) == OPEN && x->round.load(std::memory_order_relaxed) == k) {
@@ -282,7 +287,15 @@ int post_and_wait(nrg_combiner* m, uint32_t token, bool write, const void* ops, 
             break;
         }
         x->writers.fetch_sub(1, std::memory_order_relaxed);
-        _mm_pause();
+        // the batch is sealed and the next one not open yet (the combiner waits for a slot's
+        // clients to copy their responses out): do not take their cores, park until it opens
+        if (spins < 64) {
+            _mm_pause();
+            continue;
+        }
+        m->open_sleepers.fetch_add(1, std::memory_order_seq_cst);
+        if (m->open.load(std::memory_order_seq_cst) == k) futex_wait(&m->opened, seen);
+        m->open_sleepers.fetch_sub(1, std::memory_order_seq_cst);
     }
     if (m->parked.load(std::memory_order_seq_cst)) {  // wake the combiner thread
         m->work.fetch_add(1, std::memory_order_seq_cst);

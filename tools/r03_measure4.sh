@@ -4,11 +4,9 @@
 # limit; the script stops at the first failure.
 mkdir -p gpurun_out/m4
 export TMPDIR=/tmp
-timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+timeout -k 10 300 python -u -m pytest tests/test_gpu_combiner.py -x -q --timeout 120 --timeout-method thread \
     > gpurun_out/m4/tests.log 2>&1
 rc=$?; tail -4 gpurun_out/m4/tests.log; [ $rc -ne 0 ] && exit $rc
-timeout -k 10 120 ./microbench/combiner_bench 2 > gpurun_out/m4/combiner.txt 2>&1; rc=$?
-cat gpurun_out/m4/combiner.txt; [ $rc -ne 0 ] && exit $rc
 B="python3 bench.py --no-cpu-baseline"
 for w in stack synthetic; do
   timeout -k 10 200 $B --workload $w > gpurun_out/m4/$w.json 2> gpurun_out/m4/$w.err || exit 1
@@ -34,4 +32,6 @@ timeout -k 10 240 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/m4/kt_sy
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/m4/kt_c2 -o run -- \
     python3 bench.py --no-cpu-baseline --no-prev-variant --steps 50 --ops-per-gpu 4500000 --write-ratio 89 --pool 8 \
     > gpurun_out/m4/kt_c2.json 2>/dev/null || exit 1
+timeout -k 10 150 ./microbench/combiner_bench 2 > gpurun_out/m4/combiner.txt 2>&1; rc=$?
+cat gpurun_out/m4/combiner.txt; [ $rc -ne 0 ] && exit $rc
 echo done
