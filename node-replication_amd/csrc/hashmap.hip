@@ -467,35 +467,69 @@ __device__ __forceinline__ bool resolve(u64 val, u64 st, const ReadJob& j, u64* 
     return true;
 }
 
+// RPT Gets per thread, q = blk * TPB * RPT + r * TPB + tid: every key load and every home-line
+// load of the thread in flight together (fewer blocks: one dispatch wave of read blocks at B1)
+#ifndef NRG_RPT
+#define NRG_RPT 2
+#endif
+constexpr int RPT = NRG_RPT;
+
 __device__ __forceinline__ void read_role(const ReadJob& j, u32 blk, const Slot* table, u32 shift, u64 tmask,
                                           const DevCtl* ctl) {
-    const u64 q = (u64)blk * TPB + threadIdx.x;
-    if (q >= j.R) return;
-    const u64 k = j.keys[q];
     const u32 par = j.epoch & 1;
-    u64 v = 0;
-    bool f = false;
-    if (k == EMPTY_KEY) {
-        if (ctl->sp_claim) f = resolve(ctl->sp.val, ctl->sp.st[par], j, &v);
-    } else {
-        u64 s = table_home(k, shift);
-        for (u64 pr = 0; pr <= tmask; pr++) {
-            // {key, val} and the stamp: two loads of one line, issued together
-            const u64x2 w = *(const u64x2*)&table[s];
-            u64 st = table[s].st[par];
-            u64 kk = w.x, vv = w.y;
-            asm volatile("" : "+v"(kk), "+v"(vv), "+v"(st));
-            if (kk == k) {
-                f = resolve(vv, st, j, &v);
-                break;
-            }
-            if (kk == EMPTY_KEY) break;
-            s = (s + 1) & tmask;
+    const u64 q0 = (u64)blk * TPB * RPT + threadIdx.x;
+    u64 k[RPT], s[RPT];
+    bool on[RPT];
+#pragma unroll
+    for (int r = 0; r < RPT; r++) {
+        const u64 q = q0 + (u64)r * TPB;
+        on[r] = q < j.R;
+        k[r] = on[r] ? j.keys[q] : EMPTY_KEY;
+    }
+    // first probe of every key: {key, val} and the stamp, two loads of one line, all issued together
+    u64x2 w[RPT];
+    u64 st[RPT];
+#pragma unroll
+    for (int r = 0; r < RPT; r++) {
+        s[r] = table_home(k[r], shift);
+        const bool probe = on[r] && k[r] != EMPTY_KEY;
+        w[r].x = EMPTY_KEY;
+        w[r].y = 0;
+        st[r] = 0;
+        if (probe) {
+            w[r] = *(const u64x2*)&table[s[r]];
+            st[r] = table[s[r]].st[par];
         }
     }
-    if (!f) v = 0;
-    j.vals[q] = v;
-    j.found[q] = f ? 1 : 0;
+#pragma unroll
+    for (int r = 0; r < RPT; r++) {
+        if (!on[r]) continue;
+        u64 v = 0;
+        bool f = false;
+        if (k[r] == EMPTY_KEY) {
+            if (ctl->sp_claim) f = resolve(ctl->sp.val, ctl->sp.st[par], j, &v);
+        } else {
+            u64 kk = w[r].x, vv = w[r].y, stt = st[r], sl = s[r];
+            asm volatile("" : "+v"(kk), "+v"(vv), "+v"(stt));
+            for (u64 pr = 0; pr <= tmask; pr++) {
+                if (kk == k[r]) {
+                    f = resolve(vv, stt, j, &v);
+                    break;
+                }
+                if (kk == EMPTY_KEY) break;
+                sl = (sl + 1) & tmask;
+                const u64x2 x = *(const u64x2*)&table[sl];
+                stt = table[sl].st[par];
+                kk = x.x;
+                vv = x.y;
+                asm volatile("" : "+v"(kk), "+v"(vv), "+v"(stt));
+            }
+        }
+        if (!f) v = 0;
+        const u64 q = q0 + (u64)r * TPB;
+        j.vals[q] = v;
+        j.found[q] = f ? 1 : 0;
+    }
 }
 
 // index-role kinds of a round launch
@@ -1295,7 +1329,7 @@ static void launch_round(nrg_ctx* c, const Launch& L, u32 blocks, unsigned lds) 
 }
 
 static hipError_t launch(nrg_ctx* c, Launch& L) {
-    L.rj.nblocks = (u32)((L.rj.R + TPB - 1) / TPB);
+    L.rj.nblocks = (u32)((L.rj.R + TPB * RPT - 1) / (TPB * RPT));
     const u32 nix = L.ix == IX_STAMP ? L.sj.nblocks : L.ij.nblocks;
     u32 blocks = nix + L.aj.nblocks + L.rj.nblocks;
     if (blocks == 0) return hipSuccess;

@@ -22,7 +22,8 @@ timeout -k 10 900 python3 tools/sweep.py \
   'w50_stamp||--write-ratio 50 --knob SORT_MIN=0' 'w50_sorted||--write-ratio 50 --knob SORT_MIN=1' \
   'c2_stamp||--ops-per-gpu 4500000 --write-ratio 89 --knob SORT_MIN=0 --pool 16' \
   'c2_sorted||--ops-per-gpu 4500000 --write-ratio 89 --knob SORT_MIN=1 --pool 16' \
-  'b1_sorted||--knob SORT_MIN=1' \
+  'b1_sorted||--knob SORT_MIN=1' 'b1_rpt2||' 'b1_rpt1|NRGPU_LIB=node-replication_amd/lib/libnrgpu_rpt1.so|' \
+  'r100_rpt2||--write-ratio 0' 'r100_rpt1|NRGPU_LIB=node-replication_amd/lib/libnrgpu_rpt1.so|--write-ratio 0' \
   > gpurun_out/m4/sweep.txt 2>&1
 rc=$?; cat gpurun_out/m4/sweep.txt; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/m4/kt_stack -o run -- \
