@@ -8,6 +8,8 @@
 // Build: g++ -O2 -std=c++17 -pthread microbench/combiner_bench.cpp -o microbench/combiner_bench \
 //            -Lnode-replication_amd/lib -lnrgpu -Wl,-rpath,$ORIGIN/../node-replication_amd/lib
 // Run:   ./microbench/combiner_bench [seconds]
+#include <sched.h>
+
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -97,8 +99,23 @@ static int run(int threads, int batch, double secs, bool stack) {
     return err.load();
 }
 
+static void show_cpus() {  // what the host gives this process: affinity and cgroup CPU quota
+    cpu_set_t set;
+    const int aff = sched_getaffinity(0, sizeof(set), &set) == 0 ? CPU_COUNT(&set) : -1;
+    char q[64] = "none";
+    const char* files[] = {"/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"};
+    for (const char* fn : files)
+        if (FILE* f = std::fopen(fn, "r")) {
+            if (!std::fgets(q, sizeof(q), f)) q[0] = 0;
+            std::fclose(f);
+            break;
+        }
+    std::printf("cpus: hardware %u affinity %d cgroup quota %s\n", std::thread::hardware_concurrency(), aff, q);
+}
+
 int main(int argc, char** argv) {
     const double secs = argc > 1 ? std::atof(argv[1]) : 2.0;
+    show_cpus();
     const int cases[][3] = {{8, 1, 0},   {8, 32, 0},  {64, 1, 0}, {64, 32, 0},
                             {128, 32, 0}, {256, 32, 0}, {64, 32, 1}, {256, 32, 1}};
     for (auto& c : cases)

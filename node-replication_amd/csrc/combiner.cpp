@@ -35,7 +35,10 @@
 #include <time.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <thread>
@@ -57,12 +60,29 @@ void futex_wait(std::atomic<uint32_t>* w, uint32_t seen) {
 }
 void futex_wake_all(std::atomic<uint32_t>* w) { syscall(SYS_futex, (uint32_t*)w, FUTEX_WAKE_PRIVATE, INT32_MAX, nullptr, nullptr, 0); }
 
-// CPUs this process may run on (the GPU box gives a job a share of a larger host)
+// CPUs this process may keep busy: its affinity mask, capped by a cgroup CPU quota (a job given a
+// share of a larger host sees every CPU but is throttled for a whole period once spinning threads
+// have burnt the quota)
 uint32_t cpus_allowed() {
     cpu_set_t set;
-    if (sched_getaffinity(0, sizeof(set), &set) == 0) return (uint32_t)CPU_COUNT(&set);
-    const unsigned n = std::thread::hardware_concurrency();
-    return n ? n : 1;
+    uint32_t n = 0;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) n = (uint32_t)CPU_COUNT(&set);
+    if (!n) n = std::max(1u, std::thread::hardware_concurrency());
+    double quota = -1, period = 0;
+    if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {  // cgroup v2: "<quota|max> <period>"
+        char q[32] = {0};
+        if (std::fscanf(f, "%31s %lf", q, &period) == 2 && std::strcmp(q, "max")) quota = std::atof(q);
+        std::fclose(f);
+    } else if (FILE* g = std::fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r")) {  // cgroup v1
+        if (std::fscanf(g, "%lf", &quota) != 1) quota = -1;
+        std::fclose(g);
+        if (FILE* h = std::fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r")) {
+            if (std::fscanf(h, "%lf", &period) != 1) period = 0;
+            std::fclose(h);
+        }
+    }
+    if (quota > 0 && period > 0) n = std::min(n, std::max(1u, (uint32_t)(quota / period)));
+    return n;
 }
 
 struct alignas(64) Batch {
@@ -126,7 +146,8 @@ struct nrg_combiner {
     alignas(64) std::atomic<uint64_t> completed{0};  // rounds < completed are done
     std::atomic<uint64_t> launched{0};               // rounds < launched are enqueued (combiner thread)
     std::atomic<uint64_t> rounds{0}, ops{0};
-    uint32_t cpus = 1;                               // clients spin longer while fewer than this
+    int32_t spin_cap = 0;                            // clients that may spin at once
+    alignas(64) std::atomic<int32_t> spinning{0};
     // the combiner thread
     std::thread worker;
     std::atomic<bool> stop{false};
@@ -301,11 +322,12 @@ int post_and_wait(nrg_combiner* m, uint32_t token, bool write, const void* ops, 
         m->work.fetch_add(1, std::memory_order_seq_cst);
         syscall(SYS_futex, (uint32_t*)&m->work, FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
     }
-    // spin, then park on the batch's futex: spin long (about a round) while the clients fit the
-    // cores, briefly when they do not
-    const uint32_t spin_rounds = m->next_tok.load(std::memory_order_relaxed) < m->cpus ? 2048 : 32;
+    // wait for the round: spin (about a round) if a spinning slot is free -- at most the cores
+    // the process may keep busy, less the combiner thread's -- else park on the batch's futex
+    const bool spin = m->spinning.fetch_add(1, std::memory_order_relaxed) < m->spin_cap;
+    if (!spin) m->spinning.fetch_sub(1, std::memory_order_relaxed);
     for (uint32_t spins = 0; m->completed.load(std::memory_order_acquire) <= k; spins++) {
-        if (spins < spin_rounds) {
+        if (spin && spins < 4096) {
             for (int i = 0; i < 8; i++) _mm_pause();
             continue;
         }
@@ -314,6 +336,7 @@ int post_and_wait(nrg_combiner* m, uint32_t token, bool write, const void* ops, 
         if (m->completed.load(std::memory_order_seq_cst) <= k) futex_wait(&x->wake, seen);
         x->sleepers.fetch_sub(1, std::memory_order_seq_cst);
     }
+    if (spin) m->spinning.fetch_sub(1, std::memory_order_relaxed);
     std::memcpy(out, (write ? x->wresp : x->rresp) + (uint64_t)off * out_b, (size_t)n * out_b);
     std::memcpy(some, (write ? x->wsome : x->rsome) + off, n);
     const int rc = x->rc;
@@ -364,7 +387,7 @@ extern "C" int nrg_combiner_open(nrg_ctx* ctx, uint32_t max_threads, nrg_combine
     }
     m->saved_pipeline = ctx->pipeline;
     ctx->pipeline = false;
-    m->cpus = cpus_allowed();
+    m->spin_cap = (int32_t)cpus_allowed() - 2;
     m->b[0].round.store(0);
     m->b[0].state.store(OPEN);
     try {

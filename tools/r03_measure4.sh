@@ -26,13 +26,10 @@ timeout -k 10 900 python3 tools/sweep.py \
   'r100_rpt2||--write-ratio 0' 'r100_rpt1|NRGPU_LIB=node-replication_amd/lib/libnrgpu_rpt1.so|--write-ratio 0' \
   > gpurun_out/m4/sweep.txt 2>&1
 rc=$?; cat gpurun_out/m4/sweep.txt; [ $rc -ne 0 ] && exit $rc
-timeout -k 10 240 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/m4/kt_stack -o run -- \
-    python3 bench.py --no-cpu-baseline --workload stack --steps 200 > gpurun_out/m4/kt_stack.json 2>/dev/null || exit 1
-timeout -k 10 240 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/m4/kt_synth -o run -- \
-    python3 bench.py --no-cpu-baseline --workload synthetic --steps 200 > gpurun_out/m4/kt_synth.json 2>/dev/null || exit 1
-timeout -k 10 240 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/m4/kt_c2 -o run -- \
-    python3 bench.py --no-cpu-baseline --no-prev-variant --steps 50 --ops-per-gpu 4500000 --write-ratio 89 --pool 8 \
-    > gpurun_out/m4/kt_c2.json 2>/dev/null || exit 1
+P="--steps 200"
+bash tools/profile.sh r03_stack --workload stack $P && bash tools/profile.sh r03_synth --workload synthetic $P || exit 1
+C="--steps 50 --ops-per-gpu 4500000 --write-ratio 89 --pool 8"
+bash tools/profile.sh r03_c2_sorted $C && bash tools/profile.sh r03_c2_stamp $C --knob SORT_MIN=0 || exit 1
 timeout -k 10 150 ./microbench/combiner_bench 2 > gpurun_out/m4/combiner.txt 2>&1; rc=$?
 cat gpurun_out/m4/combiner.txt; [ $rc -ne 0 ] && exit $rc
 echo done
