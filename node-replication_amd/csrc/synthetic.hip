@@ -230,6 +230,9 @@ constexpr u32 SY_MAX_NB = 512, SY_MAX_HOT = 16, SY_MAX_TILES = 4096, SY_MAX_CW =
 #ifndef NRG_SYB_PER
 #define NRG_SYB_PER 8  // 1M-op rounds: 4 -> 63.2 us, 8 -> 62.4 us, 12 -> 100.5 us (VGPR cap)
 #endif
+#ifndef NRG_SYB_XCD
+#define NRG_SYB_XCD 1  // 0: bucket = blockIdx.x (A/B builds)
+#endif
 constexpr int SYB_TPB = 512, SYB_WAVES = SYB_TPB / 64, SYB_PER = NRG_SYB_PER;
 constexpr u32 SYB_PASS = SYB_TPB * SYB_PER;  // touches per pass of a bucket workgroup
 constexpr int SYC_TPB = 512;
@@ -539,7 +542,10 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
     u32* s_pre = s_dyn;
     unsigned short* s_off = (unsigned short*)(s_dyn + ntiles + 1);
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    const u32 b = blockIdx.x;
+    // buckets in contiguous runs per XCD (workgroups go to XCDs round-robin): neighbouring
+    // buckets share the lines at their segments' edges in E and V, and those stay in one L2
+    const u32 nxcd = NRG_SYB_XCD ? 8 : 1, q = gridDim.x / nxcd, rem = gridDim.x % nxcd, xcd = blockIdx.x % nxcd;
+    const u32 b = xcd * q + (xcd < rem ? xcd : rem) + blockIdx.x / nxcd;
     const u64 w0 = b ? (u64)HR + 1 + (u64)(b - 1) * W : (u64)HR;  // bucket 0: cold word 0 alone
     const u32 nw = b ? W : 1u;
     for (u32 t = tid; t < ntiles; t += SYB_TPB) {

@@ -24,6 +24,7 @@ timeout -k 10 900 python3 tools/sweep.py \
   'c2_sorted||--ops-per-gpu 4500000 --write-ratio 89 --knob SORT_MIN=1 --pool 16' \
   'b1_sorted||--knob SORT_MIN=1' 'b1_rpt2||' 'b1_rpt1|NRGPU_LIB=node-replication_amd/lib/libnrgpu_rpt1.so|' \
   'r100_rpt2||--write-ratio 0' 'r100_rpt1|NRGPU_LIB=node-replication_amd/lib/libnrgpu_rpt1.so|--write-ratio 0' \
+  'sy_xcd||--workload synthetic' 'sy_noxcd|NRGPU_LIB=node-replication_amd/lib/libnrgpu_noremap.so|--workload synthetic' \
   > gpurun_out/m4/sweep.txt 2>&1
 rc=$?; cat gpurun_out/m4/sweep.txt; [ $rc -ne 0 ] && exit $rc
 P="--steps 200"
