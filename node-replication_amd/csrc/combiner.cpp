@@ -93,6 +93,7 @@ struct alignas(64) Batch {
     std::atomic<uint32_t> nw{0}, nr{0};            // write records / reads reserved
     alignas(64) std::atomic<uint32_t> wake{0};     // futex word: bumped when the round completes
     std::atomic<uint32_t> sleepers{0};             // clients parked on it
+    std::atomic<uint32_t> bcast{0};                // a client has woken the parked ones
     int rc = NRG_OK;                               // launch or device error of the round
     // host buffers (mapped, coherent; device addresses equal the host ones under UVA)
     char* recs = nullptr;   // cap write records
@@ -186,7 +187,9 @@ void retire(nrg_combiner* m) {
         x.state.store(DONE, std::memory_order_release);
         m->completed.store(++k, std::memory_order_seq_cst);
         x.wake.fetch_add(1, std::memory_order_seq_cst);
-        if (x.sleepers.load(std::memory_order_seq_cst)) futex_wake_all(&x.wake);
+        // one parked client only: waking the rest is that client's job, off this thread's path
+        if (x.sleepers.load(std::memory_order_seq_cst))
+            syscall(SYS_futex, (uint32_t*)&x.wake, FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
     }
 }
 
@@ -246,6 +249,7 @@ bool advance(nrg_combiner* m) {
     y.nw.store(0, std::memory_order_relaxed);
     y.nr.store(0, std::memory_order_relaxed);
     y.rc = NRG_OK;
+    y.bcast.store(0, std::memory_order_relaxed);
     y.round.store(k + 1, std::memory_order_relaxed);
     y.state.store(OPEN, std::memory_order_seq_cst);
     m->open.store(k + 1, std::memory_order_seq_cst);
@@ -337,6 +341,9 @@ int post_and_wait(nrg_combiner* m, uint32_t token, bool write, const void* ops, 
         x->sleepers.fetch_sub(1, std::memory_order_seq_cst);
     }
     if (spin) m->spinning.fetch_sub(1, std::memory_order_relaxed);
+    // the first client past the wait wakes the batch's other parked clients
+    if (x->sleepers.load(std::memory_order_seq_cst) && !x->bcast.exchange(1, std::memory_order_acq_rel))
+        futex_wake_all(&x->wake);
     std::memcpy(out, (write ? x->wresp : x->rresp) + (uint64_t)off * out_b, (size_t)n * out_b);
     std::memcpy(some, (write ? x->wsome : x->rsome) + off, n);
     const int rc = x->rc;
