@@ -677,7 +677,8 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
             }
             for (int ww = 0; ww < SYB_WAVES; ww++) {
                 if (ww == w) {
-#pragma unroll
+                    // not unrolled: unrolled inside the wave loop, the ranking spills ~900 B/lane
+#pragma unroll 1
                     for (int q = 0; q < SYB_PER; q++) {
                         const u32 i = base + (u32)w * (SYB_PER * 64) + q * 64 + lane;
                         const bool valid = i < total;
