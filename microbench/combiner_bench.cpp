@@ -7,13 +7,15 @@
 // The stack cases (benches/stack.rs: 50/50 push/pop, 50,000 initial elements) follow.
 // Build: g++ -O2 -std=c++17 -pthread microbench/combiner_bench.cpp -o microbench/combiner_bench \
 //            -Lnode-replication_amd/lib -lnrgpu -Wl,-rpath,$ORIGIN/../node-replication_amd/lib
-// Run:   ./microbench/combiner_bench [seconds]
+// Run:   ./microbench/combiner_bench [seconds [threads ops/call kind(0 hashmap, 1 stack)] ...]
 #include <sched.h>
 
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <thread>
 #include <vector>
 
@@ -99,6 +101,27 @@ static int run(int threads, int batch, double secs, bool stack) {
     return err.load();
 }
 
+// cgroup v2 cpu.stat: CPU time used and how often the group's quota throttled it
+struct Throttle {
+    bool ok = false;
+    unsigned long long usage_us = 0, nr_periods = 0, nr_throttled = 0, throttled_us = 0;
+};
+static Throttle throttle() {
+    Throttle t;
+    FILE* f = std::fopen("/sys/fs/cgroup/cpu.stat", "r");
+    if (!f) return t;
+    char k[64];
+    unsigned long long v;
+    while (std::fscanf(f, "%63s %llu", k, &v) == 2) {
+        if (!std::strcmp(k, "usage_usec")) t.usage_us = v, t.ok = true;
+        if (!std::strcmp(k, "nr_periods")) t.nr_periods = v;
+        if (!std::strcmp(k, "nr_throttled")) t.nr_throttled = v;
+        if (!std::strcmp(k, "throttled_usec")) t.throttled_us = v;
+    }
+    std::fclose(f);
+    return t;
+}
+
 static void show_cpus() {  // what the host gives this process: affinity and cgroup CPU quota
     cpu_set_t set;
     const int aff = sched_getaffinity(0, sizeof(set), &set) == 0 ? CPU_COUNT(&set) : -1;
@@ -114,14 +137,27 @@ static void show_cpus() {  // what the host gives this process: affinity and cgr
 }
 
 int main(int argc, char** argv) {
+    // combiner_bench [seconds [threads ops/call kind] ...]  (kind 0 hashmap, 1 stack); without
+    // cases: the default set
     const double secs = argc > 1 ? std::atof(argv[1]) : 2.0;
     show_cpus();
-    const int cases[][3] = {{8, 1, 0},   {8, 32, 0},  {64, 1, 0}, {64, 32, 0},
-                            {128, 32, 0}, {256, 32, 0}, {64, 32, 1}, {256, 32, 1}};
-    for (auto& c : cases)
+    std::vector<std::array<int, 3>> cases = {{8, 1, 0},    {8, 32, 0},   {16, 32, 0}, {64, 1, 0}, {64, 32, 0},
+                                             {128, 32, 0}, {256, 32, 0}, {16, 32, 1}, {64, 32, 1}, {256, 32, 1}};
+    if (argc > 4) {
+        cases.clear();
+        for (int i = 2; i + 2 < argc; i += 3) cases.push_back({std::atoi(argv[i]), std::atoi(argv[i + 1]), std::atoi(argv[i + 2])});
+    }
+    for (auto& c : cases) {
+        const Throttle t0 = throttle();
         if (int r = run(c[0], c[1], secs, c[2] != 0)) {
             std::printf("error %d (%s)\n", r, nrg_strerror(r));
             return 1;
         }
+        const Throttle t1 = throttle();
+        if (t0.ok && t1.ok)
+            std::printf("        cgroup: throttled %llu of %llu periods, %.1f ms throttled, %.2f CPU-s used\n",
+                        (unsigned long long)(t1.nr_throttled - t0.nr_throttled), (unsigned long long)(t1.nr_periods - t0.nr_periods),
+                        (t1.throttled_us - t0.throttled_us) / 1e3, (t1.usage_us - t0.usage_us) / 1e6);
+    }
     return 0;
 }

@@ -233,6 +233,11 @@ constexpr u32 SY_MAX_NB = 512, SY_MAX_HOT = 16, SY_MAX_TILES = 4096, SY_MAX_CW =
 #ifndef NRG_SYB_XCD
 #define NRG_SYB_XCD 1  // 0: bucket = blockIdx.x (A/B builds)
 #endif
+#ifndef NRG_SY_BALLOT
+// 1: per-wave rankings by matching the key bit by bit with ballots (A/B builds). Measured slower
+// than the LDS peer masks: 75.7-76.0 vs 61.1-61.9 us per 1M-op round (profiles/r03_synth_rank_ab.txt)
+#define NRG_SY_BALLOT 0
+#endif
 constexpr int SYB_TPB = 512, SYB_WAVES = SYB_TPB / 64, SYB_PER = NRG_SYB_PER;
 constexpr u32 SYB_PASS = SYB_TPB * SYB_PER;  // touches per pass of a bucket workgroup
 constexpr int SYC_TPB = 512;
@@ -313,6 +318,30 @@ __device__ __forceinline__ u32 wave_rank_bits(bool on, u32 key, int lane, CNT* c
     return c0 + (u32)__popcll(peers & ((1ull << lane) - 1));
 }
 
+// Stable ranking of one wave round in a wave-private (mask, count) table: every lane with a
+// key ORs its bit into mask[key]; the mask read back is the set of lanes with that key. Returns
+// count[key] + the number of lower lanes with the same key; the highest such lane advances count
+// and clears mask. (NRG_SY_BALLOT=0 builds; three LDS round trips per ranking)
+template <typename CNT>
+__device__ __forceinline__ u32 wave_rank_mask(bool on, u32 key, int lane, u64* mask, CNT* count, u64* peers_out) {
+    if (on) atomicOr((unsigned long long*)&mask[key], 1ull << lane);
+    wave_lds_sync();
+    u64 peers = 0;
+    u32 c0 = 0;
+    if (on) {
+        peers = mask[key];
+        c0 = count[key];
+    }
+    wave_lds_sync();
+    if (on && 63 - __clzll(peers) == lane) {
+        mask[key] = 0;
+        count[key] = (CNT)(c0 + (u32)__popcll(peers));
+    }
+    wave_lds_sync();
+    *peers_out = peers;
+    return c0 + (u32)__popcll(peers & ((1ull << lane) - 1));
+}
+
 // Arguments of the partition pass of chunk e and of the sums of chunk e-1, which share a launch.
 struct SyPartArgs {
     const nrg_synth_op* src;  // the chunk's ops in a caller buffer, or nullptr (ring)
@@ -348,6 +377,9 @@ struct SyPartLds {
     unsigned short wcnt[SYA_WAVES][SY_MAX_NB];
     union {
         struct {
+#if !NRG_SY_BALLOT
+            u64 mask[SYA_WAVES][SY_MAX_NB];
+#endif
             u32 words[SYA_WAVES][64 * CW];
         } r;
         u32 stage[SYA_OPS * CW];
@@ -376,6 +408,9 @@ __device__ __forceinline__ void sy_part_role(const SyPartArgs& A, u32 tile, SyPa
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const u64 op0 = (u64)tile * SYA_OPS;
     for (u32 i = tid; i < SYA_WAVES * SY_MAX_NB / 2; i += SYA_TPB) ((u32*)&s_wcnt[0][0])[i] = 0;
+#if !NRG_SY_BALLOT
+    for (u32 i = tid; i < SYA_WAVES * SY_MAX_NB; i += SYA_TPB) (&s_u.r.mask[0][0])[i] = 0;
+#endif
     if (lane < SY_MAX_HOT) s_hot[w][lane] = SyHot{0, 0, 0};
     __syncthreads();
     u32 xs[SYA_OROUNDS * CW];
@@ -457,7 +492,11 @@ __device__ __forceinline__ void sy_part_role(const SyPartArgs& A, u32 tile, SyPa
 #pragma unroll
         for (int r = 0; r < CW; r++) {
             u64 peers;
+#if NRG_SY_BALLOT
             const u32 rank = wave_rank_bits<9>(vw[r] != NOTOUCH, bw[r], lane, s_wcnt[w], &peers);
+#else
+            const u32 rank = wave_rank_mask(vw[r] != NOTOUCH, bw[r], lane, s_u.r.mask[w], s_wcnt[w], &peers);
+#endif
             xs[orr * CW + r] = vw[r];
             pk[orr * CW + r] = (bw[r] << 16) | rank;
         }
@@ -537,6 +576,9 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
     extern __shared__ u32 s_dyn[];  // s_pre[ntiles + 1], s_off[ntiles] (u16)
     __shared__ u64 s_cur[SYB_WORDS];
     __shared__ u32 s_wc[SYB_WAVES][SYB_WORDS];
+#if !NRG_SY_BALLOT
+    __shared__ u64 s_mk[SYB_WAVES][SYB_WORDS];
+#endif
     __shared__ unsigned short s_tile[2][SYB_PASS];  // tile of every touch of a pass (double buffered)
     __shared__ u32 s_part[SYB_WAVES];
     u32* s_pre = s_dyn;
@@ -555,6 +597,9 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
     }
     for (u32 i = tid; i < SYB_WORDS; i += SYB_TPB) s_cur[i] = i < nw && w0 + i < N ? words[w0 + i] : 0ull;
     for (u32 i = tid; i < SYB_WAVES * SYB_WORDS; i += SYB_TPB) (&s_wc[0][0])[i] = 0;
+#if !NRG_SY_BALLOT
+    for (u32 i = tid; i < SYB_WAVES * SYB_WORDS; i += SYB_TPB) (&s_mk[0][0])[i] = 0;
+#endif
     __syncthreads();
     SY_MARK(1);
     // exclusive scan of the per-tile counts: thread owns tiles [tid*K, tid*K + K)
@@ -643,7 +688,11 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
                 for (int q = 0; q < SYB_PER; q++) {
                     const u32 i = base + (u32)w * (SYB_PER * 64) + q * 64 + lane;
                     u64 peers;
+#if NRG_SY_BALLOT
                     sv[q] = wave_rank_bits<SYB_SHIFT>(i < total, ent_word(ent[q]), lane, s_wc[w], &peers);
+#else
+                    sv[q] = wave_rank_mask(i < total, ent_word(ent[q]), lane, s_mk[w], s_wc[w], &peers);
+#endif
                 }
             }
             __syncthreads();
@@ -685,7 +734,11 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
                         const u32 xl = ent_word(ent[q]);
                         const bool isset = valid && ent_set(ent[q]);
                         u64 peers;
+#if NRG_SY_BALLOT
                         (void)wave_rank_bits<SYB_SHIFT>(valid, xl, lane, s_wc[w], &peers);
+#else
+                        (void)wave_rank_mask(valid, xl, lane, s_mk[w], s_wc[w], &peers);
+#endif
                         const u64 P = peers & ((1ull << lane) - 1);
                         const u64 S = __ballot(isset) & P;
                         const int sl = S ? 63 - __clzll(S) : lane;

@@ -88,7 +88,7 @@ def test_group_hashmap_members(nrg, orc, G, pipeline, max_batch, sort_min):
     cfg.log_bytes = 64 * (1 << 16)
     g, ctxs = _open(L, lib, G, cfg)
     for c in ctxs:
-        L.check(lib.nrg_test_set_knob(c, L.KNOBS["SORT_MIN"], sort_min if sort_min else 1 << 19))
+        L.check(lib.nrg_test_set_knob(c, L.KNOBS["SORT_MIN"], sort_min))
     for c in ctxs:
         L.check(lib.nrg_hashmap_prefill_range(c, 4000, 1))
     om = orc.HashMap()
