@@ -679,8 +679,10 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
         if (!anyset) {
             if (b == 0) {  // one word: a touch's rank in its wave is its position there
                 const u32 w0i = base + (u32)w * (SYB_PER * 64);
+                u32 l = (u32)lane;
+                asm volatile("" : "+v"(l));  // computed per pass: hoisted, these 8 constants spilled
 #pragma unroll
-                for (int q = 0; q < SYB_PER; q++) sv[q] = (u64)(q * 64 + lane);
+                for (int q = 0; q < SYB_PER; q++) sv[q] = (u64)(q * 64 + l);
                 if (lane == 0)
                     s_wc[w][0] = total > w0i ? (total - w0i < SYB_PER * 64 ? total - w0i : SYB_PER * 64) : 0u;
             } else {
@@ -726,8 +728,12 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
             }
             for (int ww = 0; ww < SYB_WAVES; ww++) {
                 if (ww == w) {
-                    // not unrolled: unrolled inside the wave loop, the ranking spills ~900 B/lane
+#if NRG_SY_BALLOT
+                    // not unrolled: unrolled inside the wave loop, the ballot ranking spills ~900 B/lane
 #pragma unroll 1
+#else
+#pragma unroll
+#endif
                     for (int q = 0; q < SYB_PER; q++) {
                         const u32 i = base + (u32)w * (SYB_PER * 64) + q * 64 + lane;
                         const bool valid = i < total;
