@@ -17,7 +17,8 @@ import nrgpu  # noqa: E402
 from nrgpu import _lib as L  # noqa: E402
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
-dev = nrgpu.DeviceReplica(L.NRG_DS_SYNTHETIC, 0, knobs={"EXP": 2}, max_batch=N, log_bytes=64 * 4 * max(N, 8192))
+dev = nrgpu.DeviceReplica(L.NRG_DS_SYNTHETIC, 0, knobs={"EXP": 2}, max_batch=N, log_bytes=64 * 4 * max(N, 8192),
+                           pipeline=1)  # as bench.py: the sums of round e-1 ride in round e's partition launch
 dev.use_torch_stream()
 g = torch.Generator(device="cuda")
 g.manual_seed(7)
@@ -33,21 +34,41 @@ W = -(-(SPAN - 1) // 511)
 NB = 1 + -(-(SPAN - 1) // W)  # bucket 0: cold word 0 alone
 R = 20
 acc = np.zeros((NB, 9))
+T = -(-N // 2048)  # partition tiles (synthetic.hip SYA_OPS)
+pacc = np.zeros((T, 5))
+sacc = np.zeros((T, 3))
 hw = None
 for r in range(R + 3):
     dev.sy_round_device(ops, N, 1, resp, some)
     torch.cuda.synchronize()
-    buf = np.zeros(NB * 16, np.uint64)
-    L.check(L.load().nrg_test_debug_read(dev.handle, buf.ctypes.data_as(C.c_void_p), NB * 16))
-    t = buf.reshape(NB, 16)[:, :9].astype(np.float64)
-    t0 = t[:, 0].min()
+    buf = np.zeros(3072 * 16, np.uint64)  # synthetic.hip SY_DBG_ROWS
+    L.check(L.load().nrg_test_debug_read(dev.handle, buf.ctypes.data_as(C.c_void_p), buf.size))
+    rows = buf.reshape(3072, 16)
+    t = rows[:NB, :9].astype(np.float64)
+    pt = rows[1024:1024 + T, :5].astype(np.float64)  # this round's partition tiles
+    st = rows[2048:2048 + T, :3].astype(np.float64)  # the previous round's sums (same launch)
+    t0 = pt[:, 0].min()  # the round's launch starts with the partition
     for k in (0, 1, 2, 7):
         t[:, k] -= t0
+    pt -= t0
+    st -= t0
     if r >= 3:
         acc += t
+        pacc += pt
+        sacc += st
     if r == R + 2:
-        hw = buf.reshape(NB, 16)[:, 9:12].astype(np.int64)
+        hw = rows[:NB, 9:12].astype(np.int64)
 acc /= R
+pacc /= R
+sacc /= R
+print(f"partition tiles {T}: start {pacc[:, 0].min() / 100:.2f}..{pacc[:, 0].max() / 100:.2f} us, last end {pacc[:, 4].max() / 100:.2f} us")
+for nm, d in [("load+rank", pacc[:, 1] - pacc[:, 0]), ("offsets", pacc[:, 2] - pacc[:, 1]), ("stage LDS", pacc[:, 3] - pacc[:, 2]),
+              ("E stores", pacc[:, 4] - pacc[:, 3]), ("tile span", pacc[:, 4] - pacc[:, 0])]:
+    print(f"  {nm:12s} mean {d.mean() / 100:7.2f} us  max {d.max() / 100:7.2f} us")
+print(f"sum workgroups (previous round) start {sacc[:, 0].min() / 100:.2f}..{sacc[:, 0].max() / 100:.2f} us, last end {sacc[:, 2].max() / 100:.2f} us")
+for nm, d in [("atomics", sacc[:, 1] - sacc[:, 0]), ("responses", sacc[:, 2] - sacc[:, 1])]:
+    print(f"  {nm:12s} mean {d.mean() / 100:7.2f} us  max {d.max() / 100:7.2f} us")
+print(f"bucket pass starts {acc[:, 0].min() / 100:.2f} us after the partition launch started")
 print(f"N={N} buckets={NB} passes={acc[:, 8].mean():.2f}: start spread {acc[:, 0].min() / 100:.2f}..{acc[:, 0].max() / 100:.2f} us")
 for nm, d in [("prologue", acc[:, 1] - acc[:, 0]), ("count scan", acc[:, 2] - acc[:, 1]), ("map+issue", acc[:, 3]),
               ("gather wait", acc[:, 4]), ("rank+place", acc[:, 5]), ("V stores", acc[:, 6])]:

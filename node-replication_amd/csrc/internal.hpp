@@ -126,6 +126,7 @@ struct nrg_ctx {
     uint32_t st_par = 0;      // stack: buffer parity of the next chunk
     nrg::SyDeferred sy_pend;  // synthetic: the last chunk's sums, if deferred
     uint32_t sy_par = 0;      // synthetic: buffer parity of the next chunk
+    uint32_t sy_round = 0;    // synthetic: chunks replayed (the epoch of the 32-bit seen-value test)
     uint64_t* d_created = nullptr;  // [HM_CREATED_SLOTS] keys created by replay rounds
     void* d_bk_ent = nullptr;       // [index tiles][tile] 16-B {id << 32 | i+1, value}
     uint64_t* d_bk_key = nullptr;   // [index tiles][tile] key of each entry
@@ -247,5 +248,6 @@ hipError_t sy_replay_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 resp_hi, 
 hipError_t sy_read(nrg_ctx* c, const nrg_synth_rd* d_ops, u64 n, u64* d_sums);
 bool sy_bucket_eligible(const nrg_config& cf);  // configs the sort-free bucket replay handles
 u64 sy_bucket_aux_bytes(const nrg_config& cf);  // size of nrg_ctx::d_sy_aux
+hipError_t sy_aux_init(nrg_ctx* c);              // after (re)allocating d_sy_aux
 hipError_t sy_maxscan(nrg_ctx* c, const u32* sk, const u32* sv, u64 n, u32* M);
 }  // namespace nrg

@@ -381,7 +381,10 @@ int nrg_open(int dev, const nrg_config* cfg_in, nrg_ctx** out) {
         if (sort_alloc(c->sort, mb * T) != NRG_OK) { nrg_close(c); return NRG_E_NOMEM; }
         // sort-free bucket replay where the config allows it (the sort path stays for the rest;
         // nrg_test_set_knob(NRG_KNOB_SY_SORT) forces it for tests)
-        if (sy_bucket_eligible(cf)) OPEN_CHK(hipMalloc(&c->d_sy_aux, sy_bucket_aux_bytes(cf)));
+        if (sy_bucket_eligible(cf)) {
+            OPEN_CHK(hipMalloc(&c->d_sy_aux, sy_bucket_aux_bytes(cf)));
+            OPEN_CHK(sy_aux_init(c));
+        }
         c->pipeline = cf.pipeline != 0;
         OPEN_CHK(sy_init(c));
     }
@@ -1115,12 +1118,12 @@ extern "C" int nrg_test_set_knob(nrg_ctx* c, int knob, uint64_t v) {
             if (v > 0xFFFFFFFFull) return NRG_E_INVAL;
             c->exp = (uint32_t)v;
             // timestamp buffer: hashmap elector blocks, stack tiles (+ finish workgroups at 128..),
-            // synthetic buckets (<= 1024); 16 words each
+            // synthetic buckets (<= 1024), partition tiles and sum workgroups; 16 words each
             uint64_t words = 0;
             if (hm && (c->exp & 0x10000)) words = (uint64_t)HM_BK_MAX * 16;
             if (c->cfg.ds_kind == NRG_DS_STACK && (c->exp & 2))
                 words = std::max<uint64_t>(256, (c->cfg.max_batch + 2047) / 2048) * 16;
-            if (sy && (c->exp & 2)) words = 1024 * 16;
+            if (sy && (c->exp & 2)) words = 3072 * 16;  // synthetic.hip SY_DBG_ROWS
             if (words > c->dbg_words) {
                 if (c->d_dbg) HIPCHK(hipFree(c->d_dbg));
                 c->d_dbg = nullptr;
@@ -1138,6 +1141,7 @@ extern "C" int nrg_test_set_knob(nrg_ctx* c, int knob, uint64_t v) {
                 c->d_sy_aux = nullptr;
             } else if (!v && !c->d_sy_aux && sy_bucket_eligible(c->cfg)) {
                 HIPCHK(hipMalloc(&c->d_sy_aux, sy_bucket_aux_bytes(c->cfg)));
+                HIPCHK(sy_aux_init(c));
             }
             return NRG_OK;
         case NRG_KNOB_SORT_MIN:

@@ -238,6 +238,10 @@ constexpr u32 SY_MAX_NB = 512, SY_MAX_HOT = 16, SY_MAX_TILES = 4096, SY_MAX_CW =
 // than the LDS peer masks: 75.7-76.0 vs 61.1-61.9 us per 1M-op round (profiles/r03_synth_rank_ab.txt)
 #define NRG_SY_BALLOT 0
 #endif
+#ifndef NRG_SYP_PD
+#define NRG_SYP_PD 1  // partition: wave rounds of op records in flight ahead of the one ranked
+#endif
+constexpr int SYP_PD = NRG_SYP_PD;
 constexpr int SYB_TPB = 512, SYB_WAVES = SYB_TPB / 64, SYB_PER = NRG_SYB_PER;
 constexpr u32 SYB_PASS = SYB_TPB * SYB_PER;  // touches per pass of a bucket workgroup
 constexpr int SYC_TPB = 512;
@@ -342,6 +346,20 @@ __device__ __forceinline__ u32 wave_rank_mask(bool on, u32 key, int lane, u64* m
     return c0 + (u32)__popcll(peers & ((1ull << lane) - 1));
 }
 
+// 32-bit seen values. Every cold touch's seen value is < 2^32 when, at the chunk's start, every
+// word is < 2^31 and no WriteOnly of the chunk writes a tid >= 2^31 (a seen value is a word's or
+// a SET's value plus fewer than 2^31 touches). The bucket pass then stores 4-B seen values (half
+// the V traffic of the bucket pass and of the sums). Device-side, per chunk epoch e:
+//   big[e & 1] = e   written by any bucket workgroup whose words end chunk e with a value >= 2^31
+//   set_epoch = e    written by any partition tile holding such a WriteOnly
+//   v32[par]         the bucket pass's decision, read by the chunk's sums
+// Every bucket workgroup decides alike: v32 = big[(e-1) & 1] != e-1 && set_epoch != e.
+struct SyFlags {
+    u32 big[2];
+    u32 set_epoch;
+    u32 v32[2];
+};
+
 // Arguments of the partition pass of chunk e and of the sums of chunk e-1, which share a launch.
 struct SyPartArgs {
     const nrg_synth_op* src;  // the chunk's ops in a caller buffer, or nullptr (ring)
@@ -356,7 +374,13 @@ struct SyPartArgs {
     u32* E;
     u32* cnt_bt;
     SyHot* hot;
+    SyFlags* fl;
+    u32 epoch;
+    u64* dbg;  // NRG_EXP & 2 (diagnostic): phase stamps of tile t in row SY_DBG_PART + t
 };
+// rows of the diagnostic stamp buffer: bucket b in row b, partition tile t in SY_DBG_PART + t,
+// sum workgroup k in SY_DBG_SUM + k (tiles beyond 1024 are not stamped)
+constexpr u32 SY_DBG_PART = 1024, SY_DBG_SUM = 2048, SY_DBG_ROWS = 3072;
 struct SySumArgs {
     u32 blocks;  // workgroups of the sum role (0: none)
     const u32* E;
@@ -368,6 +392,8 @@ struct SySumArgs {
     const SyHot* hot;
     u32 ntiles, HR, CW;
     u64* words;
+    const u32* v32;  // the chunk's seen-value width flag (SyFlags::v32[par]): 1 = 4-B seen values
+    u64* dbg;
 };
 
 // LDS of a partition workgroup: ranking tables and staged words, then (same bytes) the tile's
@@ -407,26 +433,39 @@ __device__ __forceinline__ void sy_part_role(const SyPartArgs& A, u32 tile, SyPa
     auto& s_part = L.part;
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const u64 op0 = (u64)tile * SYA_OPS;
+    // [0] start [1] ops loaded and ranked [2] bucket offsets [3] staged in LDS [4] end, [9] HW_ID [10] XCC_ID
+    u64* dbg = (A.dbg && tile < SY_DBG_SUM - SY_DBG_PART && threadIdx.x == 0) ? A.dbg + (u64)(SY_DBG_PART + tile) * 16 : nullptr;
+#define SYP_MARK(K) \
+    if (dbg) dbg[K] = wall_clock64()
+    SYP_MARK(0);
     for (u32 i = tid; i < SYA_WAVES * SY_MAX_NB / 2; i += SYA_TPB) ((u32*)&s_wcnt[0][0])[i] = 0;
 #if !NRG_SY_BALLOT
     for (u32 i = tid; i < SYA_WAVES * SY_MAX_NB; i += SYA_TPB) (&s_u.r.mask[0][0])[i] = 0;
 #endif
     if (lane < SY_MAX_HOT) s_hot[w][lane] = SyHot{0, 0, 0};
     __syncthreads();
-    u32 xs[SYA_OROUNDS * CW];
+    // a ranked cold touch: valid (bit 31), SET (29), word in bucket (20..28), bucket (11..19),
+    // rank in the wave's count of its bucket (0..10; < 4 * 64 * CW <= 2048)
     u32 pk[SYA_OROUNDS * CW];
     const u32 opw = (u32)(w * SYA_OROUNDS) * 64 + lane;  // this lane's op in round 0, within the tile
-    nrg_synth_op nx{0, 0, 0, 0};
-    if (op0 + opw < n) nx = src ? src[op0 + opw] : ring[(lo + op0 + opw) & ring_mask];
+    // the records of the next SYP_PD wave rounds are in flight
+    nrg_synth_op nx[SYP_PD];
+#pragma unroll
+    for (int q = 0; q < SYP_PD; q++) {
+        nx[q] = nrg_synth_op{0, 0, 0, 0};
+        if (op0 + opw + q * 64 < n) nx[q] = src ? src[op0 + opw + q * 64] : ring[(lo + op0 + opw + q * 64) & ring_mask];
+    }
 #pragma unroll
     for (int orr = 0; orr < SYA_OROUNDS; orr++) {
-        // 64 consecutive ops per wave round; lane = op; the next round's record is in flight
+        // 64 consecutive ops per wave round; lane = op
         const bool valid = op0 + opw + orr * 64 < n;
-        const nrg_synth_op o = nx;
-        if (orr + 1 < SYA_OROUNDS && op0 + opw + (orr + 1) * 64 < n)
-            nx = src ? src[op0 + opw + (orr + 1) * 64] : ring[(lo + op0 + opw + (orr + 1) * 64) & ring_mask];
+        const nrg_synth_op o = nx[orr % SYP_PD];
+        if (orr + SYP_PD < SYA_OROUNDS && op0 + opw + (orr + SYP_PD) * 64 < n)
+            nx[orr % SYP_PD] = src ? src[op0 + opw + (orr + SYP_PD) * 64]
+                                   : ring[(lo + op0 + opw + (orr + SYP_PD) * 64) & ring_mask];
         if (src && valid) ring[(lo + op0 + opw + orr * 64) & ring_mask] = o;
         const bool set = valid && o.op == NRG_SYNTH_WRITE_ONLY;
+        if (set && (o.tid >> 31)) A.fl->set_epoch = A.epoch;  // this chunk's seen values may pass 2^32
         // hot touches (r2 + j) % HR, j < HW, skipped when r2 + HW wraps; ordered (lane, j)
         const bool hot_ok = valid && (o.r2 + HW >= o.r2);
         const u32 h0 = hot_ok ? (u32)mod_recip(o.r2, HR, hr_m) : 0u;
@@ -497,11 +536,13 @@ __device__ __forceinline__ void sy_part_role(const SyPartArgs& A, u32 tile, SyPa
 #else
             const u32 rank = wave_rank_mask(vw[r] != NOTOUCH, bw[r], lane, s_u.r.mask[w], s_wcnt[w], &peers);
 #endif
-            xs[orr * CW + r] = vw[r];
-            pk[orr * CW + r] = (bw[r] << 16) | rank;
+            const u32 xl = word_in_bucket((vw[r] & ~SETBIT) - HR, bw[r], W);
+            pk[orr * CW + r] = vw[r] == NOTOUCH ? 0u
+                                                : (1u << 31) | ((vw[r] & SETBIT) ? 1u << 29 : 0u) | (xl << 20) | (bw[r] << 11) | rank;
         }
     }
     __syncthreads();
+    SYP_MARK(1);
     // bucket totals over the waves; wave prefixes; thread t owns bucket t
     const u32 bt = tid;
     u32 tot = 0;
@@ -531,23 +572,29 @@ __device__ __forceinline__ void sy_part_role(const SyPartArgs& A, u32 tile, SyPa
         hot[(u64)tile * HR + tid] = a;
     }
     __syncthreads();
+    SYP_MARK(2);
 #pragma unroll
     for (int orr = 0; orr < SYA_OROUNDS; orr++) {
 #pragma unroll
         for (int r = 0; r < CW; r++) {
-            const u32 v = xs[orr * CW + r];
-            if (v == NOTOUCH) continue;
             const u32 p = pk[orr * CW + r];
+            if (!(p >> 31)) continue;
             const u32 t = r * 64 + lane;
             const u32 opl = (u32)(w * SYA_OROUNDS + orr) * 64 + t / CW;
-            const u32 xl = word_in_bucket((v & ~SETBIT) - HR, p >> 16, W);
-            s_u.stage[s_wcnt[w][p >> 16] + (p & 0xFFFFu)] = ent_make(xl, (v & SETBIT) != 0, t % CW, opl);
+            s_u.stage[s_wcnt[w][(p >> 11) & 511u] + (p & 2047u)] = ent_make((p >> 20) & 511u, (p >> 29) & 1u, t % CW, opl);
         }
     }
     __syncthreads();
+    SYP_MARK(3);
     const u32 nops = (u32)(n - op0 < SYA_OPS ? n - op0 : SYA_OPS);
     u32* Et = E + (u64)tile * (SYA_OPS * CW);
     for (u32 i = tid; i < nops * CW; i += SYA_TPB) Et[i] = s_u.stage[i];
+    if (dbg) {
+        dbg[4] = wall_clock64();
+        dbg[9] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+        dbg[10] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+    }
+#undef SYP_MARK
 }
 
 // One workgroup per bucket. Passes of SYB_PASS touches in log order; wave w takes the pass's
@@ -559,6 +606,7 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
                                                             u32 ntiles, u32 tile_entries, u64* __restrict__ V,
                                                             u64* __restrict__ words, u64 N, u32 HR, u32 W,
                                                             const nrg_synth_op* __restrict__ ring, u64 ring_mask, u64 lo,
+                                                            SyFlags* __restrict__ fl, u32 epoch, u32 par,
                                                             u64* __restrict__ dbg) {
     // dbg (NRG_EXP & 2, diagnostic): per block, thread 0's wall clock at the phase edges
     // [0] start [1] prologue loaded [2] scanned, then summed over passes [3] tile map [4] gather
@@ -581,6 +629,7 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
 #endif
     __shared__ unsigned short s_tile[2][SYB_PASS];  // tile of every touch of a pass (double buffered)
     __shared__ u32 s_part[SYB_WAVES];
+    __shared__ u32 s_big;  // a word ends the chunk >= 2^31 (SyFlags)
     u32* s_pre = s_dyn;
     unsigned short* s_off = (unsigned short*)(s_dyn + ntiles + 1);
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
@@ -590,12 +639,15 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
     const u32 b = xcd * q + (xcd < rem ? xcd : rem) + blockIdx.x / nxcd;
     const u64 w0 = b ? (u64)HR + 1 + (u64)(b - 1) * W : (u64)HR;  // bucket 0: cold word 0 alone
     const u32 nw = b ? W : 1u;
+    // 4-B seen values this chunk (SyFlags): decided alike by every workgroup
+    const bool v32 = fl->big[(epoch - 1) & 1] != epoch - 1 && fl->set_epoch != epoch;
     for (u32 t = tid; t < ntiles; t += SYB_TPB) {
         const u32 p = cnt_bt[(u64)b * ntiles + t];
         s_off[t] = (unsigned short)(p >> 16);
         s_pre[t] = p & 0xFFFFu;
     }
     for (u32 i = tid; i < SYB_WORDS; i += SYB_TPB) s_cur[i] = i < nw && w0 + i < N ? words[w0 + i] : 0ull;
+    if (tid == 0) s_big = 0;
     for (u32 i = tid; i < SYB_WAVES * SYB_WORDS; i += SYB_TPB) (&s_wc[0][0])[i] = 0;
 #if !NRG_SY_BALLOT
     for (u32 i = tid; i < SYB_WAVES * SYB_WORDS; i += SYB_TPB) (&s_mk[0][0])[i] = 0;
@@ -765,14 +817,28 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
             }
         }
         SY_ACC(2);
+        if (v32) {
 #pragma unroll
-        for (int q = 0; q < SYB_PER; q++)
-            if (base + (u32)w * (SYB_PER * 64) + q * 64 + lane < total) V[gpos[q]] = sv[q];
+            for (int q = 0; q < SYB_PER; q++)
+                if (base + (u32)w * (SYB_PER * 64) + q * 64 + lane < total) ((u32*)V)[gpos[q]] = (u32)sv[q];
+        } else {
+#pragma unroll
+            for (int q = 0; q < SYB_PER; q++)
+                if (base + (u32)w * (SYB_PER * 64) + q * 64 + lane < total) V[gpos[q]] = sv[q];
+        }
         SY_ACC(3);
     }
     __syncthreads();
+    bool big = false;
     for (u32 i = tid; i < nw; i += SYB_TPB)
-        if (w0 + i < N) words[w0 + i] = s_cur[i];
+        if (w0 + i < N) {
+            words[w0 + i] = s_cur[i];
+            big |= (s_cur[i] >> 31) != 0;
+        }
+    if (big) s_big = 1u;  // (an LDS flag: __syncthreads_or here kept the thread-id math live and spilled)
+    __syncthreads();
+    if (s_big && tid == 0) fl->big[epoch & 1] = epoch;
+    if (blockIdx.x == 0 && tid == 0) fl->v32[par] = v32 ? 1u : 0u;
     if (dbg && threadIdx.x == 0) {
         for (int k = 0; k < 4; k++) dbg[(u64)blockIdx.x * 16 + 3 + k] = tm_acc[k];
         dbg[(u64)blockIdx.x * 16 + 8] = (total + SYB_PASS - 1) / SYB_PASS;
@@ -797,6 +863,9 @@ __device__ __forceinline__ void sy_sum_role(const SySumArgs& S, u32 blk, u64* s_
     const SyHot* __restrict__ hot = S.hot;
     u64* __restrict__ words = S.words;
     const int tid = threadIdx.x;
+    // [0] start [1] sums added [2] responses stored [3] hot fold done (workgroup 0)
+    u64* dbg = (S.dbg && blk < SY_DBG_ROWS - SY_DBG_SUM && threadIdx.x == 0) ? S.dbg + (u64)(SY_DBG_SUM + blk) * 16 : nullptr;
+    if (dbg) dbg[0] = wall_clock64();
     if (want) {
         const u64 tile = tile0 + blk;
         const u64 op0 = tile * SYA_OPS;
@@ -804,11 +873,29 @@ __device__ __forceinline__ void sy_sum_role(const SySumArgs& S, u32 blk, u64* s_
         for (u32 i = tid; i < SYA_OPS; i += SYC_TPB) s_sum[i] = 0;
         __syncthreads();
         const u32* Et = E + tile * SYA_OPS * CW;
-        const u64* Vt = V + tile * SYA_OPS * CW;
         const u32 ne = nops * CW;
-        for (u32 e = tid; e < ne; e += SYC_TPB)
-            atomicAdd((unsigned long long*)&s_sum[ent_op(Et[e])], (unsigned long long)Vt[e]);
+        // SYS_U entries per thread in flight before their LDS adds (one at a time, every add
+        // waited for its own two loads: 8-10 us per workgroup)
+        constexpr int SYS_U = 10;
+        auto add_all = [&](auto Vt) {
+            for (u32 e0 = tid; e0 < ne; e0 += SYC_TPB * SYS_U) {
+                u32 ee[SYS_U];
+                u64 vv[SYS_U];
+#pragma unroll
+                for (int q = 0; q < SYS_U; q++) {
+                    const u32 e = e0 + q * SYC_TPB;
+                    ee[q] = e < ne ? Et[e] : 0u;
+                    vv[q] = e < ne ? (u64)Vt[e] : 0ull;
+                }
+#pragma unroll
+                for (int q = 0; q < SYS_U; q++)
+                    if (e0 + q * SYC_TPB < ne) atomicAdd((unsigned long long*)&s_sum[ent_op(ee[q])], (unsigned long long)vv[q]);
+            }
+        };
+        if (*S.v32) add_all((const u32*)V + tile * SYA_OPS * CW);  // 4-B seen values (SyFlags)
+        else add_all(V + tile * SYA_OPS * CW);
         __syncthreads();
+        if (dbg) dbg[1] = wall_clock64();
         for (u32 i = tid; i < nops; i += SYC_TPB) {
             const u64 g = lo + op0 + i;
             if (g >= resp_lo && g < resp_hi) {
@@ -816,6 +903,11 @@ __device__ __forceinline__ void sy_sum_role(const SySumArgs& S, u32 blk, u64* s_
                 if (some) some[g - resp_lo] = 1;
             }
         }
+    }
+    if (dbg) {
+        dbg[2] = wall_clock64();
+        dbg[9] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+        dbg[10] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
     }
     if (blk != 0) return;
     // hot words: ordered fold of the tiles' summaries
@@ -840,6 +932,7 @@ __device__ __forceinline__ void sy_sum_role(const SySumArgs& S, u32 blk, u64* s_
         }
         __syncthreads();
     }
+    if (dbg) dbg[3] = wall_clock64();
 }
 
 // One launch: the partition of chunk e in workgroups [0, A.ntiles) (on the critical path: the
@@ -863,10 +956,11 @@ bool sy_bucket_eligible(const nrg_config& cf) {
 // [bucket][tile] counts and the hot summaries; a chunk's sums may run in the next chunk's
 // partition launch, so E and the hot summaries alternate between two parities
 struct SyAux {
-    u64* V;
+    u64* V;  // u64 seen values, or u32 ones (SyFlags) in the same bytes
     u32* E[2];
     u32* cnt;
     SyHot* hot[2];
+    SyFlags* fl;
 };
 static u64 sy_nb(const nrg_config& cf) {
     const u64 span = cf.synth_n - cf.synth_hot_reads;
@@ -883,13 +977,24 @@ static SyAux sy_aux(void* base, const nrg_config& cf) {
     x.cnt = x.E[1] + te;
     x.hot[0] = (SyHot*)(((uintptr_t)(x.cnt + sy_nb(cf) * tiles) + 15) & ~(uintptr_t)15);
     x.hot[1] = x.hot[0] + tiles * cf.synth_hot_reads;
+    x.fl = (SyFlags*)(((uintptr_t)(x.hot[1] + tiles * cf.synth_hot_reads) + 15) & ~(uintptr_t)15);
     return x;
 }
 
 u64 sy_bucket_aux_bytes(const nrg_config& cf) {
     const u64 tiles = (cf.max_batch + SYA_OPS - 1) / SYA_OPS;
     const u64 te = tiles * SYA_OPS * cf.synth_cold_writes;
-    return te * (8 + 4 + 4) + sy_nb(cf) * tiles * 4 + 2 * tiles * cf.synth_hot_reads * sizeof(SyHot) + 256;
+    return te * (8 + 4 + 4) + sy_nb(cf) * tiles * 4 + 2 * tiles * cf.synth_hot_reads * sizeof(SyHot) + 256 +
+           sizeof(SyFlags) + 16;
+}
+
+// Fresh scratch: the words may hold anything (sort-path chunks ran before), so the next chunk
+// (epoch sy_round + 1) takes 8-B seen values: big[sy_round & 1] = sy_round.
+hipError_t sy_aux_init(nrg_ctx* c) {
+    SyAux x = sy_aux(c->d_sy_aux, c->cfg);
+    SyFlags f{};
+    f.big[0] = f.big[1] = c->sy_round;  // the other slot is compared with sy_round + 1 + 2k: never equal
+    return hipMemcpy(x.fl, &f, sizeof f, hipMemcpyHostToDevice);
 }
 
 static SySumArgs sy_sum_args(nrg_ctx* c, const SyDeferred& d) {
@@ -912,6 +1017,8 @@ static SySumArgs sy_sum_args(nrg_ctx* c, const SyDeferred& d) {
     S.HR = cf.synth_hot_reads;
     S.CW = cf.synth_cold_writes;
     S.words = c->d_words;
+    S.v32 = &x.fl->v32[d.par];
+    S.dbg = (c->exp & 2) ? c->d_dbg : nullptr;
     return S;
 }
 
@@ -968,6 +1075,9 @@ static hipError_t sy_bucket_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 re
     A.E = x.E[par];
     A.cnt_bt = x.cnt;
     A.hot = x.hot[par];
+    A.fl = x.fl;
+    A.epoch = ++c->sy_round;
+    A.dbg = (c->exp & 2) ? c->d_dbg : nullptr;
     SySumArgs S{};
     if (c->sy_pend.valid) S = sy_sum_args(c, c->sy_pend);
     c->sy_pend.valid = false;
@@ -976,7 +1086,8 @@ static hipError_t sy_bucket_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 re
     if (e != hipSuccess) return e;
     const size_t dyn = (size_t)(ntiles + 1) * 4 + (size_t)ntiles * 2;
     sy_bucket_kernel<<<NB, SYB_TPB, dyn, st>>>(x.E[par], x.cnt, ntiles, SYA_OPS * CW, x.V, c->d_words, cf.synth_n, HR,
-                                               W, A.ring, A.ring_mask, lo, (c->exp & 2) ? c->d_dbg : nullptr);
+                                               W, A.ring, A.ring_mask, lo, x.fl, A.epoch, par,
+                                               (c->exp & 2) ? c->d_dbg : nullptr);
     timer_end(c, "sy_replay");
     if ((e = hipGetLastError()) != hipSuccess) return e;
     // this chunk's sums: in the next chunk's partition launch (pipeline = 1) or now

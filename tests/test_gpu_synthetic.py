@@ -87,6 +87,36 @@ def test_synth_one_word(nrg, orc, path, wo):
     dev.close()
 
 
+def test_synth_wide_values(nrg, orc, path):
+    """Seen values past 2^32. The bucket pass stores 4-B seen values only while every word is
+    < 2^31 and no WriteOnly of the chunk writes a tid >= 2^31 (synthetic.hip SyFlags): a chunk
+    whose WriteOnlys write 2^40-scale tids, chunks that read the words they left (8-B seen
+    values), then WriteOnlys with small tids over every word, which bring the 4-B path back."""
+    n = 30_000
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_SYNTHETIC, 0, knobs=path, max_batch=1 << 15)
+    os_ = orc.Synthetic()
+    big = [(1 << 40) + 3, (1 << 31), 0xFFFFFFFFFFFFFFF0]
+
+    def wide(ops):
+        ops["tid"][::5] = np.asarray(big, np.uint64)[np.arange(len(ops["tid"][::5])) % 3]
+        ops["op"][::5] = 0  # WriteOnly
+    _check_rounds(nrg, orc, dev, os_, 1, n, 31, [1, 2, 3], 0)      # 4-B seen values
+    _check_rounds(nrg, orc, dev, os_, 1, n, 32, [1, 2, 3], 0, wide)  # big tids this chunk
+    _check_rounds(nrg, orc, dev, os_, 2, n, 34, [1, 2, 3], 0)      # big words left over
+    # WriteOnly with tid 1 on every cold word: op i's touches are words [5i, 5i + 5) (r1 = 5i, r2 = 1)
+    w = np.zeros(40_000, nrg.SYNTH_OP_DTYPE)
+    w["tid"], w["r1"], w["r2"], w["op"] = 1, np.arange(40_000, dtype=np.uint64) * 5, 1, 0
+    for a in range(0, 40_000, 10_000):
+        first = dev.log_append(w[a:a + 10_000], 1)
+        dev.log_exec(first, first + 10_000)
+        os_.replay(np.stack([w["tid"][a:a + 10_000], w["r1"][a:a + 10_000], w["r2"][a:a + 10_000],
+                             w["op"][a:a + 10_000]], axis=1))
+    np.testing.assert_array_equal(dev.sy_dump(), os_.dump())
+    assert int(dev.sy_dump()[2:].max()) < (1 << 31)
+    _check_rounds(nrg, orc, dev, os_, 2, n, 36, [1, 2, 3], 0)      # 4-B seen values again
+    dev.close()
+
+
 def test_synth_partial_tiles_mixed(nrg, orc, path):
     """Round sizes that end mid-tile and mid-wave, WriteOnly runs, wrapped hot ranges."""
     def tweak(ops):
