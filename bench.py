@@ -226,11 +226,15 @@ class Env:
             dist.barrier()
         torch.cuda.synchronize()
         t = time.perf_counter()
+        marks = [t]
         for i in range(n):
             step(i)
+            if i < 3:
+                marks.append(time.perf_counter())
         rep.join()  # launches the last round's deferred apply + reads: inside the timed region
         if host_s is not None:
             host_s[0] = time.perf_counter() - t
+            host_s[1:] = [round((b - a) * 1e6, 2) for a, b in zip(marks, marks[1:])]
         torch.cuda.synchronize()
         if self.world > 1:
             dist.barrier()
@@ -484,6 +488,7 @@ def run_hashmap(args, env):
         "algorithmic_bytes": int(round_bytes),
         "achieved_GBps": round(round_bytes / (elapsed / args.steps) / 1e9, 1),
         "host_enqueue_us": round(host_s[0] * 1e6 / args.steps, 2),
+        "host_first_steps_us": host_s[1:],
         "distinct_get_keys": int(u_r),
         "distinct_put_keys": int(u_w),
     }

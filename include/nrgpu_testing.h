@@ -41,6 +41,10 @@ int nrg_test_debug_read(nrg_ctx* ctx, uint64_t* out, uint64_t words);
 #define NRG_KNOB_PIPELINE 8    /* overrides nrg_config.pipeline                                    */
 #define NRG_KNOB_SORT_MIN 9    /* hashmap: rounds of at least this many Puts on an unskewed stream
                                   replay as sorted rounds (0: never)                              */
+#define NRG_KNOB_COMB_SPIN 10   /* combiner (read by nrg_combiner_open): client threads that may spin
+                                   while their round runs (default 0: every waiting client parks
+                                   on a futex)                                                   */
+#define NRG_KNOB_COMB_DEPTH 11  /* combiner: rounds in flight (1..4, default 2)                      */
 int nrg_test_set_knob(nrg_ctx* ctx, int knob, uint64_t value);
 
 /* Replica groups created after nrg_test_loopback_collectives(1) (nrg_group_open,

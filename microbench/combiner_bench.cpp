@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "../include/nrgpu.h"
+#include "../include/nrgpu_testing.h"
 
 static uint64_t sm64(uint64_t& s) {  // splitmix64
     uint64_t z = (s += 0x9E3779B97F4A7C15ull);
@@ -28,7 +29,7 @@ static uint64_t sm64(uint64_t& s) {  // splitmix64
     return z ^ (z >> 31);
 }
 
-static int run(int threads, int batch, double secs, bool stack) {
+static int run(int threads, int batch, double secs, bool stack, int spin, int depth) {
     nrg_config cfg;
     nrg_config_default(&cfg, stack ? NRG_DS_STACK : NRG_DS_HASHMAP);
     cfg.log2_slots = 26;
@@ -43,6 +44,10 @@ static int run(int threads, int batch, double secs, bool stack) {
     } else if (int r = nrg_hashmap_prefill_range(ctx, 1ull << 23, 1)) {
         return r;
     }
+    if (spin >= 0)
+        if (int r = nrg_test_set_knob(ctx, NRG_KNOB_COMB_SPIN, (uint64_t)spin)) return r;
+    if (depth > 0)
+        if (int r = nrg_test_set_knob(ctx, NRG_KNOB_COMB_DEPTH, (uint64_t)depth)) return r;
     nrg_combiner* comb = nullptr;
     if (int r = nrg_combiner_open(ctx, (uint32_t)threads, &comb)) return r;
     std::atomic<bool> stop{false};
@@ -92,9 +97,9 @@ static int run(int threads, int batch, double secs, bool stack) {
     uint64_t rounds = 0, ops = 0, tot = 0;
     nrg_combiner_stats(comb, &rounds, &ops);
     for (uint64_t d : done) tot += d;
-    std::printf("%s threads %4d ops/call %3d: %9.3f Mops/s  rounds %7llu  ops/round %7.1f  round rate %6.1f k/s%s\n",
-                stack ? "stack  " : "hashmap", threads, batch, tot / dt / 1e6, (unsigned long long)rounds, rounds ? (double)ops / rounds : 0.0,
-                rounds / dt / 1e3, err ? "  ERROR" : "");
+    std::printf("%s threads %4d ops/call %3d spin %3d depth %d: %9.3f Mops/s  rounds %7llu  ops/round %7.1f  round rate %6.1f k/s%s\n",
+                stack ? "stack  " : "hashmap", threads, batch, spin, depth, tot / dt / 1e6, (unsigned long long)rounds,
+                rounds ? (double)ops / rounds : 0.0, rounds / dt / 1e3, err ? "  ERROR" : "");
     std::fflush(stdout);
     nrg_combiner_close(comb);
     nrg_close(ctx);
@@ -137,19 +142,23 @@ static void show_cpus() {  // what the host gives this process: affinity and cgr
 }
 
 int main(int argc, char** argv) {
-    // combiner_bench [seconds [threads ops/call kind] ...]  (kind 0 hashmap, 1 stack); without
-    // cases: the default set
+    // combiner_bench [seconds [threads ops/call kind spin depth] ...]  (kind 0 hashmap, 1 stack;
+    // spin -1 and depth 0: the library's defaults); without cases: the default set
     const double secs = argc > 1 ? std::atof(argv[1]) : 2.0;
     show_cpus();
-    std::vector<std::array<int, 3>> cases = {{8, 1, 0},    {8, 32, 0},   {16, 32, 0}, {64, 1, 0}, {64, 32, 0},
-                                             {128, 32, 0}, {256, 32, 0}, {16, 32, 1}, {64, 32, 1}, {256, 32, 1}};
-    if (argc > 4) {
+    std::vector<std::array<int, 5>> cases = {{8, 1, 0, -1, 0},   {8, 32, 0, -1, 0},  {16, 32, 0, -1, 0},
+                                             {64, 1, 0, -1, 0},  {64, 32, 0, -1, 0}, {128, 32, 0, -1, 0},
+                                             {256, 32, 0, -1, 0}, {16, 32, 1, -1, 0}, {64, 32, 1, -1, 0},
+                                             {256, 32, 1, -1, 0}};
+    if (argc > 6) {
         cases.clear();
-        for (int i = 2; i + 2 < argc; i += 3) cases.push_back({std::atoi(argv[i]), std::atoi(argv[i + 1]), std::atoi(argv[i + 2])});
+        for (int i = 2; i + 4 < argc; i += 5)
+            cases.push_back({std::atoi(argv[i]), std::atoi(argv[i + 1]), std::atoi(argv[i + 2]), std::atoi(argv[i + 3]),
+                             std::atoi(argv[i + 4])});
     }
     for (auto& c : cases) {
         const Throttle t0 = throttle();
-        if (int r = run(c[0], c[1], secs, c[2] != 0)) {
+        if (int r = run(c[0], c[1], secs, c[2] != 0, c[3], c[4])) {
             std::printf("error %d (%s)\n", r, nrg_strerror(r));
             return 1;
         }

@@ -20,9 +20,9 @@
 // The combining role belongs to the library's combiner thread rather than to whichever client
 // takes a lock (nr/src/replica.rs:508-540): a round completes asynchronously on the GPU and needs a
 // host thread polling it, and with hundreds of clients on a few cores a client that holds the
-// role is descheduled while everyone waits. Clients spin briefly (longer while there are fewer
-// clients than cores) and then park on a futex of their batch; the combiner thread parks when
-// there is nothing to do and the first post wakes it.
+// role is descheduled while everyone waits. Clients park on a futex of their batch (a test knob
+// lets some of them spin instead); the combiner thread parks when there is nothing to do and the
+// first post wakes it.
 // Reads ride in the round that collects them, after its writes: they see every write completed
 // before they were posted (sync-to-tail) and never wait behind a later write round.
 //
@@ -49,8 +49,8 @@ namespace {
 
 constexpr uint32_t MAX_PENDING = 32;  // nr/src/context.rs:12 MAX_PENDING_OPS
 constexpr int NB = 6;                 // batch slots
-constexpr uint64_t DEPTH = 2;         // rounds in flight (NB >= DEPTH + 2: a slot's clients copy
-                                      // their responses out while later rounds run)
+constexpr uint64_t DEPTH = 2;         // default rounds in flight (NRG_KNOB_COMB_DEPTH, <= NB - 2: a
+                                      // slot's clients copy their responses out while later rounds run)
 
 enum : uint32_t { FREE = 0, OPEN = 1, SEALED = 2, DONE = 3 };
 
@@ -59,31 +59,6 @@ void futex_wait(std::atomic<uint32_t>* w, uint32_t seen) {
     syscall(SYS_futex, (uint32_t*)w, FUTEX_WAIT_PRIVATE, seen, &ts, nullptr, 0);
 }
 void futex_wake_all(std::atomic<uint32_t>* w) { syscall(SYS_futex, (uint32_t*)w, FUTEX_WAKE_PRIVATE, INT32_MAX, nullptr, nullptr, 0); }
-
-// CPUs this process may keep busy: its affinity mask, capped by a cgroup CPU quota (a job given a
-// share of a larger host sees every CPU but is throttled for a whole period once spinning threads
-// have burnt the quota)
-uint32_t cpus_allowed() {
-    cpu_set_t set;
-    uint32_t n = 0;
-    if (sched_getaffinity(0, sizeof(set), &set) == 0) n = (uint32_t)CPU_COUNT(&set);
-    if (!n) n = std::max(1u, std::thread::hardware_concurrency());
-    double quota = -1, period = 0;
-    if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {  // cgroup v2: "<quota|max> <period>"
-        char q[32] = {0};
-        if (std::fscanf(f, "%31s %lf", q, &period) == 2 && std::strcmp(q, "max")) quota = std::atof(q);
-        std::fclose(f);
-    } else if (FILE* g = std::fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r")) {  // cgroup v1
-        if (std::fscanf(g, "%lf", &quota) != 1) quota = -1;
-        std::fclose(g);
-        if (FILE* h = std::fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r")) {
-            if (std::fscanf(h, "%lf", &period) != 1) period = 0;
-            std::fclose(h);
-        }
-    }
-    if (quota > 0 && period > 0) n = std::min(n, std::max(1u, (uint32_t)(quota / period)));
-    return n;
-}
 
 struct alignas(64) Batch {
     std::atomic<uint32_t> state{FREE};
@@ -148,6 +123,7 @@ struct nrg_combiner {
     std::atomic<uint64_t> launched{0};               // rounds < launched are enqueued (combiner thread)
     std::atomic<uint64_t> rounds{0}, ops{0};
     int32_t spin_cap = 0;                            // clients that may spin at once
+    uint64_t depth = DEPTH;                          // rounds in flight
     alignas(64) std::atomic<int32_t> spinning{0};
     // the combiner thread
     std::thread worker;
@@ -237,7 +213,7 @@ int launch(nrg_combiner* m, Batch& x, uint32_t W, uint32_t R) {
 bool advance(nrg_combiner* m) {
     const uint64_t k = m->open.load(std::memory_order_relaxed);
     Batch& x = m->b[k % NB];
-    if (m->launched.load(std::memory_order_relaxed) - m->completed.load(std::memory_order_acquire) >= DEPTH) return false;
+    if (m->launched.load(std::memory_order_relaxed) - m->completed.load(std::memory_order_acquire) >= m->depth) return false;
     if (!x.nw.load(std::memory_order_seq_cst) && !x.nr.load(std::memory_order_seq_cst)) return false;
     x.state.store(SEALED, std::memory_order_seq_cst);
     while (x.writers.load(std::memory_order_seq_cst)) _mm_pause();
@@ -326,8 +302,8 @@ int post_and_wait(nrg_combiner* m, uint32_t token, bool write, const void* ops, 
         m->work.fetch_add(1, std::memory_order_seq_cst);
         syscall(SYS_futex, (uint32_t*)&m->work, FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
     }
-    // wait for the round: spin (about a round) if a spinning slot is free -- at most the cores
-    // the process may keep busy, less the combiner thread's -- else park on the batch's futex
+    // wait for the round: spin (about a round) if a spinning slot is free (NRG_KNOB_COMB_SPIN;
+    // none by default), else park on the batch's futex
     const bool spin = m->spinning.fetch_add(1, std::memory_order_relaxed) < m->spin_cap;
     if (!spin) m->spinning.fetch_sub(1, std::memory_order_relaxed);
     for (uint32_t spins = 0; m->completed.load(std::memory_order_acquire) <= k; spins++) {
@@ -394,7 +370,12 @@ extern "C" int nrg_combiner_open(nrg_ctx* ctx, uint32_t max_threads, nrg_combine
     }
     m->saved_pipeline = ctx->pipeline;
     ctx->pipeline = false;
-    m->spin_cap = (int32_t)cpus_allowed() - 2;
+    // waiting clients park at once by default: spinning ones only burnt CPU. 16 threads ran as
+    // fast parked as with 14 spinning (11.5 vs 11.4 M ops/s) on 1/8 of the CPU time; at 64 threads
+    // spinning took the job's whole cgroup quota and throttled it (22.3 vs 24.5 M ops/s parked;
+    // profiles/r03_combiner_policy.txt)
+    m->spin_cap = ctx->comb_spin >= 0 ? ctx->comb_spin : 0;
+    if (ctx->comb_depth) m->depth = std::min<uint64_t>(ctx->comb_depth, NB - 2);
     m->b[0].round.store(0);
     m->b[0].state.store(OPEN);
     try {

@@ -1148,6 +1148,14 @@ extern "C" int nrg_test_set_knob(nrg_ctx* c, int knob, uint64_t v) {
             if (!hm) return NRG_E_INVAL;
             c->sort_min = v;
             return NRG_OK;
+        case NRG_KNOB_COMB_SPIN:
+            if (v > 4096) return NRG_E_INVAL;
+            c->comb_spin = (int32_t)v;
+            return NRG_OK;
+        case NRG_KNOB_COMB_DEPTH:
+            if (v < 1 || v > 4) return NRG_E_INVAL;
+            c->comb_depth = (uint32_t)v;
+            return NRG_OK;
         case NRG_KNOB_PIPELINE:
             if (v > 1) return NRG_E_INVAL;
             c->pipeline = v != 0;
