@@ -45,6 +45,9 @@ int nrg_test_debug_read(nrg_ctx* ctx, uint64_t* out, uint64_t words);
                                    while their round runs (default 0: every waiting client parks
                                    on a futex)                                                   */
 #define NRG_KNOB_COMB_DEPTH 11  /* combiner: rounds in flight (1..4, default 2)                      */
+#define NRG_KNOB_SMALL_MAX 12   /* hashmap: rounds of at most this many Puts (<= 2048, and <= 8192
+                                   Gets) replay in one one-workgroup launch (0: never; the
+                                   combiner sets 2048 while it is open)                          */
 int nrg_test_set_knob(nrg_ctx* ctx, int knob, uint64_t value);
 
 /* Replica groups created after nrg_test_loopback_collectives(1) (nrg_group_open,

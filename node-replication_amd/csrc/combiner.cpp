@@ -114,6 +114,7 @@ struct nrg_combiner {
     uint64_t cap = 0;  // ops of each kind per batch: max_threads * MAX_PENDING
     uint32_t rec_b = 0, rd_b = 0, wr_b = 0, rr_b = 0;  // write record / read record / responses
     bool saved_pipeline = false;
+    uint64_t saved_small = 0;
     std::atomic<uint32_t> next_tok{0};
     Batch b[NB];
     alignas(64) std::atomic<uint64_t> open{0};       // round number of the OPEN batch
@@ -370,6 +371,9 @@ extern "C" int nrg_combiner_open(nrg_ctx* ctx, uint32_t max_threads, nrg_combine
     }
     m->saved_pipeline = ctx->pipeline;
     ctx->pipeline = false;
+    // hashmap rounds of up to 2048 Puts in one launch (hashmap.hip hm_small_round_kernel)
+    m->saved_small = ctx->small_max;
+    if (kind == NRG_DS_HASHMAP) ctx->small_max = 2048;
     // waiting clients park at once by default: spinning ones only burnt CPU. 16 threads ran as
     // fast parked as with 14 spinning (11.5 vs 11.4 M ops/s) on 1/8 of the CPU time; at 64 threads
     // spinning took the job's whole cgroup quota and throttled it (22.3 vs 24.5 M ops/s parked;
@@ -382,6 +386,7 @@ extern "C" int nrg_combiner_open(nrg_ctx* ctx, uint32_t max_threads, nrg_combine
         m->worker = std::thread(combiner_main, m);
     } catch (...) {
         ctx->pipeline = m->saved_pipeline;
+        ctx->small_max = m->saved_small;
         comb_free(m);
         return NRG_E_NOMEM;
     }
@@ -400,6 +405,7 @@ extern "C" int nrg_combiner_close(nrg_combiner* m) {
     (void)nrg::ctx_use_device(m->ctx);
     if (hipStreamSynchronize((hipStream_t)nrg_get_stream(m->ctx)) != hipSuccess) rc = NRG_E_HIP;
     m->ctx->pipeline = m->saved_pipeline;
+    m->ctx->small_max = m->saved_small;
     comb_free(m);
     return rc;
 }

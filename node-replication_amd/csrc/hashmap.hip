@@ -1103,6 +1103,212 @@ __global__ __launch_bounds__(TPB) void hm_sr_apply_kernel(SortedJob j) {
     }
 }
 
+// ---- small rounds: one workgroup, one launch (the flat combiner's batches) ----------------------
+// A round of at most SM_W Puts and SM_R Gets, whole in one 1024-thread workgroup: the Puts are
+// hashed by key in LDS (how many, the last one); one thread per distinct key finds or claims
+// its slot, answers the previous values of the key's Puts in log order (the slot's value before
+// the round for the first; nr/examples/hashmap.rs:46-50) and stores the last value; then every
+// Get probes the table. No deferred half and no device atomics per Put: the combiner's
+// index + elector + reads launches (about 20 us of GPU time for a few hundred ops) become one.
+// Runs with no other round in flight (the caller flushes first). Keys present in the table are
+// present (quiescent: no claim in flight); fresh claims get epoch-1 stamps, as the elector's.
+constexpr int SM_TPB = 1024;
+constexpr u32 SM_W = 2048, SM_R = 8192, SM_HT = 4096;  // SM_HT: LDS hash entries (+1: the side key)
+struct SmallJob {
+    RecSrc rec;
+    nrg_put* ring_out;  // log copy to write (nullptr: the records are in the ring)
+    u32 n;
+    u64 lo, resp_lo, resp_hi;
+    u64* prev;
+    uint8_t* prevf;
+    const u64* keys;  // Gets
+    u32 R;
+    u64* vals;
+    uint8_t* found;
+    u32* e_out;  // the replica's error latch after the round (the combiner's batch), or nullptr
+    u64* created_acc;
+};
+
+__global__ __launch_bounds__(SM_TPB) void hm_small_round_kernel(SmallJob j, Slot* table, u32 shift, u64 tmask,
+                                                                DevCtl* ctl) {
+    __shared__ u64 s_val[SM_W];
+    __shared__ uint16_t s_ent[SM_W];    // hash entry of each Put
+    __shared__ u64 s_hk[SM_HT];
+    __shared__ u32 s_cnt[SM_HT + 1];    // Puts of the key; [SM_HT]: the side key
+    __shared__ u32 s_last[SM_HT + 1];   // its last Put + 1
+    __shared__ u32 s_created;
+    const int tid = threadIdx.x;
+    for (int h = tid; h <= (int)SM_HT; h += SM_TPB) {
+        if (h < (int)SM_HT) s_hk[h] = EMPTY_KEY;
+        s_cnt[h] = 0;
+        s_last[h] = 0;
+    }
+    if (tid == 0) s_created = 0;
+    nrg_put r[SM_W / SM_TPB];
+#pragma unroll
+    for (int q = 0; q < (int)(SM_W / SM_TPB); q++) {
+        const u32 i = q * SM_TPB + tid;
+        if (i < j.n) {
+            r[q] = j.rec.at(i);
+            if (j.ring_out) j.ring_out[(j.rec.lo + i) & j.rec.mask] = r[q];
+            s_val[i] = r[q].val;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < (int)(SM_W / SM_TPB); q++) {
+        const u32 i = q * SM_TPB + tid;
+        if (i >= j.n) continue;
+        const u64 k = r[q].key;
+        u32 h = SM_HT;
+        if (k != EMPTY_KEY) {
+            h = (u32)(mix64(k) >> 40) & (SM_HT - 1);
+            for (;;) {  // at most SM_W keys in SM_HT entries: an entry is always found
+                const u64 old = atomicCAS((unsigned long long*)&s_hk[h], (unsigned long long)EMPTY_KEY,
+                                          (unsigned long long)k);
+                if (old == EMPTY_KEY || old == k) break;
+                h = (h + 1) & (SM_HT - 1);
+            }
+        }
+        s_ent[i] = (uint16_t)h;
+        atomicAdd(&s_cnt[h], 1u);
+        atomicMax(&s_last[h], i + 1);
+    }
+    __syncthreads();
+    // one thread per distinct key: its slot, its Puts' previous values, its last value
+    u32 created = 0;
+    for (int h = tid; h <= (int)SM_HT; h += SM_TPB) {
+        const u32 c = s_cnt[h];
+        if (!c) continue;
+        u64 cur = 0;
+        bool has = false;
+        Slot* slot = nullptr;
+        if (h == (int)SM_HT) {  // the key EMPTY_KEY lives in the side slot
+            has = ctl->sp_claim != 0;
+            if (has) {
+                cur = ctl->sp.val;
+            } else {
+                ctl->sp_claim = 1;
+                ctl->sp.st[0] = ctl->sp.st[1] = STAMP_PRESENT;
+                created++;
+            }
+        } else {
+            bool fresh = false;
+            const u64 k = s_hk[h];
+            const long long sl = claim_slot(table, k, table_home(k, shift), tmask, &fresh);
+            if (sl < 0) {
+                atomicOr(&ctl->err, ERR_TABLE_FULL);
+                continue;
+            }
+            slot = &table[sl];
+            if (fresh) {
+                slot->st[0] = slot->st[1] = STAMP_PRESENT;
+                created++;
+            } else {
+                cur = slot->val;
+                has = true;
+            }
+        }
+        const u32 last = s_last[h] - 1;
+        if (c == 1) {  // the common case: one Put of the key in the round
+            const u64 g = j.lo + last;
+            if (j.prev && g >= j.resp_lo && g < j.resp_hi) {
+                j.prev[g - j.resp_lo] = has ? cur : 0;
+                j.prevf[g - j.resp_lo] = has ? 1 : 0;
+            }
+            cur = s_val[last];
+        } else {  // the key's Puts in log order (a scan of the round; rare for uniform keys)
+            for (u32 i = 0, seen = 0; seen < c; i++) {
+                if (s_ent[i] != (uint16_t)h) continue;
+                seen++;
+                const u64 g = j.lo + i;
+                if (j.prev && g >= j.resp_lo && g < j.resp_hi) {
+                    j.prev[g - j.resp_lo] = has ? cur : 0;
+                    j.prevf[g - j.resp_lo] = has ? 1 : 0;
+                }
+                cur = s_val[i];
+                has = true;
+            }
+        }
+        if (slot) slot->val = cur;
+        else ctl->sp.val = cur;
+    }
+    if (created) atomicAdd(&s_created, created);
+    __syncthreads();  // every store of the round before any Get
+    if (tid == 0 && s_created) atomicAdd(&j.created_acc[0], (u64)s_created);
+    constexpr int RQ = (int)(SM_R / SM_TPB);
+    u64 k[RQ], s[RQ];
+    u64x2 w[RQ];
+#pragma unroll
+    for (int q = 0; q < RQ; q++) {
+        const u32 i = q * SM_TPB + tid;
+        k[q] = i < j.R ? j.keys[i] : EMPTY_KEY;
+        s[q] = table_home(k[q], shift);
+        w[q].x = EMPTY_KEY;
+        w[q].y = 0;
+        if (i < j.R && k[q] != EMPTY_KEY) w[q] = *(const u64x2*)&table[s[q]];
+    }
+#pragma unroll
+    for (int q = 0; q < RQ; q++) {
+        const u32 i = q * SM_TPB + tid;
+        if (i >= j.R) continue;
+        u64 v = 0;
+        bool f = false;
+        if (k[q] == EMPTY_KEY) {
+            f = ctl->sp_claim != 0;
+            v = f ? ctl->sp.val : 0;
+        } else {
+            u64 kk = w[q].x, vv = w[q].y, sl = s[q];
+            for (u64 pr = 0; pr <= tmask; pr++) {
+                if (kk == k[q]) {
+                    f = true;
+                    v = vv;
+                    break;
+                }
+                if (kk == EMPTY_KEY) break;
+                sl = (sl + 1) & tmask;
+                const u64x2 x = *(const u64x2*)&table[sl];
+                kk = x.x;
+                vv = x.y;
+            }
+        }
+        j.vals[i] = v;
+        j.found[i] = f ? 1 : 0;
+    }
+    if (j.e_out) {
+        __syncthreads();
+        if (tid == 0) *j.e_out = atomicExch(&ctl->err, 0u);
+    }
+}
+
+static RecSrc ring_src(nrg_ctx* c, const nrg_put* src, u64 lo);
+
+// A round through hm_small_round_kernel (hm_replay_chunk decides; n <= SM_W, R <= SM_R).
+static hipError_t small_round(nrg_ctx* c, const nrg_put* src, u64 lo, u64 n, bool write_ring, const u64* keys, u64 R,
+                              u64* vals, uint8_t* found, u64 resp_lo, u64 resp_hi, u64* prev, uint8_t* prevf) {
+    hipError_t e = hm_flush(c);
+    if (e != hipSuccess) return e;
+    SmallJob j;
+    j.rec = ring_src(c, src, lo);
+    j.ring_out = write_ring ? (nrg_put*)c->d_ring : nullptr;
+    j.n = (u32)n;
+    j.lo = lo;
+    j.resp_lo = resp_lo;
+    j.resp_hi = resp_hi;
+    j.prev = prev;
+    j.prevf = prev ? prevf : nullptr;
+    j.keys = keys;
+    j.R = keys ? (u32)R : 0u;
+    j.vals = vals;
+    j.found = found;
+    j.e_out = c->err_out;
+    c->err_out = nullptr;
+    j.created_acc = c->d_created;
+    NRG_LAUNCH(c, "hm_small", hm_small_round_kernel, 1, SM_TPB, 0, c->stream, j, c->d_table, c->slot_shift,
+               (u64)(c->slots - 1), c->d_ctl);
+    return hipGetLastError();
+}
+
 __global__ __launch_bounds__(TPB) void hm_init_table_kernel(Slot* table, u64 slots) {
     for (u64 s = blockIdx.x * (u64)TPB + threadIdx.x; s < slots; s += (u64)gridDim.x * TPB) {
         u64x2 z;
@@ -1513,6 +1719,12 @@ hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool
     if (n > HM_MAX_BATCH) return hipErrorInvalidValue;
     const nrg_put* src = (const nrg_put*)src_recs;
     const bool want_prev = d_prev && resp_lo < lo + n && resp_hi > lo;
+    if (n <= c->small_max && n <= SM_W && R <= SM_R) {  // one launch, nothing deferred
+        hipError_t e = small_round(c, src, lo, n, write_ring, d_get_keys, R, d_get_vals, d_get_found, resp_lo, resp_hi,
+                                   want_prev ? d_prev : nullptr, d_prev_found);
+        c->rounds++;
+        return e;
+    }
     // records the deferred half reads: the caller's buffer only when no ring copy is written
     const nrg_put* keep = (src && !write_ring) ? src : nullptr;
     hipError_t e;

@@ -128,6 +128,7 @@ struct nrg_ctx {
     uint32_t sy_par = 0;      // synthetic: buffer parity of the next chunk
     uint32_t sy_round = 0;    // synthetic: chunks replayed (the epoch of the 32-bit seen-value test)
     int32_t comb_spin = -1;   // combiner knobs (NRG_KNOB_COMB_SPIN / _DEPTH): -1 / 0 = defaults
+    uint64_t small_max = 0;   // hashmap: rounds of <= small_max Puts take the one-launch small round
     uint32_t comb_depth = 0;
     uint64_t* d_created = nullptr;  // [HM_CREATED_SLOTS] keys created by replay rounds
     void* d_bk_ent = nullptr;       // [index tiles][tile] 16-B {id << 32 | i+1, value}

@@ -1148,6 +1148,10 @@ extern "C" int nrg_test_set_knob(nrg_ctx* c, int knob, uint64_t v) {
             if (!hm) return NRG_E_INVAL;
             c->sort_min = v;
             return NRG_OK;
+        case NRG_KNOB_SMALL_MAX:
+            if (!hm || v > 2048) return NRG_E_INVAL;
+            c->small_max = v;
+            return NRG_OK;
         case NRG_KNOB_COMB_SPIN:
             if (v > 4096) return NRG_E_INVAL;
             c->comb_spin = (int32_t)v;

@@ -33,8 +33,9 @@ def _check_state(dev, om):
     assert dev.hm_digest() == om.digest()
 
 
-# knobs of the replay paths: default selection, and sorted rounds forced for every size
-PATHS = {"default": {}, "sorted": {"SORT_MIN": 1}}
+# knobs of the replay paths: default selection, sorted rounds forced for every size, and the
+# one-launch small rounds (the combiner's) for rounds of up to 2048 Puts
+PATHS = {"default": {}, "sorted": {"SORT_MIN": 1}, "small": {"SMALL_MAX": 2048}}
 
 
 @pytest.mark.parametrize("path", list(PATHS))
@@ -183,6 +184,57 @@ def test_pipelined_rounds_back_to_back(nrg, orc, path):
         np.testing.assert_array_equal(got[r][0], want[r][0], err_msg=f"round {r} vals")
     dev.sync()
     _check_state(dev, om)
+
+
+@pytest.mark.parametrize("span", [40, 3000, 1 << 40])
+def test_small_rounds_device(nrg, orc, span):
+    """One-launch small rounds (hashmap.hip hm_small_round_kernel, the combiner's path):
+    previous values of every Put with duplicate keys in log order (span 40: every key many
+    times per round), the side-slot key, fresh claims, Gets after the round's writes, pipelined
+    and plain contexts, rounds at the size limits (2048 Puts, 8192 Gets) and past them."""
+    import torch
+
+    for pipeline in (0, 1):
+        dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, knobs={"SMALL_MAX": 2048}, log2_slots=15,
+                                max_batch=1 << 13, max_reads=1 << 14, pipeline=pipeline)
+        dev.use_torch_stream()
+        om = orc.HashMap()
+        dev.hm_prefill_range(min(span, 500), 1)
+        om.prefill_range(min(span, 500), 1)
+        for r, (W, R) in enumerate([(1, 0), (300, 700), (2048, 8192), (2049, 100), (0, 500), (1000, 8193), (17, 5)]):
+            keys = orc.gen_uniform(max(W, 1), 500 + r, span)[:W]
+            vals = orc.gen_raw(max(W, 1), 600 + r)[:W]
+            keys[::37] = EMPTY
+            gk = orc.gen_uniform(max(R, 1), 700 + r, span + 50)[:R]
+            gk[::41] = EMPTY
+            d_puts = torch.from_numpy(_puts(keys, vals).view(np.int64).copy()).cuda()
+            d_gk = torch.from_numpy(gk.view(np.int64).copy()).cuda()
+            d_gv = torch.full((max(R, 1),), -1, dtype=torch.int64, device="cuda")
+            d_gf = torch.full((max(R, 1),), 7, dtype=torch.uint8, device="cuda")
+            d_pv = torch.full((max(W, 1),), -1, dtype=torch.int64, device="cuda")
+            d_pf = torch.full((max(W, 1),), 7, dtype=torch.uint8, device="cuda")
+            dev.hm_round_device(d_puts, W, 1, d_gk, R, d_gv, d_gf, d_pv, d_pf)
+            dev.join()
+            torch.cuda.synchronize()
+            oprev, opf = om.replay(keys, vals)
+            ov, of = om.get_batch(gk)
+            np.testing.assert_array_equal(d_pf.cpu().numpy()[:W], opf, err_msg=f"round {r}")
+            np.testing.assert_array_equal(d_pv.cpu().numpy().view(np.uint64)[:W], oprev, err_msg=f"round {r}")
+            np.testing.assert_array_equal(d_gf.cpu().numpy()[:R], of, err_msg=f"round {r}")
+            np.testing.assert_array_equal(d_gv.cpu().numpy().view(np.uint64)[:R], ov, err_msg=f"round {r}")
+        dev.sync()
+        _check_state(dev, om)
+        dev.close()
+
+
+def test_small_round_table_full(nrg, orc):
+    """A small round that cannot claim a slot latches NRG_E_TABLE_FULL (as the other paths)."""
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, knobs={"SMALL_MAX": 2048}, log2_slots=8, max_batch=1024)
+    keys = orc.gen_uniform(300, 9, 1 << 40)
+    first = dev.log_append(_puts(keys, keys), 1)
+    with pytest.raises(Exception):
+        dev.log_exec(first, first + 300)
+    dev.close()
 
 
 def test_device_generator_matches_oracle(nrg, orc):
