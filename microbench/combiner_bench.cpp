@@ -9,6 +9,7 @@
 //            -Lnode-replication_amd/lib -lnrgpu -Wl,-rpath,$ORIGIN/../node-replication_amd/lib
 // Run:   ./microbench/combiner_bench [seconds [threads ops/call kind(0 hashmap, 1 stack)] ...]
 #include <sched.h>
+#include <sys/resource.h>
 
 #include <array>
 #include <atomic>
@@ -53,6 +54,7 @@ static int run(int threads, int batch, double secs, bool stack, int spin, int de
     std::atomic<bool> stop{false};
     std::atomic<int> err{0};
     std::vector<uint64_t> done(threads, 0);
+    std::atomic<uint64_t> usr_us{0}, sys_us{0};  // client threads' CPU time (getrusage per thread)
     std::vector<std::thread> th;
     for (int i = 0; i < threads; i++)
         th.emplace_back([&, i] {
@@ -88,6 +90,11 @@ static int run(int threads, int batch, double secs, bool stack, int spin, int de
                 n += batch;
             }
             done[i] = n;
+            rusage ru;
+            if (getrusage(RUSAGE_THREAD, &ru) == 0) {
+                usr_us += (uint64_t)ru.ru_utime.tv_sec * 1000000 + ru.ru_utime.tv_usec;
+                sys_us += (uint64_t)ru.ru_stime.tv_sec * 1000000 + ru.ru_stime.tv_usec;
+            }
         });
     const auto t0 = std::chrono::steady_clock::now();
     std::this_thread::sleep_for(std::chrono::duration<double>(secs));
@@ -100,6 +107,7 @@ static int run(int threads, int batch, double secs, bool stack, int spin, int de
     std::printf("%s threads %4d ops/call %3d spin %3d depth %d: %9.3f Mops/s  rounds %7llu  ops/round %7.1f  round rate %6.1f k/s%s\n",
                 stack ? "stack  " : "hashmap", threads, batch, spin, depth, tot / dt / 1e6, (unsigned long long)rounds,
                 rounds ? (double)ops / rounds : 0.0, rounds / dt / 1e3, err ? "  ERROR" : "");
+    std::printf("        clients' CPU: user %.2f s, system %.2f s\n", usr_us.load() / 1e6, sys_us.load() / 1e6);
     std::fflush(stdout);
     nrg_combiner_close(comb);
     nrg_close(ctx);

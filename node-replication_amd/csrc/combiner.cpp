@@ -59,6 +59,10 @@ void futex_wait(std::atomic<uint32_t>* w, uint32_t seen) {
     syscall(SYS_futex, (uint32_t*)w, FUTEX_WAIT_PRIVATE, seen, &ts, nullptr, 0);
 }
 void futex_wake_all(std::atomic<uint32_t>* w) { syscall(SYS_futex, (uint32_t*)w, FUTEX_WAKE_PRIVATE, INT32_MAX, nullptr, nullptr, 0); }
+void wake_one(std::atomic<uint32_t>* w) {
+    w->fetch_add(1, std::memory_order_seq_cst);
+    syscall(SYS_futex, (uint32_t*)w, FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
+}
 
 struct alignas(64) Batch {
     std::atomic<uint32_t> state{FREE};
@@ -66,9 +70,13 @@ struct alignas(64) Batch {
     alignas(64) std::atomic<uint32_t> writers{0};  // clients copying ops in
     std::atomic<uint32_t> readers{0};              // clients yet to copy their responses out
     std::atomic<uint32_t> nw{0}, nr{0};            // write records / reads reserved
-    alignas(64) std::atomic<uint32_t> wake{0};     // futex word: bumped when the round completes
-    std::atomic<uint32_t> sleepers{0};             // clients parked on it
-    std::atomic<uint32_t> bcast{0};                // a client has woken the parked ones
+    // Waiting clients take numbers 0, 1, 2, ... and park each on its own futex word wk[i], so
+    // wake-ups never contend on one kernel futex bucket (one word for the whole batch spent the
+    // job's CPU quota in the kernel at 128+ threads). They wake as a binary tree: the combiner
+    // thread wakes waiter 0 and waiter i wakes 2i+1 and 2i+2 -- off the combiner's path, and
+    // about log2(waiters) wake-up latencies for the last one.
+    alignas(64) std::atomic<uint32_t> nwait{0};
+    std::atomic<uint32_t>* wk = nullptr;  // [max_threads]
     int rc = NRG_OK;                               // launch or device error of the round
     // host buffers (mapped, coherent; device addresses equal the host ones under UVA)
     char* recs = nullptr;   // cap write records
@@ -148,6 +156,7 @@ void comb_free(nrg_combiner* m) {
         for (void* p : ps)
             if (p) (void)hipHostFree(p);
         if (x.done) (void)hipEventDestroy(x.done);
+        delete[] x.wk;
     }
     delete m;
 }
@@ -163,10 +172,7 @@ void retire(nrg_combiner* m) {
         if (x.rc == NRG_OK) x.rc = err_code(*(volatile uint32_t*)x.err);
         x.state.store(DONE, std::memory_order_release);
         m->completed.store(++k, std::memory_order_seq_cst);
-        x.wake.fetch_add(1, std::memory_order_seq_cst);
-        // one parked client only: waking the rest is that client's job, off this thread's path
-        if (x.sleepers.load(std::memory_order_seq_cst))
-            syscall(SYS_futex, (uint32_t*)&x.wake, FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
+        if (x.nwait.load(std::memory_order_seq_cst)) wake_one(&x.wk[0]);  // the root of the wake tree
     }
 }
 
@@ -226,7 +232,7 @@ bool advance(nrg_combiner* m) {
     y.nw.store(0, std::memory_order_relaxed);
     y.nr.store(0, std::memory_order_relaxed);
     y.rc = NRG_OK;
-    y.bcast.store(0, std::memory_order_relaxed);
+    y.nwait.store(0, std::memory_order_relaxed);
     y.round.store(k + 1, std::memory_order_relaxed);
     y.state.store(OPEN, std::memory_order_seq_cst);
     m->open.store(k + 1, std::memory_order_seq_cst);
@@ -280,15 +286,19 @@ int post_and_wait(nrg_combiner* m, uint32_t token, bool write, const void* ops, 
         const uint32_t seen = m->opened.load(std::memory_order_seq_cst);
         k = m->open.load(std::memory_order_seq_cst);
         x = &m->b[k % NB];
-        x->writers.fetch_add(1, std::memory_order_seq_cst);
-        if (x->state.load(std::memory_order_seq_cst) == OPEN && x->round.load(std::memory_order_relaxed) == k) {
+        // a sealed batch's `writers` is left alone: the combiner thread waits for it to reach 0,
+        // and hundreds of clients bumping it on every retry kept it from ever reaching 0
+        const bool open = x->state.load(std::memory_order_seq_cst) == OPEN &&
+                          x->round.load(std::memory_order_relaxed) == k;
+        if (open) x->writers.fetch_add(1, std::memory_order_seq_cst);
+        if (open && x->state.load(std::memory_order_seq_cst) == OPEN && x->round.load(std::memory_order_relaxed) == k) {
             off = (write ? x->nw : x->nr).fetch_add(n, std::memory_order_seq_cst);
             x->readers.fetch_add(1, std::memory_order_relaxed);
             if (in_b && ops) std::memcpy((write ? x->recs : x->reads) + (uint64_t)off * in_b, ops, (size_t)n * in_b);
             x->writers.fetch_sub(1, std::memory_order_release);
             break;
         }
-        x->writers.fetch_sub(1, std::memory_order_relaxed);
+        if (open) x->writers.fetch_sub(1, std::memory_order_relaxed);
         // the batch is sealed and the next one not open yet (the combiner waits for a slot's
         // clients to copy their responses out): do not take their cores, park until it opens
         if (spins < 64) {
@@ -305,22 +315,25 @@ int post_and_wait(nrg_combiner* m, uint32_t token, bool write, const void* ops, 
     }
     // wait for the round: spin (about a round) if a spinning slot is free (NRG_KNOB_COMB_SPIN;
     // none by default), else park on the batch's futex
-    const bool spin = m->spinning.fetch_add(1, std::memory_order_relaxed) < m->spin_cap;
-    if (!spin) m->spinning.fetch_sub(1, std::memory_order_relaxed);
+    const bool spin = m->spin_cap > 0 && m->spinning.fetch_add(1, std::memory_order_relaxed) < m->spin_cap;
+    if (m->spin_cap > 0 && !spin) m->spinning.fetch_sub(1, std::memory_order_relaxed);
+    uint32_t me = UINT32_MAX;  // this client's number among the batch's waiters
     for (uint32_t spins = 0; m->completed.load(std::memory_order_acquire) <= k; spins++) {
         if (spin && spins < 4096) {
             for (int i = 0; i < 8; i++) _mm_pause();
             continue;
         }
-        const uint32_t seen = x->wake.load(std::memory_order_seq_cst);
-        x->sleepers.fetch_add(1, std::memory_order_seq_cst);
-        if (m->completed.load(std::memory_order_seq_cst) <= k) futex_wait(&x->wake, seen);
-        x->sleepers.fetch_sub(1, std::memory_order_seq_cst);
+        if (me == UINT32_MAX) me = x->nwait.fetch_add(1, std::memory_order_seq_cst);
+        const uint32_t seen = x->wk[me].load(std::memory_order_seq_cst);
+        if (m->completed.load(std::memory_order_seq_cst) <= k) futex_wait(&x->wk[me], seen);
     }
     if (spin) m->spinning.fetch_sub(1, std::memory_order_relaxed);
-    // the first client past the wait wakes the batch's other parked clients
-    if (x->sleepers.load(std::memory_order_seq_cst) && !x->bcast.exchange(1, std::memory_order_acq_rel))
-        futex_wake_all(&x->wake);
+    // waiter `me` wakes its two children; every waiter that took a number does, parked or not,
+    // and a child that takes its number after the round completed sees it and does not park
+    if (me != UINT32_MAX) {
+        const uint32_t nw = x->nwait.load(std::memory_order_seq_cst);
+        for (uint32_t c = 2 * me + 1; c <= 2 * me + 2 && c < nw; c++) wake_one(&x->wk[c]);
+    }
     std::memcpy(out, (write ? x->wresp : x->rresp) + (uint64_t)off * out_b, (size_t)n * out_b);
     std::memcpy(some, (write ? x->wsome : x->rsome) + off, n);
     const int rc = x->rc;
@@ -363,6 +376,7 @@ extern "C" int nrg_combiner_open(nrg_ctx* ctx, uint32_t max_threads, nrg_combine
         ok = ok && (x.rsome = (uint8_t*)host_alloc(cap));
         ok = ok && (x.err = (uint32_t*)host_alloc(64));
         ok = ok && hipEventCreateWithFlags(&x.done, hipEventDisableTiming) == hipSuccess;
+        ok = ok && (x.wk = new (std::nothrow) std::atomic<uint32_t>[max_threads]());
         if (ok) *x.err = 0;
     }
     if (!ok) {
