@@ -1107,9 +1107,14 @@ __global__ __launch_bounds__(TPB) void hm_sr_apply_kernel(SortedJob j) {
 // A round of at most SM_W Puts and SM_R Gets, whole in one 1024-thread workgroup: the Puts are
 // hashed by key in LDS (how many, the last one); one thread per distinct key finds or claims
 // its slot, answers the previous values of the key's Puts in log order (the slot's value before
-// the round for the first; nr/examples/hashmap.rs:46-50) and stores the last value; then every
-// Get probes the table. No deferred half and no device atomics per Put: the combiner's
-// index + elector + reads launches (about 20 us of GPU time for a few hundred ops) become one.
+// the round for the first; nr/examples/hashmap.rs:46-50) and stores the last value. No deferred
+// half and no device atomics per Put: the combiner's index + elector + reads launches (about
+// 20 us of GPU time for a few hundred ops) become one.
+// The Gets do not wait for the Puts: a Get of a key the round Puts is answered from the LDS hash
+// (the key's last value), and for any other key the round changes nothing the Get reads -- a
+// present key's probe chain holds no empty slot, so claims (which fill empty slots) cannot
+// change where its chain ends, and only Put keys' values are stored. So every Get's table probe
+// is issued with the Put records, and resolves while the Puts claim and store.
 // Runs with no other round in flight (the caller flushes first). Keys present in the table are
 // present (quiescent: no claim in flight); fresh claims get epoch-1 stamps, as the elector's.
 constexpr int SM_TPB = 1024;
@@ -1129,6 +1134,8 @@ struct SmallJob {
     u64* created_acc;
 };
 
+__device__ __forceinline__ u32 sm_hash(u64 k) { return (u32)(mix64(k) >> 40) & (SM_HT - 1); }
+
 __global__ __launch_bounds__(SM_TPB) void hm_small_round_kernel(SmallJob j, Slot* table, u32 shift, u64 tmask,
                                                                 DevCtl* ctl) {
     __shared__ u64 s_val[SM_W];
@@ -1138,35 +1145,50 @@ __global__ __launch_bounds__(SM_TPB) void hm_small_round_kernel(SmallJob j, Slot
     __shared__ u32 s_last[SM_HT + 1];   // its last Put + 1
     __shared__ u32 s_created;
     const int tid = threadIdx.x;
+    constexpr int WQ = (int)(SM_W / SM_TPB), RQ = (int)(SM_R / SM_TPB);
+    // every Put record, every Get key and every Get's first probe in flight together
+    nrg_put r[WQ];
+#pragma unroll
+    for (int q = 0; q < WQ; q++) {
+        const u32 i = q * SM_TPB + tid;
+        r[q] = i < j.n ? j.rec.at(i) : nrg_put{EMPTY_KEY, 0};
+    }
+    u64 k[RQ], s[RQ];
+    u64x2 w[RQ];
+#pragma unroll
+    for (int q = 0; q < RQ; q++) {
+        const u32 i = q * SM_TPB + tid;
+        k[q] = i < j.R ? j.keys[i] : EMPTY_KEY;
+    }
+#pragma unroll
+    for (int q = 0; q < RQ; q++) {
+        const u32 i = q * SM_TPB + tid;
+        s[q] = table_home(k[q], shift);
+        w[q].x = EMPTY_KEY;
+        w[q].y = 0;
+        if (i < j.R && k[q] != EMPTY_KEY) w[q] = *(const u64x2*)&table[s[q]];
+    }
     for (int h = tid; h <= (int)SM_HT; h += SM_TPB) {
         if (h < (int)SM_HT) s_hk[h] = EMPTY_KEY;
         s_cnt[h] = 0;
         s_last[h] = 0;
     }
     if (tid == 0) s_created = 0;
-    nrg_put r[SM_W / SM_TPB];
-#pragma unroll
-    for (int q = 0; q < (int)(SM_W / SM_TPB); q++) {
-        const u32 i = q * SM_TPB + tid;
-        if (i < j.n) {
-            r[q] = j.rec.at(i);
-            if (j.ring_out) j.ring_out[(j.rec.lo + i) & j.rec.mask] = r[q];
-            s_val[i] = r[q].val;
-        }
-    }
     __syncthreads();
 #pragma unroll
-    for (int q = 0; q < (int)(SM_W / SM_TPB); q++) {
+    for (int q = 0; q < WQ; q++) {
         const u32 i = q * SM_TPB + tid;
         if (i >= j.n) continue;
-        const u64 k = r[q].key;
+        if (j.ring_out) j.ring_out[(j.rec.lo + i) & j.rec.mask] = r[q];
+        s_val[i] = r[q].val;
+        const u64 kk = r[q].key;
         u32 h = SM_HT;
-        if (k != EMPTY_KEY) {
-            h = (u32)(mix64(k) >> 40) & (SM_HT - 1);
+        if (kk != EMPTY_KEY) {
+            h = sm_hash(kk);
             for (;;) {  // at most SM_W keys in SM_HT entries: an entry is always found
                 const u64 old = atomicCAS((unsigned long long*)&s_hk[h], (unsigned long long)EMPTY_KEY,
-                                          (unsigned long long)k);
-                if (old == EMPTY_KEY || old == k) break;
+                                          (unsigned long long)kk);
+                if (old == EMPTY_KEY || old == kk) break;
                 h = (h + 1) & (SM_HT - 1);
             }
         }
@@ -1194,10 +1216,11 @@ __global__ __launch_bounds__(SM_TPB) void hm_small_round_kernel(SmallJob j, Slot
             }
         } else {
             bool fresh = false;
-            const u64 k = s_hk[h];
-            const long long sl = claim_slot(table, k, table_home(k, shift), tmask, &fresh);
+            const u64 kk = s_hk[h];
+            const long long sl = claim_slot(table, kk, table_home(kk, shift), tmask, &fresh);
             if (sl < 0) {
                 atomicOr(&ctl->err, ERR_TABLE_FULL);
+                s_cnt[h] = 0;  // the Gets of this key find it absent, as the other paths leave it
                 continue;
             }
             slot = &table[sl];
@@ -1234,29 +1257,30 @@ __global__ __launch_bounds__(SM_TPB) void hm_small_round_kernel(SmallJob j, Slot
         else ctl->sp.val = cur;
     }
     if (created) atomicAdd(&s_created, created);
-    __syncthreads();  // every store of the round before any Get
+    // Gets: keys of the round's Puts from the LDS hash (read only after the barrier: a full
+    // table zeroes the key's count above), every other key from its probe chain
+    const u64 sp_val = ctl->sp.val;
+    const bool sp_has = ctl->sp_claim != 0;
+    __syncthreads();
     if (tid == 0 && s_created) atomicAdd(&j.created_acc[0], (u64)s_created);
-    constexpr int RQ = (int)(SM_R / SM_TPB);
-    u64 k[RQ], s[RQ];
-    u64x2 w[RQ];
-#pragma unroll
-    for (int q = 0; q < RQ; q++) {
-        const u32 i = q * SM_TPB + tid;
-        k[q] = i < j.R ? j.keys[i] : EMPTY_KEY;
-        s[q] = table_home(k[q], shift);
-        w[q].x = EMPTY_KEY;
-        w[q].y = 0;
-        if (i < j.R && k[q] != EMPTY_KEY) w[q] = *(const u64x2*)&table[s[q]];
-    }
 #pragma unroll
     for (int q = 0; q < RQ; q++) {
         const u32 i = q * SM_TPB + tid;
         if (i >= j.R) continue;
         u64 v = 0;
         bool f = false;
-        if (k[q] == EMPTY_KEY) {
-            f = ctl->sp_claim != 0;
-            v = f ? ctl->sp.val : 0;
+        u32 h = SM_HT;
+        if (k[q] != EMPTY_KEY) {
+            h = sm_hash(k[q]);
+            while (s_hk[h] != k[q] && s_hk[h] != EMPTY_KEY) h = (h + 1) & (SM_HT - 1);
+            if (s_hk[h] != k[q]) h = SM_HT + 1;  // not a key of the round's Puts
+        }
+        if (h <= SM_HT && s_cnt[h]) {
+            f = true;
+            v = s_val[s_last[h] - 1];
+        } else if (k[q] == EMPTY_KEY) {
+            f = sp_has;
+            v = f ? sp_val : 0;
         } else {
             u64 kk = w[q].x, vv = w[q].y, sl = s[q];
             for (u64 pr = 0; pr <= tmask; pr++) {
