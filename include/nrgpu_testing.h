@@ -36,7 +36,8 @@ int nrg_test_debug_read(nrg_ctx* ctx, uint64_t* out, uint64_t words);
 #define NRG_KNOB_BK_ENT 5      /* hashmap: target entries per elector bucket (0: default)          */
 #define NRG_KNOB_EXP 6         /* diagnostic bits: phase timestamps (stack/synthetic 2, hashmap
                                   0x10000) and ablations that make RESULTS WRONG (hashmap bits
-                                  0xFF, 0xFF00; synthetic 1, 4, ...) -- measurement only            */
+                                  0xFF, 0xFF00; round-launch roles 0xF00000: no stamp atomics,
+                                  no apply, no index, no reads) -- measurement only              */
 #define NRG_KNOB_SY_SORT 7     /* synthetic: 1 = sort-based replay instead of the bucket path      */
 #define NRG_KNOB_PIPELINE 8    /* overrides nrg_config.pipeline                                    */
 #define NRG_KNOB_SORT_MIN 9    /* hashmap: rounds of at least this many Puts on an unskewed stream

@@ -320,12 +320,19 @@ struct StampJob {
     u32 nblocks;
     u32 epoch;
     u32* put_slot;  // [n] slot of each Put (SIDE_SLOT, FULL_SLOT)
+    u32* win;       // [n] = epoch: the Put took its slot's stamp (it was the largest so far)
+    u32* over;      // [n] = epoch: a later Put of the key took the stamp from it
     u64* created_acc;
+    // diagnostic ablations of a round launch (NRG_KNOB_EXP >> 20; RESULTS WRONG, timing only):
+    // 1 no stamp atomics, 2 no apply role, 4 no index role, 8 no read role
+    u32 exp;
 };
 struct ApplyJob {
     RecSrc rec;
     u64 n;
     const u32* put_slot;
+    const u32* win;
+    const u32* over;
     u32 epoch;
     u32 nblocks;
 };
@@ -429,11 +436,21 @@ __device__ __forceinline__ void stamp_index_role(const StampJob& j, u32 blk, Slo
     if (created) atomicAdd(&s_created, created);
     if (dup) atomicAdd(&s_dup, dup);
     __syncthreads();
-    // one stamp atomic per distinct slot of the block (a hot key costs one per block)
+    // one stamp atomic per distinct slot of the block (a hot key costs one per block). Its old
+    // value settles who stores: a Put that raised the stamp is the winner so far (win = e); if the
+    // stamp was already this round's, the Put it took it from is overtaken (over = e). So apply
+    // finds the last writer from two coalesced words per Put, not from a random read of the
+    // slot's stamp (n8: 31 us of apply for 800k Puts).
     for (int q = threadIdx.x; q < HT; q += TPB) {
         const u32 sl = s_slot[q];
-        if (sl != 0xFFFFFFFFu)
-            atomicMax((unsigned long long*)&table[sl].st[par], (unsigned long long)stamp_make(e, s_max[q]));
+        if (sl != 0xFFFFFFFFu && !(j.exp & 1)) {
+            const u64 mine = stamp_make(e, s_max[q]);
+            const u64 old = atomicMax((unsigned long long*)&table[sl].st[par], (unsigned long long)mine);
+            if (old < mine) {
+                j.win[s_max[q] - 1] = e;
+                if (stamp_epoch(old) == e && (u32)old) j.over[(u32)old - 1] = e;
+            }
+        }
     }
     if (threadIdx.x == 0) {
         if (s_side) atomicMax((unsigned long long*)&ctl->sp.st[par], (unsigned long long)stamp_make(e, s_side));
@@ -452,7 +469,7 @@ __device__ __forceinline__ void apply_role(const ApplyJob& j, u32 blk, Slot* tab
     if (s == SIDE_SLOT) {
         if (ctl->sp.st[par] == want) ctl->sp.val = j.rec.at(i).val;
     } else if (s != FULL_SLOT) {
-        if (table[s].st[par] == want) table[s].val = j.rec.at(i).val;
+        if (j.win[i] == j.epoch && j.over[i] != j.epoch) table[s].val = j.rec.at(i).val;
     }
 }
 
@@ -564,17 +581,18 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_num_sgpr(80))) void hm_r
     }
     const u32 nix = IX == IX_STAMP ? sj.nblocks : ij.nblocks;
     if (b < nix) {
+        if (sj.exp & 4) return;
         if constexpr (IX == IX_STAMP) stamp_index_role<K1>(sj, b, table, shift, tmask, ctl, s_lds);
         else index_role<K1, IX == IX_BUCKET>(ij, b, table, shift, tmask, s_lds);
         return;
     }
     b -= nix;
     if (b < aj.nblocks) {
-        apply_role(aj, b, table, ctl);
+        if (!(sj.exp & 2)) apply_role(aj, b, table, ctl);
         return;
     }
     b -= aj.nblocks;
-    read_role(rj, b, table, shift, tmask, ctl);
+    if (!(sj.exp & 8)) read_role(rj, b, table, shift, tmask, ctl);
 }
 
 // ---- hm_elect_kernel: last writer per key, claims of new keys, value stores -----------------------
@@ -1545,6 +1563,8 @@ static void attach_deferred(nrg_ctx* c, Launch& L) {
             L.aj.rec = rs;
             L.aj.n = p.n;
             L.aj.put_slot = c->d_put_slot[p.epoch & 1];
+            L.aj.win = L.aj.put_slot + c->stamp_alloc;
+            L.aj.over = L.aj.put_slot + 2 * c->stamp_alloc;
             L.aj.epoch = p.epoch;
             L.aj.nblocks = (u32)((p.n + TPB - 1) / TPB);
         }
@@ -1560,6 +1580,7 @@ static void launch_round(nrg_ctx* c, const Launch& L, u32 blocks, unsigned lds) 
 
 static hipError_t launch(nrg_ctx* c, Launch& L) {
     L.rj.nblocks = (u32)((L.rj.R + TPB * RPT - 1) / (TPB * RPT));
+    L.sj.exp = c->exp >> 20;
     const u32 nix = L.ix == IX_STAMP ? L.sj.nblocks : L.ij.nblocks;
     u32 blocks = nix + L.aj.nblocks + L.rj.nblocks;
     if (blocks == 0) return hipSuccess;
@@ -1629,8 +1650,12 @@ hipError_t hm_alloc(nrg_ctx* c, u64 mb) {
     if ((e = hipMalloc(&c->d_bk_key, ents * 8)) != hipSuccess) return e;
     if ((e = hipMalloc(&c->d_bk_cnt, (u64)HM_BK_MAX * tiles * sizeof(u32))) != hipSuccess) return e;
     if (c->stamp_max > mb) c->stamp_max = mb;
-    for (int i = 0; i < 2 && c->stamp_max; i++)
-        if ((e = hipMalloc(&c->d_put_slot[i], c->stamp_max * sizeof(u32))) != hipSuccess) return e;
+    // per parity: put_slot, win and over (stamp_max each; epoch tags, zeroed here and whenever
+    // the epochs restart, hm_renorm)
+    for (int i = 0; i < 2 && c->stamp_max; i++) {
+        if ((e = hipMalloc(&c->d_put_slot[i], 3 * c->stamp_max * sizeof(u32))) != hipSuccess) return e;
+        if ((e = hipMemsetAsync(c->d_put_slot[i], 0, 3 * c->stamp_max * sizeof(u32), c->stream)) != hipSuccess) return e;
+    }
     if ((e = hipMalloc(&c->d_dup, HM_DUP_SLOTS * sizeof(u64))) != hipSuccess) return e;
     if ((e = hipMemsetAsync(c->d_dup, 0, HM_DUP_SLOTS * sizeof(u64), c->stream)) != hipSuccess) return e;
     void* h = nullptr;
@@ -1682,6 +1707,9 @@ static hipError_t next_epoch(nrg_ctx* c, u32* e) {
         if (r != hipSuccess) return r;
         hm_renorm_kernel<<<grid_for(c->slots, 16384), TPB, 0, c->stream>>>(c->d_table, c->slots, c->d_ctl);
         if ((r = hipGetLastError()) != hipSuccess) return r;
+        for (int i = 0; i < 2 && c->d_put_slot[i]; i++)  // win / over epoch tags of the old epochs
+            if ((r = hipMemsetAsync(c->d_put_slot[i], 0, 3 * c->stamp_alloc * sizeof(u32), c->stream)) != hipSuccess)
+                return r;
         c->epoch = 1;
     }
     *e = ++c->epoch;
@@ -1774,6 +1802,8 @@ hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool
         L.sj.nblocks = (u32)((n + tile - 1) / tile);
         L.sj.epoch = epoch;
         L.sj.put_slot = c->d_put_slot[epoch & 1];
+        L.sj.win = L.sj.put_slot + c->stamp_alloc;
+        L.sj.over = L.sj.put_slot + 2 * c->stamp_alloc;
         L.sj.created_acc = c->d_created;
         L.sj.dup_acc = c->d_dup;
         attach_deferred(c, L);
