@@ -692,18 +692,18 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
             for (u32 j = a; j < z; j++) map[j - base] = (unsigned short)t;
         }
     };
-    u32 nent[SYB_PER], ngpos[SYB_PER];
+    u32 nent[SYB_PER];
+    // E position of touch i of the pass at `base` (its tile from the pass's map); recomputed
+    // where needed rather than kept per touch (frees 2 * SYB_PER registers for larger passes)
+    auto gpos_of = [&](u32 base, const unsigned short* map, u32 i) -> u32 {
+        const u32 t = map[i - base];
+        return t * tile_entries + s_off[t] + (i - s_pre[t]);
+    };
     auto load_pass = [&](u32 base, const unsigned short* map) {
 #pragma unroll
         for (int q = 0; q < SYB_PER; q++) {
             const u32 i = base + (u32)w * (SYB_PER * 64) + q * 64 + lane;
-            ngpos[q] = 0;
-            nent[q] = 0;
-            if (i < total) {
-                const u32 t = map[i - base];
-                ngpos[q] = t * tile_entries + s_off[t] + (i - s_pre[t]);
-                nent[q] = E[ngpos[q]];
-            }
+            nent[q] = i < total ? E[gpos_of(base, map, i)] : 0u;
         }
     };
     if (total) {
@@ -713,13 +713,13 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
     }
     // Software pipelined: the next pass's entries are in flight while this pass is ranked.
     for (u32 base = 0, pb = 0; base < total; base += SYB_PASS, pb ^= 1) {
-        u32 ent[SYB_PER], gpos[SYB_PER];
+        u32 ent[SYB_PER];
+        const unsigned short* cmap = s_tile[pb];
         u64 sv[SYB_PER];
         bool myset = false;
 #pragma unroll
         for (int q = 0; q < SYB_PER; q++) {
             ent[q] = nent[q];
-            gpos[q] = ngpos[q];
             myset |= ent_set(ent[q]);
         }
         SY_ACC(1);
@@ -775,7 +775,8 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
 #pragma unroll
             for (int q = 0; q < SYB_PER; q++) {
                 const bool isset = ent_set(ent[q]);  // 0 for touches past the end
-                const u64 op = (u64)(gpos[q] / tile_entries) * SYA_OPS + ent_op(ent[q]);
+                const u32 iq = base + (u32)w * (SYB_PER * 64) + q * 64 + lane;
+                const u64 op = iq < total ? (u64)cmap[iq - base] * SYA_OPS + ent_op(ent[q]) : 0ull;
                 sv[q] = isset ? ring[(lo + op) & ring_mask].tid : 0ull;
             }
             for (int ww = 0; ww < SYB_WAVES; ww++) {
@@ -820,11 +821,13 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
         if (v32) {
 #pragma unroll
             for (int q = 0; q < SYB_PER; q++)
-                if (base + (u32)w * (SYB_PER * 64) + q * 64 + lane < total) ((u32*)V)[gpos[q]] = (u32)sv[q];
+                if (base + (u32)w * (SYB_PER * 64) + q * 64 + lane < total)
+                    ((u32*)V)[gpos_of(base, cmap, base + (u32)w * (SYB_PER * 64) + q * 64 + lane)] = (u32)sv[q];
         } else {
 #pragma unroll
             for (int q = 0; q < SYB_PER; q++)
-                if (base + (u32)w * (SYB_PER * 64) + q * 64 + lane < total) V[gpos[q]] = sv[q];
+                if (base + (u32)w * (SYB_PER * 64) + q * 64 + lane < total)
+                    V[gpos_of(base, cmap, base + (u32)w * (SYB_PER * 64) + q * 64 + lane)] = sv[q];
         }
         SY_ACC(3);
     }
