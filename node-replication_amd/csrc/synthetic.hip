@@ -228,7 +228,8 @@ constexpr int SYA_TPB = 512, SYA_WAVES = SYA_TPB / 64, SYA_OROUNDS = 4;
 constexpr u32 SYA_OPS = SYA_WAVES * SYA_OROUNDS * 64;  // ops per tile (11 bits)
 constexpr u32 SY_MAX_NB = 512, SY_MAX_HOT = 16, SY_MAX_TILES = 4096, SY_MAX_CW = 8;
 #ifndef NRG_SYB_PER
-#define NRG_SYB_PER 8  // 1M-op rounds: 4 -> 63.2 us, 8 -> 62.4 us, 12 -> 100.5 us (VGPR cap)
+#define NRG_SYB_PER 10  // 1M-op rounds: 8 -> 57.2 us, 10 -> 56.4 (two passes per bucket, not three; E positions
+                        // recomputed, not kept per touch); 12 spills (profiles/r03_synth_pass_size.txt)
 #endif
 #ifndef NRG_SYB_XCD
 #define NRG_SYB_XCD 1  // 0: bucket = blockIdx.x (A/B builds)
