@@ -21,6 +21,7 @@ Prints ONE JSON line on rank 0.
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -222,23 +223,29 @@ class Env:
         """Barrier + sync, K steps, the replica's deferred work launched, sync + barrier; max over
         ranks of the wall time."""
         torch, dist = self.torch, self.dist
-        if self.world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t = time.perf_counter()
-        marks = [t]
-        for i in range(n):
-            step(i)
-            if i < 3:
-                marks.append(time.perf_counter())
-        rep.join()  # launches the last round's deferred apply + reads: inside the timed region
-        if host_s is not None:
-            host_s[0] = time.perf_counter() - t
-            host_s[1:] = [round((b - a) * 1e6, 2) for a, b in zip(marks, marks[1:])]
-        torch.cuda.synchronize()
-        if self.world > 1:
-            dist.barrier()
-        el = time.perf_counter() - t
+        # Python's cyclic GC runs on allocation counts: held off inside the timed region (a
+        # collection right before it made the first host call 50+ us: caches walked cold)
+        gc.disable()
+        try:
+            if self.world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            marks = [t]
+            for i in range(n):
+                step(i)
+                if i < 3:
+                    marks.append(time.perf_counter())
+            rep.join()  # launches the last round's deferred apply + reads: inside the timed region
+            if host_s is not None:
+                host_s[0] = time.perf_counter() - t
+                host_s[1:] = [round((b - a) * 1e6, 2) for a, b in zip(marks, marks[1:])]
+            torch.cuda.synchronize()
+            if self.world > 1:
+                dist.barrier()
+            el = time.perf_counter() - t
+        finally:
+            gc.enable()
         if self.world > 1:
             x = torch.tensor([el], dtype=torch.float64, device=self.dev)
             dist.all_reduce(x, op=dist.ReduceOp.MAX)
