@@ -1528,11 +1528,15 @@ static u32 k1_for(const nrg_ctx* c, u64 n) {
     return k;
 }
 
-// Stamp rounds: 2 Puts per index thread (B1: 1 and 2 measured equal in round 1, 4 slower;
-// Zipf rounds gain from fewer blocks per hot key). NRG_K1 overrides.
-static u32 stamp_k1_for(const nrg_ctx* c) {
+// Stamp rounds: 2 Puts per index thread, 4 for rounds of >= 640k Puts with at least as many
+// Gets (their read blocks, behind the index blocks, then start earlier). Measured K1 2 vs 4 in us
+// per round (profiles/r03_stamp_k1.txt): 200k Puts + 900k Gets 45.3 / 47.2, 400k + 900k 60.9 /
+// 66.0, 600k + 900k 83.7 / 84.7, 800k + 900k (the N = 8 per-GPU round) 110.3 / 100.4; without
+// that many Gets 4 loses (500k + 500k 60.8 / 66.6, 1M Puts 97.6 / 100.7, B1 36.2 / 39.7).
+// NRG_KNOB_K1 overrides.
+static u32 stamp_k1_for(const nrg_ctx* c, u64 n, u64 R) {
     if (c->k1_items) return c->k1_items >= 4 ? 4u : c->k1_items >= 2 ? 2u : 1u;
-    return 2u;
+    return n >= 655360 && R >= n ? 4u : 2u;
 }
 
 // The jobs of one hm_round_kernel launch.
@@ -1792,7 +1796,7 @@ hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool
             return e;
     } else if (stamp) {
         // ---- stamp round: one launch {index(e) | apply(e-1) | reads(e-1)} ----
-        const u32 K1 = stamp_k1_for(c);
+        const u32 K1 = stamp_k1_for(c, n, R);
         const u32 tile = TPB * K1;
         L.ix = IX_STAMP;
         L.K1 = K1;
