@@ -48,6 +48,10 @@
 namespace {
 
 constexpr uint32_t MAX_PENDING = 32;  // nr/src/context.rs:12 MAX_PENDING_OPS
+#ifndef NRG_WAKE_FAN
+#define NRG_WAKE_FAN 2
+#endif
+constexpr uint32_t WAKE_FAN = NRG_WAKE_FAN;  // children each woken waiter wakes (A/B builds)
 constexpr int NB = 6;                 // batch slots
 constexpr uint64_t DEPTH = 2;         // default rounds in flight (NRG_KNOB_COMB_DEPTH, <= NB - 2: a
                                       // slot's clients copy their responses out while later rounds run)
@@ -332,7 +336,7 @@ int post_and_wait(nrg_combiner* m, uint32_t token, bool write, const void* ops, 
     // and a child that takes its number after the round completed sees it and does not park
     if (me != UINT32_MAX) {
         const uint32_t nw = x->nwait.load(std::memory_order_seq_cst);
-        for (uint32_t c = 2 * me + 1; c <= 2 * me + 2 && c < nw; c++) wake_one(&x->wk[c]);
+        for (uint32_t c = WAKE_FAN * me + 1; c <= WAKE_FAN * me + WAKE_FAN && c < nw; c++) wake_one(&x->wk[c]);
     }
     std::memcpy(out, (write ? x->wresp : x->rresp) + (uint64_t)off * out_b, (size_t)n * out_b);
     std::memcpy(some, (write ? x->wsome : x->rsome) + off, n);

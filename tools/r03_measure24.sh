@@ -1,0 +1,9 @@
+#!/bin/bash
+# Round 3, session 2: combiner wake tree fan-out 2 vs 4 (alternating runs on one box).
+mkdir -p gpurun_out/m24
+C="2 16 32 0 -1 0  64 32 0 -1 0  128 32 0 -1 0  256 32 0 -1 0"
+for r in a b; do
+  timeout -k 10 150 ./microbench/combiner_bench $C > gpurun_out/m24/fan2_$r.txt 2>&1 || exit 1
+  timeout -k 10 150 ./microbench/combiner_bench_f4 $C > gpurun_out/m24/fan4_$r.txt 2>&1 || exit 1
+done
+for f in fan2_a fan4_a fan2_b fan4_b; do echo "== $f"; grep Mops gpurun_out/m24/$f.txt; done
