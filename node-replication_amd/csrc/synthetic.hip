@@ -234,11 +234,6 @@ constexpr u32 SY_MAX_NB = 512, SY_MAX_HOT = 16, SY_MAX_TILES = 4096, SY_MAX_CW =
 #ifndef NRG_SYB_XCD
 #define NRG_SYB_XCD 1  // 0: bucket = blockIdx.x (A/B builds)
 #endif
-#ifndef NRG_SY_VOP
-// 1: the bucket pass stores each seen value at its op's position in the tile (op * CW + k), so
-// the sums read V alone, coalesced, with no LDS adds and no second read of E (A/B builds)
-#define NRG_SY_VOP 0
-#endif
 #ifndef NRG_SY_BALLOT
 // 1: per-wave rankings by matching the key bit by bit with ballots (A/B builds). Measured slower
 // than the LDS peer masks: 75.7-76.0 vs 61.1-61.9 us per 1M-op round (profiles/r03_synth_rank_ab.txt)
@@ -270,7 +265,6 @@ __device__ __forceinline__ u32 ent_make(u32 xl, bool set, u32 k, u32 opl) {
 __device__ __forceinline__ u32 ent_word(u32 e) { return e & (SYB_WORDS - 1); }
 __device__ __forceinline__ bool ent_set(u32 e) { return (e >> 9) & 1u; }
 __device__ __forceinline__ u32 ent_op(u32 e) { return e >> 13; }
-__device__ __forceinline__ u32 ent_k(u32 e) { return (e >> 10) & 7u; }
 
 // x mod d for d < 2^32 with m = floor((2^64 - 1) / d): the quotient estimate is at most two low
 // (a software 64-bit division costs ~10x more: 10 us of a 1M-op partition pass)
@@ -706,11 +700,9 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
         const u32 t = map[i - base];
         return t * tile_entries + s_off[t] + (i - s_pre[t]);
     };
-    // where touch i's seen value goes: its E position, or (NRG_SY_VOP) its op's position
-    auto vpos_of = [&](u32 base, const unsigned short* map, u32 i, u32 e) -> u32 {
-        if (NRG_SY_VOP) return map[i - base] * tile_entries + ent_op(e) * (tile_entries / SYA_OPS) + ent_k(e);
-        return gpos_of(base, map, i);
-    };
+    // (measured and dropped: seen values stored at their op's position in the tile, op * CW + k,
+    // so the sums read V alone -- 89 vs 56.5 us per round: the scattered 4-B stores cost more
+    // than the second read of E; profiles/r03_synth_opmajor_dropped.txt)
     auto load_pass = [&](u32 base, const unsigned short* map) {
 #pragma unroll
         for (int q = 0; q < SYB_PER; q++) {
@@ -834,12 +826,12 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
 #pragma unroll
             for (int q = 0; q < SYB_PER; q++)
                 if (base + (u32)w * (SYB_PER * 64) + q * 64 + lane < total)
-                    ((u32*)V)[vpos_of(base, cmap, base + (u32)w * (SYB_PER * 64) + q * 64 + lane, ent[q])] = (u32)sv[q];
+                    ((u32*)V)[gpos_of(base, cmap, base + (u32)w * (SYB_PER * 64) + q * 64 + lane)] = (u32)sv[q];
         } else {
 #pragma unroll
             for (int q = 0; q < SYB_PER; q++)
                 if (base + (u32)w * (SYB_PER * 64) + q * 64 + lane < total)
-                    V[vpos_of(base, cmap, base + (u32)w * (SYB_PER * 64) + q * 64 + lane, ent[q])] = sv[q];
+                    V[gpos_of(base, cmap, base + (u32)w * (SYB_PER * 64) + q * 64 + lane)] = sv[q];
         }
         // the stores above read this pass's tile map (cmap); the next pass's map is built into
         // the other buffer, but the pass after that overwrites this one: every wave must be done
@@ -910,15 +902,7 @@ __device__ __forceinline__ void sy_sum_role(const SySumArgs& S, u32 blk, u64* s_
                     if (e0 + q * SYC_TPB < ne) atomicAdd((unsigned long long*)&s_sum[ent_op(ee[q])], (unsigned long long)vv[q]);
             }
         };
-        if (NRG_SY_VOP) {  // op-major seen values: op i's CW values are consecutive
-            const bool v32 = *S.v32 != 0;
-            for (u32 i = tid; i < nops; i += SYC_TPB) {
-                u64 a = 0;
-                const u64 p = tile * SYA_OPS * CW + (u64)i * CW;
-                for (u32 k = 0; k < CW; k++) a += v32 ? (u64)((const u32*)V)[p + k] : V[p + k];
-                s_sum[i] = a;
-            }
-        } else if (*S.v32) {
+        if (*S.v32) {
             add_all((const u32*)V + tile * SYA_OPS * CW);  // 4-B seen values (SyFlags)
         } else {
             add_all(V + tile * SYA_OPS * CW);
