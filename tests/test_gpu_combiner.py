@@ -18,9 +18,12 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def test_combiner_threads(nrg, orc):
-    T, ITERS, SPAN = 8, 40, 5000
-    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=18, max_batch=1 << 12, max_reads=1 << 12,
+@pytest.mark.parametrize("T,ITERS", [(8, 40), (64, 12)])
+def test_combiner_threads(nrg, orc, T, ITERS):
+    """T client threads; at 64 the rounds are larger, waiters wake through the futex tree and
+    rounds of up to 2048 Puts take the one-launch small rounds."""
+    SPAN = 5000
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=20, max_batch=1 << 12, max_reads=1 << 12,
                             log_bytes=64 * (1 << 16))
     dev.hm_prefill_range(1000, 1)  # keys 0..999 -> k + 1: thread 0's range starts with them
     comb = nrg.Combiner(dev, T)
