@@ -485,9 +485,10 @@ __device__ __forceinline__ bool resolve(u64 val, u64 st, const ReadJob& j, u64* 
 }
 
 // RPT Gets per thread, q = blk * TPB * RPT + r * TPB + tid: every key load and every home-line
-// load of the thread in flight together (fewer blocks: one dispatch wave of read blocks at B1)
+// load of the thread in flight together. Measured on one box (profiles/r03_read_rpt.txt), B1 per
+// round: RPT 1 34.4 us, 2 36.2, 4 39.8; the N=8 per-GPU round 99.3 / 100.8 / 105.4 us.
 #ifndef NRG_RPT
-#define NRG_RPT 2
+#define NRG_RPT 1
 #endif
 constexpr int RPT = NRG_RPT;
 
