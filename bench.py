@@ -219,6 +219,8 @@ class Env:
             else:
                 dist.init_process_group("gloo")
 
+    first_calls = []  # host us of the first step of every timed region of the process (diagnostic)
+
     def timed(self, n, step, rep, host_s=None):
         """Barrier + sync, K steps, the replica's deferred work launched, sync + barrier; max over
         ranks of the wall time."""
@@ -240,6 +242,8 @@ class Env:
             if host_s is not None:
                 host_s[0] = time.perf_counter() - t
                 host_s[1:] = [round((b - a) * 1e6, 2) for a, b in zip(marks, marks[1:])]
+            if len(marks) > 1:
+                Env.first_calls.append(round((marks[1] - marks[0]) * 1e6, 1))
             torch.cuda.synchronize()
             if self.world > 1:
                 dist.barrier()
@@ -496,6 +500,7 @@ def run_hashmap(args, env):
         "achieved_GBps": round(round_bytes / (elapsed / args.steps) / 1e9, 1),
         "host_enqueue_us": round(host_s[0] * 1e6 / args.steps, 2),
         "host_first_steps_us": host_s[1:],
+        "host_first_step_by_region_us": Env.first_calls,
         "distinct_get_keys": int(u_r),
         "distinct_put_keys": int(u_w),
     }
