@@ -1529,14 +1529,15 @@ static u32 k1_for(const nrg_ctx* c, u64 n) {
     return k;
 }
 
-// Stamp rounds: 2 Puts per index thread, 4 for rounds of >= 640k Puts with at least as many
-// Gets (their read blocks, behind the index blocks, then start earlier). Measured K1 2 vs 4 in us
-// per round (profiles/r03_stamp_k1.txt): 200k Puts + 900k Gets 45.3 / 47.2, 400k + 900k 60.9 /
-// 66.0, 600k + 900k 83.7 / 84.7, 800k + 900k (the N = 8 per-GPU round) 110.3 / 100.4; without
-// that many Gets 4 loses (500k + 500k 60.8 / 66.6, 1M Puts 97.6 / 100.7, B1 36.2 / 39.7).
-// NRG_KNOB_K1 overrides.
+// Stamp rounds: Puts per index thread by round size (one Get per read thread). K1 1 / 2 / 4 in us
+// per round (profiles/r03_stamp_k1.txt): 50k Puts + 950k Gets 31.4 / 32.0, B1 (100k + 900k)
+// 33.7 / 34.2 / 38.7, 200k + 800k 39.0 / 39.5, 200k + 900k 41.5 / 41.9, 400k + 900k 63.2 / 59.0,
+// 500k + 500k 62.5 / 58.3 / 63.8, 800k + 900k (the N = 8 per-GPU round) - / 106.6 / 98.9; at
+// 4 there the read blocks behind the index blocks start earlier, but without that many Gets 4
+// loses (1M Puts, 2M Puts). NRG_KNOB_K1 overrides.
 static u32 stamp_k1_for(const nrg_ctx* c, u64 n, u64 R) {
     if (c->k1_items) return c->k1_items >= 4 ? 4u : c->k1_items >= 2 ? 2u : 1u;
+    if (n <= (1u << 18)) return 1u;
     return n >= 655360 && R >= n ? 4u : 2u;
 }
 
