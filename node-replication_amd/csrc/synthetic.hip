@@ -246,6 +246,17 @@ constexpr int SYP_PD = NRG_SYP_PD;
 constexpr int SYB_TPB = 512, SYB_WAVES = SYB_TPB / 64, SYB_PER = NRG_SYB_PER;
 constexpr u32 SYB_PASS = SYB_TPB * SYB_PER;  // touches per pass of a bucket workgroup
 constexpr int SYC_TPB = 512;
+#ifndef NRG_SYS_T
+// tiles per sum workgroup (A/B builds). With 1 the 489 sum workgroups of a 1M-op chunk queue
+// behind the partition tiles for the launch's LDS slots (3 per CU) and end ~4 us after them;
+// 2 puts every workgroup of the launch on the chip at once but doubles each sum workgroup's
+// span: 58.3-58.6 vs 56.6-57.2 us per round (profiles/r03_synth_sum_tiles.txt)
+#define NRG_SYS_T 1
+#endif
+#ifndef NRG_SYS_U
+#define NRG_SYS_U 10  // touch entries per thread in flight before their LDS adds
+#endif
+constexpr int SYS_T = NRG_SYS_T, SYS_U = NRG_SYS_U;
 constexpr u32 NOTOUCH = 0xFFFFFFFFu;
 
 // Buckets of cold words (x relative to hot_reads). Cold word 0 has bucket 0 to itself: an op's
@@ -389,7 +400,7 @@ struct SySumArgs {
     u64 n, lo, resp_lo, resp_hi;
     u64* resp;
     uint8_t* some;
-    u32 tile0, want;
+    u32 tile0, tile1, want;  // response tiles [tile0, tile1), SYS_T per workgroup
     const SyHot* hot;
     u32 ntiles, HR, CW;
     u64* words;
@@ -410,7 +421,7 @@ struct SyPartLds {
             u32 words[SYA_WAVES][64 * CW];
         } r;
         u32 stage[SYA_OPS * CW];
-        u64 sum[SYA_OPS];
+        u64 sum[SYS_T * SYA_OPS];
     } u;
     SyHot hot[SYA_WAVES][SY_MAX_HOT];
     u32 part[SYA_WAVES];
@@ -877,16 +888,20 @@ __device__ __forceinline__ void sy_sum_role(const SySumArgs& S, u32 blk, u64* s_
     u64* dbg = (S.dbg && blk < SY_DBG_ROWS - SY_DBG_SUM && threadIdx.x == 0) ? S.dbg + (u64)(SY_DBG_SUM + blk) * 16 : nullptr;
     if (dbg) dbg[0] = wall_clock64();
     if (want) {
-        const u64 tile = tile0 + blk;
-        const u64 op0 = tile * SYA_OPS;
-        const u32 nops = (u32)(n - op0 < SYA_OPS ? n - op0 : SYA_OPS);
-        for (u32 i = tid; i < SYA_OPS; i += SYC_TPB) s_sum[i] = 0;
+        // SYS_T consecutive tiles: their entries are contiguous (TE per tile; only the chunk's
+        // last tile is partial), sums in s_sum[j * SYA_OPS + op]
+        const u32 t0 = tile0 + blk * SYS_T;
+        const u32 nt = S.tile1 - t0 < (u32)SYS_T ? S.tile1 - t0 : (u32)SYS_T;
+        const u64 op0 = (u64)t0 * SYA_OPS;
+        const u64 nops = n - op0 < (u64)nt * SYA_OPS ? n - op0 : (u64)nt * SYA_OPS;  // ops of the run
+        for (u32 i = tid; i < SYS_T * SYA_OPS; i += SYC_TPB) s_sum[i] = 0;
         __syncthreads();
-        const u32* Et = E + tile * SYA_OPS * CW;
-        const u32 ne = nops * CW;
+        const u32 TE = SYA_OPS * CW;
+        const u32* Et = E + (u64)t0 * TE;
+        // the run's entries: whole tiles of TE, then the last tile's nops % SYA_OPS ops
+        const u32 ne = (u32)(nops / SYA_OPS) * TE + (u32)(nops % SYA_OPS) * CW;
         // SYS_U entries per thread in flight before their LDS adds (one at a time, every add
         // waited for its own two loads: 8-10 us per workgroup)
-        constexpr int SYS_U = 10;
         auto add_all = [&](auto Vt) {
             for (u32 e0 = tid; e0 < ne; e0 += SYC_TPB * SYS_U) {
                 u32 ee[SYS_U];
@@ -898,14 +913,17 @@ __device__ __forceinline__ void sy_sum_role(const SySumArgs& S, u32 blk, u64* s_
                     vv[q] = e < ne ? (u64)Vt[e] : 0ull;
                 }
 #pragma unroll
-                for (int q = 0; q < SYS_U; q++)
-                    if (e0 + q * SYC_TPB < ne) atomicAdd((unsigned long long*)&s_sum[ent_op(ee[q])], (unsigned long long)vv[q]);
+                for (int q = 0; q < SYS_U; q++) {
+                    const u32 e = e0 + q * SYC_TPB;
+                    const u32 j = SYS_T == 1 ? 0u : SYS_T == 2 ? (u32)(e >= TE) : e / TE;
+                    if (e < ne) atomicAdd((unsigned long long*)&s_sum[j * SYA_OPS + ent_op(ee[q])], (unsigned long long)vv[q]);
+                }
             }
         };
         if (*S.v32) {
-            add_all((const u32*)V + tile * SYA_OPS * CW);  // 4-B seen values (SyFlags)
+            add_all((const u32*)V + (u64)t0 * TE);  // 4-B seen values (SyFlags)
         } else {
-            add_all(V + tile * SYA_OPS * CW);
+            add_all(V + (u64)t0 * TE);
         }
         __syncthreads();
         if (dbg) dbg[1] = wall_clock64();
@@ -1014,7 +1032,7 @@ static SySumArgs sy_sum_args(nrg_ctx* c, const SyDeferred& d) {
     const nrg_config& cf = c->cfg;
     SyAux x = sy_aux(c->d_sy_aux, cf);
     SySumArgs S{};
-    S.blocks = d.t1 - d.t0;
+    S.blocks = (d.t1 - d.t0 + SYS_T - 1) / SYS_T;
     S.E = x.E[d.par];
     S.V = x.V;
     S.n = d.n;
@@ -1024,6 +1042,7 @@ static SySumArgs sy_sum_args(nrg_ctx* c, const SyDeferred& d) {
     S.resp = d.resp;
     S.some = d.some;
     S.tile0 = d.t0;
+    S.tile1 = d.t1;
     S.want = d.want;
     S.hot = x.hot[d.par];
     S.ntiles = d.ntiles;
