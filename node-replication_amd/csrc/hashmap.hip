@@ -459,6 +459,11 @@ __device__ __forceinline__ void stamp_index_role(const StampJob& j, u32 blk, Slo
     }
 }
 
+#ifndef NRG_APPLY16
+// A/B builds: the elected writer stores {key, val} (16 B) instead of val (8 B). No change: 100 %
+// writes 97.6 us either way, configs[2]'s 4.5M-op round 413.4-414.2 (profiles/r03_apply_store_width.txt)
+#define NRG_APPLY16 0
+#endif
 // apply(e): per Put, the elected writer stores its value
 __device__ __forceinline__ void apply_role(const ApplyJob& j, u32 blk, Slot* table, DevCtl* ctl) {
     const u64 i = (u64)blk * TPB + threadIdx.x;
@@ -469,7 +474,17 @@ __device__ __forceinline__ void apply_role(const ApplyJob& j, u32 blk, Slot* tab
     if (s == SIDE_SLOT) {
         if (ctl->sp.st[par] == want) ctl->sp.val = j.rec.at(i).val;
     } else if (s != FULL_SLOT) {
-        if (j.win[i] == j.epoch && j.over[i] != j.epoch) table[s].val = j.rec.at(i).val;
+        if (j.win[i] == j.epoch && j.over[i] != j.epoch) {
+#if NRG_APPLY16
+            const nrg_put r = j.rec.at(i);  // {key, val} in one 16-B store (the key is the slot's own)
+            u64x2 kv;
+            kv.x = r.key;
+            kv.y = r.val;
+            *(u64x2*)&table[s] = kv;
+#else
+            table[s].val = j.rec.at(i).val;
+#endif
+        }
     }
 }
 
