@@ -410,6 +410,7 @@ def run_hashmap(args, env):
     gv_p, gf_p, pv_p, pf_p = gvals.data_ptr(), gfound.data_ptr(), pvals.data_ptr(), pfound.data_ptr()
     gathered = {}
     mode = {"prev": False, "n": 0}
+    seg_lens = [W] * world
 
     def step(i):
         p = i % P
@@ -419,7 +420,10 @@ def run_hashmap(args, env):
             pgroup.round(pp, W, gp, R, gv_p, gf_p, pv_p if prev else None, pf_p if prev else None)
         elif cgroup is not None:
             pp, gp = ptrs[p]
-            cgroup.round_async(pp, W, pv_p if prev else None, pf_p if prev else None, gp, R, gv_p, gf_p)
+            # every rank's segment is W records: seg_lens keeps the round stream ordered (no length
+            # exchange); the round header still checks it on every rank
+            cgroup.round_async(pp, W, pv_p if prev else None, pf_p if prev else None, gp, R, gv_p, gf_p,
+                               seg_lens=seg_lens)
         elif group is None:
             pp, gp = ptrs[p]
             rc = round_fn(h, pp, W, rank + 1, gp, R, gv_p, gf_p, pv_p if prev else None, pf_p if prev else None)
@@ -601,12 +605,13 @@ def run_synthetic(args, env):
     rps = [(r.data_ptr(), s_.data_ptr()) for r, s_ in zip(resps, somes)]
     gathered = {}
     mode = {"n": 0}
+    seg_lens = [N] * world
 
     def step(i):
         p = i % P
         r_p, s_p = rps[i & 1]
         if cgroup is not None:
-            cgroup.round_async(ptrs[p], N, r_p, s_p)
+            cgroup.round_async(ptrs[p], N, r_p, s_p, seg_lens=seg_lens)
         elif group is None:
             # Replica::combine of the batch: Log::append fused into the partition pass
             rc = round_fn(h, ptrs[p], N, rank + 1, r_p, s_p)
@@ -705,12 +710,13 @@ def run_stack(args, env):
     rps = [(r.data_ptr(), s_.data_ptr()) for r, s_ in zip(resps, somes)]
     gathered = {}
     mode = {"n": 0}
+    seg_lens = [N] * world
 
     def step(i):
         p = i % P
         r_p, s_p = rps[i & 1]
         if cgroup is not None:
-            cgroup.round_async(ptrs[p], N, r_p, s_p)
+            cgroup.round_async(ptrs[p], N, r_p, s_p, seg_lens=seg_lens)
         elif group is None:
             # Replica::combine of the batch: Log::append fused into the replay pass
             rc = round_fn(h, ptrs[p], N, rank + 1, r_p, s_p)

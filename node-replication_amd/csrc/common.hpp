@@ -17,6 +17,7 @@ constexpr u64 EMPTY_KEY = ~0ull;
 // Device error bits latched in DevCtl::err and reported by nrg_sync.
 constexpr u32 ERR_TABLE_FULL = 1u;
 constexpr u32 ERR_CAPACITY = 4u;
+constexpr u32 ERR_GROUP = 8u;  // a replica group's ranks disagreed on a round's segment lengths (group.cpp)
 
 // Counters of keys created by replay rounds (elector blocks add to slot blk % HM_CREATED_SLOTS).
 constexpr u64 HM_CREATED_SLOTS = 8192;

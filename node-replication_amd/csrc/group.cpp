@@ -103,6 +103,15 @@ struct Member {
     std::vector<uint64_t> hcnt;  // [nranks][2 * nranks + XW_N] counts, capacities, flags
     uint64_t xwords[8] = {};     // this rank's host words of the exchange
     hipEvent_t pt_ev = nullptr;
+    // Round headers and the length exchange (allocated at join, so a round cannot fail on them):
+    //   hdr[b]  {n, fingerprint of seg_lens} sent with round b's segment; ghdr[b] every rank's
+    //   lx      {n, local error} for a round whose lengths are exchanged; glx every rank's
+    uint64_t* hdr[NBUF] = {};
+    uint64_t* ghdr[NBUF] = {};
+    uint64_t* lx = nullptr;
+    uint64_t* glx = nullptr;
+    uint64_t* h_glx = nullptr;  // pinned host copy of glx
+    void* xmem = nullptr;
 };
 
 int hip_rc(hipError_t e) { return e == hipSuccess ? NRG_OK : (e == hipErrorOutOfMemory ? NRG_E_NOMEM : NRG_E_HIP); }
@@ -113,7 +122,44 @@ int hip_rc(hipError_t e) { return e == hipSuccess ? NRG_OK : (e == hipErrorOutOf
         if (_e != hipSuccess) return hip_rc(_e); \
     } while (0)
 
-int member_init(Member& m) {
+#define RCHK(x)                                   \
+    do {                                          \
+        int _r = (x);                             \
+        if (_r != NRG_OK) return _r;              \
+    } while (0)
+
+int grow(Member& m, PtBuf k, uint64_t bytes) {
+    DBuf& d = m.pt[k];
+    if (d.bytes >= bytes) return NRG_OK;
+    GCHK(hipStreamSynchronize(m.cstream));
+    GCHK(hipStreamSynchronize(m.ctx->stream));
+    if (d.p) GCHK(hipFree(d.p));
+    d.p = nullptr;
+    d.bytes = 0;
+    uint64_t b = bytes < 4096 ? 4096 : bytes + bytes / 4;  // headroom: rounds vary in size
+    GCHK(hipMalloc(&d.p, b));
+    d.bytes = b;
+    return NRG_OK;
+}
+
+// `to` waits for the work queued on `from` so far
+int order(Member& m, hipStream_t from, hipStream_t to) {
+    GCHK(hipEventRecord(m.pt_ev, from));
+    GCHK(hipStreamWaitEvent(to, m.pt_ev, 0));
+    return NRG_OK;
+}
+
+// Exchange words per rank (u64) of a partitioned round: [0, G) Puts per owner, [G, 2G) Gets per
+// owner, then
+enum : uint64_t {
+    XW_PREV = 0,    // 1 when this rank wants its Puts' previous values
+    XW_RP_CAP = 1,  // received Puts its buffers hold now
+    XW_RK_CAP = 2,  // received Get keys its buffers hold now
+    XW_ERR = 3,     // -NRG_E_* of a local failure before the exchange, else 0
+    XW_N = 4,
+};
+
+int member_init(Member& m, int nranks) {
     int r = nrg::ctx_use_device(m.ctx);
     if (r) return r;
     GCHK(hipStreamCreateWithFlags(&m.cstream, hipStreamNonBlocking));
@@ -123,7 +169,45 @@ int member_init(Member& m) {
         GCHK(hipEventCreateWithFlags(&m.gathered[b], hipEventDisableTiming));
         GCHK(hipEventCreateWithFlags(&m.freed[b], hipEventDisableTiming));
     }
+    const uint64_t G = (uint64_t)nranks;
+    GCHK(hipMalloc(&m.xmem, (NBUF * (2 + 2 * G) + 2 + 2 * G) * 8));
+    uint64_t* x = (uint64_t*)m.xmem;
+    for (int b = 0; b < NBUF; b++, x += 2 + 2 * G) {
+        m.hdr[b] = x;
+        m.ghdr[b] = x + 2;
+    }
+    m.lx = x;
+    m.glx = x + 2;
+    GCHK(hipHostMalloc(&m.h_glx, 2 * G * 8, hipHostMallocDefault));
+    // the fixed-size buffers of a partitioned round's count and status exchanges
+    const uint64_t CW = 2 * G + XW_N;
+    if ((r = grow(m, PB_CNT, CW * 8)) || (r = grow(m, PB_ALLCNT, G * CW * 8)) || (r = grow(m, PB_ST, 8)) ||
+        (r = grow(m, PB_ALLST, G * 8)))
+        return r;
     return NRG_OK;
+}
+
+// Round header check (on the comm stream, after the all-gather): every rank's {n, fingerprint}
+// must match this rank's view of the round. A mismatch latches ERR_GROUP in the replica, which
+// nrg_sync / nrg_group_sync report as NRG_E_INVAL.
+struct LensArg {
+    uint64_t v[64];
+};
+__global__ void grp_check_kernel(const uint64_t* ghdr, uint32_t G, LensArg lens, uint64_t fp, uint32_t* err) {
+    const uint32_t r = threadIdx.x;
+    if (r < G && (ghdr[2 * r] != lens.v[r] || ghdr[2 * r + 1] != fp)) atomicOr(err, nrg::ERR_GROUP);
+}
+
+// dst[0] = a, dst[1] = b in stream order (kernel arguments are captured at launch)
+__global__ void grp_put2_kernel(uint64_t* dst, uint64_t a, uint64_t b) {
+    if (threadIdx.x < 2) dst[threadIdx.x] = threadIdx.x ? b : a;
+}
+
+// fingerprint of a round's segment lengths (every rank must pass the same ones)
+uint64_t lens_fp(const std::vector<uint64_t>& lens) {
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ lens.size();
+    for (uint64_t l : lens) h = nrg::mix64(h ^ l) + 0x632BE59BD9B4E019ull;
+    return h;
 }
 
 void member_free(Member& m, const Rccl* R) {
@@ -137,6 +221,8 @@ void member_free(Member& m, const Rccl* R) {
         if (m.freed[b]) (void)hipEventDestroy(m.freed[b]);
     }
     if (m.sbuf) (void)hipFree(m.sbuf);
+    if (m.xmem) (void)hipFree(m.xmem);
+    if (m.h_glx) (void)hipHostFree(m.h_glx);
     for (DBuf& d : m.pt)
         if (d.p) (void)hipFree(d.p);
     if (m.pt_ev) (void)hipEventDestroy(m.pt_ev);
@@ -188,7 +274,7 @@ int nrg_group_join(nrg_ctx* replica, const uint8_t id[NRG_GROUP_ID_BYTES], int n
     Member& m = g->m[0];
     m.ctx = replica;
     m.rank = rank;
-    int r = member_init(m);
+    int r = member_init(m, nranks);
     ncclUniqueId u;
     std::memcpy(&u, id, NRG_GROUP_ID_BYTES);
     if (r == NRG_OK && R->init_rank(&m.comm, nranks, u, rank) != ncclSuccess) r = NRG_E_COMM;
@@ -219,7 +305,7 @@ int nrg_group_open(const int* devices, int n, const nrg_config* cfg, nrg_group**
         c.replica_id = (uint32_t)i + 1;  // Log::register hands out ids from 1 (nr/src/log.rs:272-292)
         r = nrg_open(devices[i], &c, &g->m[i].ctx);
         g->m[i].rank = i;
-        if (r == NRG_OK) r = member_init(g->m[i]);
+        if (r == NRG_OK) r = member_init(g->m[i], n);
     }
     if (r == NRG_OK) {
         std::vector<ncclComm_t> comms(n);
@@ -267,43 +353,96 @@ int nrg_group_set_input_stream(nrg_group* g, int member, void* s) {
     return NRG_OK;
 }
 
+// Every rank's segment length of a round whose caller gave none (seg_lens == NULL, one member per
+// process): each rank all-gathers {n, local error} and the host reads them back (one host round
+// trip). A rank whose own part is bad makes every rank return NRG_E_INVAL, so no rank is left
+// inside a collective its peers never post.
+static int exchange_lengths(nrg_group* g, const nrg_round* rounds, const std::vector<int>& bad,
+                            std::vector<uint64_t>& lens) {
+    const Rccl* R = g->R;
+    const int nl = (int)g->m.size(), G = g->nranks;
+    for (int i = 0; i < nl; i++) {
+        Member& m = g->m[i];
+        RCHK(nrg::ctx_use_device(m.ctx));
+        grp_put2_kernel<<<1, 64, 0, m.cstream>>>(m.lx, rounds[i].n, bad[i] ? 1 : 0);
+        GCHK(hipGetLastError());
+    }
+    if (R->group_start() != ncclSuccess) return NRG_E_COMM;
+    ncclResult_t res = ncclSuccess;
+    for (int i = 0; i < nl && res == ncclSuccess; i++)
+        res = R->all_gather(g->m[i].lx, g->m[i].glx, 2, ncclUint64, g->m[i].comm, g->m[i].cstream);
+    if (R->group_end() != ncclSuccess || res != ncclSuccess) return NRG_E_COMM;
+    for (int i = 0; i < nl; i++) {
+        Member& m = g->m[i];
+        RCHK(nrg::ctx_use_device(m.ctx));
+        GCHK(hipMemcpyAsync(m.h_glx, m.glx, 2 * (uint64_t)G * 8, hipMemcpyDeviceToHost, m.cstream));
+        GCHK(hipStreamSynchronize(m.cstream));
+    }
+    const uint64_t* H = g->m[0].h_glx;  // identical on every rank
+    bool any_bad = false;
+    for (int r = 0; r < G; r++) {
+        lens[r] = H[2 * r];
+        any_bad |= H[2 * r + 1] != 0;
+    }
+    return any_bad ? NRG_E_INVAL : NRG_OK;
+}
+
 int nrg_group_round_async(nrg_group* g, const nrg_round* rounds, const uint64_t* seg_lens) {
     if (!g || !rounds) return NRG_E_INVAL;
     const Rccl* R = g->R;
     if (!R) return NRG_E_COMM;
-    const int nl = (int)g->m.size();
+    const int nl = (int)g->m.size(), G = g->nranks;
     const uint32_t kind = g->m[0].ctx->cfg.ds_kind;
     const uint64_t rb = g->m[0].ctx->rec_bytes;
     // every rank's segment length, in rank order
-    std::vector<uint64_t> lens(g->nranks);
-    for (int r = 0; r < g->nranks; r++) {
-        if (seg_lens) lens[r] = seg_lens[r];
-        else if (nl == g->nranks) lens[r] = rounds[r].n;
-        else lens[r] = rounds[0].n;
+    std::vector<uint64_t> lens(G);
+    std::vector<int> bad(nl, 0);
+    for (int i = 0; i < nl; i++)
+        bad[i] = g->m[i].ctx->cfg.ds_kind != kind || (rounds[i].n && !rounds[i].recs);
+    // Three ways to know them:
+    //   whole   this process drives every rank: the members' n (or seg_lens, checked against them)
+    //   given   seg_lens from the caller, who promises every rank passes the same array: a header
+    //           {n, fingerprint of seg_lens} travels with each segment and a kernel on the comm
+    //           stream compares it with this rank's view (mismatch -> NRG_E_INVAL at the next sync)
+    //   exchanged  seg_lens == NULL: exchange_lengths (one host round trip)
+    const bool whole = nl == G;
+    const bool given = !whole && seg_lens;
+    if (whole) {
+        for (int i = 0; i < nl; i++) {
+            const uint64_t n = rounds[i].n;
+            if (bad[i] || (seg_lens && seg_lens[g->m[i].rank] != n)) return NRG_E_INVAL;
+            lens[g->m[i].rank] = n;
+        }
+    } else if (given) {
+        for (int r = 0; r < G; r++) lens[r] = seg_lens[r];
+        for (int i = 0; i < nl; i++) bad[i] |= rounds[i].n != lens[g->m[i].rank];
+    } else {
+        RCHK(exchange_lengths(g, rounds, bad, lens));
     }
     uint64_t stride = 0;
     for (uint64_t l : lens) stride = l > stride ? l : stride;
-    for (int i = 0; i < nl; i++) {
-        const nrg_round& x = rounds[i];
-        if (g->m[i].ctx->cfg.ds_kind != kind || x.n != lens[g->m[i].rank] || (x.n && !x.recs)) return NRG_E_INVAL;
-    }
-    std::vector<uint32_t> origins(g->nranks);
-    for (int r = 0; r < g->nranks; r++) origins[r] = (uint32_t)r + 1;
+    const uint64_t fp = lens_fp(lens);
+    LensArg la{};
+    for (int r = 0; r < G; r++) la.v[r] = lens[r];
+    std::vector<uint32_t> origins(G);
+    for (int r = 0; r < G; r++) origins[r] = (uint32_t)r + 1;
     const int b = (int)(g->round % NBUF);
     const uint64_t seg_bytes = stride * rb;
     std::vector<const void*> send(nl);
-    if (stride) {
+    if (stride || given) {
         for (int i = 0; i < nl; i++) {
             Member& m = g->m[i];
             const nrg_round& x = rounds[i];
-            int r = nrg::ctx_use_device(m.ctx);
-            if (r) return r;
+            RCHK(nrg::ctx_use_device(m.ctx));
             // the all-gather reads the caller's segment: ordered after its producer
             GCHK(hipEventRecord(m.in_ev, m.in_set ? m.in_stream : m.ctx->stream));
             GCHK(hipStreamWaitEvent(m.cstream, m.in_ev, 0));
             // and it overwrites gathered buffer b: ordered after the replay that read it
             if (m.used[b]) GCHK(hipStreamWaitEvent(m.cstream, m.freed[b], 0));
-            const uint64_t need = (uint64_t)g->nranks * seg_bytes;
+            if (given) grp_put2_kernel<<<1, 64, 0, m.cstream>>>(m.hdr[b], bad[i] ? ~0ull : x.n, fp);
+            GCHK(hipGetLastError());
+            if (!stride) continue;
+            const uint64_t need = (uint64_t)G * seg_bytes;
             if (m.gbytes[b] < need) {
                 GCHK(hipStreamSynchronize(m.cstream));
                 if (m.gbuf[b]) GCHK(hipFree(m.gbuf[b]));
@@ -312,9 +451,9 @@ int nrg_group_round_async(nrg_group* g, const nrg_round* rounds, const uint64_t*
                 GCHK(hipMalloc(&m.gbuf[b], need));
                 m.gbytes[b] = need;
             }
-            if (x.n == stride) {
+            if (x.n == stride && !bad[i]) {
                 send[i] = x.recs;
-            } else {  // pad a short segment to the common stride
+            } else {  // pad a short segment to the common stride (a bad one sends zeros)
                 if (m.sbytes < seg_bytes) {
                     GCHK(hipStreamSynchronize(m.cstream));
                     if (m.sbuf) GCHK(hipFree(m.sbuf));
@@ -323,8 +462,9 @@ int nrg_group_round_async(nrg_group* g, const nrg_round* rounds, const uint64_t*
                     GCHK(hipMalloc(&m.sbuf, seg_bytes));
                     m.sbytes = seg_bytes;
                 }
-                if (x.n) GCHK(hipMemcpyAsync(m.sbuf, x.recs, x.n * rb, hipMemcpyDeviceToDevice, m.cstream));
-                GCHK(hipMemsetAsync((char*)m.sbuf + x.n * rb, 0, seg_bytes - x.n * rb, m.cstream));
+                const uint64_t keep = bad[i] ? 0 : x.n;
+                if (keep) GCHK(hipMemcpyAsync(m.sbuf, x.recs, keep * rb, hipMemcpyDeviceToDevice, m.cstream));
+                GCHK(hipMemsetAsync((char*)m.sbuf + keep * rb, 0, seg_bytes - keep * rb, m.cstream));
                 send[i] = m.sbuf;
             }
         }
@@ -332,31 +472,45 @@ int nrg_group_round_async(nrg_group* g, const nrg_round* rounds, const uint64_t*
         ncclResult_t res = ncclSuccess;
         for (int i = 0; i < nl && res == ncclSuccess; i++) {
             Member& m = g->m[i];
-            res = R->all_gather(send[i], m.gbuf[b], seg_bytes / 8, ncclUint64, m.comm, m.cstream);
+            if (given) res = R->all_gather(m.hdr[b], m.ghdr[b], 2, ncclUint64, m.comm, m.cstream);
+            if (stride && res == ncclSuccess)
+                res = R->all_gather(send[i], m.gbuf[b], seg_bytes / 8, ncclUint64, m.comm, m.cstream);
         }
         if (R->group_end() != ncclSuccess || res != ncclSuccess) return NRG_E_COMM;
+        if (given)
+            for (int i = 0; i < nl; i++) {
+                Member& m = g->m[i];
+                RCHK(nrg::ctx_use_device(m.ctx));
+                grp_check_kernel<<<1, 64, 0, m.cstream>>>(m.ghdr[b], (uint32_t)G, la, fp, &m.ctx->d_ctl->err);
+                GCHK(hipGetLastError());
+            }
     }
+    int rc = NRG_OK;
     for (int i = 0; i < nl; i++) {
         Member& m = g->m[i];
         const nrg_round& x = rounds[i];
         nrg_ctx* c = m.ctx;
-        int r = nrg::ctx_use_device(c);
-        if (r) return r;
+        RCHK(nrg::ctx_use_device(c));
+        if (bad[i]) {  // took part in the collectives, replays nothing
+            rc = NRG_E_INVAL;
+            continue;
+        }
         if (stride) {
             GCHK(hipEventRecord(m.gathered[b], m.cstream));
             GCHK(hipStreamWaitEvent(c->stream, m.gathered[b], 0));
         }
+        int r = NRG_OK;
         if (kind == NRG_DS_HASHMAP) {
             if (stride)
-                r = nrg_hashmap_round_segments_async(c, (const nrg_put*)m.gbuf[b], (uint32_t)g->nranks, stride,
-                                                     lens.data(), origins.data(), (uint32_t)m.rank, x.get_keys,
-                                                     x.n_gets, x.get_vals, x.get_found, (uint64_t*)x.resp, x.some);
+                r = nrg_hashmap_round_segments_async(c, (const nrg_put*)m.gbuf[b], (uint32_t)G, stride, lens.data(),
+                                                     origins.data(), (uint32_t)m.rank, x.get_keys, x.n_gets,
+                                                     x.get_vals, x.get_found, (uint64_t*)x.resp, x.some);
             else
                 r = nrg_hashmap_round_async(c, nullptr, 0, origins[m.rank], x.get_keys, x.n_gets, x.get_vals,
                                             x.get_found, nullptr, nullptr);
         } else if (stride) {
-            std::vector<uint64_t> firsts(g->nranks);
-            r = nrg_log_append_segments_async(c, m.gbuf[b], (uint32_t)g->nranks, stride, lens.data(), origins.data(),
+            std::vector<uint64_t> firsts(G);
+            r = nrg_log_append_segments_async(c, m.gbuf[b], (uint32_t)G, stride, lens.data(), origins.data(),
                                               firsts.data());
             if (r == NRG_OK)
                 r = nrg_log_exec_async(c, firsts[m.rank], firsts[m.rank] + lens[m.rank], x.resp, x.some);
@@ -368,46 +522,12 @@ int nrg_group_round_async(nrg_group* g, const nrg_round* rounds, const uint64_t*
         }
     }
     g->round++;
-    return NRG_OK;
+    return rc;
 }
 
 // ---- cnr-style key-partitioned rounds (cnr/src/replica.rs:430-445, :673-736) ----
 
-static int grow(Member& m, PtBuf k, uint64_t bytes) {
-    DBuf& d = m.pt[k];
-    if (d.bytes >= bytes) return NRG_OK;
-    GCHK(hipStreamSynchronize(m.cstream));
-    GCHK(hipStreamSynchronize(m.ctx->stream));
-    if (d.p) GCHK(hipFree(d.p));
-    d.p = nullptr;
-    d.bytes = 0;
-    uint64_t b = bytes < 4096 ? 4096 : bytes + bytes / 4;  // headroom: rounds vary in size
-    GCHK(hipMalloc(&d.p, b));
-    d.bytes = b;
-    return NRG_OK;
-}
 
-// `to` waits for the work queued on `from` so far
-static int order(Member& m, hipStream_t from, hipStream_t to) {
-    GCHK(hipEventRecord(m.pt_ev, from));
-    GCHK(hipStreamWaitEvent(to, m.pt_ev, 0));
-    return NRG_OK;
-}
-
-#define RCHK(x)                                   \
-    do {                                          \
-        int _r = (x);                             \
-        if (_r != NRG_OK) return _r;              \
-    } while (0)
-
-// Exchange words per rank (u64): [0, G) Puts per owner, [G, 2G) Gets per owner, then
-enum : uint64_t {
-    XW_PREV = 0,    // 1 when this rank wants its Puts' previous values
-    XW_RP_CAP = 1,  // received Puts its buffers hold now
-    XW_RK_CAP = 2,  // received Get keys its buffers hold now
-    XW_ERR = 3,     // -NRG_E_* of a local failure before the exchange, else 0
-    XW_N = 4,
-};
 
 int nrg_group_partitioned_round(nrg_group* g, const nrg_round* rounds) {
     if (!g || !rounds) return NRG_E_INVAL;
@@ -420,6 +540,8 @@ int nrg_group_partitioned_round(nrg_group* g, const nrg_round* rounds) {
     // posts a send or receive: a rank that returned alone would leave its peers waiting in RCCL.
     // Local failures before the count exchange travel in its XW_ERR word; buffer growth after it
     // is known to every rank from the exchanged capacities and confirmed by a status all-gather.
+    // What remains are HIP runtime failures of stream/event calls (and a partition kernel whose
+    // counts disagree with its input), which leave the device unusable: fatal to the group.
     for (int i = 0; i < nl; i++) {
         Member& m = g->m[i];
         const nrg_round& x = rounds[i];
@@ -430,12 +552,8 @@ int nrg_group_partitioned_round(nrg_group* g, const nrg_round* rounds) {
         else if (x.n >= (1ull << 32) || x.n_gets >= (1ull << 32))
             err = NRG_E_CAPACITY;
         nrg_ctx* c = m.ctx;
+        // (the exchange buffers PB_CNT / PB_ALLCNT / PB_ST / PB_ALLST were sized at join)
         RCHK(nrg::ctx_use_device(c));
-        // exchange buffers first: without them this rank cannot take part at all
-        RCHK(grow(m, PB_CNT, CW * 8));
-        RCHK(grow(m, PB_ALLCNT, (uint64_t)G * CW * 8));
-        RCHK(grow(m, PB_ST, 8));
-        RCHK(grow(m, PB_ALLST, (uint64_t)G * 8));
         if (err == NRG_OK) {
             const PtBuf local[] = {PB_POUT, PB_PPOS, PB_KOUT, PB_GPOS, PB_AVAL, PB_AFOUND, PB_APREV, PB_APREVF};
             const uint64_t bytes[] = {x.n * 16, x.n * 4, x.n_gets * 8, x.n_gets * 4,

@@ -102,6 +102,7 @@ int check_err(nrg_ctx* c) {
         HIPCHK(sync_all(c));
         if (err & ERR_TABLE_FULL) return NRG_E_TABLE_FULL;
         if (err & ERR_CAPACITY) return NRG_E_CAPACITY;
+        if (err & ERR_GROUP) return NRG_E_INVAL;
         return NRG_E_HIP;
     }
     return NRG_OK;

@@ -39,21 +39,33 @@ class ReplicaGroup:
 
     The group id (ncclUniqueId) is created by rank 0 and broadcast over the default
     torch.distributed process group; every rank then joins with its own replica
-    (nrg_group_join, ncclCommInitRank on the replica's GPU)."""
+    (nrg_group_join, ncclCommInitRank on the replica's GPU), which blocks until every rank has
+    joined. A caller that ships the id itself (`uid`, from unique_id()) needs no process group:
+    tests run one thread per rank over the loopback collectives that way."""
+
+    @staticmethod
+    def unique_id() -> bytes:
+        """nrg_group_unique_id (ncclGetUniqueId, or a loopback id while those are selected)."""
+        uid = (C.c_uint8 * L.NRG_GROUP_ID_BYTES)()
+        L.check(L.load().nrg_group_unique_id(uid), "nrg_group_unique_id")
+        return bytes(uid)
 
     def __init__(self, replica, rank: Optional[int] = None, world: Optional[int] = None,
-                 pg: Optional[dist.ProcessGroup] = None):
+                 pg: Optional[dist.ProcessGroup] = None, uid: Optional[bytes] = None):
         lib = L.load()
         self.replica = replica
         self.rank = dist.get_rank(pg) if rank is None else rank
         self.world = dist.get_world_size(pg) if world is None else world
-        uid = (C.c_uint8 * L.NRG_GROUP_ID_BYTES)()
-        if self.rank == 0:
-            L.check(lib.nrg_group_unique_id(uid), "nrg_group_unique_id")
-        if self.world > 1:
-            obj = [bytes(uid)]
-            dist.broadcast_object_list(obj, src=0, group=pg)
-            uid = (C.c_uint8 * L.NRG_GROUP_ID_BYTES).from_buffer_copy(obj[0])
+        if uid is not None:
+            uid = (C.c_uint8 * L.NRG_GROUP_ID_BYTES).from_buffer_copy(uid)
+        else:
+            uid = (C.c_uint8 * L.NRG_GROUP_ID_BYTES)()
+            if self.rank == 0:
+                L.check(lib.nrg_group_unique_id(uid), "nrg_group_unique_id")
+            if self.world > 1:
+                obj = [bytes(uid)]
+                dist.broadcast_object_list(obj, src=0, group=pg)
+                uid = (C.c_uint8 * L.NRG_GROUP_ID_BYTES).from_buffer_copy(obj[0])
         h = C.c_void_p()
         L.check(lib.nrg_group_join(replica.handle, uid, self.world, self.rank, C.byref(h)), "nrg_group_join")
         self._h = h
@@ -67,7 +79,11 @@ class ReplicaGroup:
 
     def round_async(self, recs, n: int, resp=None, some=None, get_keys=None, n_gets: int = 0, get_vals=None,
                     get_found=None, seg_lens: Optional[Sequence[int]] = None):
-        """One NR round (device tensors or raw pointers): all-gather + replay + local reads."""
+        """One NR round (device tensors or raw pointers): all-gather + replay + local reads.
+
+        seg_lens: every rank's segment length, the same list on every rank (the stream-ordered
+        path; a header checks it on every rank). None: the lengths are exchanged first, which
+        costs one host round trip but lets every rank's n differ."""
         r = self._round
         r.recs, r.n, r.resp, r.some = _ptr(recs), n, _ptr(resp), _ptr(some)
         r.get_keys, r.n_gets, r.get_vals, r.get_found = _ptr(get_keys), n_gets, _ptr(get_vals), _ptr(get_found)
