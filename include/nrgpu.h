@@ -349,9 +349,21 @@ nrg_ctx* nrg_group_replica(nrg_group* g, int member);
 int nrg_group_set_input_stream(nrg_group* g, int member, void* hip_stream);
 /* One NR round on every local member: all-gather of the members' write segments (RCCL), then on
  * each replica Log::append of the gathered segments in rank order + Log::exec + its reads.
- * `seg_lens[r]` = rank r's segment length (NULL: every rank has rounds[0].n records; a
- * single-process group takes its members' n). Stream ordered; borrows buffers until the
- * replica stream passes this round (config.pipeline = 1: until nrg_join / the next call). */
+ * Appends of any length interleave, as in the reference (nr/src/log.rs:343-427): ranks may hold
+ * different segment lengths, and every rank must learn all of them before the all-gather.
+ *   seg_lens == NULL   the ranks exchange {n, local error} first (one 8-B-per-rank all-gather and
+ *                      one host round trip); a rank with a bad segment makes the round return
+ *                      NRG_E_INVAL on EVERY rank, before any data moves.
+ *   seg_lens != NULL   seg_lens[r] = rank r's segment length; every rank must pass the same array.
+ *                      The round stays stream ordered: a header {n, fingerprint of seg_lens}
+ *                      travels with each segment and is compared on every rank's comm stream. A
+ *                      rank whose n differs from seg_lens[rank] still takes part (with zeros) and
+ *                      returns NRG_E_INVAL; any disagreement makes the next nrg_group_sync /
+ *                      nrg_sync of every rank return NRG_E_INVAL. (Arrays whose longest segment
+ *                      differs would give all-gathers of different sizes: RCCL cannot check that.)
+ * A single-process group (nrg_group_open) takes its members' n (seg_lens, if given, must agree).
+ * Stream ordered; borrows buffers until the replica stream passes this round (config.pipeline =
+ * 1: until nrg_join / the next call). */
 int nrg_group_round_async(nrg_group* g, const nrg_round* rounds, const uint64_t* seg_lens);
 /* Wait for all queued group work and report latched device errors of every local replica. */
 int nrg_group_sync(nrg_group* g);

@@ -55,9 +55,10 @@ int nrg_test_set_knob(nrg_ctx* ctx, int knob, uint64_t value);
  * nrg_group_unique_id / nrg_group_join) use an in-process stand-in for RCCL instead of RCCL:
  * all-gathers and send/recv pairs become device copies on the members' streams, ordered with
  * events exactly where RCCL orders them. With it, nrg_group_open(devices = {0, 0, ...}) runs a
- * G-member group on one GPU -- the multi-rank code of nrg_group_round_async and
- * nrg_group_partitioned_round -- so tests check it against the oracle. One process must drive
- * every member (nrg_group_join: groups of one). 0 switches back to RCCL for later groups. */
+ * G-member group on one GPU from one thread, and G threads that each nrg_group_join the same
+ * loopback id (one replica each, any device) form a G-rank group as G processes would: join
+ * blocks until all ranks joined, and each collective blocks its thread until its peers posted
+ * theirs. Tests check both shapes against the oracle. 0 switches back to RCCL for later groups. */
 int nrg_test_loopback_collectives(int on);
 // Hashmap: 1 when the sampled key skew sends rounds to the bucket elector (hashmap.hip
 // skew_sample), 0 when they take the one-launch stamp rounds.
