@@ -40,8 +40,6 @@ int nrg_test_debug_read(nrg_ctx* ctx, uint64_t* out, uint64_t words);
                                   no apply, no index, no reads) -- measurement only              */
 #define NRG_KNOB_SY_SORT 7     /* synthetic: 1 = sort-based replay instead of the bucket path      */
 #define NRG_KNOB_PIPELINE 8    /* overrides nrg_config.pipeline                                    */
-#define NRG_KNOB_SORT_MIN 9    /* hashmap: rounds of at least this many Puts on an unskewed stream
-                                  replay as sorted rounds (0: never)                              */
 #define NRG_KNOB_COMB_SPIN 10   /* combiner (read by nrg_combiner_open): client threads that may spin
                                    while their round runs (default 0: every waiting client parks
                                    on a futex)                                                   */
@@ -49,6 +47,10 @@ int nrg_test_debug_read(nrg_ctx* ctx, uint64_t* out, uint64_t words);
 #define NRG_KNOB_SMALL_MAX 12   /* hashmap: rounds of at most this many Puts (<= 2048, and <= 8192
                                    Gets) replay in one one-workgroup launch (0: never; the
                                    combiner sets 2048 while it is open)                          */
+#define NRG_KNOB_PART 13        /* hashmap: partition rounds (Puts grouped by home-slot bucket, one
+                                   workgroup per bucket finds/claims and stores each key: no
+                                   device atomic per Put) -- 0 off, 1 instead of the bucket rounds,
+                                   2 instead of the stamp and the bucket rounds                  */
 int nrg_test_set_knob(nrg_ctx* ctx, int knob, uint64_t value);
 
 /* Replica groups created after nrg_test_loopback_collectives(1) (nrg_group_open,

@@ -48,10 +48,7 @@
 namespace {
 
 constexpr uint32_t MAX_PENDING = 32;  // nr/src/context.rs:12 MAX_PENDING_OPS
-#ifndef NRG_WAKE_FAN
-#define NRG_WAKE_FAN 2
-#endif
-constexpr uint32_t WAKE_FAN = NRG_WAKE_FAN;  // children each woken waiter wakes (A/B builds)
+constexpr uint32_t WAKE_FAN = 2;  // children each woken waiter wakes (a binary wake-up tree)
 constexpr int NB = 6;                 // batch slots
 constexpr uint64_t DEPTH = 2;         // default rounds in flight (NRG_KNOB_COMB_DEPTH, <= NB - 2: a
                                       // slot's clients copy their responses out while later rounds run)

@@ -60,6 +60,7 @@ struct IndexJob {
     u32 bk_shift;  // bucket of a slot id = id >> bk_shift
     u64x2* ent;    // [nblocks][tile] {id << 32 | i+1, value}
     u64* ekey;     // [nblocks][tile] key
+    u32* eidx;     // partition rounds: [nblocks][tile] round offset i of each entry (previous values)
     u32* cnt;      // [bucket][nblocks] start << 16 | count
     u32 exp;       // diagnostic knobs (NRG_EXP; results are wrong when set): 1 no dedup, 2 no
                    // probe (every key new), 4 no ranking/entries
@@ -291,6 +292,168 @@ __device__ __forceinline__ void index_role(const IndexJob& j, u32 blk, const Slo
     }
 }
 
+// ---- role: partition(e) (partition rounds) -------------------------------------------------------
+// The tile's Puts go to the bucket of their key's HOME slot (home >> bk_shift; the side key to
+// bucket 0), grouped by bucket in log order inside a bucket: {key, value} entries (+ the round
+// offset i when previous values are wanted) and a count word cnt[bucket][tile] = start << 16 | count.
+// Tile = TPB * K1 Puts; wave w owns [w*64*K1, (w+1)*64*K1) of it, so (q, lane) order inside a wave
+// is log order and waves follow each other. DEDUP drops a Put that a later Put of the same key in
+// the tile overwrites (rounds without previous values). The table is not touched: the previous
+// round's reads run beside this pass in the same launch, and hm_papply_kernel does the rest.
+template <int K1>
+struct PartLds {
+    static constexpr int TILE = TPB * K1;
+    static constexpr int HSZ = TILE / 2;  // lossy dedup entries (u64 key + u32 position)
+    static constexpr int PROBES = 16;
+    static unsigned bytes(bool dedup, u32 nb) {
+        const unsigned rank = nb * 4 + 4 * nb * 2;
+        return dedup && HSZ * 12 > (int)rank ? (unsigned)(HSZ * 12) : rank;
+    }
+};
+
+template <int K1, bool DEDUP>
+__device__ __forceinline__ void part_role(const IndexJob& j, u32 blk, u32 shift, char* lds) {
+    constexpr int WT = 64 * K1;
+    constexpr int TILE = PartLds<K1>::TILE;
+    constexpr int HSZ = PartLds<K1>::HSZ;
+    constexpr u32 NOH = 0xFFFFFFFFu;  // the key found no dedup entry: always emitted
+    __shared__ u32 s_side;  // dedup of the side-slot key: largest tile position + 1
+    __shared__ u32 s_dup;   // Puts whose key another Put of the tile already entered
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const u64 base = (u64)blk * TILE;
+    const u32 nb = 1u << j.nb_log;
+    u64* s_hk = (u64*)lds;               // [HSZ] dedup keys
+    u32* s_hp = (u32*)(lds + HSZ * 8);   // [HSZ] largest tile position + 1 per key
+    if (DEDUP) {
+        for (int q = threadIdx.x; q < HSZ; q += TPB) {
+            s_hk[q] = EMPTY_KEY;
+            s_hp[q] = 0;
+        }
+        if (threadIdx.x == 0) s_side = s_dup = 0;
+    }
+    nrg_put rec[K1];
+    u32 bkt[K1];
+    bool valid[K1];
+#pragma unroll
+    for (int q = 0; q < K1; q++) {
+        const u64 i = base + (u64)(w * WT + q * 64 + lane);
+        valid[q] = i < j.n;
+        rec[q] = valid[q] ? j.rec.at(i) : nrg_put{0, 0};
+    }
+#pragma unroll
+    for (int q = 0; q < K1; q++) {
+        const u64 i = base + (u64)(w * WT + q * 64 + lane);
+        if (valid[q] && j.ring_out) j.ring_out[(j.rec.lo + i) & j.rec.mask] = rec[q];
+        bkt[q] = rec[q].key == EMPTY_KEY ? 0u : (u32)(table_home(rec[q].key, shift) >> j.bk_shift);
+    }
+    bool emit[K1];
+    if (DEDUP) {
+        __syncthreads();  // hash initialised
+        u32 hq[K1];
+        u32 dup = 0;
+#pragma unroll
+        for (int q = 0; q < K1; q++) {
+            if (!valid[q]) continue;
+            const u32 pos1 = (u32)(w * WT + q * 64 + lane) + 1;
+            if (rec[q].key == EMPTY_KEY) {
+                atomicMax(&s_side, pos1);
+                continue;
+            }
+            // Lossy: a key that finds no entry within PROBES steps is not deduplicated. That is
+            // consistent for all Puts of a key (entries are never freed, so every Put of a key that
+            // got one walks into it); hot keys, the ones that matter, get one early.
+            u32 h = (u32)(((mix64(rec[q].key) >> 32) * (u64)HSZ) >> 32);
+            hq[q] = NOH;
+            for (int pr = 0; pr < PartLds<K1>::PROBES; pr++) {
+                const u64 old = atomicCAS((unsigned long long*)&s_hk[h], (unsigned long long)EMPTY_KEY,
+                                          (unsigned long long)rec[q].key);
+                if (old == EMPTY_KEY || old == rec[q].key) {
+                    dup += old == rec[q].key ? 1u : 0u;
+                    hq[q] = h;
+                    break;
+                }
+                h = h + 1 == (u32)HSZ ? 0u : h + 1;
+            }
+            if (hq[q] != NOH) atomicMax(&s_hp[h], pos1);
+        }
+        if (dup) atomicAdd(&s_dup, dup);
+        __syncthreads();
+        if (threadIdx.x == 0 && s_dup && j.dup_acc) atomicAdd(&j.dup_acc[blk % HM_DUP_SLOTS], (u64)s_dup);
+#pragma unroll
+        for (int q = 0; q < K1; q++) {
+            const u32 pos1 = (u32)(w * WT + q * 64 + lane) + 1;
+            emit[q] = valid[q] && (rec[q].key == EMPTY_KEY ? s_side == pos1 : hq[q] == NOH || s_hp[hq[q]] == pos1);
+        }
+        __syncthreads();  // the hash region is reused below
+    } else {
+#pragma unroll
+        for (int q = 0; q < K1; q++) emit[q] = valid[q];
+    }
+    // ---- stable grouping by bucket: wave-private counts, then a prefix over waves ----
+    u32* s_start = (u32*)lds;                       // [nb] bucket start in the tile
+    uint16_t* s_wc = (uint16_t*)(lds + nb * 4);     // [4][nb] per-wave counts -> wave offsets
+    for (u32 b = threadIdx.x; b < 4 * nb; b += TPB) s_wc[b] = 0;
+    __syncthreads();
+    u32 rnk[K1];
+#pragma unroll
+    for (int q = 0; q < K1; q++) {
+        const u32 b = emit[q] ? bkt[q] : 0u;
+        u64 peers = __ballot(emit[q]);
+        for (u32 bit = 0; bit < j.nb_log; bit++) {
+            const bool one = (b >> bit) & 1u;
+            const u64 bal = __ballot(one);
+            peers &= one ? bal : ~bal;
+        }
+        if (emit[q]) {
+            const u64 below = peers & ((1ull << lane) - 1);
+            const u32 cur = s_wc[w * nb + b];
+            rnk[q] = cur + (u32)__popcll(below);
+            if (below == 0) s_wc[w * nb + b] = (uint16_t)(cur + (u32)__popcll(peers));
+        }
+    }
+    __syncthreads();
+    constexpr int PER = HM_BK_MAX / TPB;  // buckets per thread (contiguous ownership)
+    u32 tot[PER], loc = 0;
+#pragma unroll
+    for (int r = 0; r < PER; r++) {
+        const u32 b = threadIdx.x * PER + r;
+        tot[r] = 0;
+        if (b < nb) {
+            u32 run = 0;
+#pragma unroll
+            for (int v = 0; v < 4; v++) {
+                const u32 c = s_wc[v * nb + b];
+                s_wc[v * nb + b] = (uint16_t)run;
+                run += c;
+            }
+            tot[r] = run;
+            loc += run;
+        }
+    }
+    u32 off = block_scan_excl(loc, nullptr);
+#pragma unroll
+    for (int r = 0; r < PER; r++) {
+        const u32 b = threadIdx.x * PER + r;
+        if (b < nb) {
+            j.cnt[(u64)blk * nb + b] = (off << 16) | tot[r];
+            s_start[b] = off;
+        }
+        off += tot[r];
+    }
+    __syncthreads();
+    u64x2* ent = j.ent + (u64)blk * TILE;
+#pragma unroll
+    for (int q = 0; q < K1; q++) {
+        if (!emit[q]) continue;
+        const u32 p = s_start[bkt[q]] + s_wc[w * nb + bkt[q]] + rnk[q];
+        u64x2 e;
+        e.x = rec[q].key;
+        e.y = rec[q].val;
+        ent[p] = e;
+        if (j.eidx) j.eidx[(u64)blk * TILE + p] = (u32)(base + (u64)(w * WT + q * 64 + lane));
+    }
+}
+
 // claim (or find) k's slot from its home slot; *fresh = this call inserted it; -1: table full
 __device__ __forceinline__ long long claim_slot(Slot* table, u64 k, u64 s, u64 tmask, bool* fresh) {
     *fresh = false;
@@ -459,11 +622,6 @@ __device__ __forceinline__ void stamp_index_role(const StampJob& j, u32 blk, Slo
     }
 }
 
-#ifndef NRG_APPLY16
-// A/B builds: the elected writer stores {key, val} (16 B) instead of val (8 B). No change: 100 %
-// writes 97.6 us either way, configs[2]'s 4.5M-op round 413.4-414.2 (profiles/r03_apply_store_width.txt)
-#define NRG_APPLY16 0
-#endif
 // apply(e): per Put, the elected writer stores its value
 __device__ __forceinline__ void apply_role(const ApplyJob& j, u32 blk, Slot* table, DevCtl* ctl) {
     const u64 i = (u64)blk * TPB + threadIdx.x;
@@ -474,17 +632,9 @@ __device__ __forceinline__ void apply_role(const ApplyJob& j, u32 blk, Slot* tab
     if (s == SIDE_SLOT) {
         if (ctl->sp.st[par] == want) ctl->sp.val = j.rec.at(i).val;
     } else if (s != FULL_SLOT) {
-        if (j.win[i] == j.epoch && j.over[i] != j.epoch) {
-#if NRG_APPLY16
-            const nrg_put r = j.rec.at(i);  // {key, val} in one 16-B store (the key is the slot's own)
-            u64x2 kv;
-            kv.x = r.key;
-            kv.y = r.val;
-            *(u64x2*)&table[s] = kv;
-#else
-            table[s].val = j.rec.at(i).val;
-#endif
-        }
+        // (a 16-B {key, val} store costs the same: a partial-line write is priced per line,
+        // profiles/r03_apply_store_width.txt)
+        if (j.win[i] == j.epoch && j.over[i] != j.epoch) table[s].val = j.rec.at(i).val;
     }
 }
 
@@ -502,10 +652,7 @@ __device__ __forceinline__ bool resolve(u64 val, u64 st, const ReadJob& j, u64* 
 // RPT Gets per thread, q = blk * TPB * RPT + r * TPB + tid: every key load and every home-line
 // load of the thread in flight together. Measured on one box (profiles/r03_read_rpt.txt), B1 per
 // round: RPT 1 34.4 us, 2 36.2, 4 39.8; the N=8 per-GPU round 99.3 / 100.8 / 105.4 us.
-#ifndef NRG_RPT
-#define NRG_RPT 1
-#endif
-constexpr int RPT = NRG_RPT;
+constexpr int RPT = 1;
 
 __device__ __forceinline__ void read_role(const ReadJob& j, u32 blk, const Slot* table, u32 shift, u64 tmask,
                                           const DevCtl* ctl) {
@@ -569,16 +716,25 @@ __device__ __forceinline__ void read_role(const ReadJob& j, u32 blk, const Slot*
 constexpr int IX_BUCKET = 0;      // bucket round, dedup (hm_elect_kernel<false> follows)
 constexpr int IX_BUCKET_ALL = 1;  // bucket round, every Put kept (previous values)
 constexpr int IX_STAMP = 2;       // stamp round
+constexpr int IX_PART = 3;        // partition round, dedup (hm_papply_kernel<false> follows)
+constexpr int IX_PART_ALL = 4;    // partition round, every Put kept (previous values)
+constexpr int IX_PART_NODUP = 5;  // partition round, every Put kept, no previous values (uniform keys)
 
 // One launch = {index(e)} + {apply(e-1)} + {reads(e-1)} over disjoint block ranges (any may be
 // empty). Index blocks come first so the latency-bound pass starts first.
 // <= 80 SGPRs: 256-thread blocks are admitted 8 per CU only up to 80 SGPRs (82-96: 7 per CU,
 // MI355X_MICROARCH.md "Residency"), and the read role needs every resident wave.
-template <int K1, int IX>
+// DIAG: the instantiation that honours the diagnostic ablation bits (NRG_KNOB_EXP); the release
+// instantiations fold them away and are the only ones launched unless such a bit is set.
+template <int K1, int IX, bool DIAG>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_num_sgpr(80))) void hm_round_kernel(IndexJob ij, StampJob sj,
                                                                                              ApplyJob aj, ReadJob rj,
                                                        Slot* table, u32 shift, u64 tmask, DevCtl* ctl) {
     extern __shared__ __attribute__((aligned(16))) char s_lds[];
+    if constexpr (!DIAG) {
+        ij.exp = 0;
+        sj.exp = 0;
+    }
     u32 b = blockIdx.x;
     if ((rj.s_seq || rj.e_out) && b == gridDim.x - 1) {  // the tail block
         if (rj.e_out && threadIdx.x == 0) *rj.e_out = atomicExch(&ctl->err, 0u);
@@ -599,6 +755,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_num_sgpr(80))) void hm_r
     if (b < nix) {
         if (sj.exp & 4) return;
         if constexpr (IX == IX_STAMP) stamp_index_role<K1>(sj, b, table, shift, tmask, ctl, s_lds);
+        else if constexpr (IX == IX_PART || IX == IX_PART_ALL || IX == IX_PART_NODUP)
+            part_role<K1, IX == IX_PART>(ij, b, shift, s_lds);
         else index_role<K1, IX == IX_BUCKET>(ij, b, table, shift, tmask, s_lds);
         return;
     }
@@ -994,147 +1152,372 @@ __global__ __launch_bounds__(TPB) void hm_elect_kernel(ElectJob j) {
 #undef EL_MARK
 }
 
-// ---- sorted rounds: large uniform write rounds -------------------------------
-// A stable radix sort of the round's Puts by the top 32 bits of mix64(key) -- whose leading bits
-// are the home slot, so the sorted order sweeps the table -- puts every key's Puts next to each
-// other in log order (two distinct keys share a sort key with probability ~2^-32; the scans below
-// compare full keys). Then, per Put, O(1) neighbour checks:
-//   last of its key  -> it alone finds or claims the key's slot and stores its value (no atomics
-//                       per Put, one table line per distinct key, visited in table order);
-//   previous value   -> the value of the key's preceding Put, or for its first Put the table's
-//                       value before the round (read by hm_sr_prev_kernel before any store).
-// Per Put: 16 B of records (+ the log copy), a 4-B sort key and 8 B per sort pass of streaming
-// traffic, one gather of its record in sorted order; per distinct key one table line.
-struct SortedJob {
-    RecSrc rec;
-    const u32* sk;  // sorted keys (top half of mix64(key))
-    const u32* sv;  // round offsets of the Puts in sorted order
-    u64 n;
+// ---- hm_papply_kernel: partition rounds' table pass, one workgroup per bucket ---------------------
+// The bucket's entries (every tile's run, tile order = log order) are taken in chunks of PA_C:
+// an LDS hash finds each key's last entry in the chunk, whose thread finds the key's slot from
+// its home (or claims an empty one: a new key) and stores the value -- one table line read and
+// written per distinct key, no device atomics per Put. All Puts of a key share a bucket (the
+// bucket is the home slot's), so one workgroup decides each key; a later chunk of the bucket
+// overwrites an earlier one's store in log order. Claims of other buckets' workgroups only fill
+// empty slots and cannot cut a present key's probe chain.
+// PREV (HashMap::insert's previous values, nr/examples/hashmap.rs:46-50): every Put has an entry;
+// the first entry of a key in the chunk finds (or claims) the slot and its value before the
+// chunk; wave 0 then walks the chunk in log order, 64 entries a step: a Put's previous value is
+// its predecessor's value, else the key's value before the chunk, else None.
+struct PApplyJob {
+    const u64x2* ent;  // [tiles][tile] {key, value}
+    const u32* eidx;   // [tiles][tile] round offset (PREV)
+    const u32* cnt;    // [tiles][bucket] start << 16 | count
+    u32 ntiles, tile, nb;
     Slot* table;
     u32 shift;
     u64 tmask;
     DevCtl* ctl;
     u64* created_acc;
-    u64* dup_acc;   // Puts with a later Put of their key in the same 512-Put tile (key skew)
     u64 lo, resp_lo, resp_hi;
     u64* prev;
     uint8_t* prevf;
 };
 
-// the key pass: sort keys, the log copy, and the sort's four digit histograms in one read
-__global__ __launch_bounds__(TPB) void hm_sr_keys_kernel(RecSrc rec, nrg_put* ring_out, u64 n, u32* keys, u32* hist) {
-    __shared__ u32 sh[4 * 256];
-    for (int q = threadIdx.x; q < 4 * 256; q += TPB) sh[q] = 0;
-    __syncthreads();
-    for (u64 i = blockIdx.x * (u64)TPB + threadIdx.x; i < n; i += (u64)gridDim.x * TPB) {
-        const nrg_put r = rec.at(i);
-        if (ring_out) ring_out[(rec.lo + i) & rec.mask] = r;
-        const u32 k = (u32)(mix64(r.key) >> 32);
-        keys[i] = k;
+constexpr int PA_TPB = 256;
+template <bool PREV>
+struct PaGeo {
+    static constexpr int C = PREV ? 512 : 1024;  // entries per chunk
+    static constexpr int HT = 2 * C;             // LDS hash entries (load <= 1/2)
+    static constexpr int PER = C / PA_TPB;
+};
+
+__device__ __forceinline__ u32 pa_hash(u64 k, u32 ht) { return (u32)(mix64(k) >> 40) & (ht - 1); }
+
+// Find or claim the slots of up to N keys of one thread together: every probe load, then every
+// CAS on an empty slot, of all N keys is in flight before any is resolved (one or two memory
+// round trips for most keys instead of one or two per key). on[r]: key r takes part (not the
+// side key). Out: slot[r] (-1: table full), fresh[r] (this call claimed it: epoch-1 stamps
+// written), val[r] = the slot's value before this call (found keys; WANT_VAL).
+template <int N, bool WANT_VAL>
+__device__ __forceinline__ void pa_resolve(Slot* table, u32 shift, u64 tmask, const u64* k, const bool* on,
+                                           long long* slot, bool* fresh, u64* val) {
+    u64 s[N], kk[N], vv[N];
+    u32 st[N];  // 0 done, 1 key loaded, 2 CAS needed
 #pragma unroll
-        for (int p = 0; p < 4; p++) atomicAdd(&sh[p * 256 + ((k >> (8 * p)) & 255u)], 1u);
-    }
-    __syncthreads();
-    for (int q = threadIdx.x; q < 4 * 256; q += TPB)
-        if (sh[q]) atomicAdd(&hist[q], sh[q]);
-}
-
-// value of key k before the round (read-only probe); false: absent
-__device__ __forceinline__ bool sr_table_value(const SortedJob& j, u64 k, u64* v) {
-    if (k == EMPTY_KEY) {
-        if (!j.ctl->sp_claim) return false;
-        *v = j.ctl->sp.val;
-        return true;
-    }
-    u64 s = table_home(k, j.shift);
-    for (u64 pr = 0; pr <= j.tmask; pr++) {
-        const u64x2 w = *(const u64x2*)&j.table[s];
-        if (w.x == k) {
-            *v = w.y;
-            return true;
-        }
-        if (w.x == EMPTY_KEY) return false;
-        s = (s + 1) & j.tmask;
-    }
-    return false;
-}
-
-// previous values (HashMap::insert's return, nr/examples/hashmap.rs:46-50), before any store
-__global__ __launch_bounds__(TPB) void hm_sr_prev_kernel(SortedJob j) {
-    const u64 p = blockIdx.x * (u64)TPB + threadIdx.x;
-    if (p >= j.n) return;
-    const u32 i = j.sv[p];
-    const u64 g = j.lo + i;
-    if (g < j.resp_lo || g >= j.resp_hi) return;
-    const u32 hk = j.sk[p];
-    const u64 k = j.rec.at(i).key;
-    u64 v = 0;
-    bool f = false, found_pred = false;
-    for (u64 q = p; q-- > 0 && j.sk[q] == hk;) {  // the key's preceding Put (same sort key, log order)
-        const nrg_put r = j.rec.at(j.sv[q]);
-        if (r.key == k) {
-            v = r.val;
-            f = found_pred = true;
-            break;
-        }
-    }
-    if (!found_pred) f = sr_table_value(j, k, &v);
-    j.prev[g - j.resp_lo] = f ? v : 0;
-    j.prevf[g - j.resp_lo] = f ? 1 : 0;
-}
-
-// the last Put of every key stores its value (claiming a slot for a new key)
-__global__ __launch_bounds__(TPB) void hm_sr_apply_kernel(SortedJob j) {
-    __shared__ u32 s_created, s_dup;
-    if (threadIdx.x == 0) s_created = s_dup = 0;
-    __syncthreads();
-    const u64 p = blockIdx.x * (u64)TPB + threadIdx.x;
-    u32 created = 0, dup = 0;
-    if (p < j.n) {
-        const u32 i = j.sv[p];
-        const u32 hk = j.sk[p];
-        const nrg_put r = j.rec.at(i);
-        bool last = true;
-        for (u64 q = p + 1; q < j.n && j.sk[q] == hk; q++) {
-            const u32 iq = j.sv[q];
-            if (j.rec.at(iq).key == r.key) {
-                last = false;
-                dup = (iq >> 9) == (i >> 9);  // the skew statistic of the index rounds: same 512-Put tile
-                break;
+    for (int r = 0; r < N; r++) {
+        st[r] = on[r] ? 1u : 0u;
+        s[r] = on[r] ? table_home(k[r], shift) : 0;
+        slot[r] = -1;
+        fresh[r] = false;
+        kk[r] = EMPTY_KEY;
+        vv[r] = 0;
+        if (on[r]) {
+            if (WANT_VAL) {
+                const u64x2 x = *(const u64x2*)&table[s[r]];
+                kk[r] = x.x;
+                vv[r] = x.y;
+            } else {
+                kk[r] = ld_relaxed(&table[s[r]].key);
             }
         }
-        if (last) {
-            if (r.key == EMPTY_KEY) {  // one last Put per key: a plain store claims the side slot
-                if (!j.ctl->sp_claim) {
-                    j.ctl->sp_claim = 1;
-                    j.ctl->sp.st[0] = j.ctl->sp.st[1] = STAMP_PRESENT;
-                    created = 1;
-                }
-                j.ctl->sp.val = r.val;
+    }
+    for (u64 pr = 0; pr <= tmask; pr++) {
+        bool any = false;
+#pragma unroll
+        for (int r = 0; r < N; r++) {
+            if (st[r] != 1) continue;
+            if (kk[r] == k[r]) {
+                slot[r] = (long long)s[r];
+                if (WANT_VAL) val[r] = vv[r];
+                st[r] = 0;
+            } else if (kk[r] == EMPTY_KEY) {
+                st[r] = 2;
             } else {
-                bool fresh = false;
-                const long long sl = claim_slot(j.table, r.key, table_home(r.key, j.shift), j.tmask, &fresh);
-                if (sl < 0) {
+                s[r] = (s[r] + 1) & tmask;
+                st[r] = 3;
+            }
+            any = any || st[r] != 0;
+        }
+        if (!any) return;
+        u64 old[N];
+#pragma unroll
+        for (int r = 0; r < N; r++)
+            if (st[r] == 2)
+                old[r] = atomicCAS((unsigned long long*)&table[s[r]].key, (unsigned long long)EMPTY_KEY,
+                                   (unsigned long long)k[r]);
+#pragma unroll
+        for (int r = 0; r < N; r++) {
+            if (st[r] != 2) continue;
+            if (old[r] == EMPTY_KEY) {  // claimed: a new key, present for every later read
+                u64x2 z;
+                z.x = z.y = STAMP_PRESENT;
+                *(u64x2*)&table[s[r]].st[0] = z;
+                slot[r] = (long long)s[r];
+                fresh[r] = true;
+                st[r] = 0;
+            } else if (old[r] == k[r]) {
+                slot[r] = (long long)s[r];
+                if (WANT_VAL) val[r] = ld_relaxed(&table[s[r]].val);
+                st[r] = 0;
+            } else {
+                s[r] = (s[r] + 1) & tmask;
+                st[r] = 3;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < N; r++) {
+            if (st[r] != 3) continue;
+            if (WANT_VAL) {
+                const u64x2 x = *(const u64x2*)&table[s[r]];
+                kk[r] = x.x;
+                vv[r] = x.y;
+            } else {
+                kk[r] = ld_relaxed(&table[s[r]].key);
+            }
+            st[r] = 1;
+        }
+    }
+}
+
+template <bool PREV>
+__global__ __launch_bounds__(PA_TPB) void hm_papply_kernel(PApplyJob j) {
+    constexpr int C = PaGeo<PREV>::C, HT = PaGeo<PREV>::HT, PER = PaGeo<PREV>::PER;
+    constexpr u32 NOFIRST = 0xFFFFFFFFu;
+    extern __shared__ u32 s_dyn[];  // s_pre[ntiles + 1] entry prefix, s_off[ntiles] (u16)
+    __shared__ u64 s_hk[HT];
+    __shared__ u32 s_hp[HT + 1];   // last chunk position + 1 of the key; [HT]: the side key
+    __shared__ uint16_t s_tile[C];
+    __shared__ u32 s_h1[PREV ? HT + 1 : 1];  // PREV: first chunk position + 1
+    __shared__ u32 s_hs[PREV ? HT + 1 : 1];  // PREV: the key's slot (SIDE_ID, FULL_SLOT)
+    __shared__ u64 s_lv[PREV ? HT + 1 : 1];  // PREV: the key's value so far in the walk
+    __shared__ u32 s_hf[PREV ? HT + 1 : 1];  // PREV: s_lv holds a value
+    __shared__ u64 s_mk[PREV ? HT + 1 : 1];  // PREV: lanes of the current walk step per key
+    __shared__ u64 s_ev[PREV ? C : 1];       // PREV: the chunk's values, hash entries, round offsets
+    __shared__ uint16_t s_eh[PREV ? C : 1];
+    __shared__ u32 s_ei[PREV ? C : 1];
+    __shared__ u32 s_created;
+    const u32 nt = j.ntiles, b = blockIdx.x;
+    u32* s_pre = s_dyn;
+    uint16_t* s_off = (uint16_t*)(s_dyn + nt + 1);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    // this bucket's (offset, count) in every tile; thread owns tiles [tid*K, tid*K + K)
+    const u32 K = (nt + PA_TPB - 1) / PA_TPB;
+    u32 loc = 0;
+    for (u32 q = 0; q < K; q++) {
+        const u32 t = threadIdx.x * K + q;
+        if (t < nt) {
+            const u32 v = j.cnt[(u64)t * j.nb + b];
+            s_off[t] = (uint16_t)(v >> 16);
+            s_pre[t] = v & 0xFFFFu;
+            loc += v & 0xFFFFu;
+        }
+    }
+    for (int h = threadIdx.x; h <= HT; h += PA_TPB) {
+        if (h < HT) s_hk[h] = EMPTY_KEY;
+        s_hp[h] = 0;
+        if (PREV) {
+            s_h1[h] = NOFIRST;
+            s_mk[h] = 0;
+        }
+    }
+    u32 total;
+    u32 run = block_scan_excl(loc, &total);  // (its barriers also order the initialisation above)
+    for (u32 q = 0; q < K; q++) {
+        const u32 t = threadIdx.x * K + q;
+        if (t < nt) {
+            const u32 c = s_pre[t];
+            s_pre[t] = run;
+            run += c;
+        }
+    }
+    if (threadIdx.x == 0) {
+        s_pre[nt] = total;
+        s_created = 0;
+    }
+    __syncthreads();
+    u32 created = 0;
+    for (u32 base = 0; base < total; base += C) {
+        const u32 cn = total - base < (u32)C ? total - base : (u32)C;
+        // entry tile map of the chunk [base, base + cn)
+        for (u32 q = 0; q < K; q++) {
+            const u32 t = threadIdx.x * K + q;
+            if (t >= nt) break;
+            const u32 lo_ = s_pre[t] > base ? s_pre[t] : base;
+            const u32 hi_ = s_pre[t + 1] < base + cn ? s_pre[t + 1] : base + cn;
+            for (u32 i = lo_; i < hi_; i++) s_tile[i - base] = (uint16_t)t;
+        }
+        __syncthreads();
+        u64x2 x[PER];
+        u32 ix[PER], hh[PER];
+#pragma unroll
+        for (int r = 0; r < PER; r++) {
+            const u32 p = r * PA_TPB + threadIdx.x;
+            x[r].x = EMPTY_KEY;
+            x[r].y = 0;
+            ix[r] = 0;
+            if (p < cn) {
+                const u32 t = s_tile[p];
+                const u64 e = (u64)t * j.tile + s_off[t] + (base + p - s_pre[t]);
+                x[r] = j.ent[e];
+                if (PREV) ix[r] = j.eidx[e];
+            }
+        }
+        // one hash entry per key: its last (and first) position in the chunk
+#pragma unroll
+        for (int r = 0; r < PER; r++) {
+            const u32 p = r * PA_TPB + threadIdx.x;
+            hh[r] = HT;
+            if (p >= cn) continue;
+            const u64 k = x[r].x;
+            u32 h = HT;
+            if (k != EMPTY_KEY) {
+                h = pa_hash(k, HT);
+                for (;;) {  // at most C keys in 2C entries: an entry is always found
+                    const u64 old = atomicCAS((unsigned long long*)&s_hk[h], (unsigned long long)EMPTY_KEY,
+                                              (unsigned long long)k);
+                    if (old == EMPTY_KEY || old == k) break;
+                    h = (h + 1) & (HT - 1);
+                }
+            }
+            hh[r] = h;
+            atomicMax(&s_hp[h], p + 1);
+            if (PREV) {
+                atomicMin(&s_h1[h], p + 1);
+                s_ev[p] = x[r].y;
+                s_eh[p] = (uint16_t)h;
+                s_ei[p] = ix[r];
+            }
+        }
+        __syncthreads();
+        if (!PREV) {
+            // the key's last entry finds or claims its slot and stores its value
+            bool dec[PER], on[PER], fr[PER];
+            u64 kx[PER], vx[PER];
+            long long sl[PER];
+#pragma unroll
+            for (int r = 0; r < PER; r++) {
+                const u32 p = r * PA_TPB + threadIdx.x;
+                dec[r] = p < cn && s_hp[hh[r]] == p + 1;
+                on[r] = dec[r] && x[r].x != EMPTY_KEY;
+                kx[r] = x[r].x;
+            }
+            pa_resolve<PER, false>(j.table, j.shift, j.tmask, kx, on, sl, fr, vx);
+#pragma unroll
+            for (int r = 0; r < PER; r++) {
+                if (!dec[r]) continue;
+                if (x[r].x == EMPTY_KEY) {
+                    if (!j.ctl->sp_claim) {
+                        j.ctl->sp_claim = 1;
+                        j.ctl->sp.st[0] = j.ctl->sp.st[1] = STAMP_PRESENT;
+                        created++;
+                    }
+                    j.ctl->sp.val = x[r].y;
+                } else if (sl[r] < 0) {
                     atomicOr(&j.ctl->err, ERR_TABLE_FULL);
                 } else {
-                    j.table[sl].val = r.val;
-                    if (fresh) {
-                        u64x2 z;
-                        z.x = z.y = STAMP_PRESENT;
-                        *(u64x2*)&j.table[sl].st[0] = z;
-                        created = 1;
+                    j.table[sl[r]].val = x[r].y;
+                    created += fr[r];
+                }
+            }
+            __syncthreads();  // every decider has read s_hp
+#pragma unroll
+            for (int r = 0; r < PER; r++) {  // the deciders free their keys' entries for the next chunk
+                if (!dec[r]) continue;
+                if (hh[r] < (u32)HT) s_hk[hh[r]] = EMPTY_KEY;
+                s_hp[hh[r]] = 0;
+            }
+        } else {
+            // the key's first entry: its slot and its value before the chunk
+            bool fst[PER], on[PER], fr[PER];
+            u64 kx[PER], vx[PER];
+            long long sl[PER];
+#pragma unroll
+            for (int r = 0; r < PER; r++) {
+                const u32 p = r * PA_TPB + threadIdx.x;
+                fst[r] = p < cn && s_h1[hh[r]] == p + 1;
+                on[r] = fst[r] && x[r].x != EMPTY_KEY;
+                kx[r] = x[r].x;
+                vx[r] = 0;
+            }
+            pa_resolve<PER, true>(j.table, j.shift, j.tmask, kx, on, sl, fr, vx);
+#pragma unroll
+            for (int r = 0; r < PER; r++) {
+                if (!fst[r]) continue;
+                const u32 h = hh[r];
+                if (x[r].x == EMPTY_KEY) {
+                    s_hs[h] = SIDE_ID;
+                    if (j.ctl->sp_claim) {
+                        s_lv[h] = j.ctl->sp.val;
+                        s_hf[h] = 1;
+                    } else {
+                        j.ctl->sp_claim = 1;
+                        j.ctl->sp.st[0] = j.ctl->sp.st[1] = STAMP_PRESENT;
+                        created++;
+                        s_hf[h] = 0;
+                    }
+                } else if (sl[r] < 0) {
+                    atomicOr(&j.ctl->err, ERR_TABLE_FULL);
+                    s_hs[h] = FULL_SLOT;
+                    s_hf[h] = 0;
+                } else {
+                    s_hs[h] = (u32)sl[r];
+                    created += fr[r];
+                    s_hf[h] = fr[r] ? 0u : 1u;
+                    s_lv[h] = vx[r];
+                }
+            }
+            __syncthreads();
+            // wave 0 walks the chunk in log order, 64 entries a step
+            if (w == 0) {
+                for (u32 s0 = 0; s0 < cn; s0 += 64) {
+                    const u32 p = s0 + lane;
+                    const bool v = p < cn;
+                    const u32 h = v ? s_eh[p] : 0u;
+                    const u64 val = v ? s_ev[p] : 0ull;
+                    if (v) atomicOr((unsigned long long*)&s_mk[h], 1ull << lane);
+                    const u64 m = v ? s_mk[h] : 0ull;
+                    const u64 lower = m & ((1ull << lane) - 1);
+                    const int pl = lower ? 63 - __clzll((long long)lower) : lane;
+                    const u64 pv_lane = __shfl(val, pl, 64);
+                    if (v) {
+                        u64 pv;
+                        uint8_t pf;
+                        if (lower) {
+                            pv = pv_lane;
+                            pf = 1;
+                        } else {
+                            pf = s_hf[h] ? 1 : 0;
+                            pv = pf ? s_lv[h] : 0;
+                        }
+                        const u64 g = j.lo + s_ei[p];
+                        if (g >= j.resp_lo && g < j.resp_hi) {
+                            j.prev[g - j.resp_lo] = pv;
+                            j.prevf[g - j.resp_lo] = pf;
+                        }
+                        if ((m >> lane) == 1ull) {  // the key's last entry in this step
+                            s_lv[h] = val;
+                            s_hf[h] = 1;
+                            s_mk[h] = 0;
+                        }
                     }
                 }
             }
+            __syncthreads();
+            // the key's last entry stores its final value
+#pragma unroll
+            for (int r = 0; r < PER; r++) {
+                const u32 p = r * PA_TPB + threadIdx.x;
+                if (p >= cn || s_hp[hh[r]] != p + 1) continue;
+                const u32 h = hh[r];
+                const u32 sl = s_hs[h];
+                if (sl == SIDE_ID) j.ctl->sp.val = s_lv[h];
+                else if (sl != FULL_SLOT) j.table[sl].val = s_lv[h];
+                if (h < HT) s_hk[h] = EMPTY_KEY;
+                s_hp[h] = 0;
+                s_h1[h] = NOFIRST;
+            }
         }
+        __syncthreads();  // hash entries free, s_tile reused by the next chunk
     }
     if (created) atomicAdd(&s_created, created);
-    if (dup) atomicAdd(&s_dup, dup);
     __syncthreads();
-    if (threadIdx.x == 0) {
-        if (s_created) atomicAdd(&j.created_acc[blockIdx.x % HM_CREATED_SLOTS], (u64)s_created);
-        if (s_dup && j.dup_acc) atomicAdd(&j.dup_acc[blockIdx.x % HM_DUP_SLOTS], (u64)s_dup);
-    }
+    if (threadIdx.x == 0 && s_created) atomicAdd(&j.created_acc[b % HM_CREATED_SLOTS], (u64)s_created);
 }
 
 // ---- small rounds: one workgroup, one launch (the flat combiner's batches) ----------------------
@@ -1595,8 +1978,12 @@ static void attach_deferred(nrg_ctx* c, Launch& L) {
 
 template <int K1, int IX>
 static void launch_round(nrg_ctx* c, const Launch& L, u32 blocks, unsigned lds) {
-    NRG_LAUNCH(c, "hm_round", (hm_round_kernel<K1, IX>), blocks, TPB, lds, c->stream, L.ij, L.sj, L.aj, L.rj,
-               c->d_table, c->slot_shift, (u64)(c->slots - 1), c->d_ctl);
+    if ((L.ij.exp | L.sj.exp) != 0)
+        NRG_LAUNCH(c, "hm_round", (hm_round_kernel<K1, IX, true>), blocks, TPB, lds, c->stream, L.ij, L.sj, L.aj, L.rj,
+                   c->d_table, c->slot_shift, (u64)(c->slots - 1), c->d_ctl);
+    else
+        NRG_LAUNCH(c, "hm_round", (hm_round_kernel<K1, IX, false>), blocks, TPB, lds, c->stream, L.ij, L.sj, L.aj,
+                   L.rj, c->d_table, c->slot_shift, (u64)(c->slots - 1), c->d_ctl);
 }
 
 static hipError_t launch(nrg_ctx* c, Launch& L) {
@@ -1609,7 +1996,7 @@ static hipError_t launch(nrg_ctx* c, Launch& L) {
     // earlier kernels of the round, the elector's claims included, have latched their errors)
     const bool err_here = c->err_out && nix == 0;
     if (c->sample_seq || err_here) {  // the launch's last block
-        L.rj.s_acc = c->d_dup;
+        L.rj.s_acc = c->d_dup + ((c->dup_seq - 1) & 1) * HM_DUP_SLOTS;  // the window just ended
         L.rj.s_host = c->h_dup_dev;
         L.rj.s_seq = c->sample_seq;
         L.rj.e_out = err_here ? c->err_out : nullptr;
@@ -1621,15 +2008,27 @@ static hipError_t launch(nrg_ctx* c, Launch& L) {
     if (nix && L.ix == IX_STAMP) {
         lds = L.K1 == 4 ? StampLds<4>::BYTES : L.K1 == 2 ? StampLds<2>::BYTES : StampLds<1>::BYTES;
     } else if (nix) {
-        const bool dedup = L.ix == IX_BUCKET;
-        lds = L.K1 == 4 ? IndexLds<4>::bytes(dedup, L.nb) : L.K1 == 2 ? IndexLds<2>::bytes(dedup, L.nb)
-                                                                       : IndexLds<1>::bytes(dedup, L.nb);
+        if (L.ix == IX_PART || L.ix == IX_PART_ALL || L.ix == IX_PART_NODUP) {
+            const bool dedup = L.ix == IX_PART;
+            lds = L.K1 == 8   ? PartLds<8>::bytes(dedup, L.nb)
+                  : L.K1 == 4 ? PartLds<4>::bytes(dedup, L.nb)
+                  : L.K1 == 2 ? PartLds<2>::bytes(dedup, L.nb)
+                              : PartLds<1>::bytes(dedup, L.nb);
+        } else {
+            const bool dedup = L.ix == IX_BUCKET;
+            lds = L.K1 == 4 ? IndexLds<4>::bytes(dedup, L.nb) : L.K1 == 2 ? IndexLds<2>::bytes(dedup, L.nb)
+                                                                           : IndexLds<1>::bytes(dedup, L.nb);
+        }
     }
     if (!nix) launch_round<1, IX_BUCKET>(c, L, blocks, 0);
 #define NRG_RK(KK, XX) else if (L.K1 == KK && L.ix == XX) launch_round<KK, XX>(c, L, blocks, lds)
     NRG_RK(1, IX_BUCKET); NRG_RK(1, IX_BUCKET_ALL); NRG_RK(1, IX_STAMP);
     NRG_RK(2, IX_BUCKET); NRG_RK(2, IX_BUCKET_ALL); NRG_RK(2, IX_STAMP);
     NRG_RK(4, IX_BUCKET); NRG_RK(4, IX_BUCKET_ALL); NRG_RK(4, IX_STAMP);
+    NRG_RK(1, IX_PART); NRG_RK(1, IX_PART_ALL); NRG_RK(1, IX_PART_NODUP);
+    NRG_RK(2, IX_PART); NRG_RK(2, IX_PART_ALL); NRG_RK(2, IX_PART_NODUP);
+    NRG_RK(4, IX_PART); NRG_RK(4, IX_PART_ALL); NRG_RK(4, IX_PART_NODUP);
+    NRG_RK(8, IX_PART); NRG_RK(8, IX_PART_ALL); NRG_RK(8, IX_PART_NODUP);
 #undef NRG_RK
     else return hipErrorInvalidValue;
     return hipGetLastError();
@@ -1677,8 +2076,10 @@ hipError_t hm_alloc(nrg_ctx* c, u64 mb) {
         if ((e = hipMalloc(&c->d_put_slot[i], 3 * c->stamp_max * sizeof(u32))) != hipSuccess) return e;
         if ((e = hipMemsetAsync(c->d_put_slot[i], 0, 3 * c->stamp_max * sizeof(u32), c->stream)) != hipSuccess) return e;
     }
-    if ((e = hipMalloc(&c->d_dup, HM_DUP_SLOTS * sizeof(u64))) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(c->d_dup, 0, HM_DUP_SLOTS * sizeof(u64), c->stream)) != hipSuccess) return e;
+    // two sets of duplicate counters, by sample-window parity: the launch that takes a window's
+    // sample reads and clears its set while its own index blocks add to the other
+    if ((e = hipMalloc(&c->d_dup, 2 * HM_DUP_SLOTS * sizeof(u64))) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(c->d_dup, 0, 2 * HM_DUP_SLOTS * sizeof(u64), c->stream)) != hipSuccess) return e;
     void* h = nullptr;
     if ((e = hipHostMalloc(&h, 2 * sizeof(u64), hipHostMallocMapped)) != hipSuccess) return e;
     c->h_dup = (volatile u64*)h;
@@ -1737,52 +2138,6 @@ static hipError_t next_epoch(nrg_ctx* c, u32* e) {
     return hipSuccess;
 }
 
-// Sorted round (hm_sr_*): key pass with the log copy and the digit histograms, the 4-pass radix
-// sort, previous values if wanted, the last writers' stores. The round's reads ride in the next
-// launch like a bucket round's. The previous round completes first (its apply and reads).
-static hipError_t sorted_round(nrg_ctx* c, const nrg_put* src, u64 lo, u64 n, bool write_ring, const nrg_put* keep,
-                               u64 resp_lo, u64 resp_hi, u64* d_prev, uint8_t* d_prev_found, bool want_prev) {
-    hipError_t e = hm_flush(c);
-    if (e != hipSuccess) return e;
-    if (c->sort.cap < c->cfg.max_batch) {  // scratch on first use: sort pairs + sort keys
-        if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return e;
-        sort_free(c->sort);
-        if (c->d_sr_keys) (void)hipFree(c->d_sr_keys);
-        c->d_sr_keys = nullptr;
-        if (sort_alloc(c->sort, c->cfg.max_batch) != NRG_OK) return hipErrorOutOfMemory;
-        if ((e = hipMalloc(&c->d_sr_keys, c->cfg.max_batch * sizeof(u32))) != hipSuccess) return e;
-    }
-    u32* hist = nullptr;
-    if ((e = sort_prepare(c->sort, n, 32, c->stream, &hist)) != hipSuccess) return e;
-    timer_begin(c, "hm_sorted");
-    hm_sr_keys_kernel<<<grid_for(n, 2048), TPB, 0, c->stream>>>(ring_src(c, src, lo),
-                                                                write_ring ? (nrg_put*)c->d_ring : nullptr, n,
-                                                                c->d_sr_keys, hist);
-    u32 *sk = nullptr, *sv = nullptr;
-    if ((e = sort_run(c->sort, c->d_sr_keys, nullptr, n, 32, c->stream, &sk, &sv)) != hipSuccess) return e;
-    SortedJob j;
-    j.rec = ring_src(c, keep, lo);  // the log copy written by the key pass, or the caller's records
-    j.sk = sk;
-    j.sv = sv;
-    j.n = n;
-    j.table = c->d_table;
-    j.shift = c->slot_shift;
-    j.tmask = c->slots - 1;
-    j.ctl = c->d_ctl;
-    j.created_acc = c->d_created;
-    j.dup_acc = c->d_dup;
-    j.lo = lo;
-    j.resp_lo = resp_lo;
-    j.resp_hi = resp_hi;
-    j.prev = d_prev;
-    j.prevf = d_prev_found;
-    const unsigned g = (unsigned)((n + TPB - 1) / TPB);
-    if (want_prev) hm_sr_prev_kernel<<<g, TPB, 0, c->stream>>>(j);
-    hm_sr_apply_kernel<<<g, TPB, 0, c->stream>>>(j);
-    timer_end(c, "hm_sorted");
-    return hipGetLastError();
-}
-
 // Replay the records [lo, lo+n) (from `src_recs` if given, else from the ring; writing the
 // ring copy if write_ring) and answer R reads against the state after them.
 hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool write_ring, const u64* d_get_keys,
@@ -1804,19 +2159,69 @@ hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool
     u32 epoch;
     if ((e = next_epoch(c, &epoch)) != hipSuccess) return e;
     Launch L;
-    const bool sorted = !c->skewed && c->sort_min && n >= c->sort_min;
-    const bool stamp = !sorted && !want_prev && c->stamp_max && n <= c->stamp_max && !c->skewed;
-    if (sorted) {
-        // ---- sorted round: sort by key hash, last writers store (large uniform rounds) ----
-        if ((e = sorted_round(c, src, lo, n, write_ring, keep, resp_lo, resp_hi, d_prev, d_prev_found, want_prev)) !=
-            hipSuccess)
-            return e;
+    bool measured = false;  // the round's index role counts the Puts its per-tile dedup drops (key skew)
+    const bool stamp0 = !want_prev && c->stamp_max && n <= c->stamp_max && !c->skewed;
+    const bool part = c->part_mode >= 2 || (c->part_mode == 1 && !stamp0);
+    const bool stamp = stamp0 && !part;
+    if (part) {
+        // ---- partition round: {partition(e) | apply(e-1) | reads(e-1)}, then hm_papply_kernel(e) ----
+        // Tiles of 256..2048 Puts, buckets of >= 64 Puts up to 1024 (one apply workgroup each): the
+        // [tile][bucket] count words stay <= n / 2
+        const u32 K1 = n <= (1u << 14) ? 1u : n <= (1u << 16) ? 2u : n <= (1u << 18) ? 4u : 8u;
+        const u32 tile = TPB * K1;
+        const u32 log2_slots = 64 - c->slot_shift;
+        u32 nb_log = 0;
+        while ((64ull << nb_log) < n && (1u << nb_log) < HM_BK_MAX) nb_log++;
+        if (nb_log > log2_slots) nb_log = log2_slots;
+        // previous values keep every Put; otherwise a Put overwritten later in its tile is dropped
+        // when the key stream is skewed (uniform streams have next to no such Puts: no LDS hash)
+        // (the last round of every skew-sample window deduplicates too: it measures the skew)
+        L.ix = want_prev ? IX_PART_ALL : (c->skewed || c->dup_rounds + 1 >= c->dup_every) ? IX_PART : IX_PART_NODUP;
+        measured = L.ix == IX_PART;
+        L.K1 = K1;
+        L.nb = 1u << nb_log;
+        IndexJob& ij = L.ij;
+        ij.rec = ring_src(c, src, lo);
+        ij.ring_out = write_ring ? (nrg_put*)c->d_ring : nullptr;
+        ij.n = n;
+        ij.nblocks = (u32)((n + tile - 1) / tile);
+        ij.nb_log = nb_log;
+        ij.bk_shift = log2_slots - nb_log;
+        ij.ent = (u64x2*)c->d_bk_ent;
+        ij.eidx = want_prev ? (u32*)c->d_bk_key : nullptr;
+        ij.cnt = c->d_bk_cnt;
+        ij.exp = 0;
+        ij.dup_acc = c->d_dup + (c->dup_seq & 1) * HM_DUP_SLOTS;
+        attach_deferred(c, L);  // the previous round's apply and reads ride along (partition only reads)
+        if ((e = launch(c, L)) != hipSuccess) return e;
+        PApplyJob aj{};
+        aj.ent = ij.ent;
+        aj.eidx = ij.eidx;
+        aj.cnt = ij.cnt;
+        aj.ntiles = ij.nblocks;
+        aj.tile = tile;
+        aj.nb = 1u << nb_log;
+        aj.table = c->d_table;
+        aj.shift = c->slot_shift;
+        aj.tmask = c->slots - 1;
+        aj.ctl = c->d_ctl;
+        aj.created_acc = c->d_created;
+        aj.lo = lo;
+        aj.resp_lo = resp_lo;
+        aj.resp_hi = resp_hi;
+        aj.prev = d_prev;
+        aj.prevf = d_prev_found;
+        const unsigned dyn = ((ij.nblocks + 1) * 4 + ij.nblocks * 2 + 3) & ~3u;
+        if (want_prev) NRG_LAUNCH(c, "hm_papply", hm_papply_kernel<true>, 1u << nb_log, PA_TPB, dyn, c->stream, aj);
+        else NRG_LAUNCH(c, "hm_papply", hm_papply_kernel<false>, 1u << nb_log, PA_TPB, dyn, c->stream, aj);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
     } else if (stamp) {
         // ---- stamp round: one launch {index(e) | apply(e-1) | reads(e-1)} ----
         const u32 K1 = stamp_k1_for(c, n, R);
         const u32 tile = TPB * K1;
         L.ix = IX_STAMP;
         L.K1 = K1;
+        measured = true;
         L.sj.rec = ring_src(c, src, lo);
         L.sj.ring_out = write_ring ? (nrg_put*)c->d_ring : nullptr;
         L.sj.n = n;
@@ -1826,7 +2231,7 @@ hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool
         L.sj.win = L.sj.put_slot + c->stamp_alloc;
         L.sj.over = L.sj.put_slot + 2 * c->stamp_alloc;
         L.sj.created_acc = c->d_created;
-        L.sj.dup_acc = c->d_dup;
+        L.sj.dup_acc = c->d_dup + (c->dup_seq & 1) * HM_DUP_SLOTS;
         attach_deferred(c, L);
         if ((e = launch(c, L)) != hipSuccess) return e;
     } else {
@@ -1840,6 +2245,7 @@ hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool
         while ((1ull << nb_log) * target < n && (1u << nb_log) < HM_BK_MAX) nb_log++;
         if (nb_log > log2_slots) nb_log = log2_slots;
         L.ix = want_prev ? IX_BUCKET_ALL : IX_BUCKET;
+        measured = !want_prev;
         L.K1 = K1;
         L.nb = 1u << nb_log;
         IndexJob& ij = L.ij;
@@ -1853,7 +2259,7 @@ hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool
         ij.ekey = c->d_bk_key;
         ij.cnt = c->d_bk_cnt;
         ij.exp = c->exp & 0xFF;
-        ij.dup_acc = c->d_dup;
+        ij.dup_acc = c->d_dup + (c->dup_seq & 1) * HM_DUP_SLOTS;
         attach_deferred(c, L);  // the previous round's apply and reads ride along (index only reads)
         if ((e = launch(c, L)) != hipSuccess) return e;
         ElectJob ej{};
@@ -1881,7 +2287,7 @@ hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     c->rounds++;
-    c->dup_puts += n;
+    if (measured) c->dup_puts += n;  // the skew ratio is over the rounds that measured it
     if (++c->dup_rounds >= c->dup_every && (e = skew_sample(c)) != hipSuccess) return e;
     HmDeferred& p = c->pend;
     p.valid = true;

@@ -136,13 +136,10 @@ struct nrg_ctx {
     uint32_t* d_bk_cnt = nullptr;   // [bucket][index tiles] offset << 16 | count
     // Stamp rounds (<= stamp_max Puts, no previous values): per-Put slot ids by epoch parity.
     uint64_t stamp_max = 0;
+    // Partition rounds (hashmap.hip part_role + hm_papply_kernel), NRG_KNOB_PART: 0 off, 1 in place
+    // of the bucket rounds, 2 in place of the stamp and the bucket rounds.
+    uint32_t part_mode = 0;
     uint64_t stamp_alloc = 0;  // Puts the put_slot arrays hold (stamp_max <= stamp_alloc)
-    // Sorted rounds (hm_sr_*): rounds of at least sort_min Puts (0: never) on a stream that is not
-    // skewed sort their Puts by key hash instead of stamping or bucketing them. Off by default:
-    // measured slower than stamp rounds at every size (800k Puts + 900k Gets 213 vs 110 us,
-    // 4M Puts + 500k Gets 525 vs 409 us; profiles/r03_write_rounds.txt). NRG_KNOB_SORT_MIN.
-    uint64_t sort_min = 0;
-    uint32_t* d_sr_keys = nullptr;  // [max_batch] sort keys
     uint32_t epoch = 1;  // epoch of the last replay round (1: prefill / before any round)
     uint32_t epoch_limit = 0xFFFFFFF0u;  // renormalise stamps here (NRG_KNOB_EPOCH_LIMIT for tests)
     uint32_t* d_put_slot[2] = {nullptr, nullptr};

@@ -403,8 +403,7 @@ int nrg_close(nrg_ctx* c) {
     if (c->stream && c->stream != c->own_stream) (void)hipStreamSynchronize(c->stream);
     void* ptrs[] = {c->d_ring,    c->d_ctl,      c->d_table,    c->d_stack,  c->d_words,
                     c->d_sort_aux, c->d_tmp_u64, c->d_scan_desc, c->d_created, c->d_st_aux,
-                    c->d_sy_aux,  c->d_bk_ent,   c->d_bk_key,   c->d_bk_cnt, c->d_dbg,     c->d_pt,
-                    c->d_sr_keys};
+                    c->d_sy_aux,  c->d_bk_ent,   c->d_bk_key,   c->d_bk_cnt, c->d_dbg,     c->d_pt};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     sort_free(c->sort);
@@ -1145,9 +1144,9 @@ extern "C" int nrg_test_set_knob(nrg_ctx* c, int knob, uint64_t v) {
                 HIPCHK(sy_aux_init(c));
             }
             return NRG_OK;
-        case NRG_KNOB_SORT_MIN:
-            if (!hm) return NRG_E_INVAL;
-            c->sort_min = v;
+        case NRG_KNOB_PART:
+            if (!hm || v > 2) return NRG_E_INVAL;
+            c->part_mode = (uint32_t)v;
             return NRG_OK;
         case NRG_KNOB_SMALL_MAX:
             if (!hm || v > 2048) return NRG_E_INVAL;

@@ -231,14 +231,6 @@ constexpr u32 SY_MAX_NB = 512, SY_MAX_HOT = 16, SY_MAX_TILES = 4096, SY_MAX_CW =
 #define NRG_SYB_PER 10  // 1M-op rounds: 8 -> 57.2 us, 10 -> 56.4 (two passes per bucket, not three; E positions
                         // recomputed, not kept per touch); 12 spills (profiles/r03_synth_pass_size.txt)
 #endif
-#ifndef NRG_SYB_XCD
-#define NRG_SYB_XCD 1  // 0: bucket = blockIdx.x (A/B builds)
-#endif
-#ifndef NRG_SY_BALLOT
-// 1: per-wave rankings by matching the key bit by bit with ballots (A/B builds). Measured slower
-// than the LDS peer masks: 75.7-76.0 vs 61.1-61.9 us per 1M-op round (profiles/r03_synth_rank_ab.txt)
-#define NRG_SY_BALLOT 0
-#endif
 #ifndef NRG_SYP_PD
 #define NRG_SYP_PD 1  // partition: wave rounds of op records in flight ahead of the one ranked
 #endif
@@ -415,9 +407,7 @@ struct SyPartLds {
     unsigned short wcnt[SYA_WAVES][SY_MAX_NB];
     union {
         struct {
-#if !NRG_SY_BALLOT
             u64 mask[SYA_WAVES][SY_MAX_NB];
-#endif
             u32 words[SYA_WAVES][64 * CW];
         } r;
         u32 stage[SYA_OPS * CW];
@@ -451,9 +441,7 @@ __device__ __forceinline__ void sy_part_role(const SyPartArgs& A, u32 tile, SyPa
     if (dbg) dbg[K] = wall_clock64()
     SYP_MARK(0);
     for (u32 i = tid; i < SYA_WAVES * SY_MAX_NB / 2; i += SYA_TPB) ((u32*)&s_wcnt[0][0])[i] = 0;
-#if !NRG_SY_BALLOT
     for (u32 i = tid; i < SYA_WAVES * SY_MAX_NB; i += SYA_TPB) (&s_u.r.mask[0][0])[i] = 0;
-#endif
     if (lane < SY_MAX_HOT) s_hot[w][lane] = SyHot{0, 0, 0};
     __syncthreads();
     // a ranked cold touch: valid (bit 31), SET (29), word in bucket (20..28), bucket (11..19),
@@ -543,11 +531,7 @@ __device__ __forceinline__ void sy_part_role(const SyPartArgs& A, u32 tile, SyPa
 #pragma unroll
         for (int r = 0; r < CW; r++) {
             u64 peers;
-#if NRG_SY_BALLOT
-            const u32 rank = wave_rank_bits<9>(vw[r] != NOTOUCH, bw[r], lane, s_wcnt[w], &peers);
-#else
             const u32 rank = wave_rank_mask(vw[r] != NOTOUCH, bw[r], lane, s_u.r.mask[w], s_wcnt[w], &peers);
-#endif
             const u32 xl = word_in_bucket((vw[r] & ~SETBIT) - HR, bw[r], W);
             pk[orr * CW + r] = vw[r] == NOTOUCH ? 0u
                                                 : (1u << 31) | ((vw[r] & SETBIT) ? 1u << 29 : 0u) | (xl << 20) | (bw[r] << 11) | rank;
@@ -636,9 +620,7 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
     extern __shared__ u32 s_dyn[];  // s_pre[ntiles + 1], s_off[ntiles] (u16)
     __shared__ u64 s_cur[SYB_WORDS];
     __shared__ u32 s_wc[SYB_WAVES][SYB_WORDS];
-#if !NRG_SY_BALLOT
     __shared__ u64 s_mk[SYB_WAVES][SYB_WORDS];
-#endif
     __shared__ unsigned short s_tile[2][SYB_PASS];  // tile of every touch of a pass (double buffered)
     __shared__ u32 s_part[SYB_WAVES];
     __shared__ u32 s_big;  // a word ends the chunk >= 2^31 (SyFlags)
@@ -647,7 +629,7 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     // buckets in contiguous runs per XCD (workgroups go to XCDs round-robin): neighbouring
     // buckets share the lines at their segments' edges in E and V, and those stay in one L2
-    const u32 nxcd = NRG_SYB_XCD ? 8 : 1, q = gridDim.x / nxcd, rem = gridDim.x % nxcd, xcd = blockIdx.x % nxcd;
+    const u32 nxcd = 8, q = gridDim.x / nxcd, rem = gridDim.x % nxcd, xcd = blockIdx.x % nxcd;
     const u32 b = xcd * q + (xcd < rem ? xcd : rem) + blockIdx.x / nxcd;
     const u64 w0 = b ? (u64)HR + 1 + (u64)(b - 1) * W : (u64)HR;  // bucket 0: cold word 0 alone
     const u32 nw = b ? W : 1u;
@@ -661,9 +643,7 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
     for (u32 i = tid; i < SYB_WORDS; i += SYB_TPB) s_cur[i] = i < nw && w0 + i < N ? words[w0 + i] : 0ull;
     if (tid == 0) s_big = 0;
     for (u32 i = tid; i < SYB_WAVES * SYB_WORDS; i += SYB_TPB) (&s_wc[0][0])[i] = 0;
-#if !NRG_SY_BALLOT
     for (u32 i = tid; i < SYB_WAVES * SYB_WORDS; i += SYB_TPB) (&s_mk[0][0])[i] = 0;
-#endif
     __syncthreads();
     SY_MARK(1);
     // exclusive scan of the per-tile counts: thread owns tiles [tid*K, tid*K + K)
@@ -757,11 +737,7 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
                 for (int q = 0; q < SYB_PER; q++) {
                     const u32 i = base + (u32)w * (SYB_PER * 64) + q * 64 + lane;
                     u64 peers;
-#if NRG_SY_BALLOT
-                    sv[q] = wave_rank_bits<SYB_SHIFT>(i < total, ent_word(ent[q]), lane, s_wc[w], &peers);
-#else
                     sv[q] = wave_rank_mask(i < total, ent_word(ent[q]), lane, s_mk[w], s_wc[w], &peers);
-#endif
                 }
             }
             __syncthreads();
@@ -796,23 +772,14 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
             }
             for (int ww = 0; ww < SYB_WAVES; ww++) {
                 if (ww == w) {
-#if NRG_SY_BALLOT
-                    // not unrolled: unrolled inside the wave loop, the ballot ranking spills ~900 B/lane
-#pragma unroll 1
-#else
 #pragma unroll
-#endif
                     for (int q = 0; q < SYB_PER; q++) {
                         const u32 i = base + (u32)w * (SYB_PER * 64) + q * 64 + lane;
                         const bool valid = i < total;
                         const u32 xl = ent_word(ent[q]);
                         const bool isset = valid && ent_set(ent[q]);
                         u64 peers;
-#if NRG_SY_BALLOT
-                        (void)wave_rank_bits<SYB_SHIFT>(valid, xl, lane, s_wc[w], &peers);
-#else
                         (void)wave_rank_mask(valid, xl, lane, s_mk[w], s_wc[w], &peers);
-#endif
                         const u64 P = peers & ((1ull << lane) - 1);
                         const u64 S = __ballot(isset) & P;
                         const int sl = S ? 63 - __clzll(S) : lane;

@@ -27,9 +27,9 @@ def _puts(keys, vals):
     return r
 
 
-def _dev(nrg, max_batch):
-    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=26, max_batch=max_batch, pipeline=1,
-                            log_bytes=64 * 4 * max_batch)
+def _dev(nrg, max_batch, part=0):
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, knobs={"PART": part}, log2_slots=26, max_batch=max_batch,
+                            pipeline=1, log_bytes=64 * 4 * max_batch)
     dev.use_torch_stream()
     dev.hm_prefill_range(PREFILL, 1)
     return dev
@@ -62,11 +62,13 @@ def _check(got, want, what):
     np.testing.assert_array_equal(g, want, err_msg=what)
 
 
-def test_b1_rounds_with_previous_values(nrg, orc):
-    """configs[1] with HashMap::insert's previous values: 3 pipelined 100k + 900k rounds."""
+@pytest.mark.parametrize("part", [0, 2])
+def test_b1_rounds_with_previous_values(nrg, orc, part):
+    """configs[1] with HashMap::insert's previous values: 3 pipelined 100k + 900k rounds (bucket
+    elector, or partition rounds)."""
     import torch
 
-    dev = _dev(nrg, 1 << 20)
+    dev = _dev(nrg, 1 << 20, part)
     om = _prefilled_oracle(orc)
     outs = []
     for r in range(3):
@@ -90,16 +92,17 @@ def test_b1_rounds_with_previous_values(nrg, orc):
     dev.close()
 
 
+@pytest.mark.parametrize("part", [0, 2])
 @pytest.mark.parametrize("prev", [True, False])
-def test_configs2_per_gpu_round(nrg, orc, prev):
+def test_configs2_per_gpu_round(nrg, orc, prev, part):
     """configs[2]'s per-GPU work: 8 segments x 500k Puts (the all-gathered round of 8 ranks at 50 %
     writes, 4M Puts replayed in place) + this rank's 500k Gets, two pipelined rounds through
     nrg_hashmap_round_segments_async; with previous values for the rank's own segment (bucket
-    elector) or without (Ok(None), 4M-Put stamp rounds)."""
+    elector) or without (Ok(None), 4M-Put stamp rounds); part = 2: partition rounds either way."""
     import torch
 
     G, W, R = 8, 500_000, 500_000
-    dev = _dev(nrg, G * W)
+    dev = _dev(nrg, G * W, part)
     om = _prefilled_oracle(orc)
     outs = []
     for r, own in enumerate([3, 6]):
@@ -130,15 +133,16 @@ def test_configs2_per_gpu_round(nrg, orc, prev):
     dev.close()
 
 
+@pytest.mark.parametrize("part", [0, 2])
 @pytest.mark.parametrize("scramble", [False, True])
-def test_zipf_50pct_full_size(nrg, orc, scramble):
+def test_zipf_50pct_full_size(nrg, orc, scramble, part):
     """configs[3]: Zipf(0.99) over the 10M key space at 50 % writes (500k Puts + 500k Gets per
     round), hot keys adjacent or scrambled; last-writer-wins and every previous value under
     heavy same-key conflicts, pipelined rounds with and without responses."""
     import torch
 
     W, R = 500_000, 500_000
-    dev = _dev(nrg, 1 << 20)
+    dev = _dev(nrg, 1 << 20, part)
     om = _prefilled_oracle(orc)
     outs = []
     for r in range(3):

@@ -71,14 +71,11 @@ def _digest(lib, L, ctx):
 
 
 @pytest.mark.parametrize("G", [2, 3, 8])
-@pytest.mark.parametrize("pipeline,max_batch,sort_min", [(1, 1 << 16, 0), (0, 1 << 16, 0), (1, 3000, 0),
-                                                         (1, 1 << 16, 1)])
-def test_group_hashmap_members(nrg, orc, G, pipeline, max_batch, sort_min):
+@pytest.mark.parametrize("pipeline,max_batch", [(1, 1 << 16), (0, 1 << 16), (1, 3000)])
+def test_group_hashmap_members(nrg, orc, G, pipeline, max_batch):
     """Hashmap group rounds: every member's Gets and (for the members that ask) its own Puts'
     previous values, and every member's final contents, equal to the NR replay. max_batch 3000
-    replays the gathered log in chunks; the small ring wraps and is garbage-collected. sort_min 1:
-    every member replays the gathered log as sorted rounds (the default for rounds of >= 2^19
-    Puts, e.g. an 8-GPU round at 10 % writes)."""
+    replays the gathered log in chunks; the small ring wraps and is garbage-collected."""
     import torch
 
     L = nrg._lib
@@ -87,8 +84,6 @@ def test_group_hashmap_members(nrg, orc, G, pipeline, max_batch, sort_min):
     cfg.log2_slots, cfg.max_batch, cfg.pipeline = 17, max_batch, pipeline
     cfg.log_bytes = 64 * (1 << 16)
     g, ctxs = _open(L, lib, G, cfg)
-    for c in ctxs:
-        L.check(lib.nrg_test_set_knob(c, L.KNOBS["SORT_MIN"], sort_min))
     for c in ctxs:
         L.check(lib.nrg_hashmap_prefill_range(c, 4000, 1))
     om = orc.HashMap()

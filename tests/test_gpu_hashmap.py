@@ -33,9 +33,9 @@ def _check_state(dev, om):
     assert dev.hm_digest() == om.digest()
 
 
-# knobs of the replay paths: default selection, sorted rounds forced for every size, and the
+# knobs of the replay paths: default selection, partition rounds for every round, and the
 # one-launch small rounds (the combiner's) for rounds of up to 2048 Puts
-PATHS = {"default": {}, "sorted": {"SORT_MIN": 1}, "small": {"SMALL_MAX": 2048}}
+PATHS = {"default": {}, "part": {"PART": 2}, "small": {"SMALL_MAX": 2048}}
 
 
 @pytest.mark.parametrize("path", list(PATHS))
@@ -96,8 +96,7 @@ def test_exec_chunks_longer_than_max_batch(nrg, orc, path):
 
 @pytest.mark.parametrize("path", list(PATHS))
 def test_zipf_conflicts(nrg, orc, path):
-    """Zipf 0.99 stream: hot keys stress last-writer-wins ordering and CAS contention (sorted
-    rounds: long runs of one key next to each other)."""
+    """Zipf 0.99 stream: hot keys stress last-writer-wins ordering and CAS contention."""
     dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, knobs=PATHS[path], log2_slots=20, max_batch=1 << 17)
     om = orc.HashMap()
     dev.hm_prefill_range(10000, 1)
@@ -146,16 +145,17 @@ def test_fused_round_device(nrg, orc):
     _check_state(dev, om)
 
 
-@pytest.mark.parametrize("path", ["stamp", "bucket", "sorted"])
+@pytest.mark.parametrize("path", ["stamp", "bucket", "part"])
 def test_pipelined_rounds_back_to_back(nrg, orc, path):
     """config.pipeline = 1: rounds enqueued back to back, no host sync in between. Each round's
     reads run in the next round's launch, beside its index pass (and, for stamp rounds, beside
     the apply of their own round's writes), and must see exactly their own round's state (keys
     created by later rounds invisible, values overwritten later not yet there).
-    Knob STAMP_MAX = 0 sends every round through the bucket elector instead."""
+    Knob STAMP_MAX = 0 sends every round through the bucket elector instead, PART = 2 through
+    partition rounds."""
     import torch
 
-    knobs = {"STAMP_MAX": 0} if path == "bucket" else PATHS["sorted"] if path == "sorted" else {}
+    knobs = {"bucket": {"STAMP_MAX": 0}, "part": {"PART": 2}}.get(path, {})
     dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, knobs=knobs, log2_slots=17, max_batch=1 << 14, pipeline=1)
     dev.use_torch_stream()
     om = orc.HashMap()
@@ -472,7 +472,7 @@ def test_epoch_renormalisation(nrg, orc):
     new keys, overwrites and side-slot keys across several renormalisations, against the oracle."""
     import torch
 
-    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, knobs={"EPOCH_LIMIT": 6, "STAMP_MAX": 5000, "SORT_MIN": 6500},
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, knobs={"EPOCH_LIMIT": 6, "STAMP_MAX": 5000},
                             log2_slots=16, max_batch=8192, pipeline=1)
     dev.use_torch_stream()
     om = orc.HashMap()
@@ -480,7 +480,7 @@ def test_epoch_renormalisation(nrg, orc):
     om.prefill_range(500, 1)
     outs, want = [], []
     for r in range(17):
-        W = 3000 if r % 3 else (7000 if r % 2 else 6000)  # 7000: a sorted round, 6000: a bucket round
+        W = 3000 if r % 3 else (7000 if r % 2 else 6000)  # > STAMP_MAX: bucket rounds
         keys = orc.gen_uniform(W, 900 + r, 4000 + 150 * r)
         keys[::113] = EMPTY
         vals = orc.gen_raw(W, 950 + r)
@@ -503,18 +503,21 @@ def test_epoch_renormalisation(nrg, orc):
     _check_state(dev, om)
 
 
-def test_skew_switches_round_kind(nrg, orc):
+@pytest.mark.parametrize("part", [0, 2])
+def test_skew_switches_round_kind(nrg, orc, part):
     """Stamp rounds (one launch, one stamp atomic per distinct key per block) are faster for
     uniform keys, bucket rounds (no atomics per Put) for skewed ones; the replica switches from
     the sampled share of Puts combined inside their block (every 2 rounds here). Uniform rounds,
     then Zipf(0.99), then uniform again, pipelined: every Get and the final state bit-exact
-    across both switches, and the switches happen."""
+    across both switches, and the switches happen. part = 2: partition rounds, which drop the
+    Puts overwritten inside their tile only while the stream is skewed (and in the last round of
+    every sample window, which measures it)."""
     import ctypes as C
 
     import torch
 
-    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, knobs={"SKEW_EVERY": 2}, log2_slots=19, max_batch=1 << 15,
-                            pipeline=1)
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, knobs={"SKEW_EVERY": 2, "PART": part}, log2_slots=19,
+                            max_batch=1 << 15, pipeline=1)
     dev.use_torch_stream()
     om = orc.HashMap()
     dev.hm_prefill_range(5000, 1)
