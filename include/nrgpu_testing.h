@@ -51,6 +51,11 @@ int nrg_test_debug_read(nrg_ctx* ctx, uint64_t* out, uint64_t words);
                                    workgroup per bucket finds/claims and stores each key: no
                                    device atomic per Put) -- 0 off, 1 instead of the bucket rounds,
                                    2 instead of the stamp and the bucket rounds                  */
+#define NRG_KNOB_STALL 14       /* tests: 1 = odd waves sleep ~30 us where a workgroup next reuses LDS
+                                   another wave may still read (synthetic bucket pass, hashmap
+                                   elector and partition-round apply chunks, stack queries/table);
+                                   2 (+1) = synthetic only, also drop the barrier that guards the
+                                   bucket pass's tile map (diagnostic: results WRONG)            */
 int nrg_test_set_knob(nrg_ctx* ctx, int knob, uint64_t value);
 
 /* Replica groups created after nrg_test_loopback_collectives(1) (nrg_group_open,

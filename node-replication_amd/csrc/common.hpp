@@ -93,6 +93,14 @@ __device__ __forceinline__ u32 ld_relaxed32(const u32* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Test-only stall (NRG_KNOB_STALL): odd waves sleep ~30 us at a point where the workgroup's
+// waves next reuse LDS another wave may still read, so a missing barrier shows up as a wrong
+// result instead of a rare timing accident.
+__device__ __forceinline__ void test_stall(u32 on, int wave) {
+    if (on && (wave & 1))
+        for (int i = 0; i < 32; i++) __builtin_amdgcn_s_sleep(127);
+}
+
 // Wave-wide (64-lane) inclusive scan helpers.
 __device__ __forceinline__ u32 lane_id() { return threadIdx.x & 63; }
 

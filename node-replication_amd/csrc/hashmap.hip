@@ -74,6 +74,8 @@ struct ReadJob {
     u32 nblocks;
     u32 epoch;    // the reads see the state after round `epoch`
     bool use_rec; // that round's apply may run in the same launch: take its winners' records
+    bool quiet;   // nothing in this launch writes the table (no stamp index, no apply): a key is
+                  // present iff its probe chain holds it, and the stamps are not read
     RecSrc rec;
     // key-skew sample riding in this launch (skew_sample): the launch's last block moves the
     // duplicate counters to mapped host memory as {seq, dups}; seq 0 = none
@@ -678,7 +680,7 @@ __device__ __forceinline__ void read_role(const ReadJob& j, u32 blk, const Slot*
         st[r] = 0;
         if (probe) {
             w[r] = *(const u64x2*)&table[s[r]];
-            st[r] = table[s[r]].st[par];
+            if (!j.quiet) st[r] = table[s[r]].st[par];
         }
     }
 #pragma unroll
@@ -687,7 +689,28 @@ __device__ __forceinline__ void read_role(const ReadJob& j, u32 blk, const Slot*
         u64 v = 0;
         bool f = false;
         if (k[r] == EMPTY_KEY) {
-            if (ctl->sp_claim) f = resolve(ctl->sp.val, ctl->sp.st[par], j, &v);
+            if (ctl->sp_claim) {
+                if (j.quiet) {
+                    f = true;
+                    v = ctl->sp.val;
+                } else {
+                    f = resolve(ctl->sp.val, ctl->sp.st[par], j, &v);
+                }
+            }
+        } else if (j.quiet) {
+            u64 kk = w[r].x, vv = w[r].y, sl = s[r];
+            for (u64 pr = 0; pr <= tmask; pr++) {
+                if (kk == k[r]) {
+                    f = true;
+                    v = vv;
+                    break;
+                }
+                if (kk == EMPTY_KEY) break;
+                sl = (sl + 1) & tmask;
+                const u64x2 x = *(const u64x2*)&table[sl];
+                kk = x.x;
+                vv = x.y;
+            }
         } else {
             u64 kk = w[r].x, vv = w[r].y, stt = st[r], sl = s[r];
             asm volatile("" : "+v"(kk), "+v"(vv), "+v"(stt));
@@ -788,6 +811,7 @@ struct ElectJob {
     uint8_t* prevf;
     u32 exp;  // diagnostic knobs (NRG_EXP >> 8; wrong results): 1 counts only, 2 + pass 1 only, 4 no claims
     u64* dbg; // NRG_EXP & 0x10000 (diagnostic): per block, thread 0's wall clock at the phase edges
+    u32 stall;  // NRG_KNOB_STALL (tests)
 };
 
 constexpr int EL_HT = 2048;  // LDS hash entries (distinct keys of one part of a bucket)
@@ -874,6 +898,7 @@ __global__ __launch_bounds__(TPB) void hm_elect_kernel(ElectJob j) {
     auto load_chunk = [&](u32 base) {
         fill_tiles(base);
         __syncthreads();
+        test_stall(j.stall & 1, w);  // (tests) slow waves read s_tile below
 #pragma unroll
         for (int r = 0; r < EL_PER; r++) {
             const u32 i = base + r * TPB + threadIdx.x;
@@ -1177,6 +1202,7 @@ struct PApplyJob {
     u64 lo, resp_lo, resp_hi;
     u64* prev;
     uint8_t* prevf;
+    u32 stall;  // NRG_KNOB_STALL (tests)
 };
 
 constexpr int PA_TPB = 256;
@@ -1343,6 +1369,7 @@ __global__ __launch_bounds__(PA_TPB) void hm_papply_kernel(PApplyJob j) {
             for (u32 i = lo_; i < hi_; i++) s_tile[i - base] = (uint16_t)t;
         }
         __syncthreads();
+        test_stall(j.stall & 1, w);  // (tests) slow waves read s_tile below
         u64x2 x[PER];
         u32 ix[PER], hh[PER];
 #pragma unroll
@@ -1990,6 +2017,9 @@ static hipError_t launch(nrg_ctx* c, Launch& L) {
     L.rj.nblocks = (u32)((L.rj.R + TPB * RPT - 1) / (TPB * RPT));
     L.sj.exp = c->exp >> 20;
     const u32 nix = L.ix == IX_STAMP ? L.sj.nblocks : L.ij.nblocks;
+    // reads beside a bucket or partition pass (which only read the table, or not even that), or
+    // alone, with no stamp round's apply riding along: the table is quiescent
+    L.rj.quiet = (L.ix != IX_STAMP || nix == 0) && L.aj.nblocks == 0;
     u32 blocks = nix + L.aj.nblocks + L.rj.nblocks;
     if (blocks == 0) return hipSuccess;
     // a pending skew sample, or the error copy of a launch that ends a round (no index role:
@@ -2211,6 +2241,7 @@ hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool
         aj.resp_hi = resp_hi;
         aj.prev = d_prev;
         aj.prevf = d_prev_found;
+        aj.stall = c->stall;
         const unsigned dyn = ((ij.nblocks + 1) * 4 + ij.nblocks * 2 + 3) & ~3u;
         if (want_prev) NRG_LAUNCH(c, "hm_papply", hm_papply_kernel<true>, 1u << nb_log, PA_TPB, dyn, c->stream, aj);
         else NRG_LAUNCH(c, "hm_papply", hm_papply_kernel<false>, 1u << nb_log, PA_TPB, dyn, c->stream, aj);
@@ -2281,6 +2312,7 @@ hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool
         ej.prevf = d_prev_found;
         ej.exp = (c->exp >> 8) & 0xFF;
         ej.dbg = (c->exp & 0x10000) ? c->d_dbg : nullptr;
+        ej.stall = c->stall;
         const unsigned dyn = (ij.nblocks + 1) * 4 + ij.nblocks * 2;
         if (want_prev) NRG_LAUNCH(c, "hm_elect", hm_elect_kernel<true>, 1u << nb_log, TPB, dyn, c->stream, ej);
         else NRG_LAUNCH(c, "hm_elect", hm_elect_kernel<false>, 1u << nb_log, TPB, dyn, c->stream, ej);

@@ -130,6 +130,8 @@ struct nrg_ctx {
     int32_t comb_spin = -1;   // combiner knobs (NRG_KNOB_COMB_SPIN / _DEPTH): -1 / 0 = defaults
     uint64_t small_max = 0;   // hashmap: rounds of <= small_max Puts take the one-launch small round
     uint32_t comb_depth = 0;
+    uint32_t stall = 0;       // NRG_KNOB_STALL (tests): 1 odd waves sleep at LDS reuse points, 2 (synthetic,
+                              // diagnostic: wrong results) without the bucket pass's tile-map barrier
     uint64_t* d_created = nullptr;  // [HM_CREATED_SLOTS] keys created by replay rounds
     void* d_bk_ent = nullptr;       // [index tiles][tile] 16-B {id << 32 | i+1, value}
     uint64_t* d_bk_key = nullptr;   // [index tiles][tile] key of each entry

@@ -1144,6 +1144,10 @@ extern "C" int nrg_test_set_knob(nrg_ctx* c, int knob, uint64_t v) {
                 HIPCHK(sy_aux_init(c));
             }
             return NRG_OK;
+        case NRG_KNOB_STALL:
+            if (v > 3) return NRG_E_INVAL;
+            c->stall = (uint32_t)v;
+            return NRG_OK;
         case NRG_KNOB_PART:
             if (!hm || v > 2) return NRG_E_INVAL;
             c->part_mode = (uint32_t)v;

@@ -191,6 +191,7 @@ struct StPass {
     u64 rlo, rhi;             // response window (log indices)
     u32* resp;
     uint8_t* some;
+    u32 stall;  // NRG_KNOB_STALL (tests)
 };
 
 __device__ __forceinline__ void wave_sync() {  // LDS written by other lanes of this wave
@@ -553,6 +554,7 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
     // lowest level: with the unclamped structures nothing depends on the start depth D. ----
     constexpr int QI = 4;
     auto queries = [&](int lw, int slot, int nslots) {
+        test_stall(A.stall & 1, wv);  // (tests) slow waves read the query structures below
         const u32* up = s_wave[lw] + W_STK;
         const int tot = s_tot[lw];
         for (int h0 = slot * 64 * QI + lane; h0 < tot; h0 += 64 * QI * nslots) {
@@ -709,6 +711,7 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
     ST_MARK(6);
 
     // ---- 5. the tile's last-Push table for levels [T0, tile end) ----
+    test_stall(A.stall & 1, wv);  // (tests) slow waves read their lane stacks below
     {
         u32* tab = tl.table + (u64)tile * ST_TILE;
         const int hi = aend_r < later ? aend_r : later;
@@ -822,6 +825,7 @@ static StPass st_pass(nrg_ctx* c, u32 par) {
     const u64 mt = st_max_tiles(c);
     StPass s{};
     s.par = par;
+    s.stall = c->stall;
     s.ring = (nrg_stack_op*)c->d_ring;
     s.ring_mask = c->log_size - 1;
     // descriptors: [32 u64 unused] [parity][max tiles] u64; zero at open, and each chunk's finish

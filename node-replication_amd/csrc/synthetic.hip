@@ -603,7 +603,7 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
                                                             u64* __restrict__ words, u64 N, u32 HR, u32 W,
                                                             const nrg_synth_op* __restrict__ ring, u64 ring_mask, u64 lo,
                                                             SyFlags* __restrict__ fl, u32 epoch, u32 par,
-                                                            u64* __restrict__ dbg) {
+                                                            u64* __restrict__ dbg, u32 stall) {
     // dbg (NRG_EXP & 2, diagnostic): per block, thread 0's wall clock at the phase edges
     // [0] start [1] prologue loaded [2] scanned, then summed over passes [3] tile map [4] gather
     // [5] rank + place [6] stores, [7] end, [8] passes
@@ -800,21 +800,29 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
             }
         }
         SY_ACC(2);
+        test_stall(stall & 1, w);  // (tests) slow waves still read cmap below
+        // (stall & 2, diagnostic: a map overwritten under a slow wave gives a wild position; the
+        // store is dropped instead of landing outside V)
+        const u32 vcap = (stall & 2) ? ntiles * tile_entries : ~0u;
         if (v32) {
 #pragma unroll
             for (int q = 0; q < SYB_PER; q++)
-                if (base + (u32)w * (SYB_PER * 64) + q * 64 + lane < total)
-                    ((u32*)V)[gpos_of(base, cmap, base + (u32)w * (SYB_PER * 64) + q * 64 + lane)] = (u32)sv[q];
+                if (base + (u32)w * (SYB_PER * 64) + q * 64 + lane < total) {
+                    const u32 gp = gpos_of(base, cmap, base + (u32)w * (SYB_PER * 64) + q * 64 + lane);
+                    if (gp < vcap) ((u32*)V)[gp] = (u32)sv[q];
+                }
         } else {
 #pragma unroll
             for (int q = 0; q < SYB_PER; q++)
-                if (base + (u32)w * (SYB_PER * 64) + q * 64 + lane < total)
-                    V[gpos_of(base, cmap, base + (u32)w * (SYB_PER * 64) + q * 64 + lane)] = sv[q];
+                if (base + (u32)w * (SYB_PER * 64) + q * 64 + lane < total) {
+                    const u32 gp = gpos_of(base, cmap, base + (u32)w * (SYB_PER * 64) + q * 64 + lane);
+                    if (gp < vcap) V[gp] = sv[q];
+                }
         }
         // the stores above read this pass's tile map (cmap); the next pass's map is built into
         // the other buffer, but the pass after that overwrites this one: every wave must be done
         // with it before any wave starts the next iteration's map_pass
-        __syncthreads();
+        if (!(stall & 2)) __syncthreads();  // (stall & 2: diagnostic only, results wrong)
         SY_ACC(3);
     }
     bool big = false;
@@ -1086,7 +1094,7 @@ static hipError_t sy_bucket_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 re
     const size_t dyn = (size_t)(ntiles + 1) * 4 + (size_t)ntiles * 2;
     sy_bucket_kernel<<<NB, SYB_TPB, dyn, st>>>(x.E[par], x.cnt, ntiles, SYA_OPS * CW, x.V, c->d_words, cf.synth_n, HR,
                                                W, A.ring, A.ring_mask, lo, x.fl, A.epoch, par,
-                                               (c->exp & 2) ? c->d_dbg : nullptr);
+                                               (c->exp & 2) ? c->d_dbg : nullptr, c->stall);
     timer_end(c, "sy_replay");
     if ((e = hipGetLastError()) != hipSuccess) return e;
     // this chunk's sums: in the next chunk's partition launch (pipeline = 1) or now

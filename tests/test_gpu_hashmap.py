@@ -337,12 +337,16 @@ def _mix64(x):
         return x ^ (x >> np.uint64(31))
 
 
-def test_one_bucket_rounds(nrg, orc):
+@pytest.mark.parametrize("knobs", [{}, {"STAMP_MAX": 0, "STALL": 1}, {"PART": 2}, {"PART": 2, "STALL": 1}])
+def test_one_bucket_rounds(nrg, orc, knobs):
     """Pipelined rounds whose keys all fall into ONE elector bucket (many chunks, finer parts,
-    duplicates across index tiles), with side-slot keys and a Zipf round, against the oracle."""
+    duplicates across index tiles), with side-slot keys and a Zipf round, against the oracle.
+    Also as partition rounds (PART = 2: one apply workgroup takes the bucket in many chunks), and
+    with odd waves stalled where a chunk's tile map is read (STALL = 1) before the next chunk
+    rebuilds it."""
     import torch
 
-    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=17, max_batch=8192, pipeline=1)
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, knobs=knobs, log2_slots=17, max_batch=8192, pipeline=1)
     dev.use_torch_stream()
     om = orc.HashMap()
     dev.hm_prefill_range(3000, 1)

@@ -149,16 +149,19 @@ def test_stack_eight_segment_round(nrg, orc, init_n):
     dev.close()
 
 
-@pytest.mark.parametrize("init_n,n,rounds", [(50000, 200000, 4), (3, 20000, 3), (0, 8192 * 3 + 77, 3)])
-def test_stack_pipelined_rounds(nrg, orc, init_n, n, rounds):
+@pytest.mark.parametrize("init_n,n,rounds,stall", [(50000, 200000, 4, 0), (50000, 200000, 4, 1), (3, 20000, 3, 0),
+                                                  (3, 20000, 3, 1), (0, 8192 * 3 + 77, 3, 0)])
+def test_stack_pipelined_rounds(nrg, orc, init_n, n, rounds, stall):
     """pipeline=1: a chunk's finish (cross-tile Pops, commit) rides in the next chunk's launch
     (Replica::combine rounds back to back, nr/src/replica.rs:544-595); every round answers into
     its own buffers, complete after nrg_join. Then chunked exec (several chunks per call, each
-    fused with the previous chunk's finish) and a final dump, all against the Vec oracle."""
+    fused with the previous chunk's finish) and a final dump, all against the Vec oracle.
+    stall = 1 (NRG_KNOB_STALL): odd waves sleep before reading the query structures and their
+    lane stacks."""
     import torch
 
-    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_STACK, 0, max_batch=1 << 18, stack_capacity=1 << 22, pipeline=1,
-                            log_bytes=64 * 4 * (1 << 20))
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_STACK, 0, knobs={"STALL": stall}, max_batch=1 << 18,
+                            stack_capacity=1 << 22, pipeline=1, log_bytes=64 * 4 * (1 << 20))
     init = np.arange(init_n, dtype=np.uint32)
     dev.st_init(init)
     os_ = orc.Stack(init)

@@ -171,17 +171,39 @@ def test_synth_bench_size_rounds(nrg, orc):
     np.testing.assert_array_equal(dev.sy_dump(), os_.dump())
 
 
+def _heavy(ops):
+    ops["tid"][::3] = 0
+    ops["r2"][::20] = 0
+
+
+@pytest.mark.parametrize("stall", [0, 1])
 @pytest.mark.parametrize("wo", [0, 40])
-def test_synth_heavy_buckets(nrg, orc, wo):
+def test_synth_heavy_buckets(nrg, orc, wo, stall):
     """Skewed rounds: tid 0 (whose cold touches start at word hot_reads) on 30 % of the ops and
     r2 = 0 (all of an op's cold touches on one word) on 5 %, so a few buckets carry several times
-    the mean and take many passes; WriteOnly ops make the values depend on each word's last SET."""
-    def tweak(ops):
-        ops["tid"][::3] = 0
-        ops["r2"][::20] = 0
-
-    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_SYNTHETIC, 0, max_batch=1 << 18)
+    the mean and take many passes; WriteOnly ops make the values depend on each word's last SET.
+    stall = 1 (NRG_KNOB_STALL): odd waves of every bucket workgroup sleep before each pass's value
+    stores, which read the pass's tile map while the next-but-one pass rebuilds it."""
+    tweak = _heavy
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_SYNTHETIC, 0, knobs={"STALL": stall}, max_batch=1 << 18)
     _check_rounds(nrg, orc, dev, orc.Synthetic(), 4, 200_000, 0x4EA + wo, list(range(64)), wo, tweak)
+    dev.close()
+
+
+def test_stall_exposes_a_missing_barrier(nrg, orc):
+    """The stall knob makes the race that 2a46f39's barrier closes deterministic: with the barrier
+    after each pass's value stores dropped (STALL = 3, diagnostic only) the slow waves store
+    through a tile map the fast waves have already rebuilt for a later pass, and the heavy rounds
+    come out wrong every time; test_synth_heavy_buckets[stall=1] is the same stall with the
+    barrier in place. (Stores the broken map would send outside V are dropped.)"""
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_SYNTHETIC, 0, knobs={"STALL": 3}, max_batch=1 << 18)
+    os_ = orc.Synthetic()
+    ops = _ops(orc, 200_000, 0x4EA, list(range(64)), 0)
+    _heavy(ops)
+    first = dev.log_append(ops, 1)
+    resp, _ = dev.log_exec(first, first + len(ops))
+    oresp = os_.replay(np.stack([ops["tid"], ops["r1"], ops["r2"], ops["op"]], axis=1))
+    assert np.count_nonzero(resp != oresp) > 0, "the stall did not expose the missing barrier"
     dev.close()
 
 
