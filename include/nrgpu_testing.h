@@ -49,8 +49,9 @@ int nrg_test_debug_read(nrg_ctx* ctx, uint64_t* out, uint64_t words);
                                    combiner sets 2048 while it is open)                          */
 #define NRG_KNOB_PART 13        /* hashmap: partition rounds (Puts grouped by home-slot bucket, one
                                    workgroup per bucket finds/claims and stores each key: no
-                                   device atomic per Put) -- 0 off, 1 instead of the bucket rounds,
-                                   2 instead of the stamp and the bucket rounds                  */
+                                   device atomic per Put) -- 1 (default) for previous values,
+                                   skewed streams and rounds of >= 393216 Puts, 2 for every round,
+                                   0 never (the bucket elector instead)                          */
 #define NRG_KNOB_STALL 14       /* tests: 1 = odd waves sleep ~30 us where a workgroup next reuses LDS
                                    another wave may still read (synthetic bucket pass, hashmap
                                    elector and partition-round apply chunks, stack queries/table);

@@ -86,13 +86,23 @@ struct alignas(64) Batch {
     uint8_t* wsome = nullptr;
     char* rresp = nullptr;  // cap read responses
     uint8_t* rsome = nullptr;
-    uint32_t* err = nullptr;  // the replica's error latch after the round
+    uint32_t* err = nullptr;  // the replica's error latch after the round (ERR_PENDING until then)
+    uint32_t polls = 0;       // retire's polls of the word (the event is queried every 256th)
     hipEvent_t done = nullptr;
 };
 
+// Completion of a round: its last write is the replica's error latch, copied into the batch's
+// mapped word (host memory) -- by the one-workgroup small round kernel itself, or by this kernel
+// behind the round. The combiner thread polls the word: no event record or query per round.
+constexpr uint32_t ERR_PENDING = 0xFFFFFFFFu;  // the round's error word until the round completes
+
 // device: the error latch of the replica, copied to host memory and cleared after a round
 __global__ void comb_err_kernel(nrg::DevCtl* ctl, uint32_t* out) {
-    if (threadIdx.x == 0) out[0] = atomicExch(&ctl->err, 0u);
+    if (threadIdx.x == 0) {
+        const uint32_t e = atomicExch(&ctl->err, 0u);
+        __threadfence_system();
+        *(volatile uint32_t*)out = e;
+    }
 }
 
 // device: n Peeks of the stack after the round (nr/tests/stack.rs:26-29, benches/stack.rs)
@@ -162,14 +172,21 @@ void comb_free(nrg_combiner* m) {
     delete m;
 }
 
-// Retire completed rounds in order and wake their clients (combiner thread).
+// Retire completed rounds in order and wake their clients (combiner thread). A round is complete
+// when its error word leaves ERR_PENDING; its event is queried only now and then, to catch a
+// round that failed on the device and will never write the word.
 void retire(nrg_combiner* m) {
     uint64_t k = m->completed.load(std::memory_order_relaxed);
     while (k < m->launched.load(std::memory_order_acquire)) {
         Batch& x = m->b[k % NB];
-        const hipError_t q = hipEventQuery(x.done);
-        if (q == hipErrorNotReady) break;
-        if (q != hipSuccess && x.rc == NRG_OK) x.rc = NRG_E_HIP;
+        const uint32_t ew = *(volatile uint32_t*)x.err;
+        if (ew == ERR_PENDING && x.rc == NRG_OK) {
+            if ((++x.polls & 255) != 0) break;
+            const hipError_t q = hipEventQuery(x.done);
+            if (q == hipErrorNotReady) break;
+            if (*(volatile uint32_t*)x.err == ERR_PENDING) x.rc = NRG_E_HIP;  // done, and the word never came
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);  // responses after the word
         if (x.rc == NRG_OK) x.rc = err_code(*(volatile uint32_t*)x.err);
         x.state.store(DONE, std::memory_order_release);
         m->completed.store(++k, std::memory_order_seq_cst);
@@ -184,9 +201,16 @@ int launch(nrg_combiner* m, Batch& x, uint32_t W, uint32_t R) {
     if (rc) return rc;
     hipStream_t st = (hipStream_t)nrg_get_stream(c);
     const uint32_t origin = c->cfg.replica_id;
+    *(volatile uint32_t*)x.err = ERR_PENDING;
+    x.polls = 0;
+    // hashmap rounds of <= 2048 Puts (>= 1) and <= 8192 Gets run as ONE small-round workgroup
+    // (hashmap.hip small_round), whose last write can be the error copy
+    const bool small = m->kind == NRG_DS_HASHMAP && W > 0 && W <= c->small_max && W <= 2048 && R <= 8192;
     switch (m->kind) {
         case NRG_DS_HASHMAP:  // Put -> HashMap::insert's previous value (nr/examples/hashmap.rs:46-50)
-            c->err_out = x.err;  // the round's last launch copies the error latch (no extra kernel)
+            // a small round (one workgroup, the round's only launch) copies the error latch as its
+            // last write; any other round gets comb_err_kernel behind it
+            if (small) c->err_out = x.err;
             rc = nrg_hashmap_round_async(c, (const nrg_put*)x.recs, W, origin, (const uint64_t*)x.reads, R,
                                          (uint64_t*)x.rresp, x.rsome, (uint64_t*)x.wresp, x.wsome);
             break;
@@ -207,7 +231,8 @@ int launch(nrg_combiner* m, Batch& x, uint32_t W, uint32_t R) {
             break;
     }
     if (!rc && nrg_join(c)) rc = NRG_E_HIP;  // a deferred round tail would write responses later
-    if (!rc && (m->kind != NRG_DS_HASHMAP || c->err_out)) {  // no launch took the error copy
+    if (!rc && (!small || c->err_out)) {
+        // no small round took the error copy as its last write
         c->err_out = nullptr;
         comb_err_kernel<<<1, 64, 0, st>>>(c->d_ctl, x.err);
         if (hipGetLastError() != hipSuccess) rc = NRG_E_HIP;
@@ -242,6 +267,7 @@ bool advance(nrg_combiner* m) {
     x.rc = launch(m, x, W, R);
     hipStream_t st = (hipStream_t)nrg_get_stream(m->ctx);
     if (hipEventRecord(x.done, st) != hipSuccess && x.rc == NRG_OK) x.rc = NRG_E_HIP;
+    if (x.rc != NRG_OK) *(volatile uint32_t*)x.err = 0;  // nothing will write it: retire at once
     m->launched.store(k + 1, std::memory_order_release);
     m->rounds.fetch_add(1, std::memory_order_relaxed);
     m->ops.fetch_add(W + R, std::memory_order_relaxed);

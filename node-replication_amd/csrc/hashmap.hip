@@ -1743,9 +1743,13 @@ __global__ __launch_bounds__(SM_TPB) void hm_small_round_kernel(SmallJob j, Slot
         j.vals[i] = v;
         j.found[i] = f ? 1 : 0;
     }
-    if (j.e_out) {
+    if (j.e_out) {  // the round's last write: the host (nrg_combiner) polls it as the round's completion
         __syncthreads();
-        if (tid == 0) *j.e_out = atomicExch(&ctl->err, 0u);
+        if (tid == 0) {
+            const u32 e = atomicExch(&ctl->err, 0u);
+            __threadfence_system();
+            *(volatile u32*)j.e_out = e;
+        }
     }
 }
 
@@ -2177,7 +2181,7 @@ hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool
     if (n > HM_MAX_BATCH) return hipErrorInvalidValue;
     const nrg_put* src = (const nrg_put*)src_recs;
     const bool want_prev = d_prev && resp_lo < lo + n && resp_hi > lo;
-    if (n <= c->small_max && n <= SM_W && R <= SM_R) {  // one launch, nothing deferred
+    if (c->small_max && n <= c->small_max && n <= SM_W && R <= SM_R) {  // one launch, nothing deferred
         hipError_t e = small_round(c, src, lo, n, write_ring, d_get_keys, R, d_get_vals, d_get_found, resp_lo, resp_hi,
                                    want_prev ? d_prev : nullptr, d_prev_found);
         c->rounds++;
@@ -2190,8 +2194,15 @@ hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool
     if ((e = next_epoch(c, &epoch)) != hipSuccess) return e;
     Launch L;
     bool measured = false;  // the round's index role counts the Puts its per-tile dedup drops (key skew)
+    // Round kinds (NRG_KNOB_PART 1, the default): stamp rounds (one launch, one stamp atomic per
+    // distinct key per block) for unskewed rounds without previous values of fewer than
+    // PART_MIN Puts; partition rounds (two launches, no device atomic per Put) for the rest.
+    // Measured per round (profiles/r04_part_sweep.txt): B1 100k Puts + 900k Gets 34.8 stamp vs
+    // 38.1 partition us, 200k + 900k 41.9 / 44.2, 400k + 900k 59.7 / 57.7, 800k + 900k 99.0 / 84.8,
+    // 4M + 500k 413 / 271; previous values and skewed streams: partition rounds everywhere.
+    constexpr u64 PART_MIN = 3ull << 17;
     const bool stamp0 = !want_prev && c->stamp_max && n <= c->stamp_max && !c->skewed;
-    const bool part = c->part_mode >= 2 || (c->part_mode == 1 && !stamp0);
+    const bool part = c->part_mode >= 2 || (c->part_mode == 1 && (!stamp0 || n >= PART_MIN));
     const bool stamp = stamp0 && !part;
     if (part) {
         // ---- partition round: {partition(e) | apply(e-1) | reads(e-1)}, then hm_papply_kernel(e) ----

@@ -138,9 +138,10 @@ struct nrg_ctx {
     uint32_t* d_bk_cnt = nullptr;   // [bucket][index tiles] offset << 16 | count
     // Stamp rounds (<= stamp_max Puts, no previous values): per-Put slot ids by epoch parity.
     uint64_t stamp_max = 0;
-    // Partition rounds (hashmap.hip part_role + hm_papply_kernel), NRG_KNOB_PART: 0 off, 1 in place
-    // of the bucket rounds, 2 in place of the stamp and the bucket rounds.
-    uint32_t part_mode = 0;
+    // Partition rounds (hashmap.hip part_role + hm_papply_kernel), NRG_KNOB_PART: 1 (default) for
+    // previous values, skewed streams and rounds of >= 393216 Puts; 2 for every round; 0 never
+    // (the older bucket elector instead).
+    uint32_t part_mode = 1;
     uint64_t stamp_alloc = 0;  // Puts the put_slot arrays hold (stamp_max <= stamp_alloc)
     uint32_t epoch = 1;  // epoch of the last replay round (1: prefill / before any round)
     uint32_t epoch_limit = 0xFFFFFFF0u;  // renormalise stamps here (NRG_KNOB_EPOCH_LIMIT for tests)

@@ -2,7 +2,8 @@
 """Run bench.py under several settings (one subprocess each) and print a compact table.
 
 Usage: tools/sweep.py 'NAME|ENV=V ENV2=V2|--bench --args' ...
-(replica tuning knobs are bench.py arguments: --knob K1=2 --knob BK_ENT=256)
+(replica tuning knobs are bench.py arguments: --knob K1=2 --knob BK_ENT=256; --with-prev also runs
+the previous-value variant and prints its rate)
 """
 import json
 import os
@@ -20,7 +21,12 @@ def main():
         for kv in envs.split():
             k, v = kv.split("=", 1)
             env[k] = v
-        cmd = [sys.executable, os.path.join(ROOT, "bench.py")] + base + args.split()
+        a = args.split()
+        b = list(base)
+        if "--with-prev" in a:
+            a.remove("--with-prev")
+            b.remove("--no-prev-variant")
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py")] + b + a
         try:
             p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
         except subprocess.TimeoutExpired:
@@ -32,7 +38,8 @@ def main():
         d = json.loads(p.stdout.strip().splitlines()[-1])
         r = d["roofline"]
         print(f"{name:28s} {d['value']:10.1f} Mops/s  {d['ms_per_step'] * 1e3:8.2f} us/round  "
-              f"kernel {r['avg_launch_us']} us x{r['launches']}  frac {r['frac']}  host {d['round'].get('host_enqueue_us')} us", flush=True)
+              f"kernel {r['avg_launch_us']} us x{r['launches']}  frac {r['frac']}  host {d['round'].get('host_enqueue_us')} us"
+              + (f"  prev {d['variants']['prev_value_responses_Mops']} Mops/s" if "variants" in d else ""), flush=True)
     return 0
 
 
