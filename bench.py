@@ -453,10 +453,8 @@ def run_hashmap(args, env):
     # round of work each).
     host_s = [0.0]
     elapsed = run(args.steps, host_s=host_s)  # no events in the timed region
-    kt = roofline_region(args, rep, run, ["hm_round", "hm_elect", "hm_papply"])
-    (k_n, k_ms), (e_n, e_ms), (a_n, a_ms) = kt["hm_round"], kt["hm_elect"], kt["hm_papply"]
-    if e_n and k_n:  # bucket-elected rounds: the round's kernels are hm_round + hm_elect
-        k_ms = k_ms + e_ms * k_n / e_n
+    kt = roofline_region(args, rep, run, ["hm_round", "hm_papply"])
+    (k_n, k_ms), (a_n, a_ms) = kt["hm_round"], kt["hm_papply"]
     if a_n and k_n:  # partition rounds: hm_round (partition + reads) + hm_papply (the table pass)
         k_ms = k_ms + a_ms * k_n / a_n
     rep.sync()
@@ -499,7 +497,7 @@ def run_hashmap(args, env):
         "put_responses": "Ok(None) as benches/hashmap.rs:114-119",
         "parallelism": "replicas%d" % world,
     })
-    res["roofline"] = roofline("hm_round+hm_elect" if e_n else "hm_round+hm_papply" if a_n else "hm_round",
+    res["roofline"] = roofline("hm_round+hm_papply" if a_n else "hm_round",
                                round_bytes, k_n, k_ms, args,
                                measured_traffic(args))
     res["round"] = {

@@ -21,23 +21,22 @@ int nrg_test_maxscan(nrg_ctx* ctx, const uint32_t* d_keys, const uint32_t* d_val
  * (rec bytes per ds kind); syncs first. Lets tests check Log::index (nr/src/log.rs:528-530)
  * against what the replica's HBM ring actually holds. */
 int nrg_test_ring_read(nrg_ctx* ctx, uint64_t phys, void* out);
-/* diagnostic phase timestamps of the last replay (a context with NRG_KNOB_EXP bit 2 (stack,
- * synthetic) or 0x10000 (hashmap elector) set); NRG_E_INVAL when `words` exceeds the buffer */
+/* diagnostic phase timestamps of the last replay (a stack or synthetic context with NRG_KNOB_EXP
+ * bit 2 set); NRG_E_INVAL when `words` exceeds the buffer */
 int nrg_test_debug_read(nrg_ctx* ctx, uint64_t* out, uint64_t words);
 
 /* Tuning and diagnostic knobs of an OPEN context. The product never reads the environment:
  * these setters are the only way to change them, so a stray variable in a caller's environment
  * cannot alter a replica. Each call first completes the context's queued work. */
 #define NRG_KNOB_STAMP_MAX 1   /* hashmap: largest round replayed by one-launch stamp rounds
-                                  (0: every round takes the bucket elector; clamped to max_batch) */
+                                  (0: every round is a partition round; clamped to max_batch)     */
 #define NRG_KNOB_SKEW_EVERY 2  /* hashmap: rounds between key-skew samples (>= 1, default 16)      */
 #define NRG_KNOB_EPOCH_LIMIT 3 /* hashmap: renormalise stamps when the round epoch reaches this    */
-#define NRG_KNOB_K1 4          /* hashmap: Puts per index thread (0: by round size; 1, 2 or 4)     */
-#define NRG_KNOB_BK_ENT 5      /* hashmap: target entries per elector bucket (0: default)          */
-#define NRG_KNOB_EXP 6         /* diagnostic bits: phase timestamps (stack/synthetic 2, hashmap
-                                  0x10000) and ablations that make RESULTS WRONG (hashmap bits
-                                  0xFF, 0xFF00; round-launch roles 0xF00000: no stamp atomics,
-                                  no apply, no index, no reads) -- measurement only              */
+#define NRG_KNOB_K1 4          /* hashmap: Puts per stamp-round index thread (0: by round size;
+                                  1, 2 or 4)                                                      */
+#define NRG_KNOB_EXP 6         /* diagnostic bits: phase timestamps (stack/synthetic 2) and stamp-
+                                  round ablations that make RESULTS WRONG (0xF00000: no stamp
+                                  atomics, no apply, no index, no reads) -- measurement only     */
 #define NRG_KNOB_SY_SORT 7     /* synthetic: 1 = sort-based replay instead of the bucket path      */
 #define NRG_KNOB_PIPELINE 8    /* overrides nrg_config.pipeline                                    */
 #define NRG_KNOB_COMB_SPIN 10   /* combiner (read by nrg_combiner_open): client threads that may spin
@@ -51,7 +50,8 @@ int nrg_test_debug_read(nrg_ctx* ctx, uint64_t* out, uint64_t words);
                                    workgroup per bucket finds/claims and stores each key: no
                                    device atomic per Put) -- 1 (default) for previous values,
                                    skewed streams and rounds of >= 393216 Puts, 2 for every round,
-                                   0 never (the bucket elector instead)                          */
+                                   0 only where a stamp round cannot (previous values, skew,
+                                   rounds above STAMP_MAX)                                        */
 #define NRG_KNOB_STALL 14       /* tests: 1 = odd waves sleep ~30 us where a workgroup next reuses LDS
                                    another wave may still read (synthetic bucket pass, hashmap
                                    elector and partition-round apply chunks, stack queries/table);

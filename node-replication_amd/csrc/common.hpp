@@ -23,7 +23,7 @@ constexpr u32 ERR_GROUP = 8u;  // a replica group's ranks disagreed on a round's
 constexpr u64 HM_CREATED_SLOTS = 8192;
 // Counters of Puts combined inside their index block (key skew statistic, hm_dup_sample_kernel).
 constexpr u64 HM_DUP_SLOTS = 64;
-// Slot buckets of a replay round (hashmap.hip hm_elect_kernel): at most this many.
+// Slot buckets of a partition round (hashmap.hip part_role / hm_papply_kernel): at most this many.
 constexpr u32 HM_BK_MAX = 1024;
 // Largest hashmap replay chunk: keeps the elector's per-tile LDS tables (one u32 + one u16
 // per index tile of >= 1024 Puts) and 16-bit tile offsets within bounds.

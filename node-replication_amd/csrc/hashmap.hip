@@ -19,18 +19,18 @@
 //              epoch is e-1 the value is the elected record's (apply may be storing it).
 //   index(e) touches only st[e&1], claims of empty slots and values apply never reads; apply and
 //   reads look only at st[(e-1)&1]. The latency-bound index pass overlaps the reads.
-// Bucket rounds (skewed key streams -- see skew_sample -- and rounds that return
-//   HashMap::insert's previous values):
-//   hm_round_kernel {index(e) | apply(e-1) | reads(e-1)} where index(e) only READS the table and
-//   writes one entry {id, i+1, value; key} per surviving Put into its tile, grouped by slot
-//   bucket in log order; then hm_elect_kernel: one block per bucket gathers its entries from
-//   every tile in log order, keeps one LDS hash entry per key (the largest i+1 = last writer),
-//   claims slots for new keys and stores each key's final value -- no device atomics per Put.
-//   With previous values wanted every Put keeps its entry and one wave walks the bucket in log
-//   order: a Put's previous value is its predecessor's, or the slot's value before the round, or
-//   None for a key the round created. A key lives in exactly one bucket (found keys by slot, new
-//   keys by home slot: nothing claims slots while a bucket index pass runs, so all Puts of a key
-//   agree), and the round's reads run in the launch after the elector.
+// Partition rounds (previous-value responses, skewed key streams -- see skew_sample -- and rounds
+//   of >= PART_MIN Puts): TWO launches per round and no device atomic per Put.
+//   hm_round_kernel {partition(e) | reads(e-1)}: partition(e) only reads the records; each tile
+//   writes its Puts grouped by the bucket of their key's HOME slot, in log order inside a
+//   bucket, and a [bucket][tile] count word (the table is not touched, so the previous round's
+//   reads run beside it against a quiescent table, without stamps);
+//   hm_papply_kernel(e): one workgroup per bucket takes the bucket's entries (every tile's run,
+//   tile order = log order) in chunks, finds each key's last writer in an LDS hash, and that
+//   thread finds or claims the key's slot and stores its value: one table line read and written
+//   per distinct key. All Puts of a key share its home bucket, so one workgroup decides each key.
+//   With previous values every Put keeps its entry and one wave walks each chunk in log order:
+//   a Put's previous value is its predecessor's, else the key's value before the chunk, else None.
 #include "internal.hpp"
 
 namespace nrg {
@@ -38,10 +38,8 @@ namespace nrg {
 typedef u64 u64x2 __attribute__((ext_vector_type(2)));
 
 constexpr int TPB = 256;
-constexpr u32 SIDE_ID = 0x7FFFFFFFu;  // entry id of the key EMPTY_KEY (slot ids are < 2^30)
-constexpr u32 NEW_BIT = 0x80000000u;  // entry id flag: key absent when indexed (id = home slot)
-constexpr u32 ID_MASK = 0x7FFFFFFFu;
-constexpr u32 FULL_SLOT = 0xFFFFFFFFu;  // elector: no slot could be claimed (table full)
+constexpr u32 SIDE_ID = 0x7FFFFFFFu;    // slot id standing for the side slot (slot ids are < 2^30)
+constexpr u32 FULL_SLOT = 0xFFFFFFFFu;  // no slot could be claimed (table full)
 
 // record i of a round: from a caller's buffer when given, else from the log ring
 struct RecSrc {
@@ -59,7 +57,6 @@ struct IndexJob {
     u32 nb_log;    // slot buckets = 1 << nb_log
     u32 bk_shift;  // bucket of a slot id = id >> bk_shift
     u64x2* ent;    // [nblocks][tile] {id << 32 | i+1, value}
-    u64* ekey;     // [nblocks][tile] key
     u32* eidx;     // partition rounds: [nblocks][tile] round offset i of each entry (previous values)
     u32* cnt;      // [bucket][nblocks] start << 16 | count
     u32 exp;       // diagnostic knobs (NRG_EXP; results are wrong when set): 1 no dedup, 2 no
@@ -86,7 +83,6 @@ struct ReadJob {
     u32* e_out;
 };
 
-__device__ __forceinline__ u32 bucket_of_id(u32 id, u32 bk_shift) { return id == SIDE_ID ? 0u : (id & ID_MASK) >> bk_shift; }
 
 // Block-wide exclusive prefix sum of one u32 per thread (TPB threads); *total gets the sum.
 __device__ __forceinline__ u32 block_scan_excl(u32 v, u32* total) {
@@ -109,189 +105,6 @@ __device__ __forceinline__ u32 block_scan_excl(u32 v, u32* total) {
     __syncthreads();
     if (total) *total = tot;
     return pre + inc - v;
-}
-
-// ---- role: index(e) ---------------------------------------------------------------------------
-// Tile of a block = TPB * K1 consecutive Puts; wave w owns the 64 * K1 Puts [w*64*K1, (w+1)*64*K1)
-// of it, so the order (item q, lane) inside a wave is log order and waves follow each other.
-template <int K1>
-struct IndexLds {
-    static constexpr int TILE = TPB * K1;
-    static constexpr int HSZ = TILE * 3 / 2;  // dedup hash entries (load <= 2/3)
-    static constexpr int DEDUP_BYTES = HSZ * 12;
-    static unsigned bytes(bool dedup, u32 nb) {
-        const unsigned rank = nb * 4 + 4 * nb * 2;
-        return dedup && DEDUP_BYTES > (int)rank ? (unsigned)DEDUP_BYTES : rank;
-    }
-};
-
-template <int K1, bool DEDUP>
-__device__ __forceinline__ void index_role(const IndexJob& j, u32 blk, const Slot* __restrict__ table, u32 shift,
-                                           u64 tmask, char* lds) {
-    constexpr int WT = 64 * K1;
-    constexpr int TILE = IndexLds<K1>::TILE;
-    constexpr int HSZ = IndexLds<K1>::HSZ;
-    __shared__ u32 s_side;  // dedup of the side-slot key: largest tile position + 1
-    __shared__ u32 s_dup;   // Puts whose key another Put of the block already entered
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const u64 base = (u64)blk * TILE;
-    const u32 nb = 1u << j.nb_log;
-    u64* s_hk = (u64*)lds;               // [HSZ] dedup keys
-    u32* s_hp = (u32*)(lds + HSZ * 8);   // [HSZ] largest tile position + 1 per key
-    if (DEDUP) {
-        for (int q = threadIdx.x; q < HSZ; q += TPB) {
-            s_hk[q] = EMPTY_KEY;
-            s_hp[q] = 0;
-        }
-        if (threadIdx.x == 0) s_side = s_dup = 0;
-    }
-    nrg_put rec[K1];
-    u64 kk[K1];
-    u32 id[K1];
-    bool valid[K1];
-    // issue every record load, then every first probe, before waiting on any of them
-#pragma unroll
-    for (int q = 0; q < K1; q++) {
-        const u64 i = base + (u64)(w * WT + q * 64 + lane);
-        valid[q] = i < j.n;
-        rec[q] = valid[q] ? j.rec.at(i) : nrg_put{0, 0};
-    }
-#pragma unroll
-    for (int q = 0; q < K1; q++) {
-        const u64 i = base + (u64)(w * WT + q * 64 + lane);
-        if (valid[q] && j.ring_out) j.ring_out[(j.rec.lo + i) & j.rec.mask] = rec[q];
-        const bool probe = valid[q] && rec[q].key != EMPTY_KEY && !(j.exp & 2);
-        kk[q] = probe ? table[table_home(rec[q].key, shift)].key : EMPTY_KEY;
-    }
-#pragma unroll
-    for (int q = 0; q < K1; q++) {
-        id[q] = SIDE_ID;
-        if (!valid[q] || rec[q].key == EMPTY_KEY) continue;
-        const u64 k = rec[q].key;
-        const u64 home = table_home(k, shift);
-        u64 s = home;
-        u64 key = kk[q];
-        id[q] = (u32)home | NEW_BIT;  // also when the probe exhausts a full table (the claim fails)
-        for (u64 pr = 0; pr <= tmask && !(j.exp & 2); pr++) {
-            if (key == k) {
-                id[q] = (u32)s;
-                break;
-            }
-            if (key == EMPTY_KEY) break;
-            s = (s + 1) & tmask;
-            key = table[s].key;
-        }
-    }
-    // ---- drop Puts that a later Put of the same key in this block overwrites ----
-    bool emit[K1];
-    if (DEDUP && !(j.exp & 1)) {
-        __syncthreads();  // hash initialised
-        u32 hq[K1];
-        u32 dup = 0;
-#pragma unroll
-        for (int q = 0; q < K1; q++) {
-            if (!valid[q]) continue;
-            const u32 pos1 = (u32)(w * WT + q * 64 + lane) + 1;
-            if (rec[q].key == EMPTY_KEY) {
-                atomicMax(&s_side, pos1);
-                continue;
-            }
-            u32 h = (u32)(((mix64(rec[q].key) >> 32) * (u64)HSZ) >> 32);
-            for (;;) {
-                const u64 old = atomicCAS((unsigned long long*)&s_hk[h], (unsigned long long)EMPTY_KEY,
-                                          (unsigned long long)rec[q].key);
-                if (old == EMPTY_KEY || old == rec[q].key) {
-                    dup += old == rec[q].key ? 1u : 0u;
-                    break;
-                }
-                h = h + 1 == (u32)HSZ ? 0u : h + 1;
-            }
-            atomicMax(&s_hp[h], pos1);
-            hq[q] = h;
-        }
-        if (dup) atomicAdd(&s_dup, dup);
-        __syncthreads();
-        if (threadIdx.x == 0 && s_dup && j.dup_acc) atomicAdd(&j.dup_acc[blk % HM_DUP_SLOTS], (u64)s_dup);
-#pragma unroll
-        for (int q = 0; q < K1; q++) {
-            const u32 pos1 = (u32)(w * WT + q * 64 + lane) + 1;
-            emit[q] = valid[q] && (rec[q].key == EMPTY_KEY ? s_side == pos1 : s_hp[hq[q]] == pos1);
-        }
-        __syncthreads();  // the hash region is reused below
-    } else {
-#pragma unroll
-        for (int q = 0; q < K1; q++) emit[q] = valid[q];
-    }
-    if (j.exp & 4) {
-        if (emit[0]) j.ekey[base + threadIdx.x] = id[0];
-        return;
-    }
-    // ---- stable grouping by bucket: wave-private counts, then a prefix over waves ----
-    u32* s_start = (u32*)lds;                       // [nb] bucket start in the tile
-    uint16_t* s_wc = (uint16_t*)(lds + nb * 4);     // [4][nb] per-wave counts -> wave offsets
-    for (u32 b = threadIdx.x; b < 4 * nb; b += TPB) s_wc[b] = 0;
-    __syncthreads();
-    u32 bkt[K1], rnk[K1];
-#pragma unroll
-    for (int q = 0; q < K1; q++) {
-        const u32 b = emit[q] ? bucket_of_id(id[q], j.bk_shift) : 0u;
-        u64 peers = __ballot(emit[q]);
-        for (u32 bit = 0; bit < j.nb_log; bit++) {
-            const bool one = (b >> bit) & 1u;
-            const u64 bal = __ballot(one);
-            peers &= one ? bal : ~bal;
-        }
-        bkt[q] = b;
-        if (emit[q]) {
-            const u64 below = peers & ((1ull << lane) - 1);
-            const u32 cur = s_wc[w * nb + b];
-            rnk[q] = cur + (u32)__popcll(below);
-            if (below == 0) s_wc[w * nb + b] = (uint16_t)(cur + (u32)__popcll(peers));
-        }
-    }
-    __syncthreads();
-    constexpr int PER = HM_BK_MAX / TPB;  // buckets per thread (contiguous ownership)
-    u32 tot[PER], loc = 0;
-#pragma unroll
-    for (int r = 0; r < PER; r++) {
-        const u32 b = threadIdx.x * PER + r;
-        tot[r] = 0;
-        if (b < nb) {
-            u32 run = 0;
-#pragma unroll
-            for (int v = 0; v < 4; v++) {
-                const u32 c = s_wc[v * nb + b];
-                s_wc[v * nb + b] = (uint16_t)run;
-                run += c;
-            }
-            tot[r] = run;
-            loc += run;
-        }
-    }
-    u32 off = block_scan_excl(loc, nullptr);
-#pragma unroll
-    for (int r = 0; r < PER; r++) {
-        const u32 b = threadIdx.x * PER + r;
-        if (b < nb) {
-            j.cnt[(u64)b * j.nblocks + blk] = (off << 16) | tot[r];
-            s_start[b] = off;
-        }
-        off += tot[r];
-    }
-    __syncthreads();
-    u64x2* ent = j.ent + (u64)blk * TILE;
-    u64* ekey = j.ekey + (u64)blk * TILE;
-#pragma unroll
-    for (int q = 0; q < K1; q++) {
-        if (!emit[q]) continue;
-        const u64 i = base + (u64)(w * WT + q * 64 + lane);
-        const u32 p = s_start[bkt[q]] + s_wc[w * nb + bkt[q]] + rnk[q];
-        u64x2 e;
-        e.x = ((u64)id[q] << 32) | (u64)(i + 1);
-        e.y = rec[q].val;
-        ent[p] = e;
-        ekey[p] = rec[q].key;
-    }
 }
 
 // ---- role: partition(e) (partition rounds) -------------------------------------------------------
@@ -736,8 +549,6 @@ __device__ __forceinline__ void read_role(const ReadJob& j, u32 blk, const Slot*
 }
 
 // index-role kinds of a round launch
-constexpr int IX_BUCKET = 0;      // bucket round, dedup (hm_elect_kernel<false> follows)
-constexpr int IX_BUCKET_ALL = 1;  // bucket round, every Put kept (previous values)
 constexpr int IX_STAMP = 2;       // stamp round
 constexpr int IX_PART = 3;        // partition round, dedup (hm_papply_kernel<false> follows)
 constexpr int IX_PART_ALL = 4;    // partition round, every Put kept (previous values)
@@ -778,9 +589,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_num_sgpr(80))) void hm_r
     if (b < nix) {
         if (sj.exp & 4) return;
         if constexpr (IX == IX_STAMP) stamp_index_role<K1>(sj, b, table, shift, tmask, ctl, s_lds);
-        else if constexpr (IX == IX_PART || IX == IX_PART_ALL || IX == IX_PART_NODUP)
-            part_role<K1, IX == IX_PART>(ij, b, shift, s_lds);
-        else index_role<K1, IX == IX_BUCKET>(ij, b, table, shift, tmask, s_lds);
+        else part_role<K1, IX == IX_PART>(ij, b, shift, s_lds);
         return;
     }
     b -= nix;
@@ -790,391 +599,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_num_sgpr(80))) void hm_r
     }
     b -= aj.nblocks;
     if (!(sj.exp & 8)) read_role(rj, b, table, shift, tmask, ctl);
-}
-
-// ---- hm_elect_kernel: last writer per key, claims of new keys, value stores -----------------------
-struct ElectJob {
-    const u64x2* ent;
-    const u64* ekey;
-    const u32* cnt;
-    u32 nblocks;
-    u32 tile;      // entries per index tile
-    u32 bk_shift;
-    Slot* table;
-    u32 shift;
-    u64 tmask;
-    DevCtl* ctl;
-    u64* created_acc;
-    u64 lo;        // log index of the round's record 0
-    u64 resp_lo, resp_hi;
-    u64* prev;     // previous-value responses for log indices [resp_lo, resp_hi)
-    uint8_t* prevf;
-    u32 exp;  // diagnostic knobs (NRG_EXP >> 8; wrong results): 1 counts only, 2 + pass 1 only, 4 no claims
-    u64* dbg; // NRG_EXP & 0x10000 (diagnostic): per block, thread 0's wall clock at the phase edges
-    u32 stall;  // NRG_KNOB_STALL (tests)
-};
-
-constexpr int EL_HT = 2048;  // LDS hash entries (distinct keys of one part of a bucket)
-constexpr int EL_CH = 2048;  // entries gathered per chunk
-constexpr int EL_PER = EL_CH / TPB;
-constexpr int EL_WIN = 4;    // steps of 64 entries loaded ahead by the log-order walk
-
-__device__ __forceinline__ u32 el_hash(u64 k, u32 ht) { return (u32)(mix64(k) >> 40) & (ht - 1); }
-
-template <bool PREV>
-__global__ __launch_bounds__(TPB) void hm_elect_kernel(ElectJob j) {
-    // Previous-value buckets are small (about 256 entries): a 1024-entry hash leaves LDS for the
-    // bucket's entries, staged in pass 1 for the log-order walk (no second gather).
-    constexpr int HT = PREV ? 1024 : EL_HT;
-    constexpr int ST = PREV ? 1024 : 1;  // staged entries
-    constexpr uint16_t NOH = 0xFFFFu;    // staged entry outside the current part
-    extern __shared__ u32 s_dyn[];  // s_pre[nblocks + 1] entry prefix, s_off[nblocks] (u16)
-    __shared__ u64 s_hk[HT];
-    __shared__ u32 s_hp[HT + 1];  // largest bucket position + 1 of the key; [HT]: side key
-    __shared__ u32 s_hs[HT + 1];  // the key's slot (SIDE_ID, FULL_SLOT)
-    __shared__ u32 s_hf[HT + 1];  // bit 0: new key (claim), bit 1: s_lv holds a value
-    __shared__ u64 s_lv[PREV ? HT + 1 : 1];  // PREV: the key's value so far in the walk
-    __shared__ u64 s_mk[PREV ? HT + 1 : 1];  // PREV: lanes of the current walk step per key
-    __shared__ uint16_t s_tile[EL_CH];
-    __shared__ u64x2 s_sx[ST];      // PREV: the bucket's entries in log order (total <= ST)
-    __shared__ uint16_t s_sh[ST];   // their hash entries (NOH: not in this part)
-    __shared__ u32 s_created;
-    const u32 nblocks = j.nblocks;
-    u32* s_pre = s_dyn;
-    uint16_t* s_off = (uint16_t*)(s_dyn + nblocks + 1);
-    const u32 b = blockIdx.x;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#define EL_MARK(K) \
-    if (j.dbg && threadIdx.x == 0) j.dbg[(u64)blockIdx.x * 16 + (K)] = wall_clock64()
-    EL_MARK(0);
-    // this bucket's (offset, count) in every index tile; thread owns tiles [tid*K, tid*K + K)
-    const u32 K = (nblocks + TPB - 1) / TPB;
-    u32 loc = 0;
-    for (u32 q = 0; q < K; q++) {
-        const u32 t = threadIdx.x * K + q;
-        if (t < nblocks) {
-            const u32 v = j.cnt[(u64)b * nblocks + t];
-            s_off[t] = (uint16_t)(v >> 16);
-            s_pre[t] = v & 0xFFFFu;
-            loc += v & 0xFFFFu;
-        }
-    }
-    u32 total;
-    u32 run = block_scan_excl(loc, &total);
-    for (u32 q = 0; q < K; q++) {
-        const u32 t = threadIdx.x * K + q;
-        if (t < nblocks) {
-            const u32 c = s_pre[t];
-            s_pre[t] = run;
-            run += c;
-        }
-    }
-    if (threadIdx.x == 0) {
-        s_pre[nblocks] = total;
-        s_created = 0;
-    }
-    EL_MARK(1);
-    if (total == 0 || (j.exp & 1)) return;  // uniform across the block
-    // parts = 2^lp id sub-ranges of the bucket, about <= HT/2 entries each
-    u32 lp = 0;
-    while ((total >> lp) > HT / 2 && lp < j.bk_shift) lp++;
-    __syncthreads();
-    // entry tile map of the chunk [base, base + EL_CH)
-    auto fill_tiles = [&](u32 base) {
-        for (u32 q = 0; q < K; q++) {
-            const u32 t = threadIdx.x * K + q;
-            if (t >= nblocks) break;
-            const u32 lo_ = s_pre[t] > base ? s_pre[t] : base;
-            const u32 hi_ = s_pre[t + 1] < base + EL_CH ? s_pre[t + 1] : base + EL_CH;
-            for (u32 i = lo_; i < hi_; i++) s_tile[i - base] = (uint16_t)t;
-        }
-    };
-    auto ent_at = [&](u32 pos, u32 base) -> u64 {  // index of bucket position pos in the entry arrays
-        const u32 t = s_tile[pos - base];
-        return (u64)t * j.tile + s_off[t] + (pos - s_pre[t]);
-    };
-    u64x2 x[EL_PER];
-    u64 xk[EL_PER];
-    auto load_chunk = [&](u32 base) {
-        fill_tiles(base);
-        __syncthreads();
-        test_stall(j.stall & 1, w);  // (tests) slow waves read s_tile below
-#pragma unroll
-        for (int r = 0; r < EL_PER; r++) {
-            const u32 i = base + r * TPB + threadIdx.x;
-            x[r].x = 0;  // i+1 = 0: no entry
-            if (i < total) {
-                const u64 e = ent_at(i, base);
-                x[r] = j.ent[e];
-                xk[r] = j.ekey[e];
-            }
-        }
-        __syncthreads();  // s_tile is reused by the next chunk
-    };
-    auto in_part = [&](u32 id, u32 p) {
-        if (!lp) return true;
-        if (id == SIDE_ID) return p == 0;
-        return (((id & ID_MASK) >> (j.bk_shift - lp)) & ((1u << lp) - 1)) == p;
-    };
-    auto lookup = [&](u64 k) -> u32 {  // hash entry of a key inserted by pass 1
-        if (k == EMPTY_KEY) return (u32)HT;
-        u32 h = el_hash(k, HT);
-        while (s_hk[h] != k) h = (h + 1) & (HT - 1);
-        return h;
-    };
-    const bool one_chunk = total <= (u32)EL_CH;
-    const bool staged = PREV && total <= (u32)ST;
-    u32 created = 0;
-    for (u32 p = 0; p < (1u << lp);) {
-        for (int q = threadIdx.x; q <= HT; q += TPB) {
-            if (q < HT) s_hk[q] = EMPTY_KEY;
-            s_hp[q] = 0;
-            s_hf[q] = 0;
-            if (PREV) s_mk[q] = 0;
-        }
-        __syncthreads();
-        // pass 1: one hash entry per key, its last writer, its slot or that it is new. With
-        // previous values, an existing key's value before the round is loaded here too (its
-        // slot is the entry's id), in flight while the hash is built.
-        bool ovf = false;
-        for (u32 base = 0; base < total; base += EL_CH) {
-            if (!one_chunk || p == 0) load_chunk(base);
-            u64 ov[PREV ? EL_PER : 1];
-            if (PREV) {
-#pragma unroll
-                for (int r = 0; r < EL_PER; r++) {
-                    const u32 id = (u32)(x[r].x >> 32);
-                    ov[r] = ((u32)x[r].x != 0 && !(id & NEW_BIT) && id != SIDE_ID && in_part(id, p))
-                                ? j.table[id].val : 0ull;
-                }
-            }
-#pragma unroll
-            for (int r = 0; r < EL_PER; r++) {
-                const u32 pos = base + r * TPB + threadIdx.x;
-                if (staged && pos < total) {
-                    s_sx[pos] = x[r];
-                    s_sh[pos] = NOH;
-                }
-                if ((u32)x[r].x == 0) continue;
-                const u32 id = (u32)(x[r].x >> 32);
-                if (!in_part(id, p)) continue;
-                const u64 k = xk[r];
-                u32 h;
-                if (k == EMPTY_KEY) {
-                    h = (u32)HT;
-                } else {
-                    h = el_hash(k, HT);
-                    int pr = 0;
-                    for (; pr < HT; pr++) {
-                        const u64 old = atomicCAS((unsigned long long*)&s_hk[h], (unsigned long long)EMPTY_KEY,
-                                                  (unsigned long long)k);
-                        if (old == EMPTY_KEY || old == k) break;
-                        h = (h + 1) & (HT - 1);
-                    }
-                    if (pr == HT) {
-                        ovf = true;
-                        continue;
-                    }
-                }
-                atomicMax(&s_hp[h], base + r * TPB + threadIdx.x + 1);
-                if (staged) s_sh[pos] = (uint16_t)h;
-                if (id & NEW_BIT) {
-                    atomicOr(&s_hf[h], 1u);
-                } else {
-                    s_hs[h] = id;  // the same slot for every entry of the key
-                    if (PREV && id != SIDE_ID) {  // the same value too (nothing writes it yet)
-                        s_lv[h] = ov[r];
-                        atomicOr(&s_hf[h], 2u);
-                    }
-                }
-            }
-        }
-        if (j.exp & 2) return;
-        EL_MARK(2);
-        if (__syncthreads_or(ovf)) {  // more distinct keys than the table holds: finer parts
-            if (lp == j.bk_shift) {  // > HT distinct new keys sharing one home slot
-                if (threadIdx.x == 0) atomicOr(&j.ctl->err, ERR_TABLE_FULL);
-                break;
-            }
-            lp++;
-            p = 0;
-            continue;
-        }
-        // slots of new keys (claims). A thread owns hash entries tid + q*TPB: all their home-slot
-        // loads are issued first, then all CASes on empty home slots, then the results are
-        // resolved (one or two memory round trips instead of one or two per entry).
-        constexpr int HQ = (HT + TPB) / TPB;  // entries per thread, the side entry included
-        u64 kh[HQ], cas[HQ];
-#pragma unroll
-        for (int q = 0; q < HQ; q++) {
-            const int h = threadIdx.x + q * TPB;
-            kh[q] = 0;
-            if (h >= HT || !s_hp[h]) continue;
-            if (s_hf[h] & 1u) {
-                if (!(j.exp & 4)) kh[q] = ld_relaxed(&j.table[table_home(s_hk[h], j.shift)].key);
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < HQ; q++) {
-            const int h = threadIdx.x + q * TPB;
-            cas[q] = 0;
-            if (h < HT && s_hp[h] && (s_hf[h] & 1u) && !(j.exp & 4) && kh[q] == EMPTY_KEY)
-                cas[q] = atomicCAS((unsigned long long*)&j.table[table_home(s_hk[h], j.shift)].key,
-                                   (unsigned long long)EMPTY_KEY, (unsigned long long)s_hk[h]);
-        }
-#pragma unroll
-        for (int q = 0; q < HQ; q++) {
-            const int h = threadIdx.x + q * TPB;
-            if (h > HT || !s_hp[h]) continue;
-            if (h == HT) {
-                s_hs[h] = SIDE_ID;
-                const bool present = j.ctl->sp_claim != 0;
-                if (!present) {  // created by this round (no reads run beside the elector)
-                    created++;
-                    j.ctl->sp_claim = 1;
-                    j.ctl->sp.st[0] = j.ctl->sp.st[1] = STAMP_PRESENT;
-                }
-                if (PREV && present) {
-                    s_lv[h] = j.ctl->sp.val;
-                    s_hf[h] |= 2u;
-                }
-            } else if ((s_hf[h] & 1u) && (j.exp & 4)) {
-                s_hs[h] = FULL_SLOT;
-            } else if (s_hf[h] & 1u) {
-                const u64 k = s_hk[h];
-                const u64 home = table_home(k, j.shift);
-                bool fresh = false;
-                long long sl;
-                if (kh[q] == EMPTY_KEY && cas[q] == EMPTY_KEY) {
-                    sl = (long long)home;
-                    fresh = true;
-                } else if (kh[q] == k || (kh[q] == EMPTY_KEY && cas[q] == k)) {
-                    sl = (long long)home;
-                } else {  // home slot holds another key: walk the probe chain from the next slot
-                    sl = claim_slot(j.table, k, (home + 1) & j.tmask, j.tmask, &fresh);
-                }
-                if (sl < 0) {
-                    atomicOr(&j.ctl->err, ERR_TABLE_FULL);
-                    s_hs[h] = FULL_SLOT;
-                } else {
-                    s_hs[h] = (u32)sl;
-                    created += fresh;
-                    if (fresh) j.table[sl].st[0] = j.table[sl].st[1] = STAMP_PRESENT;
-                    if (PREV && !fresh) {  // inserted earlier by a round not visible to index
-                        s_lv[h] = j.table[sl].val;
-                        s_hf[h] |= 2u;
-                    }
-                }
-            }  // existing keys: slot and (previous values) value set in pass 1
-        }
-        __syncthreads();
-        EL_MARK(3);
-        if (!PREV) {
-            // pass 2: each key's last writer stores its value
-            for (u32 base = 0; base < total; base += EL_CH) {
-                if (!one_chunk) load_chunk(base);
-#pragma unroll
-                for (int r = 0; r < EL_PER; r++) {
-                    if ((u32)x[r].x == 0) continue;
-                    const u32 id = (u32)(x[r].x >> 32);
-                    if (!in_part(id, p)) continue;
-                    const u32 h = lookup(xk[r]);
-                    if (s_hp[h] != base + r * TPB + threadIdx.x + 1) continue;
-                    const u32 sl = s_hs[h];
-                    if (sl == SIDE_ID) {
-                        j.ctl->sp.val = x[r].y;
-                    } else if (sl != FULL_SLOT) {
-                        j.table[sl].val = x[r].y;
-                    }
-                }
-            }
-        } else {
-            // pass 2 (previous values): wave 0 walks the bucket in log order, 64 entries a step
-            // (from the staged entries when the bucket fits, else gathered again)
-            for (u32 base = 0; base < total; base += EL_CH) {
-                if (!staged) {
-                    fill_tiles(base);
-                    __syncthreads();
-                }
-                const u32 end = total < base + EL_CH ? total : base + EL_CH;
-                if (w == 0) {
-                    for (u32 s0 = base; s0 < end; s0 += 64 * EL_WIN) {
-                        u64x2 ex[EL_WIN];
-                        u64 ek[EL_WIN];
-                        uint16_t eh[EL_WIN];
-#pragma unroll
-                        for (int s = 0; s < EL_WIN; s++) {
-                            const u32 pos = s0 + s * 64 + lane;
-                            ex[s].x = 0;
-                            eh[s] = NOH;
-                            if (pos < end) {
-                                if (staged) {
-                                    ex[s] = s_sx[pos];
-                                    eh[s] = s_sh[pos];
-                                } else {
-                                    const u64 e = ent_at(pos, base);
-                                    ex[s] = j.ent[e];
-                                    ek[s] = j.ekey[e];
-                                }
-                            }
-                        }
-#pragma unroll
-                        for (int s = 0; s < EL_WIN; s++) {
-                            const bool v = staged ? eh[s] != NOH
-                                                  : (u32)ex[s].x != 0 && in_part((u32)(ex[s].x >> 32), p);
-                            const u32 h = !v ? 0u : staged ? (u32)eh[s] : lookup(ek[s]);
-                            if (v) atomicOr((unsigned long long*)&s_mk[h], 1ull << lane);
-                            const u64 m = v ? s_mk[h] : 0ull;
-                            const u64 lower = m & ((1ull << lane) - 1);
-                            const int pl = lower ? 63 - __clzll((long long)lower) : lane;
-                            const u64 pv_lane = __shfl(ex[s].y, pl, 64);
-                            if (v) {
-                                u64 pv;
-                                uint8_t pf;
-                                if (lower) {
-                                    pv = pv_lane;
-                                    pf = 1;
-                                } else {
-                                    pf = (s_hf[h] >> 1) & 1u;
-                                    pv = pf ? s_lv[h] : 0;
-                                }
-                                const u64 g = j.lo + (u32)ex[s].x - 1;
-                                if (g >= j.resp_lo && g < j.resp_hi) {
-                                    j.prev[g - j.resp_lo] = pv;
-                                    j.prevf[g - j.resp_lo] = pf;
-                                }
-                                if ((m >> lane) == 1ull) {  // the key's last entry in this step
-                                    s_lv[h] = ex[s].y;
-                                    s_hf[h] |= 2u;
-                                    s_mk[h] = 0;
-                                }
-                            }
-                        }
-                    }
-                }
-                __syncthreads();
-            }
-            EL_MARK(4);
-            // every key's last value
-            for (int h = threadIdx.x; h <= HT; h += TPB) {
-                if (!s_hp[h]) continue;
-                const u32 sl = s_hs[h];
-                if (sl == SIDE_ID) {
-                    j.ctl->sp.val = s_lv[h];
-                } else if (sl != FULL_SLOT) {
-                    j.table[sl].val = s_lv[h];
-                }
-            }
-        }
-        __syncthreads();
-        p++;
-    }
-    if (created) atomicAdd(&s_created, created);
-    __syncthreads();
-    if (threadIdx.x == 0 && s_created) atomicAdd(&j.created_acc[b % HM_CREATED_SLOTS], (u64)s_created);
-    EL_MARK(5);
-    if (j.dbg && threadIdx.x == 0) j.dbg[(u64)blockIdx.x * 16 + 6] = total;
-#undef EL_MARK
 }
 
 // ---- hm_papply_kernel: partition rounds' table pass, one workgroup per bucket ---------------------
@@ -1949,15 +1373,6 @@ static RecSrc ring_src(nrg_ctx* c, const nrg_put* src, u64 lo) {
     return r;
 }
 
-// Bucket rounds, Puts per index thread: 2 up to 2^18 Puts per round, 4 above (fewer, larger tiles keep the
-// elector's count rows short and the per-block dedup effective on hot keys). NRG_K1 overrides.
-static u32 k1_for(const nrg_ctx* c, u64 n) {
-    u32 k = n > (1u << 18) ? 4u : 2u;
-    if (c->k1_items) k = c->k1_items >= 4 ? 4u : c->k1_items >= 2 ? 2u : 1u;
-    while (k < 4 && (n + TPB * k - 1) / (TPB * k) > HM_MAX_BATCH / (TPB * 4)) k *= 2;  // elector LDS bound
-    return k;
-}
-
 // Stamp rounds: Puts per index thread by round size (one Get per read thread). K1 1 / 2 / 4 in us
 // per round (profiles/r03_stamp_k1.txt): 50k Puts + 950k Gets 31.4 / 32.0, B1 (100k + 900k)
 // 33.7 / 34.2 / 38.7, 200k + 800k 39.0 / 39.5, 200k + 900k 41.5 / 41.9, 400k + 900k 63.2 / 59.0,
@@ -1976,7 +1391,7 @@ struct Launch {
     StampJob sj{};
     ApplyJob aj{};
     ReadJob rj{};
-    int ix = IX_BUCKET;
+    int ix = IX_PART_NODUP;
     u32 K1 = 1;
     u32 nb = 0;
 };
@@ -2042,23 +1457,15 @@ static hipError_t launch(nrg_ctx* c, Launch& L) {
     if (nix && L.ix == IX_STAMP) {
         lds = L.K1 == 4 ? StampLds<4>::BYTES : L.K1 == 2 ? StampLds<2>::BYTES : StampLds<1>::BYTES;
     } else if (nix) {
-        if (L.ix == IX_PART || L.ix == IX_PART_ALL || L.ix == IX_PART_NODUP) {
-            const bool dedup = L.ix == IX_PART;
-            lds = L.K1 == 8   ? PartLds<8>::bytes(dedup, L.nb)
-                  : L.K1 == 4 ? PartLds<4>::bytes(dedup, L.nb)
-                  : L.K1 == 2 ? PartLds<2>::bytes(dedup, L.nb)
-                              : PartLds<1>::bytes(dedup, L.nb);
-        } else {
-            const bool dedup = L.ix == IX_BUCKET;
-            lds = L.K1 == 4 ? IndexLds<4>::bytes(dedup, L.nb) : L.K1 == 2 ? IndexLds<2>::bytes(dedup, L.nb)
-                                                                           : IndexLds<1>::bytes(dedup, L.nb);
-        }
+        const bool dedup = L.ix == IX_PART;
+        lds = L.K1 == 8   ? PartLds<8>::bytes(dedup, L.nb)
+              : L.K1 == 4 ? PartLds<4>::bytes(dedup, L.nb)
+              : L.K1 == 2 ? PartLds<2>::bytes(dedup, L.nb)
+                          : PartLds<1>::bytes(dedup, L.nb);
     }
-    if (!nix) launch_round<1, IX_BUCKET>(c, L, blocks, 0);
+    if (!nix) launch_round<1, IX_PART_NODUP>(c, L, blocks, 0);
 #define NRG_RK(KK, XX) else if (L.K1 == KK && L.ix == XX) launch_round<KK, XX>(c, L, blocks, lds)
-    NRG_RK(1, IX_BUCKET); NRG_RK(1, IX_BUCKET_ALL); NRG_RK(1, IX_STAMP);
-    NRG_RK(2, IX_BUCKET); NRG_RK(2, IX_BUCKET_ALL); NRG_RK(2, IX_STAMP);
-    NRG_RK(4, IX_BUCKET); NRG_RK(4, IX_BUCKET_ALL); NRG_RK(4, IX_STAMP);
+    NRG_RK(1, IX_STAMP); NRG_RK(2, IX_STAMP); NRG_RK(4, IX_STAMP);
     NRG_RK(1, IX_PART); NRG_RK(1, IX_PART_ALL); NRG_RK(1, IX_PART_NODUP);
     NRG_RK(2, IX_PART); NRG_RK(2, IX_PART_ALL); NRG_RK(2, IX_PART_NODUP);
     NRG_RK(4, IX_PART); NRG_RK(4, IX_PART_ALL); NRG_RK(4, IX_PART_NODUP);
@@ -2101,7 +1508,7 @@ hipError_t hm_alloc(nrg_ctx* c, u64 mb) {
     const u64 ents = tiles * TPB;
     hipError_t e;
     if ((e = hipMalloc(&c->d_bk_ent, ents * 16)) != hipSuccess) return e;
-    if ((e = hipMalloc(&c->d_bk_key, ents * 8)) != hipSuccess) return e;
+    if ((e = hipMalloc(&c->d_bk_idx, ents * 4)) != hipSuccess) return e;
     if ((e = hipMalloc(&c->d_bk_cnt, (u64)HM_BK_MAX * tiles * sizeof(u32))) != hipSuccess) return e;
     if (c->stamp_max > mb) c->stamp_max = mb;
     // per parity: put_slot, win and over (stamp_max each; epoch tags, zeroed here and whenever
@@ -2229,7 +1636,7 @@ hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool
         ij.nb_log = nb_log;
         ij.bk_shift = log2_slots - nb_log;
         ij.ent = (u64x2*)c->d_bk_ent;
-        ij.eidx = want_prev ? (u32*)c->d_bk_key : nullptr;
+        ij.eidx = want_prev ? c->d_bk_idx : nullptr;
         ij.cnt = c->d_bk_cnt;
         ij.exp = 0;
         ij.dup_acc = c->d_dup + (c->dup_seq & 1) * HM_DUP_SLOTS;
@@ -2276,58 +1683,6 @@ hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool
         L.sj.dup_acc = c->d_dup + (c->dup_seq & 1) * HM_DUP_SLOTS;
         attach_deferred(c, L);
         if ((e = launch(c, L)) != hipSuccess) return e;
-    } else {
-        // ---- bucket round: {index(e) | apply(e-1) | reads(e-1)}, then hm_elect_kernel(e) ----
-        const u32 K1 = k1_for(c, n);
-        const u32 tile = TPB * K1;
-        // slot buckets of about bk_ent entries (previous values keep every Put: smaller buckets)
-        const u64 target = c->bk_ent ? c->bk_ent : (want_prev ? 256 : 512);
-        const u32 log2_slots = 64 - c->slot_shift;
-        u32 nb_log = 6;
-        while ((1ull << nb_log) * target < n && (1u << nb_log) < HM_BK_MAX) nb_log++;
-        if (nb_log > log2_slots) nb_log = log2_slots;
-        L.ix = want_prev ? IX_BUCKET_ALL : IX_BUCKET;
-        measured = !want_prev;
-        L.K1 = K1;
-        L.nb = 1u << nb_log;
-        IndexJob& ij = L.ij;
-        ij.rec = ring_src(c, src, lo);
-        ij.ring_out = write_ring ? (nrg_put*)c->d_ring : nullptr;
-        ij.n = n;
-        ij.nblocks = (u32)((n + tile - 1) / tile);
-        ij.nb_log = nb_log;
-        ij.bk_shift = log2_slots - nb_log;
-        ij.ent = (u64x2*)c->d_bk_ent;
-        ij.ekey = c->d_bk_key;
-        ij.cnt = c->d_bk_cnt;
-        ij.exp = c->exp & 0xFF;
-        ij.dup_acc = c->d_dup + (c->dup_seq & 1) * HM_DUP_SLOTS;
-        attach_deferred(c, L);  // the previous round's apply and reads ride along (index only reads)
-        if ((e = launch(c, L)) != hipSuccess) return e;
-        ElectJob ej{};
-        ej.ent = ij.ent;
-        ej.ekey = ij.ekey;
-        ej.cnt = ij.cnt;
-        ej.nblocks = ij.nblocks;
-        ej.tile = tile;
-        ej.bk_shift = ij.bk_shift;
-        ej.table = c->d_table;
-        ej.shift = c->slot_shift;
-        ej.tmask = c->slots - 1;
-        ej.ctl = c->d_ctl;
-        ej.created_acc = c->d_created;
-        ej.lo = lo;
-        ej.resp_lo = resp_lo;
-        ej.resp_hi = resp_hi;
-        ej.prev = d_prev;
-        ej.prevf = d_prev_found;
-        ej.exp = (c->exp >> 8) & 0xFF;
-        ej.dbg = (c->exp & 0x10000) ? c->d_dbg : nullptr;
-        ej.stall = c->stall;
-        const unsigned dyn = (ij.nblocks + 1) * 4 + ij.nblocks * 2;
-        if (want_prev) NRG_LAUNCH(c, "hm_elect", hm_elect_kernel<true>, 1u << nb_log, TPB, dyn, c->stream, ej);
-        else NRG_LAUNCH(c, "hm_elect", hm_elect_kernel<false>, 1u << nb_log, TPB, dyn, c->stream, ej);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     c->rounds++;
     if (measured) c->dup_puts += n;  // the skew ratio is over the rounds that measured it

@@ -115,8 +115,7 @@ struct nrg_ctx {
     uint64_t rounds = 0;             // replay rounds launched (statistics)
     // tuning and diagnostic knobs: set only through nrg_test_set_knob (include/nrgpu_testing.h)
     uint32_t k1_items = 0;           // Puts per index thread (0: by round size; NRG_KNOB_K1)
-    uint32_t bk_ent = 0;             // target entries per elector bucket (0: default; NRG_KNOB_BK_ENT)
-    uint32_t exp = 0;                // diagnostic bits (NRG_KNOB_EXP; see hashmap.hip IndexJob/ElectJob)
+    uint32_t exp = 0;                // diagnostic bits (NRG_KNOB_EXP; see hashmap.hip StampJob)
     // Reads of the last replayed round: answered in the next launch beside the next round's
     // index pass, or by nrg_join / nrg_sync / any call that reads the table. With
     // pipeline == false they are flushed at the end of every call.
@@ -133,8 +132,8 @@ struct nrg_ctx {
     uint32_t stall = 0;       // NRG_KNOB_STALL (tests): 1 odd waves sleep at LDS reuse points, 2 (synthetic,
                               // diagnostic: wrong results) without the bucket pass's tile-map barrier
     uint64_t* d_created = nullptr;  // [HM_CREATED_SLOTS] keys created by replay rounds
-    void* d_bk_ent = nullptr;       // [index tiles][tile] 16-B {id << 32 | i+1, value}
-    uint64_t* d_bk_key = nullptr;   // [index tiles][tile] key of each entry
+    void* d_bk_ent = nullptr;       // partition rounds: [tiles][tile] 16-B {key, value} entries
+    uint32_t* d_bk_idx = nullptr;   // partition rounds with previous values: [tiles][tile] round offset
     uint32_t* d_bk_cnt = nullptr;   // [bucket][index tiles] offset << 16 | count
     // Stamp rounds (<= stamp_max Puts, no previous values): per-Put slot ids by epoch parity.
     uint64_t stamp_max = 0;

@@ -403,7 +403,7 @@ int nrg_close(nrg_ctx* c) {
     if (c->stream && c->stream != c->own_stream) (void)hipStreamSynchronize(c->stream);
     void* ptrs[] = {c->d_ring,    c->d_ctl,      c->d_table,    c->d_stack,  c->d_words,
                     c->d_sort_aux, c->d_tmp_u64, c->d_scan_desc, c->d_created, c->d_st_aux,
-                    c->d_sy_aux,  c->d_bk_ent,   c->d_bk_key,   c->d_bk_cnt, c->d_dbg,     c->d_pt};
+                    c->d_sy_aux,  c->d_bk_ent,   c->d_bk_idx,   c->d_bk_cnt, c->d_dbg,     c->d_pt};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     sort_free(c->sort);
@@ -1110,17 +1110,12 @@ extern "C" int nrg_test_set_knob(nrg_ctx* c, int knob, uint64_t v) {
             if (!hm || v > 4) return NRG_E_INVAL;
             c->k1_items = (uint32_t)v;
             return NRG_OK;
-        case NRG_KNOB_BK_ENT:
-            if (!hm || v > (1u << 20)) return NRG_E_INVAL;
-            c->bk_ent = (uint32_t)v;
-            return NRG_OK;
         case NRG_KNOB_EXP: {
             if (v > 0xFFFFFFFFull) return NRG_E_INVAL;
             c->exp = (uint32_t)v;
-            // timestamp buffer: hashmap elector blocks, stack tiles (+ finish workgroups at 128..),
-            // synthetic buckets (<= 1024), partition tiles and sum workgroups; 16 words each
+            // timestamp buffer: stack tiles (+ finish workgroups at 128..), synthetic buckets
+            // (<= 1024), partition tiles and sum workgroups; 16 words each
             uint64_t words = 0;
-            if (hm && (c->exp & 0x10000)) words = (uint64_t)HM_BK_MAX * 16;
             if (c->cfg.ds_kind == NRG_DS_STACK && (c->exp & 2))
                 words = std::max<uint64_t>(256, (c->cfg.max_batch + 2047) / 2048) * 16;
             if (sy && (c->exp & 2)) words = 3072 * 16;  // synthetic.hip SY_DBG_ROWS
@@ -1149,7 +1144,7 @@ extern "C" int nrg_test_set_knob(nrg_ctx* c, int knob, uint64_t v) {
             c->stall = (uint32_t)v;
             return NRG_OK;
         case NRG_KNOB_PART:
-            if (!hm || v > 2) return NRG_E_INVAL;
+            if (!hm || v > 2) return NRG_E_INVAL;  // 0: partition rounds only where stamp rounds cannot
             c->part_mode = (uint32_t)v;
             return NRG_OK;
         case NRG_KNOB_SMALL_MAX:

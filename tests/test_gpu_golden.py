@@ -22,14 +22,15 @@ def _load(name):
 
 
 @pytest.mark.parametrize("name", ["hashmap_small.npz", "hashmap_sparse.npz"])
-@pytest.mark.parametrize("path", ["stamp", "bucket", "part"])
+@pytest.mark.parametrize("path", ["stamp", "part"])
 def test_hashmap_fixture_on_gpu(nrg, name, path):
     """Rounds of Log::append + Log::exec with HashMap::insert's previous values, then the
     round's Gets; sorted final contents equal the fixture's dict. The previous-value rounds take
-    the bucket elector; the same stream without responses also runs through the stamp rounds."""
+    partition rounds; the same stream without responses also runs through the stamp rounds
+    ("stamp") and through partition rounds ("part")."""
     d = _load(name)
     W, R, rounds = int(d["W"]), int(d["R"]), int(d["rounds"])
-    knobs = {"bucket": {"STAMP_MAX": 0}, "part": {"PART": 2}}.get(path, {})
+    knobs = {"part": {"PART": 2}}.get(path, {})
     dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, knobs=knobs, log2_slots=16, max_batch=4096)
     dev.hm_prefill_range(int(d["prefill"]), 1)
     for r in range(rounds):

@@ -2,7 +2,7 @@
 """Run bench.py under several settings (one subprocess each) and print a compact table.
 
 Usage: tools/sweep.py 'NAME|ENV=V ENV2=V2|--bench --args' ...
-(replica tuning knobs are bench.py arguments: --knob K1=2 --knob BK_ENT=256; --with-prev also runs
+(replica tuning knobs are bench.py arguments: --knob K1=2 --knob PART=2; --with-prev also runs
 the previous-value variant and prints its rate)
 """
 import json
