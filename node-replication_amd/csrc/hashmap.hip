@@ -1609,7 +1609,7 @@ hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool
     // 4M + 500k 413 / 271; previous values and skewed streams: partition rounds everywhere.
     constexpr u64 PART_MIN = 3ull << 17;
     const bool stamp0 = !want_prev && c->stamp_max && n <= c->stamp_max && !c->skewed;
-    const bool part = c->part_mode >= 2 || (c->part_mode == 1 && (!stamp0 || n >= PART_MIN));
+    const bool part = !stamp0 || c->part_mode >= 2 || (c->part_mode == 1 && n >= PART_MIN);
     const bool stamp = stamp0 && !part;
     if (part) {
         // ---- partition round: {partition(e) | apply(e-1) | reads(e-1)}, then hm_papply_kernel(e) ----
