@@ -329,7 +329,7 @@ __device__ __forceinline__ u32 wave_rank_bits(bool on, u32 key, int lane, CNT* c
 // Stable ranking of one wave round in a wave-private (mask, count) table: every lane with a
 // key ORs its bit into mask[key]; the mask read back is the set of lanes with that key. Returns
 // count[key] + the number of lower lanes with the same key; the highest such lane advances count
-// and clears mask. (NRG_SY_BALLOT=0 builds; three LDS round trips per ranking)
+// and clears mask (three LDS round trips per ranking).
 template <typename CNT>
 __device__ __forceinline__ u32 wave_rank_mask(bool on, u32 key, int lane, u64* mask, CNT* count, u64* peers_out) {
     if (on) atomicOr((unsigned long long*)&mask[key], 1ull << lane);

@@ -2,7 +2,8 @@
 """Summarise a tools/profile.sh run (gpurun_out/prof_<tag>/) into profiles/<name>.txt.
 
 Per kernel: launches and average duration from the kernel-trace stats, and the average
-FETCH_SIZE / WRITE_SIZE per launch from the PMC passes. gfx950 correction (MI355X_MICROARCH.md,
+FETCH_SIZE / WRITE_SIZE per launch from the PMC passes, and (profile.sh ATOMIC=1) atomics at the
+L2, atomics sent to memory and memory read requests per launch. gfx950 correction (MI355X_MICROARCH.md,
 HBM section): FETCH_SIZE counts 128-B memory-side requests at 64 B, so it is doubled here;
 WRITE_SIZE is taken as reported. Both counters are in KB.
 
@@ -45,6 +46,8 @@ def main():
     stats = one(os.path.join(d, "trace", "**", "*kernel_stats.csv"))
     fetch = pmc(one(os.path.join(d, "fetch", "**", "*counter_collection.csv")), "FETCH_SIZE")
     write = pmc(one(os.path.join(d, "write", "**", "*counter_collection.csv")), "WRITE_SIZE")
+    apath = one(os.path.join(d, "atomic", "**", "*counter_collection.csv"))
+    atom = {c: pmc(apath, c) for c in ("TCC_ATOMIC_sum", "TCC_EA0_ATOMIC_sum", "TCC_EA0_RDREQ_sum")}
     lines = []
     bench = os.path.join(d, "bench_trace.json")
     if os.path.exists(bench):
@@ -58,8 +61,10 @@ def main():
             except (ValueError, KeyError):
                 pass
     lines.append("")
-    lines.append("%-28s %8s %11s %11s %14s %14s" % ("kernel", "calls", "avg_us", "min_us", "FETCHx2_KB/l",
-                                                    "WRITE_KB/l"))
+    hdr = ("kernel", "calls", "avg_us", "min_us", "FETCHx2_KB/l", "WRITE_KB/l")
+    if apath:
+        hdr += ("L2_ATOM/l", "EA_ATOM/l", "EA_RDREQ/l")
+    lines.append(("%-28s %8s %11s %11s %14s %14s" + " %12s" * (len(hdr) - 6)) % hdr)
     if stats:
         with open(stats) as f:
             rows = list(csv.DictReader(f))
@@ -67,9 +72,14 @@ def main():
             k = short(r["Name"])
             fe = fetch.get(k)
             wr = write.get(k)
-            lines.append("%-28s %8s %11.3f %11.3f %14s %14s" % (
+            line = "%-28s %8s %11.3f %11.3f %14s %14s" % (
                 k[:28], r["Calls"], float(r["AverageNs"]) / 1e3, float(r["MinNs"]) / 1e3,
-                "%.1f" % (2 * fe[1]) if fe else "-", "%.1f" % wr[1] if wr else "-"))
+                "%.1f" % (2 * fe[1]) if fe else "-", "%.1f" % wr[1] if wr else "-")
+            if apath:
+                for c in ("TCC_ATOMIC_sum", "TCC_EA0_ATOMIC_sum", "TCC_EA0_RDREQ_sum"):
+                    v = atom[c].get(k)
+                    line += " %12s" % ("%.0f" % v[1] if v else "-")
+            lines.append(line)
     # HBM traffic per launch of the round kernel, for bench.py's roofline.traffic
     tk = None
     try:
@@ -82,8 +92,8 @@ def main():
         parts = ["st_round_kernel"]
     elif tk and tk.startswith("synthetic"):
         parts = ["sy_part_kernel", "sy_bucket_kernel"]
-    else:
-        parts = ["hm_round_kernel"]
+    else:  # a partition round adds its apply launch
+        parts = ["hm_round_kernel"] + (["hm_papply_kernel"] if any("hm_papply" in k for k in fetch) else [])
 
     def per_unit(tab):
         got = [next((v for k, v in tab.items() if p in k), None) for p in parts]
