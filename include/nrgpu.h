@@ -246,12 +246,14 @@ int nrg_hashmap_digest(nrg_ctx* ctx, uint64_t out[3]);
 /* ---- Flat combining on the host ---------------------------------------------------------- */
 /* Replica's flat combiner for many client threads (nr/src/context.rs:88-194,
  * nr/src/replica.rs:345-356, 404-433, 483-497, 508-595), for any of the three data structures:
- * each registered thread posts up to 32 ops (MAX_PENDING_OPS) per call into the open batch;
- * whichever waiting thread takes the combiner lock turns the batch into ONE GPU round of `ctx`
- * (its writes appended and replayed in batch order, then its reads answered against the
- * post-round state) without waiting for the GPU, so the next batch fills while a round runs.
+ * each registered thread posts up to 32 ops (MAX_PENDING_OPS) per call into the open batch and
+ * parks; the combiner's own thread seals the batch into ONE GPU round of `ctx` (its writes
+ * appended and replayed in batch order, then its reads answered against the post-round state)
+ * without waiting for the GPU, so the next batch fills while a round runs (a second round is put
+ * in flight only for a batch of 512 ops or more unless NRG_KNOB_COMB_DEPTH fixes the depth).
  * Batches live in mapped pinned host memory that the round's kernels read and write directly.
- * Calls on one token are synchronous and must come from one thread at a time; while a combiner
+ * Calls on one token are synchronous and must come from one thread at a time (a second call on
+ * a token whose call is still in progress returns NRG_E_INVAL); while a combiner
  * is open, `ctx` is driven only through it, and no thread may be inside a call when it is closed.
  * Needs max_threads * 32 <= max_batch (and <= max_reads for the hashmap). */
 typedef struct nrg_combiner nrg_combiner;

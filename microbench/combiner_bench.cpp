@@ -49,6 +49,8 @@ static int run(int threads, int batch, double secs, bool stack, int spin, int de
         if (int r = nrg_test_set_knob(ctx, NRG_KNOB_COMB_SPIN, (uint64_t)spin)) return r;
     if (depth > 0)
         if (int r = nrg_test_set_knob(ctx, NRG_KNOB_COMB_DEPTH, (uint64_t)depth)) return r;
+    if (const char* g = std::getenv("CB_GATHER"))  // (this tool's own setting: the gather window, us)
+        if (int r = nrg_test_set_knob(ctx, NRG_KNOB_COMB_GATHER, std::strtoull(g, nullptr, 10))) return r;
     nrg_combiner* comb = nullptr;
     if (int r = nrg_combiner_open(ctx, (uint32_t)threads, &comb)) return r;
     std::atomic<bool> stop{false};

@@ -52,6 +52,21 @@ constexpr uint32_t WAKE_FAN = 2;  // children each woken waiter wakes (a binary 
 constexpr int NB = 6;                 // batch slots
 constexpr uint64_t DEPTH = 2;         // default rounds in flight (NRG_KNOB_COMB_DEPTH, <= NB - 2: a
                                       // slot's clients copy their responses out while later rounds run)
+// With a round in flight, the open batch is sealed into a second one only once it holds this
+// many ops: with few clients a small second round only splits them over more rounds (16 threads x
+// 32 ops: 16.4 M ops/s one round in flight vs 13.9 with two; 128 threads 55.9 vs 60.1;
+// profiles/r04_combiner.txt)
+constexpr uint32_t SECOND_MIN = 512;
+// With no round in flight, the open batch waits up to this long (NRG_KNOB_COMB_GATHER, us) for as
+// many posts as the last round carried: the clients it woke post again within a few us of each
+// other, and a batch sealed at the first post leaves the rest a whole round behind
+constexpr uint32_t GATHER_US = 10;
+
+uint64_t now_ns() {
+    timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (uint64_t)t.tv_sec * 1000000000ull + (uint64_t)t.tv_nsec;
+}
 
 enum : uint32_t { FREE = 0, OPEN = 1, SEALED = 2, DONE = 3 };
 
@@ -135,6 +150,12 @@ struct nrg_combiner {
     bool saved_pipeline = false;
     uint64_t saved_small = 0;
     std::atomic<uint32_t> next_tok{0};
+    // one post in flight per token: keeps a batch's reservations within cap and its waiters
+    // within wk[max_threads] even when two threads misuse one token
+    struct alignas(64) Tok {
+        std::atomic<uint32_t> busy{0};
+    };
+    Tok* tok = nullptr;  // [max_threads]
     Batch b[NB];
     alignas(64) std::atomic<uint64_t> open{0};       // round number of the OPEN batch
     std::atomic<uint32_t> opened{0};                 // futex word: bumped when a batch opens
@@ -144,6 +165,10 @@ struct nrg_combiner {
     std::atomic<uint64_t> rounds{0}, ops{0};
     int32_t spin_cap = 0;                            // clients that may spin at once
     uint64_t depth = DEPTH;                          // rounds in flight
+    bool depth_auto = true;                          // a second round only for a batch of SECOND_MIN ops
+    uint64_t gather_ns = GATHER_US * 1000ull;        // (combiner thread) GATHER_US window
+    uint32_t last_posts = 0;                         // posts of the last sealed batch
+    uint64_t gather_k = ~0ull, gather_t0 = 0;        // the batch being gathered, its first sight
     alignas(64) std::atomic<int32_t> spinning{0};
     // the combiner thread
     std::thread worker;
@@ -169,6 +194,7 @@ void comb_free(nrg_combiner* m) {
         if (x.done) (void)hipEventDestroy(x.done);
         delete[] x.wk;
     }
+    delete[] m->tok;
     delete m;
 }
 
@@ -246,10 +272,21 @@ int launch(nrg_combiner* m, Batch& x, uint32_t W, uint32_t R) {
 bool advance(nrg_combiner* m) {
     const uint64_t k = m->open.load(std::memory_order_relaxed);
     Batch& x = m->b[k % NB];
-    if (m->launched.load(std::memory_order_relaxed) - m->completed.load(std::memory_order_acquire) >= m->depth) return false;
-    if (!x.nw.load(std::memory_order_seq_cst) && !x.nr.load(std::memory_order_seq_cst)) return false;
+    const uint64_t inflight = m->launched.load(std::memory_order_relaxed) - m->completed.load(std::memory_order_acquire);
+    if (inflight >= m->depth) return false;
+    const uint32_t ops = x.nw.load(std::memory_order_seq_cst) + x.nr.load(std::memory_order_seq_cst);
+    if (!ops || (inflight && m->depth_auto && ops < SECOND_MIN)) return false;
+    if (!inflight && m->gather_ns && x.readers.load(std::memory_order_relaxed) < m->last_posts) {
+        const uint64_t t = now_ns();
+        if (m->gather_k != k) {
+            m->gather_k = k;
+            m->gather_t0 = t;
+        }
+        if (t - m->gather_t0 < m->gather_ns) return false;
+    }
     x.state.store(SEALED, std::memory_order_seq_cst);
     while (x.writers.load(std::memory_order_seq_cst)) _mm_pause();
+    m->last_posts = x.readers.load(std::memory_order_relaxed);  // (no client has left a sealed batch)
     const uint32_t W = x.nw.load(std::memory_order_relaxed), R = x.nr.load(std::memory_order_relaxed);
     // open round k+1 in the next slot: its previous round (k+1-NB) is complete (DEPTH < NB - 1);
     // wait for that round's clients to copy their responses out
@@ -305,6 +342,7 @@ int post_and_wait(nrg_combiner* m, uint32_t token, bool write, const void* ops, 
         return NRG_E_INVAL;
     if (n > MAX_PENDING) return NRG_E_CAPACITY;
     if (!n) return NRG_OK;
+    if (m->tok[token].busy.exchange(1, std::memory_order_acquire)) return NRG_E_INVAL;  // token in use
     const uint32_t in_b = write ? m->rec_b : m->rd_b, out_b = write ? m->wr_b : m->rr_b;
     uint64_t k;
     Batch* x;
@@ -365,6 +403,7 @@ int post_and_wait(nrg_combiner* m, uint32_t token, bool write, const void* ops, 
     std::memcpy(some, (write ? x->wsome : x->rsome) + off, n);
     const int rc = x->rc;
     x->readers.fetch_sub(1, std::memory_order_release);
+    m->tok[token].busy.store(0, std::memory_order_release);
     return rc;
 }
 
@@ -394,6 +433,7 @@ extern "C" int nrg_combiner_open(nrg_ctx* ctx, uint32_t max_threads, nrg_combine
         default: m->rd_b = sizeof(nrg_synth_rd), m->wr_b = 8, m->rr_b = 8; break;  // sums
     }
     bool ok = true;
+    ok = ok && (m->tok = new (std::nothrow) nrg_combiner::Tok[max_threads]());
     for (Batch& x : m->b) {
         ok = ok && (x.recs = (char*)host_alloc(cap * m->rec_b));
         ok = ok && (x.reads = (char*)host_alloc(cap * (m->rd_b ? m->rd_b : 1)));
@@ -420,7 +460,11 @@ extern "C" int nrg_combiner_open(nrg_ctx* ctx, uint32_t max_threads, nrg_combine
     // spinning took the job's whole cgroup quota and throttled it (22.3 vs 24.5 M ops/s parked;
     // profiles/r03_combiner_policy.txt)
     m->spin_cap = ctx->comb_spin >= 0 ? ctx->comb_spin : 0;
-    if (ctx->comb_depth) m->depth = std::min<uint64_t>(ctx->comb_depth, NB - 2);
+    if (ctx->comb_gather >= 0) m->gather_ns = (uint64_t)ctx->comb_gather * 1000ull;
+    if (ctx->comb_depth) {  // an explicit depth: no SECOND_MIN rule
+        m->depth = std::min<uint64_t>(ctx->comb_depth, NB - 2);
+        m->depth_auto = false;
+    }
     m->b[0].round.store(0);
     m->b[0].state.store(OPEN);
     try {

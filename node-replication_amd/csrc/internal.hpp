@@ -129,6 +129,7 @@ struct nrg_ctx {
     int32_t comb_spin = -1;   // combiner knobs (NRG_KNOB_COMB_SPIN / _DEPTH): -1 / 0 = defaults
     uint64_t small_max = 0;   // hashmap: rounds of <= small_max Puts take the one-launch small round
     uint32_t comb_depth = 0;
+    int32_t comb_gather = -1;  // NRG_KNOB_COMB_GATHER (us; -1 = default)
     uint32_t stall = 0;       // NRG_KNOB_STALL (tests): 1 odd waves sleep at LDS reuse points, 2 (synthetic,
                               // diagnostic: wrong results) without the bucket pass's tile-map barrier
     uint64_t* d_created = nullptr;  // [HM_CREATED_SLOTS] keys created by replay rounds

@@ -1155,6 +1155,10 @@ extern "C" int nrg_test_set_knob(nrg_ctx* c, int knob, uint64_t v) {
             if (v > 4096) return NRG_E_INVAL;
             c->comb_spin = (int32_t)v;
             return NRG_OK;
+        case NRG_KNOB_COMB_GATHER:
+            if (v > 1000) return NRG_E_INVAL;
+            c->comb_gather = (int32_t)v;
+            return NRG_OK;
         case NRG_KNOB_COMB_DEPTH:
             if (v < 1 || v > 4) return NRG_E_INVAL;
             c->comb_depth = (uint32_t)v;

@@ -18,12 +18,14 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("T,ITERS", [(8, 40), (64, 12)])
+@pytest.mark.parametrize("T,ITERS", [(8, 40), (64, 12), (256, 5)])
 def test_combiner_threads(nrg, orc, T, ITERS):
     """T client threads; at 64 the rounds are larger, waiters wake through the futex tree and
-    rounds of up to 2048 Puts take the one-launch small rounds."""
+    rounds of up to 2048 Puts take the one-launch small rounds; at 256 batches pass 512 ops and
+    two rounds run in flight, the larger ones as full (not small) rounds."""
     SPAN = 5000
-    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=20, max_batch=1 << 12, max_reads=1 << 12,
+    cap = max(1 << 12, T * 32)
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=20, max_batch=cap, max_reads=cap,
                             log_bytes=64 * (1 << 16))
     dev.hm_prefill_range(1000, 1)  # keys 0..999 -> k + 1: thread 0's range starts with them
     comb = nrg.Combiner(dev, T)
