@@ -58,9 +58,11 @@ constexpr uint64_t DEPTH = 2;         // default rounds in flight (NRG_KNOB_COMB
 // profiles/r04_combiner.txt)
 constexpr uint32_t SECOND_MIN = 512;
 // With no round in flight, the open batch waits up to this long (NRG_KNOB_COMB_GATHER, us) for as
-// many posts as the last round carried: the clients it woke post again within a few us of each
-// other, and a batch sealed at the first post leaves the rest a whole round behind
-constexpr uint32_t GATHER_US = 10;
+// many posts as the last round carried: the clients a round woke post again over the ~15 us their
+// wake-up tree takes, and a batch sealed at the first post leaves the rest a whole round behind.
+// 16 threads x 32 ops: 15.5 / 15.4 / 15.2 / 18.7 M ops/s at 0 / 5 / 10 / 20 us (256 / 256 / 285 /
+// 511 ops per round); 64 threads 35.4 / 35.7 / 37.4 / 38.9 (profiles/r04_combiner.txt)
+constexpr uint32_t GATHER_US = 20;
 
 uint64_t now_ns() {
     timespec t;
@@ -91,6 +93,9 @@ struct alignas(64) Batch {
     // job's CPU quota in the kernel at 128+ threads). They wake as a binary tree: the combiner
     // thread wakes waiter 0 and waiter i wakes 2i+1 and 2i+2 -- off the combiner's path, and
     // about log2(waiters) wake-up latencies for the last one.
+    // (Measured and dropped: the first 16 or 32 waiters parked on one shared word and woken by
+    // one FUTEX_WAKE -- 13.7 / 16.6 vs 14.5 M ops/s at 16 threads, 30.3 / 26.7 vs 36.5 at 64;
+    // profiles/r04_combiner.txt.)
     alignas(64) std::atomic<uint32_t> nwait{0};
     std::atomic<uint32_t>* wk = nullptr;  // [max_threads]
     int rc = NRG_OK;                               // launch or device error of the round

@@ -84,9 +84,10 @@ struct ReadJob {
 };
 
 
-// Block-wide exclusive prefix sum of one u32 per thread (TPB threads); *total gets the sum.
+// Block-wide exclusive prefix sum of one u32 per thread (NT threads); *total gets the sum.
+template <int NT = TPB>
 __device__ __forceinline__ u32 block_scan_excl(u32 v, u32* total) {
-    __shared__ u32 s_w[TPB / 64];
+    __shared__ u32 s_w[NT / 64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     u32 inc = v;
 #pragma unroll
@@ -98,7 +99,7 @@ __device__ __forceinline__ u32 block_scan_excl(u32 v, u32* total) {
     __syncthreads();
     u32 pre = 0, tot = 0;
 #pragma unroll
-    for (int i = 0; i < TPB / 64; i++) {
+    for (int i = 0; i < NT / 64; i++) {
         pre += i < w ? s_w[i] : 0u;
         tot += s_w[i];
     }
@@ -629,13 +630,18 @@ struct PApplyJob {
     u32 stall;  // NRG_KNOB_STALL (tests)
 };
 
-constexpr int PA_TPB = 256;
-template <bool PREV>
+// WIDE (large rounds without previous values): 1024-thread workgroups over 4x wider buckets (256
+// instead of 1024 per round). A bucket's run in a tile then holds ~4x the entries (a 128-B line
+// instead of ~32 B) and there are 4x fewer [tile][bucket] count words to gather, each a line.
+template <bool PREV, bool WIDE>
 struct PaGeo {
-    static constexpr int C = PREV ? 512 : 1024;  // entries per chunk
-    static constexpr int HT = 2 * C;             // LDS hash entries (load <= 1/2)
-    static constexpr int PER = C / PA_TPB;
+    static_assert(!(PREV && WIDE), "previous values use 256-thread workgroups");
+    static constexpr int TPB = WIDE ? 1024 : 256;
+    static constexpr int C = WIDE ? 4096 : PREV ? 512 : 1024;  // entries per chunk
+    static constexpr int HT = 2 * C;                           // LDS hash entries (load <= 1/2)
+    static constexpr int PER = C / TPB;
 };
+constexpr u32 PA_WIDE_NB_LOG = 8;  // WIDE: at most 256 buckets
 
 __device__ __forceinline__ u32 pa_hash(u64 k, u32 ht) { return (u32)(mix64(k) >> 40) & (ht - 1); }
 
@@ -725,9 +731,10 @@ __device__ __forceinline__ void pa_resolve(Slot* table, u32 shift, u64 tmask, co
     }
 }
 
-template <bool PREV>
-__global__ __launch_bounds__(PA_TPB) void hm_papply_kernel(PApplyJob j) {
-    constexpr int C = PaGeo<PREV>::C, HT = PaGeo<PREV>::HT, PER = PaGeo<PREV>::PER;
+template <bool PREV, bool WIDE>
+__global__ __launch_bounds__((PaGeo<PREV, WIDE>::TPB)) void hm_papply_kernel(PApplyJob j) {
+    using G = PaGeo<PREV, WIDE>;
+    constexpr int PA_TPB = G::TPB, C = G::C, HT = G::HT, PER = G::PER;
     constexpr u32 NOFIRST = 0xFFFFFFFFu;
     extern __shared__ u32 s_dyn[];  // s_pre[ntiles + 1] entry prefix, s_off[ntiles] (u16)
     __shared__ u64 s_hk[HT];
@@ -742,7 +749,12 @@ __global__ __launch_bounds__(PA_TPB) void hm_papply_kernel(PApplyJob j) {
     __shared__ uint16_t s_eh[PREV ? C : 1];
     __shared__ u32 s_ei[PREV ? C : 1];
     __shared__ u32 s_created;
-    const u32 nt = j.ntiles, b = blockIdx.x;
+    // Workgroups are dealt to the 8 XCDs round-robin; bucket b goes to workgroup 8 (b % per) + b / per
+    // (per = nb / 8), so each XCD takes a contiguous range of buckets. Neighbouring buckets' entry
+    // runs and count words share lines, and those lines are then fetched into one XCD's L2
+    // instead of several.
+    const u32 per = j.nb >> 3;
+    const u32 nt = j.ntiles, b = j.nb >= 64 ? (blockIdx.x & 7u) * per + (blockIdx.x >> 3) : blockIdx.x;
     u32* s_pre = s_dyn;
     uint16_t* s_off = (uint16_t*)(s_dyn + nt + 1);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -767,7 +779,7 @@ __global__ __launch_bounds__(PA_TPB) void hm_papply_kernel(PApplyJob j) {
         }
     }
     u32 total;
-    u32 run = block_scan_excl(loc, &total);  // (its barriers also order the initialisation above)
+    u32 run = block_scan_excl<PA_TPB>(loc, &total);  // (its barriers also order the initialisation above)
     for (u32 q = 0; q < K; q++) {
         const u32 t = threadIdx.x * K + q;
         if (t < nt) {
@@ -1620,6 +1632,10 @@ hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool
         const u32 log2_slots = 64 - c->slot_shift;
         u32 nb_log = 0;
         while ((64ull << nb_log) < n && (1u << nb_log) < HM_BK_MAX) nb_log++;
+        // large rounds without previous values: 1024-thread apply workgroups over <= 256 buckets
+        constexpr u64 PA_WIDE_MIN = 1ull << 16;
+        const bool wide = !want_prev && (c->pa_wide == 2 || (c->pa_wide == 1 && n >= PA_WIDE_MIN));
+        if (wide && nb_log > PA_WIDE_NB_LOG) nb_log = PA_WIDE_NB_LOG;
         if (nb_log > log2_slots) nb_log = log2_slots;
         // previous values keep every Put; otherwise a Put overwritten later in its tile is dropped
         // when the key stream is skewed (uniform streams have next to no such Puts: no LDS hash)
@@ -1661,8 +1677,12 @@ hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool
         aj.prevf = d_prev_found;
         aj.stall = c->stall;
         const unsigned dyn = ((ij.nblocks + 1) * 4 + ij.nblocks * 2 + 3) & ~3u;
-        if (want_prev) NRG_LAUNCH(c, "hm_papply", hm_papply_kernel<true>, 1u << nb_log, PA_TPB, dyn, c->stream, aj);
-        else NRG_LAUNCH(c, "hm_papply", hm_papply_kernel<false>, 1u << nb_log, PA_TPB, dyn, c->stream, aj);
+        if (want_prev)
+            NRG_LAUNCH(c, "hm_papply", (hm_papply_kernel<true, false>), 1u << nb_log, (PaGeo<true, false>::TPB), dyn, c->stream, aj);
+        else if (wide)
+            NRG_LAUNCH(c, "hm_papply", (hm_papply_kernel<false, true>), 1u << nb_log, (PaGeo<false, true>::TPB), dyn, c->stream, aj);
+        else
+            NRG_LAUNCH(c, "hm_papply", (hm_papply_kernel<false, false>), 1u << nb_log, (PaGeo<false, false>::TPB), dyn, c->stream, aj);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     } else if (stamp) {
         // ---- stamp round: one launch {index(e) | apply(e-1) | reads(e-1)} ----

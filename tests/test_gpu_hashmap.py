@@ -35,7 +35,7 @@ def _check_state(dev, om):
 
 # knobs of the replay paths: default selection, partition rounds for every round, and the
 # one-launch small rounds (the combiner's) for rounds of up to 2048 Puts
-PATHS = {"default": {}, "part": {"PART": 2}, "small": {"SMALL_MAX": 2048}}
+PATHS = {"default": {}, "part": {"PART": 2}, "wide": {"PART": 2, "PA_WIDE": 2}, "small": {"SMALL_MAX": 2048}}
 
 
 @pytest.mark.parametrize("path", list(PATHS))
@@ -145,17 +145,17 @@ def test_fused_round_device(nrg, orc):
     _check_state(dev, om)
 
 
-@pytest.mark.parametrize("path", ["stamp", "part"])
+@pytest.mark.parametrize("path", ["stamp", "part", "wide"])
 def test_pipelined_rounds_back_to_back(nrg, orc, path):
     """config.pipeline = 1: rounds enqueued back to back, no host sync in between. Each round's
     reads run in the next round's launch, beside its index pass (and, for stamp rounds, beside
     the apply of their own round's writes), and must see exactly their own round's state (keys
     created by later rounds invisible, values overwritten later not yet there).
     Knob PART = 2 sends every round through partition rounds instead (their reads ride in the
-    next round's partition launch)."""
+    next round's partition launch); PA_WIDE = 2 applies them with 1024-thread workgroups."""
     import torch
 
-    knobs = {"part": {"PART": 2}}.get(path, {})
+    knobs = {"part": {"PART": 2}, "wide": {"PART": 2, "PA_WIDE": 2}}.get(path, {})
     dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, knobs=knobs, log2_slots=17, max_batch=1 << 14, pipeline=1)
     dev.use_torch_stream()
     om = orc.HashMap()
@@ -337,7 +337,7 @@ def _mix64(x):
         return x ^ (x >> np.uint64(31))
 
 
-@pytest.mark.parametrize("knobs", [{}, {"PART": 2}, {"PART": 2, "STALL": 1}])
+@pytest.mark.parametrize("knobs", [{}, {"PART": 2}, {"PART": 2, "STALL": 1}, {"PART": 2, "PA_WIDE": 2, "STALL": 1}])
 def test_one_bucket_rounds(nrg, orc, knobs):
     """Pipelined rounds whose keys all fall into ONE elector bucket (many chunks, finer parts,
     duplicates across index tiles), with side-slot keys and a Zipf round, against the oracle.
@@ -407,12 +407,13 @@ def _bucket_rounds(nrg, orc, dev, om, rounds):
     assert dev.hm_digest() == om.digest()
 
 
-@pytest.mark.parametrize("part", [1, 2])
-def test_large_pipelined_rounds(nrg, orc, part):
-    """Large pipelined rounds (300k-400k Puts: 2048-Put partition tiles, 1024 buckets): uniform
-    and Zipf rounds with side-slot keys and a small round in between, against the sequential
-    oracle; default round kinds, and every round a partition round (PART = 2)."""
-    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, knobs={"PART": part}, log2_slots=22, max_batch=1 << 19,
+@pytest.mark.parametrize("knobs", [{"PART": 1}, {"PART": 2}, {"PART": 2, "PA_WIDE": 0}])
+def test_large_pipelined_rounds(nrg, orc, knobs):
+    """Large pipelined rounds (300k-400k Puts: 2048-Put partition tiles, 256 wide buckets, or 1024
+    with PA_WIDE = 0): uniform and Zipf rounds with side-slot keys and a small round in between,
+    against the sequential oracle; default round kinds, and every round a partition round
+    (PART = 2)."""
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, knobs=knobs, log2_slots=22, max_batch=1 << 19,
                             pipeline=1)
     dev.use_torch_stream()
     om = orc.HashMap()
@@ -425,12 +426,12 @@ def test_large_pipelined_rounds(nrg, orc, part):
     _bucket_rounds(nrg, orc, dev, om, rounds)
 
 
-@pytest.mark.parametrize("part", [1, 2])
-def test_crowded_bucket_rounds(nrg, orc, part):
+@pytest.mark.parametrize("knobs", [{"PART": 1}, {"PART": 2}, {"PART": 2, "PA_WIDE": 2}])
+def test_crowded_bucket_rounds(nrg, orc, knobs):
     """2500 new keys of a round home into the first 4096 slots of the table (one partition bucket,
     taken in several chunks; their claims crowd one region, long probe chains), repeated and
     reversed in later rounds, against the sequential oracle."""
-    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, knobs={"PART": part}, log2_slots=20, max_batch=1 << 14,
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, knobs=knobs, log2_slots=20, max_batch=1 << 14,
                             pipeline=1)
     dev.use_torch_stream()
     om = orc.HashMap()
