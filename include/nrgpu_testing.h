@@ -43,9 +43,9 @@ int nrg_test_debug_read(nrg_ctx* ctx, uint64_t* out, uint64_t words);
                                    while their round runs (default 0: every waiting client parks
                                    on a futex)                                                   */
 #define NRG_KNOB_COMB_DEPTH 11  /* combiner: rounds in flight (1..4; default 2, the 2nd for >=512 ops) */
-#define NRG_KNOB_PA_WIDE 16     /* hashmap partition rounds without previous values: apply with 1024-thread
-                                   workgroups over <= 256 buckets (0 never, 1 rounds of >= 2^16 Puts
-                                   (default), 2 always) */
+#define NRG_KNOB_PA_TPB 16      /* hashmap partition rounds without previous values: apply workgroup
+                                   width 256 / 512 / 1024 over <= 1024 / 512 / 256 buckets (0 = 1024
+                                   for rounds of >= 2^16 Puts, else 256: the default) */
 #define NRG_KNOB_COMB_GATHER 15 /* combiner: us an idle combiner waits for as many posts as the last
                                    round carried before sealing (0..1000, default 20; 0 = seal at once) */
 #define NRG_KNOB_SMALL_MAX 12   /* hashmap: rounds of at most this many Puts (<= 2048, and <= 8192

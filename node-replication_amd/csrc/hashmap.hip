@@ -630,18 +630,19 @@ struct PApplyJob {
     u32 stall;  // NRG_KNOB_STALL (tests)
 };
 
-// WIDE (large rounds without previous values): 1024-thread workgroups over 4x wider buckets (256
-// instead of 1024 per round). A bucket's run in a tile then holds ~4x the entries (a 128-B line
-// instead of ~32 B) and there are 4x fewer [tile][bucket] count words to gather, each a line.
-template <bool PREV, bool WIDE>
+// T threads per workgroup (rounds without previous values: 256, 512 or 1024 over at most 1024,
+// 512 or 256 buckets). Wider workgroups over wider buckets: a bucket's run in a tile holds more
+// entries (a 128-B line at 1024 instead of ~32 B at 256) and there are fewer [tile][bucket] count
+// words to gather, each a line.
+template <bool PREV, int T>
 struct PaGeo {
-    static_assert(!(PREV && WIDE), "previous values use 256-thread workgroups");
-    static constexpr int TPB = WIDE ? 1024 : 256;
-    static constexpr int C = WIDE ? 4096 : PREV ? 512 : 1024;  // entries per chunk
-    static constexpr int HT = 2 * C;                           // LDS hash entries (load <= 1/2)
+    static_assert(!PREV || T == 256, "previous values use 256-thread workgroups");
+    static constexpr int TPB = T;
+    static constexpr int C = PREV ? 512 : 4 * T;  // entries per chunk
+    static constexpr int HT = 2 * C;              // LDS hash entries (load <= 1/2)
     static constexpr int PER = C / TPB;
+    static constexpr u32 NB_LOG = T == 1024 ? 8 : T == 512 ? 9 : 10;  // at most this many buckets
 };
-constexpr u32 PA_WIDE_NB_LOG = 8;  // WIDE: at most 256 buckets
 
 __device__ __forceinline__ u32 pa_hash(u64 k, u32 ht) { return (u32)(mix64(k) >> 40) & (ht - 1); }
 
@@ -731,15 +732,15 @@ __device__ __forceinline__ void pa_resolve(Slot* table, u32 shift, u64 tmask, co
     }
 }
 
-template <bool PREV, bool WIDE>
-__global__ __launch_bounds__((PaGeo<PREV, WIDE>::TPB)) void hm_papply_kernel(PApplyJob j) {
-    using G = PaGeo<PREV, WIDE>;
+template <bool PREV, int T>
+__global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(PREV ? 3 : 4))) void hm_papply_kernel(PApplyJob j) {
+    using G = PaGeo<PREV, T>;
     constexpr int PA_TPB = G::TPB, C = G::C, HT = G::HT, PER = G::PER;
     constexpr u32 NOFIRST = 0xFFFFFFFFu;
     extern __shared__ u32 s_dyn[];  // s_pre[ntiles + 1] entry prefix, s_off[ntiles] (u16)
     __shared__ u64 s_hk[HT];
     __shared__ u32 s_hp[HT + 1];   // last chunk position + 1 of the key; [HT]: the side key
-    __shared__ uint16_t s_tile[C];
+    __shared__ uint16_t s_tile[2][C];        // entry tile maps of this chunk and the next
     __shared__ u32 s_h1[PREV ? HT + 1 : 1];  // PREV: first chunk position + 1
     __shared__ u32 s_hs[PREV ? HT + 1 : 1];  // PREV: the key's slot (SIDE_ID, FULL_SLOT)
     __shared__ u64 s_lv[PREV ? HT + 1 : 1];  // PREV: the key's value so far in the walk
@@ -794,33 +795,54 @@ __global__ __launch_bounds__((PaGeo<PREV, WIDE>::TPB)) void hm_papply_kernel(PAp
     }
     __syncthreads();
     u32 created = 0;
-    for (u32 base = 0; base < total; base += C) {
+    // entry tile map of the chunk at `base`
+    auto map_chunk = [&](u32 base, uint16_t* map) {
         const u32 cn = total - base < (u32)C ? total - base : (u32)C;
-        // entry tile map of the chunk [base, base + cn)
         for (u32 q = 0; q < K; q++) {
             const u32 t = threadIdx.x * K + q;
             if (t >= nt) break;
             const u32 lo_ = s_pre[t] > base ? s_pre[t] : base;
             const u32 hi_ = s_pre[t + 1] < base + cn ? s_pre[t + 1] : base + cn;
-            for (u32 i = lo_; i < hi_; i++) s_tile[i - base] = (uint16_t)t;
+            for (u32 i = lo_; i < hi_; i++) map[i - base] = (uint16_t)t;
         }
+    };
+    // this thread's entries of the chunk at `base` (issued; used a chunk later)
+    u64x2 xn[PER];
+    u32 in_[PER];
+    auto load_chunk = [&](u32 base, const uint16_t* map) {
+        const u32 cn = total - base < (u32)C ? total - base : (u32)C;
+#pragma unroll
+        for (int r = 0; r < PER; r++) {
+            const u32 p = r * PA_TPB + threadIdx.x;
+            xn[r].x = EMPTY_KEY;
+            xn[r].y = 0;
+            in_[r] = 0;
+            if (p < cn) {
+                const u32 t = map[p];
+                const u64 e = (u64)t * j.tile + s_off[t] + (base + p - s_pre[t]);
+                xn[r] = j.ent[e];
+                if (PREV) in_[r] = j.eidx[e];
+            }
+        }
+    };
+    if (total) {
+        map_chunk(0, s_tile[0]);
         __syncthreads();
-        test_stall(j.stall & 1, w);  // (tests) slow waves read s_tile below
+        test_stall(j.stall & 1, w);  // (tests) slow waves read the map while the next is built
+        load_chunk(0, s_tile[0]);
+    }
+    // Software pipelined: the next chunk's entries are in flight while this chunk resolves.
+    for (u32 base = 0, pb = 0; base < total; base += C, pb ^= 1) {
+        const u32 cn = total - base < (u32)C ? total - base : (u32)C;
         u64x2 x[PER];
         u32 ix[PER], hh[PER];
 #pragma unroll
         for (int r = 0; r < PER; r++) {
-            const u32 p = r * PA_TPB + threadIdx.x;
-            x[r].x = EMPTY_KEY;
-            x[r].y = 0;
-            ix[r] = 0;
-            if (p < cn) {
-                const u32 t = s_tile[p];
-                const u64 e = (u64)t * j.tile + s_off[t] + (base + p - s_pre[t]);
-                x[r] = j.ent[e];
-                if (PREV) ix[r] = j.eidx[e];
-            }
+            x[r] = xn[r];
+            ix[r] = in_[r];
         }
+        const u32 nbase = base + C;
+        if (nbase < total) map_chunk(nbase, s_tile[pb ^ 1]);  // (published by the barrier below)
         // one hash entry per key: its last (and first) position in the chunk
 #pragma unroll
         for (int r = 0; r < PER; r++) {
@@ -848,6 +870,10 @@ __global__ __launch_bounds__((PaGeo<PREV, WIDE>::TPB)) void hm_papply_kernel(PAp
             }
         }
         __syncthreads();
+        if (nbase < total) {
+            test_stall(j.stall & 1, w);  // (tests) slow waves read the next map after the others moved on
+            load_chunk(nbase, s_tile[pb ^ 1]);
+        }
         if (!PREV) {
             // the key's last entry finds or claims its slot and stores its value
             bool dec[PER], on[PER], fr[PER];
@@ -874,7 +900,24 @@ __global__ __launch_bounds__((PaGeo<PREV, WIDE>::TPB)) void hm_papply_kernel(PAp
                 } else if (sl[r] < 0) {
                     atomicOr(&j.ctl->err, ERR_TABLE_FULL);
                 } else {
+#if NRG_PA_FULL
+                    if (fr[r]) {  // claimed: stamps stored by pa_resolve, the 32-B sector completes here
+                        u64x2 kv;
+                        kv.x = x[r].x;
+                        kv.y = x[r].y;
+                        *(u64x2*)&j.table[sl[r]] = kv;
+                    } else {      // found: the whole 32-B slot, its stamps as they are
+                        const u64x2 stp = *(const u64x2*)&j.table[sl[r]].st[0];
+                        Slot z;
+                        z.key = x[r].x;
+                        z.val = x[r].y;
+                        z.st[0] = stp.x;
+                        z.st[1] = stp.y;
+                        j.table[sl[r]] = z;
+                    }
+#else
                     j.table[sl[r]].val = x[r].y;
+#endif
                     created += fr[r];
                 }
             }
@@ -976,7 +1019,7 @@ __global__ __launch_bounds__((PaGeo<PREV, WIDE>::TPB)) void hm_papply_kernel(PAp
                 s_h1[h] = NOFIRST;
             }
         }
-        __syncthreads();  // hash entries free, s_tile reused by the next chunk
+        __syncthreads();  // hash entries free; the next iteration builds the map after next in s_tile[pb]
     }
     if (created) atomicAdd(&s_created, created);
     __syncthreads();
@@ -1632,10 +1675,13 @@ hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool
         const u32 log2_slots = 64 - c->slot_shift;
         u32 nb_log = 0;
         while ((64ull << nb_log) < n && (1u << nb_log) < HM_BK_MAX) nb_log++;
-        // large rounds without previous values: 1024-thread apply workgroups over <= 256 buckets
+        // apply workgroup width (NRG_KNOB_PA_TPB; 0: 1024 threads over <= 256 buckets for rounds of
+        // >= PA_WIDE_MIN Puts without previous values, else 256 over <= 1024)
         constexpr u64 PA_WIDE_MIN = 1ull << 16;
-        const bool wide = !want_prev && (c->pa_wide == 2 || (c->pa_wide == 1 && n >= PA_WIDE_MIN));
-        if (wide && nb_log > PA_WIDE_NB_LOG) nb_log = PA_WIDE_NB_LOG;
+        const u32 pa_t = want_prev ? 256u : c->pa_tpb ? c->pa_tpb : n >= PA_WIDE_MIN ? 1024u : 256u;
+        const u32 pa_nb_log = pa_t == 1024 ? PaGeo<false, 1024>::NB_LOG : pa_t == 512 ? PaGeo<false, 512>::NB_LOG
+                                                                                      : PaGeo<false, 256>::NB_LOG;
+        if (nb_log > pa_nb_log) nb_log = pa_nb_log;
         if (nb_log > log2_slots) nb_log = log2_slots;
         // previous values keep every Put; otherwise a Put overwritten later in its tile is dropped
         // when the key stream is skewed (uniform streams have next to no such Puts: no LDS hash)
@@ -1677,12 +1723,10 @@ hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool
         aj.prevf = d_prev_found;
         aj.stall = c->stall;
         const unsigned dyn = ((ij.nblocks + 1) * 4 + ij.nblocks * 2 + 3) & ~3u;
-        if (want_prev)
-            NRG_LAUNCH(c, "hm_papply", (hm_papply_kernel<true, false>), 1u << nb_log, (PaGeo<true, false>::TPB), dyn, c->stream, aj);
-        else if (wide)
-            NRG_LAUNCH(c, "hm_papply", (hm_papply_kernel<false, true>), 1u << nb_log, (PaGeo<false, true>::TPB), dyn, c->stream, aj);
-        else
-            NRG_LAUNCH(c, "hm_papply", (hm_papply_kernel<false, false>), 1u << nb_log, (PaGeo<false, false>::TPB), dyn, c->stream, aj);
+        if (want_prev) NRG_LAUNCH(c, "hm_papply", (hm_papply_kernel<true, 256>), 1u << nb_log, 256, dyn, c->stream, aj);
+        else if (pa_t == 1024) NRG_LAUNCH(c, "hm_papply", (hm_papply_kernel<false, 1024>), 1u << nb_log, 1024, dyn, c->stream, aj);
+        else if (pa_t == 512) NRG_LAUNCH(c, "hm_papply", (hm_papply_kernel<false, 512>), 1u << nb_log, 512, dyn, c->stream, aj);
+        else NRG_LAUNCH(c, "hm_papply", (hm_papply_kernel<false, 256>), 1u << nb_log, 256, dyn, c->stream, aj);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     } else if (stamp) {
         // ---- stamp round: one launch {index(e) | apply(e-1) | reads(e-1)} ----

@@ -142,7 +142,7 @@ struct nrg_ctx {
     // previous values, skewed streams and rounds of >= 393216 Puts; 2 for every round; 0 never
     // (the older bucket elector instead).
     uint32_t part_mode = 1;
-    uint32_t pa_wide = 1;     // NRG_KNOB_PA_WIDE: 0 never, 1 rounds of >= 2^16 Puts, 2 always
+    uint32_t pa_tpb = 0;      // NRG_KNOB_PA_TPB: partition-round apply workgroup width (0 = by round)
     uint64_t stamp_alloc = 0;  // Puts the put_slot arrays hold (stamp_max <= stamp_alloc)
     uint32_t epoch = 1;  // epoch of the last replay round (1: prefill / before any round)
     uint32_t epoch_limit = 0xFFFFFFF0u;  // renormalise stamps here (NRG_KNOB_EPOCH_LIMIT for tests)

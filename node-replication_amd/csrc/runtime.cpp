@@ -1147,9 +1147,9 @@ extern "C" int nrg_test_set_knob(nrg_ctx* c, int knob, uint64_t v) {
             if (!hm || v > 2) return NRG_E_INVAL;  // 0: partition rounds only where stamp rounds cannot
             c->part_mode = (uint32_t)v;
             return NRG_OK;
-        case NRG_KNOB_PA_WIDE:
-            if (!hm || v > 2) return NRG_E_INVAL;
-            c->pa_wide = (uint32_t)v;
+        case NRG_KNOB_PA_TPB:
+            if (!hm || (v != 0 && v != 256 && v != 512 && v != 1024)) return NRG_E_INVAL;
+            c->pa_tpb = (uint32_t)v;
             return NRG_OK;
         case NRG_KNOB_SMALL_MAX:
             if (!hm || v > 2048) return NRG_E_INVAL;

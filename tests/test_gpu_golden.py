@@ -30,7 +30,7 @@ def test_hashmap_fixture_on_gpu(nrg, name, path):
     ("stamp") and through partition rounds ("part")."""
     d = _load(name)
     W, R, rounds = int(d["W"]), int(d["R"]), int(d["rounds"])
-    knobs = {"part": {"PART": 2}, "wide": {"PART": 2, "PA_WIDE": 2}}.get(path, {})
+    knobs = {"part": {"PART": 2}, "wide": {"PART": 2, "PA_TPB": 1024}}.get(path, {})
     dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, knobs=knobs, log2_slots=16, max_batch=4096)
     dev.hm_prefill_range(int(d["prefill"]), 1)
     for r in range(rounds):

@@ -35,7 +35,8 @@ def _check_state(dev, om):
 
 # knobs of the replay paths: default selection, partition rounds for every round, and the
 # one-launch small rounds (the combiner's) for rounds of up to 2048 Puts
-PATHS = {"default": {}, "part": {"PART": 2}, "wide": {"PART": 2, "PA_WIDE": 2}, "small": {"SMALL_MAX": 2048}}
+PATHS = {"default": {}, "part": {"PART": 2}, "wide": {"PART": 2, "PA_TPB": 1024}, "w512": {"PART": 2, "PA_TPB": 512},
+         "small": {"SMALL_MAX": 2048}}
 
 
 @pytest.mark.parametrize("path", list(PATHS))
@@ -152,10 +153,10 @@ def test_pipelined_rounds_back_to_back(nrg, orc, path):
     the apply of their own round's writes), and must see exactly their own round's state (keys
     created by later rounds invisible, values overwritten later not yet there).
     Knob PART = 2 sends every round through partition rounds instead (their reads ride in the
-    next round's partition launch); PA_WIDE = 2 applies them with 1024-thread workgroups."""
+    next round's partition launch); PA_TPB = 1024 applies them with 1024-thread workgroups."""
     import torch
 
-    knobs = {"part": {"PART": 2}, "wide": {"PART": 2, "PA_WIDE": 2}}.get(path, {})
+    knobs = {"part": {"PART": 2}, "wide": {"PART": 2, "PA_TPB": 1024}}.get(path, {})
     dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, knobs=knobs, log2_slots=17, max_batch=1 << 14, pipeline=1)
     dev.use_torch_stream()
     om = orc.HashMap()
@@ -337,7 +338,8 @@ def _mix64(x):
         return x ^ (x >> np.uint64(31))
 
 
-@pytest.mark.parametrize("knobs", [{}, {"PART": 2}, {"PART": 2, "STALL": 1}, {"PART": 2, "PA_WIDE": 2, "STALL": 1}])
+@pytest.mark.parametrize("knobs", [{}, {"PART": 2}, {"PART": 2, "STALL": 1}, {"PART": 2, "PA_TPB": 1024, "STALL": 1},
+                                   {"PART": 2, "PA_TPB": 512, "STALL": 1}])
 def test_one_bucket_rounds(nrg, orc, knobs):
     """Pipelined rounds whose keys all fall into ONE elector bucket (many chunks, finer parts,
     duplicates across index tiles), with side-slot keys and a Zipf round, against the oracle.
@@ -407,10 +409,10 @@ def _bucket_rounds(nrg, orc, dev, om, rounds):
     assert dev.hm_digest() == om.digest()
 
 
-@pytest.mark.parametrize("knobs", [{"PART": 1}, {"PART": 2}, {"PART": 2, "PA_WIDE": 0}])
+@pytest.mark.parametrize("knobs", [{"PART": 1}, {"PART": 2}, {"PART": 2, "PA_TPB": 256}])
 def test_large_pipelined_rounds(nrg, orc, knobs):
     """Large pipelined rounds (300k-400k Puts: 2048-Put partition tiles, 256 wide buckets, or 1024
-    with PA_WIDE = 0): uniform and Zipf rounds with side-slot keys and a small round in between,
+    with PA_TPB = 256): uniform and Zipf rounds with side-slot keys and a small round in between,
     against the sequential oracle; default round kinds, and every round a partition round
     (PART = 2)."""
     dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, knobs=knobs, log2_slots=22, max_batch=1 << 19,
@@ -426,7 +428,7 @@ def test_large_pipelined_rounds(nrg, orc, knobs):
     _bucket_rounds(nrg, orc, dev, om, rounds)
 
 
-@pytest.mark.parametrize("knobs", [{"PART": 1}, {"PART": 2}, {"PART": 2, "PA_WIDE": 2}])
+@pytest.mark.parametrize("knobs", [{"PART": 1}, {"PART": 2}, {"PART": 2, "PA_TPB": 1024}])
 def test_crowded_bucket_rounds(nrg, orc, knobs):
     """2500 new keys of a round home into the first 4096 slots of the table (one partition bucket,
     taken in several chunks; their claims crowd one region, long probe chains), repeated and
