@@ -628,6 +628,8 @@ struct PApplyJob {
     u64* prev;
     uint8_t* prevf;
     u32 stall;  // NRG_KNOB_STALL (tests)
+    u64* dbg;   // (NRG_KNOB_EXP bit 2, diagnostic) per bucket, 8 words: [0] start [1] counts scanned
+                // [2] first chunk hashed [3] its slots resolved [4] its stores done [5] end [6] chunks
 };
 
 // T threads per workgroup (rounds without previous values: 256, 512 or 1024 over at most 1024,
@@ -756,6 +758,9 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(PREV ? 3 : 4)
     // instead of several.
     const u32 per = j.nb >> 3;
     const u32 nt = j.ntiles, b = j.nb >= 64 ? (blockIdx.x & 7u) * per + (blockIdx.x >> 3) : blockIdx.x;
+#define PA_MARK(K, V) \
+    if (j.dbg && threadIdx.x == 0) j.dbg[(u64)b * 8 + (K)] = (V)
+    PA_MARK(0, wall_clock64());
     u32* s_pre = s_dyn;
     uint16_t* s_off = (uint16_t*)(s_dyn + nt + 1);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -794,6 +799,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(PREV ? 3 : 4)
         s_created = 0;
     }
     __syncthreads();
+    PA_MARK(1, wall_clock64());
+    PA_MARK(6, (total + C - 1) / C);
     u32 created = 0;
     // entry tile map of the chunk at `base`
     auto map_chunk = [&](u32 base, uint16_t* map) {
@@ -870,6 +877,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(PREV ? 3 : 4)
             }
         }
         __syncthreads();
+        if (base == 0) PA_MARK(2, wall_clock64());
         if (nbase < total) {
             test_stall(j.stall & 1, w);  // (tests) slow waves read the next map after the others moved on
             load_chunk(nbase, s_tile[pb ^ 1]);
@@ -887,6 +895,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(PREV ? 3 : 4)
                 kx[r] = x[r].x;
             }
             pa_resolve<PER, false>(j.table, j.shift, j.tmask, kx, on, sl, fr, vx);
+            if (base == 0) PA_MARK(3, wall_clock64());
 #pragma unroll
             for (int r = 0; r < PER; r++) {
                 if (!dec[r]) continue;
@@ -900,24 +909,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(PREV ? 3 : 4)
                 } else if (sl[r] < 0) {
                     atomicOr(&j.ctl->err, ERR_TABLE_FULL);
                 } else {
-#if NRG_PA_FULL
-                    if (fr[r]) {  // claimed: stamps stored by pa_resolve, the 32-B sector completes here
-                        u64x2 kv;
-                        kv.x = x[r].x;
-                        kv.y = x[r].y;
-                        *(u64x2*)&j.table[sl[r]] = kv;
-                    } else {      // found: the whole 32-B slot, its stamps as they are
-                        const u64x2 stp = *(const u64x2*)&j.table[sl[r]].st[0];
-                        Slot z;
-                        z.key = x[r].x;
-                        z.val = x[r].y;
-                        z.st[0] = stp.x;
-                        z.st[1] = stp.y;
-                        j.table[sl[r]] = z;
-                    }
-#else
                     j.table[sl[r]].val = x[r].y;
-#endif
                     created += fr[r];
                 }
             }
@@ -1020,10 +1012,13 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(PREV ? 3 : 4)
             }
         }
         __syncthreads();  // hash entries free; the next iteration builds the map after next in s_tile[pb]
+        if (base == 0) PA_MARK(4, wall_clock64());
     }
     if (created) atomicAdd(&s_created, created);
     __syncthreads();
     if (threadIdx.x == 0 && s_created) atomicAdd(&j.created_acc[b % HM_CREATED_SLOTS], (u64)s_created);
+    PA_MARK(5, wall_clock64());
+#undef PA_MARK
 }
 
 // ---- small rounds: one workgroup, one launch (the flat combiner's batches) ----------------------
@@ -1722,6 +1717,7 @@ hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool
         aj.prev = d_prev;
         aj.prevf = d_prev_found;
         aj.stall = c->stall;
+        aj.dbg = (c->exp & 2) ? c->d_dbg : nullptr;
         const unsigned dyn = ((ij.nblocks + 1) * 4 + ij.nblocks * 2 + 3) & ~3u;
         if (want_prev) NRG_LAUNCH(c, "hm_papply", (hm_papply_kernel<true, 256>), 1u << nb_log, 256, dyn, c->stream, aj);
         else if (pa_t == 1024) NRG_LAUNCH(c, "hm_papply", (hm_papply_kernel<false, 1024>), 1u << nb_log, 1024, dyn, c->stream, aj);

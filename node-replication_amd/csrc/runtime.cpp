@@ -1119,6 +1119,7 @@ extern "C" int nrg_test_set_knob(nrg_ctx* c, int knob, uint64_t v) {
             if (c->cfg.ds_kind == NRG_DS_STACK && (c->exp & 2))
                 words = std::max<uint64_t>(256, (c->cfg.max_batch + 2047) / 2048) * 16;
             if (sy && (c->exp & 2)) words = 3072 * 16;  // synthetic.hip SY_DBG_ROWS
+            if (hm && (c->exp & 2)) words = (uint64_t)HM_BK_MAX * 8;  // partition-round apply buckets
             if (words > c->dbg_words) {
                 if (c->d_dbg) HIPCHK(hipFree(c->d_dbg));
                 c->d_dbg = nullptr;
