@@ -2,9 +2,9 @@
 
 Mirrors the reference's per-thread registration and synchronous execute / execute_mut
 (nr/src/replica.rs:345-356, 404-433, 508-595; nr/src/context.rs:88-194): every call posts up to
-32 ops of one thread into the open batch, and whichever waiting thread takes the combiner lock
-turns the batch into one GPU round of the replica (writes, then reads) without waiting for the
-GPU. Works for the three data structures (NrHashMap, Stack, AbstractDataStructure). ctypes
+32 ops of one thread into the open batch, and the combiner's own thread turns the batch into one
+GPU round of the replica (writes, then reads) without waiting for the GPU. One call at a time per
+token: a call on a token whose previous call is still waiting is refused (NRG_E_INVAL). Works for the three data structures (NrHashMap, Stack, AbstractDataStructure). ctypes
 releases the GIL for the call, so Python threads combine for real.
 """
 import ctypes as C

@@ -105,6 +105,55 @@ def test_combiner_limits(nrg):
     dev.close()
 
 
+def test_combiner_token_in_use(nrg):
+    """One call at a time per token (include/nrgpu.h): two threads driving ONE token. A call that
+    finds its token's previous call still waiting for its round is refused with NRG_E_INVAL,
+    instead of reserving past the batch's buffers; the calls that were accepted all complete,
+    and the final table is the oracle's replay of exactly the accepted Puts."""
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=16, max_batch=4096, max_reads=4096)
+    comb = nrg.Combiner(dev, 2)
+    tok = comb.register()
+    accepted, refused, errors = [[], []], [0, 0], []
+
+    def client(who):
+        rng = np.random.default_rng(40 + who)
+        try:
+            for _ in range(300):
+                keys = rng.integers(0, 3000, 32, dtype=np.uint64)
+                vals = rng.integers(0, 2**63, 32, dtype=np.uint64)
+                try:
+                    comb.put(tok, keys, vals)
+                    accepted[who].append((keys, vals))
+                except nrg.NrgError as e:
+                    if e.code != nrg._lib.NRG_E_INVAL:
+                        raise
+                    refused[who] += 1
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    _run_threads(2, client)
+    assert not errors, errors[0]
+    assert refused[0] + refused[1] > 0  # the two threads did collide on the token
+    comb.close()
+    # each thread's accepted calls are in its own order; the two threads' keys interleave, so
+    # compare the final table only over keys one thread alone wrote
+    only = [set(), set()]
+    for w in (0, 1):
+        for k, _ in accepted[w]:
+            only[w].update(int(x) for x in k)
+    mine = [only[0] - only[1], only[1] - only[0]]
+    keys, vals = dev.hm_dump()
+    table = dict(zip((int(k) for k in keys), (int(v) for v in vals)))
+    for w in (0, 1):
+        last = {}
+        for k, v in accepted[w]:
+            for a, b in zip(k, v):
+                last[int(a)] = int(b)
+        for k in mine[w]:
+            assert table[k] == last[k], (w, k)
+    dev.close()
+
+
 def _read_log(nrg, dev, dtype):
     """The replica's log [head, tail) as records (nrgpu_testing.h nrg_test_ring_read)."""
     import ctypes as C
