@@ -23,12 +23,15 @@
 //   of >= PART_MIN Puts): TWO launches per round and no device atomic per Put.
 //   hm_round_kernel {partition(e) | reads(e-1)}: partition(e) only reads the records; each tile
 //   writes its Puts grouped by the bucket of their key's HOME slot, in log order inside a
-//   bucket, and a [bucket][tile] count word (the table is not touched, so the previous round's
+//   bucket, and a [tile][bucket] count word (the table is not touched, so the previous round's
 //   reads run beside it against a quiescent table, without stamps);
 //   hm_papply_kernel(e): one workgroup per bucket takes the bucket's entries (every tile's run,
 //   tile order = log order) in chunks, finds each key's last writer in an LDS hash, and that
 //   thread finds or claims the key's slot and stores its value: one table line read and written
 //   per distinct key. All Puts of a key share its home bucket, so one workgroup decides each key.
+//   1024-thread workgroups over <= 256 buckets for rounds of >= 64k Puts (256 over <= 1024
+//   below), buckets dealt to XCDs in contiguous ranges, the next chunk's entries loaded while a
+//   chunk resolves. It runs at the memory-side request floor (profiles/r04_papply_phases.txt).
 //   With previous values every Put keeps its entry and one wave walks each chunk in log order:
 //   a Put's previous value is its predecessor's, else the key's value before the chunk, else None.
 #include "internal.hpp"
