@@ -376,7 +376,7 @@ struct SyPartArgs {
     u64 wm;
     u32 ntiles;
     u32* E;
-    u32* cnt_bt;
+    u32* cnt_tb;
     SyHot* hot;
     SyFlags* fl;
     u32 epoch;
@@ -425,9 +425,9 @@ __device__ __forceinline__ void sy_part_role(const SyPartArgs& A, u32 tile, SyPa
     nrg_synth_op* ring = A.ring;
     const u64 ring_mask = A.ring_mask, lo = A.lo, n = A.n, span = A.span, span_m = A.span_m, hr_m = A.hr_m, wm = A.wm;
     const u32 w64 = A.w64;
-    const u32 HR = A.HR, HW = A.HW, NB = A.NB, W = A.W, ntiles = A.ntiles;
+    const u32 HR = A.HR, HW = A.HW, NB = A.NB, W = A.W;
     u32* __restrict__ E = A.E;
-    u32* __restrict__ cnt_bt = A.cnt_bt;
+    u32* __restrict__ cnt_tb = A.cnt_tb;
     SyHot* __restrict__ hot = A.hot;
     auto& s_wcnt = L.wcnt;
     auto& s_u = L.u;
@@ -560,7 +560,7 @@ __device__ __forceinline__ void sy_part_role(const SyPartArgs& A, u32 tile, SyPa
     for (int ww = 0; ww < w; ww++) toff += s_part[ww];
     if (bt < NB) {
         for (int ww = 0; ww < SYA_WAVES; ww++) s_wcnt[ww][bt] = (unsigned short)(s_wcnt[ww][bt] + toff);
-        cnt_bt[(u64)bt * ntiles + tile] = (toff << 16) | tot;
+        cnt_tb[(u64)tile * NB + bt] = (toff << 16) | tot;  // [tile][bucket]: one coalesced row per tile
     }
     if ((u32)tid < HR) {
         SyHot a{0, 0, 0};
@@ -598,7 +598,7 @@ __device__ __forceinline__ void sy_part_role(const SyPartArgs& A, u32 tile, SyPa
 // touches without barriers, then per-word prefixes over the waves place them. A pass with a
 // WriteOnly in it is applied wave by wave instead (values depend on the last SET).
 // (<= 128 VGPRs: two 8-wave workgroups per CU)
-__global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) void sy_bucket_kernel(const u32* __restrict__ E, const u32* __restrict__ cnt_bt,
+__global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) void sy_bucket_kernel(const u32* __restrict__ E, const u32* __restrict__ cnt_tb,
                                                             u32 ntiles, u32 tile_entries, u64* __restrict__ V,
                                                             u64* __restrict__ words, u64 N, u32 HR, u32 W,
                                                             const nrg_synth_op* __restrict__ ring, u64 ring_mask, u64 lo,
@@ -636,7 +636,9 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
     // 4-B seen values this chunk (SyFlags): decided alike by every workgroup
     const bool v32 = fl->big[(epoch - 1) & 1] != epoch - 1 && fl->set_epoch != epoch;
     for (u32 t = tid; t < ntiles; t += SYB_TPB) {
-        const u32 p = cnt_bt[(u64)b * ntiles + t];
+        // [tile][bucket]: a tile's word for bucket b shares its line with the neighbouring buckets,
+        // which run on this XCD (the contiguous runs above), so the line is fetched once per XCD
+        const u32 p = cnt_tb[(u64)t * gridDim.x + b];
         s_off[t] = (unsigned short)(p >> 16);
         s_pre[t] = p & 0xFFFFu;
     }
@@ -1080,7 +1082,7 @@ static hipError_t sy_bucket_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 re
     A.wm = ((1ull << 40) + W - 1) / W;
     A.ntiles = ntiles;
     A.E = x.E[par];
-    A.cnt_bt = x.cnt;
+    A.cnt_tb = x.cnt;
     A.hot = x.hot[par];
     A.fl = x.fl;
     A.epoch = ++c->sy_round;
