@@ -40,8 +40,9 @@ int nrg_test_debug_read(nrg_ctx* ctx, uint64_t* out, uint64_t words);
 #define NRG_KNOB_SY_SORT 7     /* synthetic: 1 = sort-based replay instead of the bucket path      */
 #define NRG_KNOB_PIPELINE 8    /* overrides nrg_config.pipeline                                    */
 #define NRG_KNOB_COMB_SPIN 10   /* combiner (read by nrg_combiner_open): client threads that may spin
-                                   while their round runs (default 0: every waiting client parks
-                                   on a futex)                                                   */
+                                   while their round runs (default: max_threads - 1 when every
+                                   client fits the CPUs the process may use, else 0 -- parked on
+                                   futexes)                                                      */
 #define NRG_KNOB_COMB_DEPTH 11  /* combiner: rounds in flight (1..4; default 2, the 2nd for >=512 ops) */
 #define NRG_KNOB_PA_TPB 16      /* hashmap partition rounds without previous values: apply workgroup
                                    width 256 / 512 / 1024 over <= 1024 / 512 / 256 buckets (0 = 1024

@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 #include <immintrin.h>
 #include <linux/futex.h>
+#include <sched.h>
 #include <sys/syscall.h>
 #include <time.h>
 #include <unistd.h>
@@ -65,6 +66,23 @@ constexpr uint32_t SECOND_MIN = 512;
 // 16 threads x 32 ops: 15.5 / 15.4 / 15.2 / 18.7 M ops/s at 0 / 5 / 10 / 20 us (256 / 256 / 285 /
 // 511 ops per round); 64 threads 35.4 / 35.7 / 37.4 / 38.9 (profiles/r04_combiner.txt)
 constexpr uint32_t GATHER_US = 20;
+
+// CPUs this process may run on at once: its affinity mask, capped by a cgroup v2 CPU quota
+int usable_cpus() {
+    cpu_set_t set;
+    int n = sched_getaffinity(0, sizeof(set), &set) == 0 ? CPU_COUNT(&set) : 1;
+    if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+        char q[32] = {0};
+        unsigned long long period = 0;
+        if (std::fscanf(f, "%31s %llu", q, &period) == 2 && std::strcmp(q, "max") != 0 && period) {
+            const unsigned long long quota = std::strtoull(q, nullptr, 10);
+            const int cap = (int)((quota + period - 1) / period);
+            if (cap > 0 && cap < n) n = cap;
+        }
+        std::fclose(f);
+    }
+    return n;
+}
 
 uint64_t now_ns() {
     timespec t;
@@ -462,11 +480,17 @@ extern "C" int nrg_combiner_open(nrg_ctx* ctx, uint32_t max_threads, nrg_combine
     // hashmap rounds of up to 2048 Puts in one launch (hashmap.hip hm_small_round_kernel)
     m->saved_small = ctx->small_max;
     if (kind == NRG_DS_HASHMAP) ctx->small_max = 2048;
-    // waiting clients park at once by default: spinning ones only burnt CPU. 16 threads ran as
-    // fast parked as with 14 spinning (11.5 vs 11.4 M ops/s) on 1/8 of the CPU time; at 64 threads
-    // spinning took the job's whole cgroup quota and throttled it (22.3 vs 24.5 M ops/s parked;
-    // profiles/r03_combiner_policy.txt)
-    m->spin_cap = ctx->comb_spin >= 0 ? ctx->comb_spin : 0;
+    // Waiting clients park, unless every client fits the CPUs the job may use: then up to
+    // max_threads - 1 of them spin on their round (16 threads on a 16-CPU quota: 19.6 vs 18.0-19.0
+    // M ops/s parked, profiles/r04_combiner.txt F). With more clients than CPUs spinning ones take
+    // the quota from the combiner thread (64 threads: 22.3 vs 24.5 M ops/s parked,
+    // profiles/r03_combiner_policy.txt).
+    if (ctx->comb_spin >= 0) {
+        m->spin_cap = ctx->comb_spin;
+    } else {
+        const int cpus = usable_cpus();
+        m->spin_cap = (int)max_threads <= cpus ? (int)max_threads - 1 : 0;
+    }
     if (ctx->comb_gather >= 0) m->gather_ns = (uint64_t)ctx->comb_gather * 1000ull;
     if (ctx->comb_depth) {  // an explicit depth: no SECOND_MIN rule
         m->depth = std::min<uint64_t>(ctx->comb_depth, NB - 2);
