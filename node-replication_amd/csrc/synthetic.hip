@@ -709,7 +709,14 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
         load_pass(0, s_tile[0]);
     }
     // Software pipelined: the next pass's entries are in flight while this pass is ranked.
+    const u32 late = blockIdx.x >= gridDim.x / 2 ? 1u : 0u;  // the second workgroup on its CU
     for (u32 base = 0, pb = 0; base < total; base += SYB_PASS, pb ^= 1) {
+        // alternate which of a CU's two workgroups the SIMDs prefer, pass by pass: oldest-first
+        // arbitration otherwise favours the first-dispatched one all the way through, and the
+        // second ones ended 3.6 us later (profiles/r04_stack_synth_phases.txt; 55.97-56.83 vs
+        // 56.53-57.18 us per round, profiles/r04_synth_setprio.txt)
+        if ((pb ^ late) & 1u) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
         u32 ent[SYB_PER];
         const unsigned short* cmap = s_tile[pb];
         u64 sv[SYB_PER];
