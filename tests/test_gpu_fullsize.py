@@ -97,8 +97,10 @@ def test_b1_rounds_with_previous_values(nrg, orc, part):
 def test_configs2_per_gpu_round(nrg, orc, prev, part):
     """configs[2]'s per-GPU work: 8 segments x 500k Puts (the all-gathered round of 8 ranks at 50 %
     writes, 4M Puts replayed in place) + this rank's 500k Gets, two pipelined rounds through
-    nrg_hashmap_round_segments_async; with previous values for the rank's own segment (bucket
-    elector) or without (Ok(None), 4M-Put stamp rounds); part = 2: partition rounds either way."""
+    nrg_hashmap_round_segments_async; with previous values for the rank's own segment or without
+    (Ok(None)). Rounds this large take partition rounds by default (part = 0 sends only those with
+    previous values there, the others through 4M-Put stamp rounds); part = 2: partition rounds
+    either way."""
     import torch
 
     G, W, R = 8, 500_000, 500_000
@@ -130,6 +132,32 @@ def test_configs2_per_gpu_round(nrg, orc, prev, part):
     assert dev.hm_digest() == om.digest()
     st = dev.log_state()
     assert st["tail"] == st["ltail"] == st["ctail"] == 2 * G * W
+    dev.close()
+
+
+def test_largest_round(nrg, orc):
+    """The largest round one call replays (HM_MAX_BATCH = 2^23 Puts) + 1M Gets, pipelined twice:
+    4096 partition tiles, the apply's 1024-thread workgroups with their tile prefix at its largest
+    LDS size, 256 buckets of ~32k Puts (8 chunks each), against the oracle."""
+    import torch
+
+    W, R = 1 << 23, 1_000_000
+    dev = _dev(nrg, W, 1)
+    om = _prefilled_oracle(orc)
+    outs = []
+    for r in range(2):
+        k = orc.gen_uniform(W, 0x1A7 + r, KEYS)
+        v = orc.gen_raw(W, 0x2A7 + r)
+        gk = orc.gen_uniform(R, 0x3A7 + r, KEYS)
+        d = dict(p=_cuda(_puts(k, v)), gk=_cuda(gk), gv=_out(R, torch.int64, -1), gf=_out(R, torch.uint8, 7))
+        dev.hm_round_device(d["p"], W, 1, d["gk"], R, d["gv"], d["gf"], None, None)
+        om.replay(k, v)
+        outs.append((d, om.get_batch(gk)))
+    dev.join()
+    for r, (d, (gv, gf)) in enumerate(outs):
+        _check(d["gf"], gf, f"round {r} get found")
+        _check(d["gv"], gv, f"round {r} get vals")
+    assert dev.hm_digest() == om.digest()
     dev.close()
 
 
