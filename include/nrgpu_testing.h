@@ -60,7 +60,7 @@ int nrg_test_debug_read(nrg_ctx* ctx, uint64_t* out, uint64_t words);
                                    rounds above STAMP_MAX)                                        */
 #define NRG_KNOB_STALL 14       /* tests: 1 = odd waves sleep ~30 us where a workgroup next reuses LDS
                                    another wave may still read (synthetic bucket pass, hashmap
-                                   elector and partition-round apply chunks, stack queries/table);
+                                   partition-round apply chunks, stack queries/table);
                                    2 (+1) = synthetic only, also drop the barrier that guards the
                                    bucket pass's tile map (diagnostic: results WRONG)            */
 int nrg_test_set_knob(nrg_ctx* ctx, int knob, uint64_t value);
@@ -74,8 +74,8 @@ int nrg_test_set_knob(nrg_ctx* ctx, int knob, uint64_t value);
  * blocks until all ranks joined, and each collective blocks its thread until its peers posted
  * theirs. Tests check both shapes against the oracle. 0 switches back to RCCL for later groups. */
 int nrg_test_loopback_collectives(int on);
-// Hashmap: 1 when the sampled key skew sends rounds to the bucket elector (hashmap.hip
-// skew_sample), 0 when they take the one-launch stamp rounds.
+// Hashmap: 1 when the sampled key skew sends rounds to partition rounds (hashmap.hip
+// skew_sample), 0 when the round size decides.
 int nrg_test_hm_skewed(nrg_ctx* ctx, int* out);
 #ifdef __cplusplus
 }

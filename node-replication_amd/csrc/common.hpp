@@ -19,14 +19,14 @@ constexpr u32 ERR_TABLE_FULL = 1u;
 constexpr u32 ERR_CAPACITY = 4u;
 constexpr u32 ERR_GROUP = 8u;  // a replica group's ranks disagreed on a round's segment lengths (group.cpp)
 
-// Counters of keys created by replay rounds (elector blocks add to slot blk % HM_CREATED_SLOTS).
+// Counters of keys created by replay rounds (claiming blocks add to slot blk % HM_CREATED_SLOTS).
 constexpr u64 HM_CREATED_SLOTS = 8192;
 // Counters of Puts combined inside their index block (key skew statistic, hm_dup_sample_kernel).
 constexpr u64 HM_DUP_SLOTS = 64;
 // Slot buckets of a partition round (hashmap.hip part_role / hm_papply_kernel): at most this many.
 constexpr u32 HM_BK_MAX = 1024;
-// Largest hashmap replay chunk: keeps the elector's per-tile LDS tables (one u32 + one u16
-// per index tile of >= 1024 Puts) and 16-bit tile offsets within bounds.
+// Largest hashmap replay chunk: keeps the partition apply's per-tile LDS prefix (one u32 + one
+// u16 per tile of 2048 Puts) and 16-bit tile offsets within bounds.
 constexpr u64 HM_MAX_BATCH = 1ull << 23;
 
 // splitmix64 finaliser — identical constants to oracle/nr_oracle.c (orc_mix64) so that

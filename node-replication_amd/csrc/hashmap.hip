@@ -1029,15 +1029,16 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(PREV ? 3 : 4)
 // hashed by key in LDS (how many, the last one); one thread per distinct key finds or claims
 // its slot, answers the previous values of the key's Puts in log order (the slot's value before
 // the round for the first; nr/examples/hashmap.rs:46-50) and stores the last value. No deferred
-// half and no device atomics per Put: the combiner's index + elector + reads launches (about
-// 20 us of GPU time for a few hundred ops) become one.
+// half and no device atomics per Put: round 2's index + elector + reads launches for the
+// combiner's batches (about 20 us of GPU time for a few hundred ops) became one.
 // The Gets do not wait for the Puts: a Get of a key the round Puts is answered from the LDS hash
 // (the key's last value), and for any other key the round changes nothing the Get reads -- a
 // present key's probe chain holds no empty slot, so claims (which fill empty slots) cannot
 // change where its chain ends, and only Put keys' values are stored. So every Get's table probe
 // is issued with the Put records, and resolves while the Puts claim and store.
 // Runs with no other round in flight (the caller flushes first). Keys present in the table are
-// present (quiescent: no claim in flight); fresh claims get epoch-1 stamps, as the elector's.
+// present (quiescent: no claim in flight); fresh claims get epoch-1 stamps, as the partition
+// apply's.
 constexpr int SM_TPB = 1024;
 constexpr u32 SM_W = 2048, SM_R = 8192, SM_HT = 4096;  // SM_HT: LDS hash entries (+1: the side key)
 struct SmallJob {
@@ -1495,7 +1496,7 @@ static hipError_t launch(nrg_ctx* c, Launch& L) {
     u32 blocks = nix + L.aj.nblocks + L.rj.nblocks;
     if (blocks == 0) return hipSuccess;
     // a pending skew sample, or the error copy of a launch that ends a round (no index role:
-    // earlier kernels of the round, the elector's claims included, have latched their errors)
+    // earlier kernels of the round, the partition apply's claims included, have latched their errors)
     const bool err_here = c->err_out && nix == 0;
     if (c->sample_seq || err_here) {  // the launch's last block
         L.rj.s_acc = c->d_dup + ((c->dup_seq - 1) & 1) * HM_DUP_SLOTS;  // the window just ended
@@ -1597,10 +1598,10 @@ void hm_free(nrg_ctx* c) {
 
 // Every dup_every rounds: read the previous sample (if it has landed) and decide whether the
 // stream is skewed, then sample the rounds since. Skewed: more than 1/64 of the Puts were
-// combined inside their index block (Zipf 0.99 is far above, uniform keys far below). Stamp
-// rounds then cost one same-address atomic per block for each hot key, and the bucket rounds
-// (no atomics per Put) are faster at every size; for uniform keys the stamp rounds are faster
-// at every size (50 % writes: 62.8 vs 79.6 us; Zipf 0.99 at 10 % writes: 47.7 vs 32.8 us).
+// combined inside their index block or tile (Zipf 0.99 is far above, uniform keys far below).
+// Stamp rounds then cost one same-address atomic per block for each hot key, and partition
+// rounds (no atomics per Put) are faster at every size (Zipf 0.99 at 10 % / 50 % writes: 31.9 /
+// 55.3 us, profiles/r04_part_sweep.txt); uniform streams below PART_MIN take stamp rounds.
 static hipError_t skew_sample(nrg_ctx* c) {
     if (c->dup_seq && c->h_dup[0] == c->dup_seq && c->dup_puts_sampled)
         c->skewed = c->h_dup[1] * 64 > c->dup_puts_sampled;

@@ -135,12 +135,12 @@ struct nrg_ctx {
     uint64_t* d_created = nullptr;  // [HM_CREATED_SLOTS] keys created by replay rounds
     void* d_bk_ent = nullptr;       // partition rounds: [tiles][tile] 16-B {key, value} entries
     uint32_t* d_bk_idx = nullptr;   // partition rounds with previous values: [tiles][tile] round offset
-    uint32_t* d_bk_cnt = nullptr;   // [bucket][index tiles] offset << 16 | count
+    uint32_t* d_bk_cnt = nullptr;   // [index tiles][bucket] offset << 16 | count
     // Stamp rounds (<= stamp_max Puts, no previous values): per-Put slot ids by epoch parity.
     uint64_t stamp_max = 0;
     // Partition rounds (hashmap.hip part_role + hm_papply_kernel), NRG_KNOB_PART: 1 (default) for
-    // previous values, skewed streams and rounds of >= 393216 Puts; 2 for every round; 0 never
-    // (the older bucket elector instead).
+    // previous values, skewed streams and rounds of >= 393216 Puts; 2 for every round; 0 only
+    // where a stamp round cannot (previous values, skew).
     uint32_t part_mode = 1;
     uint32_t pa_tpb = 0;      // NRG_KNOB_PA_TPB: partition-round apply workgroup width (0 = by round)
     uint64_t stamp_alloc = 0;  // Puts the put_slot arrays hold (stamp_max <= stamp_alloc)
@@ -148,7 +148,7 @@ struct nrg_ctx {
     uint32_t epoch_limit = 0xFFFFFFF0u;  // renormalise stamps here (NRG_KNOB_EPOCH_LIMIT for tests)
     uint32_t* d_put_slot[2] = {nullptr, nullptr};
     // Key skew (hm_dup_sample_kernel): Puts combined inside their index block, sampled every
-    // dup_every rounds into mapped host memory; a skewed stream takes the bucket rounds.
+    // dup_every rounds into mapped host memory; a skewed stream takes partition rounds.
     uint64_t* d_dup = nullptr;            // [HM_DUP_SLOTS]
     void* d_pt = nullptr;                 // partition.hip tile counts / offsets
     uint64_t pt_words = 0;

@@ -336,7 +336,7 @@ int nrg_open(int dev, const nrg_config* cfg_in, nrg_ctx** out) {
     const uint64_t mb = cf.max_batch;
     if (cf.ds_kind == NRG_DS_HASHMAP) {
         // slot ids are < 2^30 (entry ids carry two flag values above them, hashmap.hip);
-        // replay chunks are bounded by the elector's per-tile LDS tables (HM_MAX_BATCH)
+        // replay chunks are bounded by the partition rounds' 16-bit tile offsets (HM_MAX_BATCH)
         if (cf.log2_slots < 4 || cf.log2_slots > 30 || mb > HM_MAX_BATCH) { nrg_close(c); return NRG_E_INVAL; }
         c->slots = 1ull << cf.log2_slots;
         c->slot_shift = 64 - cf.log2_slots;
@@ -345,9 +345,9 @@ int nrg_open(int dev, const nrg_config* cfg_in, nrg_ctx** out) {
         OPEN_CHK(hipMalloc(&c->d_created, HM_CREATED_SLOTS * sizeof(uint64_t)));
         OPEN_CHK(hipMemsetAsync(c->d_created, 0, HM_CREATED_SLOTS * sizeof(uint64_t), c->stream));
         // rounds without previous values replay in one launch (stamp rounds) unless the key
-        // stream is skewed (hashmap.hip skew_sample); skewed and previous-value rounds take the
-        // bucket elector
-        c->stamp_max = HM_MAX_BATCH;  // every size; skewed streams switch to bucket rounds
+        // stream is skewed (hashmap.hip skew_sample) or the round is large (PART_MIN); skewed,
+        // large and previous-value rounds take partition rounds
+        c->stamp_max = HM_MAX_BATCH;  // (NRG_KNOB_STAMP_MAX lowers it for tests)
         OPEN_CHK(hm_alloc(c, mb));       // clamps stamp_max to max_batch (the put_slot arrays' size)
         c->stamp_alloc = c->stamp_max;
         c->pipeline = cf.pipeline != 0;

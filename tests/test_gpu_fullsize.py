@@ -64,8 +64,8 @@ def _check(got, want, what):
 
 @pytest.mark.parametrize("part", [0, 2])
 def test_b1_rounds_with_previous_values(nrg, orc, part):
-    """configs[1] with HashMap::insert's previous values: 3 pipelined 100k + 900k rounds (bucket
-    elector, or partition rounds)."""
+    """configs[1] with HashMap::insert's previous values: 3 pipelined 100k + 900k rounds (partition
+    rounds with the log-order walk; part = 2 changes nothing here but is kept as the forced path)."""
     import torch
 
     dev = _dev(nrg, 1 << 20, part)

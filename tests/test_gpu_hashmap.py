@@ -341,7 +341,7 @@ def _mix64(x):
 @pytest.mark.parametrize("knobs", [{}, {"PART": 2}, {"PART": 2, "STALL": 1}, {"PART": 2, "PA_TPB": 1024, "STALL": 1},
                                    {"PART": 2, "PA_TPB": 512, "STALL": 1}])
 def test_one_bucket_rounds(nrg, orc, knobs):
-    """Pipelined rounds whose keys all fall into ONE elector bucket (many chunks, finer parts,
+    """Pipelined rounds whose keys all fall into ONE slot bucket (many chunks, finer parts,
     duplicates across index tiles), with side-slot keys and a Zipf round, against the oracle.
     Also as partition rounds (PART = 2: one apply workgroup takes the bucket in many chunks), and
     with odd waves stalled where a chunk's tile map is read (STALL = 1) before the next chunk
@@ -480,7 +480,7 @@ def test_b1_full_size_rounds(nrg, orc):
 
 def test_epoch_renormalisation(nrg, orc):
     """Replay epochs are 32-bit; before they wrap every stamp is renormalised to epoch 1. A limit
-    of 6 (knob EPOCH_LIMIT) renormalises every few rounds: pipelined stamp and bucket rounds with
+    of 6 (knob EPOCH_LIMIT) renormalises every few rounds: pipelined stamp and partition rounds with
     new keys, overwrites and side-slot keys across several renormalisations, against the oracle."""
     import torch
 
@@ -492,7 +492,7 @@ def test_epoch_renormalisation(nrg, orc):
     om.prefill_range(500, 1)
     outs, want = [], []
     for r in range(17):
-        W = 3000 if r % 3 else (7000 if r % 2 else 6000)  # > STAMP_MAX: bucket rounds
+        W = 3000 if r % 3 else (7000 if r % 2 else 6000)  # > STAMP_MAX: partition rounds
         keys = orc.gen_uniform(W, 900 + r, 4000 + 150 * r)
         keys[::113] = EMPTY
         vals = orc.gen_raw(W, 950 + r)
@@ -518,7 +518,7 @@ def test_epoch_renormalisation(nrg, orc):
 @pytest.mark.parametrize("part", [0, 2])
 def test_skew_switches_round_kind(nrg, orc, part):
     """Stamp rounds (one launch, one stamp atomic per distinct key per block) are faster for
-    uniform keys, bucket rounds (no atomics per Put) for skewed ones; the replica switches from
+    uniform keys, partition rounds (no atomics per Put) for skewed ones; the replica switches from
     the sampled share of Puts combined inside their block (every 2 rounds here). Uniform rounds,
     then Zipf(0.99), then uniform again, pipelined: every Get and the final state bit-exact
     across both switches, and the switches happen. part = 2: partition rounds, which drop the
