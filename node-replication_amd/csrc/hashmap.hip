@@ -40,6 +40,21 @@ namespace nrg {
 
 typedef u64 u64x2 __attribute__((ext_vector_type(2)));
 
+// Streaming (nt) stores for the streamed outputs (log copy, read responses) of partition-round and
+// reads-only launches: plain stores leave them dirty in the XCD's L2 for the kernel-end write-back
+// after the last workgroup; streamed, they drain during the kernel. N = 8 per-GPU round 78.7 vs
+// 80.5 us, configs[2] 256.9 vs 263.4; stamp rounds keep plain stores (B1 34.5-34.7 plain vs
+// 34.7-35.0 streamed; profiles/r04_nt_stores.txt). NRG_KNOB_EXP bit 6 = plain everywhere (A/B).
+template <typename T>
+__device__ __forceinline__ void st_out(T* p, T v, bool plain) {
+    if (plain) *p = v;
+    else __builtin_nontemporal_store(v, p);
+}
+__device__ __forceinline__ void st_rec(nrg_put* p, const nrg_put& r, bool plain) {
+    if (plain) *p = r;
+    else __builtin_nontemporal_store(u64x2{r.key, r.val}, (u64x2*)p);
+}
+
 constexpr int TPB = 256;
 constexpr u32 SIDE_ID = 0x7FFFFFFFu;    // slot id standing for the side slot (slot ids are < 2^30)
 constexpr u32 FULL_SLOT = 0xFFFFFFFFu;  // no slot could be claimed (table full)
@@ -65,6 +80,7 @@ struct IndexJob {
     u32 exp;       // diagnostic knobs (NRG_EXP; results are wrong when set): 1 no dedup, 2 no
                    // probe (every key new), 4 no ranking/entries
     u64* dup_acc;  // [HM_DUP_SLOTS] Puts overwritten inside their block (key skew statistic)
+    bool plain;    // plain stores for the log copy (st_out)
 };
 struct ReadJob {
     const u64* keys;
@@ -84,6 +100,7 @@ struct ReadJob {
     u64 s_seq;
     // the replica's error latch, copied to (mapped) e_out and cleared by the same block (nrg_combiner)
     u32* e_out;
+    bool plain;  // plain stores for the responses (st_out)
 };
 
 
@@ -162,7 +179,7 @@ __device__ __forceinline__ void part_role(const IndexJob& j, u32 blk, u32 shift,
 #pragma unroll
     for (int q = 0; q < K1; q++) {
         const u64 i = base + (u64)(w * WT + q * 64 + lane);
-        if (valid[q] && j.ring_out) j.ring_out[(j.rec.lo + i) & j.rec.mask] = rec[q];
+        if (valid[q] && j.ring_out) st_rec(&j.ring_out[(j.rec.lo + i) & j.rec.mask], rec[q], j.plain);
         bkt[q] = rec[q].key == EMPTY_KEY ? 0u : (u32)(table_home(rec[q].key, shift) >> j.bk_shift);
     }
     bool emit[K1];
@@ -308,6 +325,7 @@ struct StampJob {
     // diagnostic ablations of a round launch (NRG_KNOB_EXP >> 20; RESULTS WRONG, timing only):
     // 1 no stamp atomics, 2 no apply role, 4 no index role, 8 no read role
     u32 exp;
+    bool plain;  // plain stores for the log copy (st_out)
 };
 struct ApplyJob {
     RecSrc rec;
@@ -377,7 +395,7 @@ __device__ __forceinline__ void stamp_index_role(const StampJob& j, u32 blk, Slo
 #pragma unroll
     for (int q = 0; q < K1; q++) {
         const u64 i = base + (u64)q * TPB + threadIdx.x;
-        if (i < j.n && j.ring_out) j.ring_out[(j.rec.lo + i) & j.rec.mask] = rec[q];
+        if (i < j.n && j.ring_out) st_rec(&j.ring_out[(j.rec.lo + i) & j.rec.mask], rec[q], j.plain);
         home[q] = table_home(rec[q].key, shift);
         key0[q] = i < j.n && rec[q].key != EMPTY_KEY ? table[home[q]].key : EMPTY_KEY;
     }
@@ -547,8 +565,8 @@ __device__ __forceinline__ void read_role(const ReadJob& j, u32 blk, const Slot*
         }
         if (!f) v = 0;
         const u64 q = q0 + (u64)r * TPB;
-        j.vals[q] = v;
-        j.found[q] = f ? 1 : 0;
+        st_out(&j.vals[q], v, j.plain);
+        st_out(&j.found[q], (uint8_t)(f ? 1 : 0), j.plain);
     }
 }
 
@@ -1490,6 +1508,7 @@ static hipError_t launch(nrg_ctx* c, Launch& L) {
     L.rj.nblocks = (u32)((L.rj.R + TPB * RPT - 1) / (TPB * RPT));
     L.sj.exp = c->exp >> 20;
     const u32 nix = L.ix == IX_STAMP ? L.sj.nblocks : L.ij.nblocks;
+    L.ij.plain = L.sj.plain = L.rj.plain = ((c->exp >> 6) & 1) || (L.ix == IX_STAMP && nix);
     // reads beside a bucket or partition pass (which only read the table, or not even that), or
     // alone, with no stamp round's apply riding along: the table is quiescent
     L.rj.quiet = (L.ix != IX_STAMP || nix == 0) && L.aj.nblocks == 0;

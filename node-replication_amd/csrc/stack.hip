@@ -192,7 +192,24 @@ struct StPass {
     u32* resp;
     uint8_t* some;
     u32 stall;  // NRG_KNOB_STALL (tests)
+    u32 plain;  // (A/B, NRG_KNOB_EXP bit 6) plain stores instead of streaming ones for the tile outputs
 };
+
+// Streaming (nt) stores for outputs no later work of this launch reads (the log copy, the
+// responses): with plain stores they stay dirty in the XCD's L2 until the kernel-end write-back,
+// which then runs after the last workgroup (~13 MB per 1M-op round); streamed, they drain while
+// the look-back waits. 15.35-15.50 -> 14.88-14.90 us per round on one box, 15.37-15.42 -> 15.14-15.24
+// on another (profiles/r04_nt_stores.txt). NRG_KNOB_EXP bit 6 = plain stores (A/B).
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void nt_store4(uint4* p, uint4 v) {
+    const u32x4_t t = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(t, (u32x4_t*)p);
+}
+__device__ __forceinline__ void nt_store2(uint2* p, uint2 v) {
+    const u32x2_t t = {v.x, v.y};
+    __builtin_nontemporal_store(t, (u32x2_t*)p);
+}
 
 __device__ __forceinline__ void wave_sync() {  // LDS written by other lanes of this wave
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -411,8 +428,13 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
     if (copy_later) {  // Log::append's copy of the wave's records
         if (ring_run) {
             uint4* w4 = (uint4*)(ring + rw0);
+            if (!A.plain) {
 #pragma unroll
-            for (int i = 0; i < SW_OPS / 2; i++) w4[64 * i + lane] = x[i];
+                for (int i = 0; i < SW_OPS / 2; i++) nt_store4(&w4[64 * i + lane], x[i]);
+            } else {
+#pragma unroll
+                for (int i = 0; i < SW_OPS / 2; i++) w4[64 * i + lane] = x[i];
+            }
         } else {
 #pragma unroll
             for (int i = 0; i < SW_OPS / 2; i++) {
@@ -430,9 +452,15 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
         u32* rp = resp + (g0 - resp_lo);
         uint8_t* sp = some + (g0 - resp_lo);
         if (in && !((uintptr_t)rp & 15) && !((uintptr_t)sp & (SW_OPS >= 16 ? 15 : 7))) {
+            if (!A.plain) {
 #pragma unroll
-            for (int j = 0; j < SW_OPS / 4; j++)
-                ((uint4*)rp)[j] = uint4{rt[4 * j], rt[4 * j + 1], rt[4 * j + 2], rt[4 * j + 3]};
+                for (int j = 0; j < SW_OPS / 4; j++)
+                    nt_store4(&((uint4*)rp)[j], uint4{rt[4 * j], rt[4 * j + 1], rt[4 * j + 2], rt[4 * j + 3]});
+            } else {
+#pragma unroll
+                for (int j = 0; j < SW_OPS / 4; j++)
+                    ((uint4*)rp)[j] = uint4{rt[4 * j], rt[4 * j + 1], rt[4 * j + 2], rt[4 * j + 3]};
+            }
             if constexpr (SW_OPS >= 16) {
 #pragma unroll
                 for (int j = 0; j < SW_OPS / 16; j++) {
@@ -443,8 +471,10 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
                     ((uint4*)sp)[j] = b;
                 }
             } else {  // 8 ops per lane: one 8-B store
-                *(uint2*)sp = uint2{((smask & 15u) * 0x204081u) & 0x01010101u,
-                                    (((smask >> 4) & 15u) * 0x204081u) & 0x01010101u};
+                const uint2 b = uint2{((smask & 15u) * 0x204081u) & 0x01010101u,
+                                      (((smask >> 4) & 15u) * 0x204081u) & 0x01010101u};
+                if (!A.plain) nt_store2((uint2*)sp, b);
+                else *(uint2*)sp = b;
             }
         } else if (resp) {
 #pragma unroll
@@ -826,6 +856,7 @@ static StPass st_pass(nrg_ctx* c, u32 par) {
     StPass s{};
     s.par = par;
     s.stall = c->stall;
+    s.plain = (c->exp >> 6) & 1;
     s.ring = (nrg_stack_op*)c->d_ring;
     s.ring_mask = c->log_size - 1;
     // descriptors: [32 u64 unused] [parity][max tiles] u64; zero at open, and each chunk's finish

@@ -18,6 +18,26 @@
 namespace nrg {
 
 constexpr u32 SETBIT = 0x80000000u;
+
+// Streaming (nt) stores for the streamed outputs (log copy, touch records, seen values,
+// responses), an A/B variant (NRG_KNOB_EXP bit 6): they drain during the kernel instead of in the
+// kernel-end L2 write-back, which pays on the stack and the hashmap's partition rounds, but not
+// here (56.6-56.9 vs 56.1-56.6 us per round plain; profiles/r04_nt_stores.txt): plain by default.
+typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
+template <typename T>
+__device__ __forceinline__ void st_out(T* p, T v, bool plain) {
+    if (plain) *p = v;
+    else __builtin_nontemporal_store(v, p);
+}
+__device__ __forceinline__ void st_op(nrg_synth_op* p, const nrg_synth_op& o, bool plain) {
+    if (plain) {
+        *p = o;
+        return;
+    }
+    const u64x2_t a = {o.tid, o.r1}, b = {o.r2, o.op};
+    __builtin_nontemporal_store(a, (u64x2_t*)p);
+    __builtin_nontemporal_store(b, (u64x2_t*)p + 1);
+}
 constexpr int MS_TPB = 256;
 constexpr int MS_ITEMS = 8;
 constexpr int MS_TILE = MS_TPB * MS_ITEMS;
@@ -381,6 +401,7 @@ struct SyPartArgs {
     SyFlags* fl;
     u32 epoch;
     u64* dbg;  // NRG_EXP & 2 (diagnostic): phase stamps of tile t in row SY_DBG_PART + t
+    bool plain;  // plain stores for the log copy and touch records (default; st_out)
 };
 // rows of the diagnostic stamp buffer: bucket b in row b, partition tile t in SY_DBG_PART + t,
 // sum workgroup k in SY_DBG_SUM + k (tiles beyond 1024 are not stamped)
@@ -398,6 +419,7 @@ struct SySumArgs {
     u64* words;
     const u32* v32;  // the chunk's seen-value width flag (SyFlags::v32[par]): 1 = 4-B seen values
     u64* dbg;
+    bool plain;  // plain stores for the responses (default; st_out)
 };
 
 // LDS of a partition workgroup: ranking tables and staged words, then (same bytes) the tile's
@@ -463,7 +485,7 @@ __device__ __forceinline__ void sy_part_role(const SyPartArgs& A, u32 tile, SyPa
         if (orr + SYP_PD < SYA_OROUNDS && op0 + opw + (orr + SYP_PD) * 64 < n)
             nx[orr % SYP_PD] = src ? src[op0 + opw + (orr + SYP_PD) * 64]
                                    : ring[(lo + op0 + opw + (orr + SYP_PD) * 64) & ring_mask];
-        if (src && valid) ring[(lo + op0 + opw + orr * 64) & ring_mask] = o;
+        if (src && valid) st_op(&ring[(lo + op0 + opw + orr * 64) & ring_mask], o, A.plain);
         const bool set = valid && o.op == NRG_SYNTH_WRITE_ONLY;
         if (set && (o.tid >> 31)) A.fl->set_epoch = A.epoch;  // this chunk's seen values may pass 2^32
         // hot touches (r2 + j) % HR, j < HW, skipped when r2 + HW wraps; ordered (lane, j)
@@ -584,7 +606,7 @@ __device__ __forceinline__ void sy_part_role(const SyPartArgs& A, u32 tile, SyPa
     SYP_MARK(3);
     const u32 nops = (u32)(n - op0 < SYA_OPS ? n - op0 : SYA_OPS);
     u32* Et = E + (u64)tile * (SYA_OPS * CW);
-    for (u32 i = tid; i < nops * CW; i += SYA_TPB) Et[i] = s_u.stage[i];
+    for (u32 i = tid; i < nops * CW; i += SYA_TPB) st_out(&Et[i], s_u.stage[i], A.plain);
     if (dbg) {
         dbg[4] = wall_clock64();
         dbg[9] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
@@ -603,7 +625,7 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
                                                             u64* __restrict__ words, u64 N, u32 HR, u32 W,
                                                             const nrg_synth_op* __restrict__ ring, u64 ring_mask, u64 lo,
                                                             SyFlags* __restrict__ fl, u32 epoch, u32 par,
-                                                            u64* __restrict__ dbg, u32 stall) {
+                                                            u64* __restrict__ dbg, u32 stall, bool plain) {
     // dbg (NRG_EXP & 2, diagnostic): per block, thread 0's wall clock at the phase edges
     // [0] start [1] prologue loaded [2] scanned, then summed over passes [3] tile map [4] gather
     // [5] rank + place [6] stores, [7] end, [8] passes
@@ -818,14 +840,14 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
             for (int q = 0; q < SYB_PER; q++)
                 if (base + (u32)w * (SYB_PER * 64) + q * 64 + lane < total) {
                     const u32 gp = gpos_of(base, cmap, base + (u32)w * (SYB_PER * 64) + q * 64 + lane);
-                    if (gp < vcap) ((u32*)V)[gp] = (u32)sv[q];
+                    if (gp < vcap) st_out(&((u32*)V)[gp], (u32)sv[q], plain);
                 }
         } else {
 #pragma unroll
             for (int q = 0; q < SYB_PER; q++)
                 if (base + (u32)w * (SYB_PER * 64) + q * 64 + lane < total) {
                     const u32 gp = gpos_of(base, cmap, base + (u32)w * (SYB_PER * 64) + q * 64 + lane);
-                    if (gp < vcap) V[gp] = sv[q];
+                    if (gp < vcap) st_out(&V[gp], sv[q], plain);
                 }
         }
         // the stores above read this pass's tile map (cmap); the next pass's map is built into
@@ -914,8 +936,8 @@ __device__ __forceinline__ void sy_sum_role(const SySumArgs& S, u32 blk, u64* s_
         for (u32 i = tid; i < nops; i += SYC_TPB) {
             const u64 g = lo + op0 + i;
             if (g >= resp_lo && g < resp_hi) {
-                resp[g - resp_lo] = s_sum[i];
-                if (some) some[g - resp_lo] = 1;
+                st_out(&resp[g - resp_lo], s_sum[i], S.plain);
+                if (some) st_out(&some[g - resp_lo], (uint8_t)1, S.plain);
             }
         }
     }
@@ -1035,6 +1057,7 @@ static SySumArgs sy_sum_args(nrg_ctx* c, const SyDeferred& d) {
     S.words = c->d_words;
     S.v32 = &x.fl->v32[d.par];
     S.dbg = (c->exp & 2) ? c->d_dbg : nullptr;
+    S.plain = !((c->exp >> 6) & 1);
     return S;
 }
 
@@ -1094,6 +1117,7 @@ static hipError_t sy_bucket_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 re
     A.fl = x.fl;
     A.epoch = ++c->sy_round;
     A.dbg = (c->exp & 2) ? c->d_dbg : nullptr;
+    A.plain = !((c->exp >> 6) & 1);
     SySumArgs S{};
     if (c->sy_pend.valid) S = sy_sum_args(c, c->sy_pend);
     c->sy_pend.valid = false;
@@ -1103,7 +1127,7 @@ static hipError_t sy_bucket_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 re
     const size_t dyn = (size_t)(ntiles + 1) * 4 + (size_t)ntiles * 2;
     sy_bucket_kernel<<<NB, SYB_TPB, dyn, st>>>(x.E[par], x.cnt, ntiles, SYA_OPS * CW, x.V, c->d_words, cf.synth_n, HR,
                                                W, A.ring, A.ring_mask, lo, x.fl, A.epoch, par,
-                                               (c->exp & 2) ? c->d_dbg : nullptr, c->stall);
+                                               (c->exp & 2) ? c->d_dbg : nullptr, c->stall, !((c->exp >> 6) & 1));
     timer_end(c, "sy_replay");
     if ((e = hipGetLastError()) != hipSuccess) return e;
     // this chunk's sums: in the next chunk's partition launch (pipeline = 1) or now
