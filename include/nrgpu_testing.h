@@ -34,11 +34,12 @@ int nrg_test_debug_read(nrg_ctx* ctx, uint64_t* out, uint64_t words);
 #define NRG_KNOB_EPOCH_LIMIT 3 /* hashmap: renormalise stamps when the round epoch reaches this    */
 #define NRG_KNOB_K1 4          /* hashmap: Puts per stamp-round index thread (0: by round size;
                                   1, 2 or 4)                                                      */
-#define NRG_KNOB_EXP 6         /* diagnostic bits: phase timestamps (stack/synthetic 2), 0x40 flips
-                                  the streamed outputs' stores (stack and hashmap partition rounds:
-                                  plain instead of streaming; synthetic: streaming instead of plain),
-                                  and stamp-round ablations that make RESULTS WRONG (0xF00000: no
-                                  stamp atomics, no apply, no index, no reads) -- measurement only */
+#define NRG_KNOB_EXP 6         /* diagnostic bits: phase timestamps (stack/synthetic 2); streamed
+                                  outputs' stores: 0x40 stack and hashmap partition rounds plain
+                                  instead of streaming, synthetic log copy streaming (0x80 touch
+                                  records, 0x100 seen values, 0x200 responses); and stamp-round
+                                  ablations that make RESULTS WRONG (0xF00000: no stamp atomics, no
+                                  apply, no index, no reads) -- measurement only                   */
 #define NRG_KNOB_SY_SORT 7     /* synthetic: 1 = sort-based replay instead of the bucket path      */
 #define NRG_KNOB_PIPELINE 8    /* overrides nrg_config.pipeline                                    */
 #define NRG_KNOB_COMB_SPIN 10   /* combiner (read by nrg_combiner_open): client threads that may spin

@@ -20,7 +20,8 @@ namespace nrg {
 constexpr u32 SETBIT = 0x80000000u;
 
 // Streaming (nt) stores for the streamed outputs (log copy, touch records, seen values,
-// responses), an A/B variant (NRG_KNOB_EXP bit 6): they drain during the kernel instead of in the
+// responses), an A/B variant (NRG_KNOB_EXP bits 6 / 7 / 8 / 9 for the log copy / touch records /
+// seen values / responses): they drain during the kernel instead of in the
 // kernel-end L2 write-back, which pays on the stack and the hashmap's partition rounds, but not
 // here (56.6-56.9 vs 56.1-56.6 us per round plain; profiles/r04_nt_stores.txt): plain by default.
 typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
@@ -401,7 +402,8 @@ struct SyPartArgs {
     SyFlags* fl;
     u32 epoch;
     u64* dbg;  // NRG_EXP & 2 (diagnostic): phase stamps of tile t in row SY_DBG_PART + t
-    bool plain;  // plain stores for the log copy and touch records (default; st_out)
+    bool plain;    // plain stores for the log copy (default; st_out)
+    bool plain_e;  // plain stores for the touch records (default)
 };
 // rows of the diagnostic stamp buffer: bucket b in row b, partition tile t in SY_DBG_PART + t,
 // sum workgroup k in SY_DBG_SUM + k (tiles beyond 1024 are not stamped)
@@ -606,7 +608,7 @@ __device__ __forceinline__ void sy_part_role(const SyPartArgs& A, u32 tile, SyPa
     SYP_MARK(3);
     const u32 nops = (u32)(n - op0 < SYA_OPS ? n - op0 : SYA_OPS);
     u32* Et = E + (u64)tile * (SYA_OPS * CW);
-    for (u32 i = tid; i < nops * CW; i += SYA_TPB) st_out(&Et[i], s_u.stage[i], A.plain);
+    for (u32 i = tid; i < nops * CW; i += SYA_TPB) st_out(&Et[i], s_u.stage[i], A.plain_e);
     if (dbg) {
         dbg[4] = wall_clock64();
         dbg[9] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
@@ -1057,7 +1059,7 @@ static SySumArgs sy_sum_args(nrg_ctx* c, const SyDeferred& d) {
     S.words = c->d_words;
     S.v32 = &x.fl->v32[d.par];
     S.dbg = (c->exp & 2) ? c->d_dbg : nullptr;
-    S.plain = !((c->exp >> 6) & 1);
+    S.plain = !((c->exp >> 9) & 1);
     return S;
 }
 
@@ -1118,6 +1120,7 @@ static hipError_t sy_bucket_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 re
     A.epoch = ++c->sy_round;
     A.dbg = (c->exp & 2) ? c->d_dbg : nullptr;
     A.plain = !((c->exp >> 6) & 1);
+    A.plain_e = !((c->exp >> 7) & 1);
     SySumArgs S{};
     if (c->sy_pend.valid) S = sy_sum_args(c, c->sy_pend);
     c->sy_pend.valid = false;
@@ -1127,7 +1130,7 @@ static hipError_t sy_bucket_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 re
     const size_t dyn = (size_t)(ntiles + 1) * 4 + (size_t)ntiles * 2;
     sy_bucket_kernel<<<NB, SYB_TPB, dyn, st>>>(x.E[par], x.cnt, ntiles, SYA_OPS * CW, x.V, c->d_words, cf.synth_n, HR,
                                                W, A.ring, A.ring_mask, lo, x.fl, A.epoch, par,
-                                               (c->exp & 2) ? c->d_dbg : nullptr, c->stall, !((c->exp >> 6) & 1));
+                                               (c->exp & 2) ? c->d_dbg : nullptr, c->stall, !((c->exp >> 8) & 1));
     timer_end(c, "sy_replay");
     if ((e = hipGetLastError()) != hipSuccess) return e;
     // this chunk's sums: in the next chunk's partition launch (pipeline = 1) or now
