@@ -201,14 +201,9 @@ struct StPass {
 // the look-back waits. 15.35-15.50 -> 14.88-14.90 us per round on one box, 15.37-15.42 -> 15.14-15.24
 // on another (profiles/r04_nt_stores.txt). NRG_KNOB_EXP bit 6 = plain stores (A/B).
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void nt_store4(uint4* p, uint4 v) {
     const u32x4_t t = {v.x, v.y, v.z, v.w};
     __builtin_nontemporal_store(t, (u32x4_t*)p);
-}
-__device__ __forceinline__ void nt_store2(uint2* p, uint2 v) {
-    const u32x2_t t = {v.x, v.y};
-    __builtin_nontemporal_store(t, (u32x2_t*)p);
 }
 
 __device__ __forceinline__ void wave_sync() {  // LDS written by other lanes of this wave
@@ -473,8 +468,7 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
             } else {  // 8 ops per lane: one 8-B store
                 const uint2 b = uint2{((smask & 15u) * 0x204081u) & 0x01010101u,
                                       (((smask >> 4) & 15u) * 0x204081u) & 0x01010101u};
-                if (!A.plain) nt_store2((uint2*)sp, b);
-                else *(uint2*)sp = b;
+                *(uint2*)sp = b;  // (streamed: +1.2 MB of partial-line writes per round, no faster)
             }
         } else if (resp) {
 #pragma unroll
