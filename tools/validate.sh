@@ -1,3 +1,7 @@
+#!/bin/bash
+# End-of-round validation on the GPU box (through gpurun, from the repo root): the GPU test suite,
+# smoke(), the default bench line, the stack bench line, and a PMC profile of the stack kernel.
+# Outputs: gpurun_out/final/, gpurun_out/prof_r04f_stack/ (tools/prof_summary.py -> profiles/).
 set -o pipefail
 mkdir -p gpurun_out/final
 timeout -k 10 900 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests -m gpu > gpurun_out/final/t.log 2>&1 &&
