@@ -13,6 +13,7 @@
 from __future__ import annotations
 
 import ctypes as C
+import sys
 import threading
 from dataclasses import dataclass
 from typing import Callable, List, Optional, Sequence
@@ -47,8 +48,40 @@ def _dptr(t) -> C.c_void_p:
     return C.c_void_p(t.data_ptr())
 
 
+def _stream_ordered(fn):
+    """Stream-ordering contract of every `*_device` helper (and join): the call is ordered AFTER
+    all work already queued on torch's current stream (so buffers torch filled or copied there
+    are ready), and torch's current stream is ordered AFTER the work the call queued on this
+    replica's stream (so torch reads of the outputs see them). When the replica already runs on
+    torch's current stream (use_torch_stream) this is free; otherwise two events cross the
+    streams. With config.pipeline = 1 a round's deferred outputs are complete only after join(),
+    which is ordered the same way. Without this, a replica on its own non-blocking stream
+    (nrg_open's default, include/nrgpu.h nrg_set_stream) races torch's null-stream fills."""
+
+    def wrapped(self, *a, **kw):
+        cross = self._cross_streams()
+        if cross is None:
+            return fn(self, *a, **kw)
+        cur, mine = cross
+        mine.wait_stream(cur)
+        try:
+            return fn(self, *a, **kw)
+        finally:
+            cur.wait_stream(mine)
+
+    wrapped.__name__ = fn.__name__
+    wrapped.__doc__ = fn.__doc__
+    return wrapped
+
+
 class DeviceReplica:
-    """Thin owner of one nrg_ctx (one replica in one GPU's HBM)."""
+    """Thin owner of one nrg_ctx (one replica in one GPU's HBM).
+
+    Stream contract: the replica queues its GPU work on its own stream (nrg_own_stream, not
+    ordered with the null stream) until use_torch_stream / set_stream says otherwise. Every
+    `*_device` method and join() is nevertheless ordered with torch's current stream in both
+    directions (`_stream_ordered`), so torch tensors may be filled, passed and read back on
+    torch's stream without extra synchronisation. Host-pointer methods are synchronous."""
 
     def __init__(self, kind: int, device: int = 0, knobs: Optional[dict] = None, **cfg):
         """`cfg`: nrg_config fields; `knobs`: {name: value} of nrg_test_set_knob (tuning and
@@ -102,9 +135,27 @@ class DeviceReplica:
     def use_own_stream(self):
         self.set_stream(self._lib.nrg_own_stream(self._h) or 0)
 
+    def _cross_streams(self):
+        """(torch's current stream, this replica's stream as a torch stream) when the two differ
+        and torch drives a GPU; None when no ordering is needed."""
+        torch = sys.modules.get("torch")
+        if torch is None or not torch.cuda.is_available():
+            return None
+        cur = torch.cuda.current_stream(self.device)
+        mine = self._lib.nrg_get_stream(self._h) or 0
+        if cur.cuda_stream == mine:
+            return None
+        cache = getattr(self, "_ext_stream", None)
+        if cache is None or cache[0] != mine:
+            s = (torch.cuda.default_stream(self.device) if mine == 0
+                 else torch.cuda.ExternalStream(mine, device=torch.device("cuda", self.device)))
+            cache = self._ext_stream = (mine, s)
+        return cur, cache[1]
+
     def sync(self):
         L.check(self._lib.nrg_sync(self._h), "nrg_sync")
 
+    @_stream_ordered
     def join(self):
         """Order outstanding side-stream reads (pipeline=1) on this replica's stream."""
         L.check(self._lib.nrg_join(self._h), "nrg_join")
@@ -121,11 +172,13 @@ class DeviceReplica:
         L.check(self._lib.nrg_log_append(self._h, _ptr(recs), len(recs), origin, C.byref(first)), "append")
         return first.value
 
+    @_stream_ordered
     def log_append_device(self, d_recs, n: int, origin: int) -> int:
         first = C.c_uint64()
         L.check(self._lib.nrg_log_append_async(self._h, _dptr(d_recs), n, origin, C.byref(first)), "append")
         return first.value
 
+    @_stream_ordered
     def log_append_segments(self, d_base, seg_stride: int, lens: Sequence[int], origins: Sequence[int]):
         key = (tuple(lens), tuple(origins))
         if getattr(self, "_seg_key", None) != key:  # marshalled once per distinct round shape
@@ -151,15 +204,18 @@ class DeviceReplica:
             L.check(self._lib.nrg_log_exec(self._h, 0, 0, None, None), "exec")
         return resp[:n], some[:n]
 
+    @_stream_ordered
     def log_exec_device(self, resp_lo=0, resp_hi=0, d_resp=None, d_some=None):
         L.check(self._lib.nrg_log_exec_async(self._h, resp_lo, resp_hi, _dptr(d_resp), _dptr(d_some)), "exec")
 
+    @_stream_ordered
     def st_round_device(self, d_ops, n: int, origin: int, d_resp=None, d_some=None):
         """Replica::combine for one stack batch on device buffers: append + exec in one replay
         pass (nrg_stack_round_async); Pop responses for these ops into d_resp / d_some."""
         L.check(self._lib.nrg_stack_round_async(self._h, _dptr(d_ops), n, origin, _dptr(d_resp), _dptr(d_some)),
                 "stack_round")
 
+    @_stream_ordered
     def sy_round_device(self, d_ops, n: int, origin: int, d_resp=None, d_some=None):
         """Replica::combine for one synthetic batch on device buffers (nrg_synth_round_async)."""
         L.check(self._lib.nrg_synth_round_async(self._h, _dptr(d_ops), n, origin, _dptr(d_resp), _dptr(d_some)),
@@ -177,15 +233,18 @@ class DeviceReplica:
         L.check(self._lib.nrg_hashmap_get(self._h, _ptr(keys), n, _ptr(vals), _ptr(found)), "get")
         return vals[:n], found[:n]
 
+    @_stream_ordered
     def hm_get_device(self, d_keys, n, d_vals, d_found):
         L.check(self._lib.nrg_hashmap_get_async(self._h, _dptr(d_keys), n, _dptr(d_vals), _dptr(d_found)), "get")
 
+    @_stream_ordered
     def hm_round_device(self, d_puts, W, origin, d_get_keys, R, d_get_vals, d_get_found, d_prev=None,
                         d_prev_found=None):
         L.check(self._lib.nrg_hashmap_round_async(self._h, _dptr(d_puts), W, origin, _dptr(d_get_keys), R,
                                                   _dptr(d_get_vals), _dptr(d_get_found), _dptr(d_prev),
                                                   _dptr(d_prev_found)), "round")
 
+    @_stream_ordered
     def hm_round_segments_device(self, d_base, seg_stride, lens, origins, resp_seg, d_get_keys, R, d_get_vals,
                                  d_get_found, d_prev=None, d_prev_found=None):
         key = (tuple(lens), tuple(origins))
@@ -210,12 +269,14 @@ class DeviceReplica:
         """NrHashMap::default restricted to key partition `part` of `parts` (nrg_key_owner)."""
         L.check(self._lib.nrg_hashmap_prefill_partition(self._h, n, off, part, parts), "prefill_partition")
 
+    @_stream_ordered
     def hm_partition_device(self, d_puts, W, d_keys, R, parts, d_puts_out, d_put_pos, d_keys_out, d_get_pos, d_counts):
         """Stable partition of a round's Puts and Get keys by owner (nrg_hashmap_partition_async)."""
         L.check(self._lib.nrg_hashmap_partition_async(self._h, _dptr(d_puts), W, _dptr(d_keys), R, parts,
                                                       _dptr(d_puts_out), _dptr(d_put_pos), _dptr(d_keys_out),
                                                       _dptr(d_get_pos), _dptr(d_counts)), "partition")
 
+    @_stream_ordered
     def route_back_device(self, d_src, d_src8, d_pos, n, d_dst, d_dst8):
         L.check(self._lib.nrg_route_back_async(self._h, _dptr(d_src), _dptr(d_src8), _dptr(d_pos), n, _dptr(d_dst),
                                                _dptr(d_dst8)), "route_back")
@@ -298,18 +359,23 @@ class DeviceReplica:
         return out
 
     # -- generators / timing -------------------------------------------------------
+    @_stream_ordered
     def gen_uniform_device(self, d_out, n, seed, span):
         L.check(self._lib.nrg_gen_uniform_async(self._h, _dptr(d_out), n, seed, span))
 
+    @_stream_ordered
     def gen_raw_device(self, d_out, n, seed):
         L.check(self._lib.nrg_gen_raw_async(self._h, _dptr(d_out), n, seed))
 
+    @_stream_ordered
     def gen_zipf_device(self, d_out, n, seed, N, theta=0.99, scramble=False):
         L.check(self._lib.nrg_gen_zipf_async(self._h, _dptr(d_out), n, seed, N, float(theta), int(scramble)), "zipf")
 
+    @_stream_ordered
     def gen_stack_ops_device(self, d_out, n, seed):
         L.check(self._lib.nrg_gen_stack_ops_async(self._h, _dptr(d_out), n, seed), "stack ops")
 
+    @_stream_ordered
     def gen_puts_device(self, d_out, d_keys, d_vals, n):
         L.check(self._lib.nrg_gen_puts_async(self._h, _dptr(d_out), _dptr(d_keys), _dptr(d_vals), n))
 
