@@ -25,6 +25,7 @@ import gc
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -36,6 +37,31 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level para
 
 def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+class Watchdog:
+    """Whole-process deadline. A rank stuck in a collective -- a peer that never joined, an RCCL
+    round that never completes, a blocked ncclCommInitRank -- ends the run non-zero with a
+    diagnostic naming the rank and the phase instead of holding the driver's slot. (The replica
+    group's own deadline, nrg_group_set_timeout / --group-timeout-ms, turns a missing peer inside a
+    round into NRG_E_TIMEOUT first; this covers what that cannot reach.)"""
+
+    def __init__(self):
+        self.phase = "start"
+        self.rank = int(os.environ.get("RANK", "0"))
+
+    def arm(self, seconds: float):
+        if seconds > 0:
+            threading.Thread(target=self._fire, args=(seconds,), daemon=True).start()
+
+    def _fire(self, seconds):
+        time.sleep(seconds)
+        log(f"watchdog: rank {self.rank} of {os.environ.get('WORLD_SIZE', '1')} still in phase '{self.phase}' "
+            f"after {seconds:.0f} s (a peer rank stalled or never joined?); exiting with status 3")
+        os._exit(3)
+
+
+WATCH = Watchdog()
 
 
 def numa_groups(cpus):
@@ -213,6 +239,7 @@ class Env:
         # stream would order against every blocking stream, RCCL's included)
         self.stream = torch.cuda.Stream(self.dev)
         torch.cuda.set_stream(self.stream)
+        WATCH.phase = "init_process_group"
         if self.world > 1:
             if args.backend == "nccl":
                 dist.init_process_group("nccl", device_id=self.dev)  # RCCL over xGMI
@@ -390,12 +417,14 @@ def run_hashmap(args, env):
 
         if args.backend != "nccl":
             raise SystemExit("--partitioned needs --backend nccl (RCCL send/recv)")
-        pgroup = PartitionedGroup(rep, rank, world)
+        WATCH.phase = "nrg_group_join (partitioned)"
+        pgroup = PartitionedGroup(rep, rank, world, timeout_ms=args.group_timeout_ms)
     elif world > 1 and args.backend == "nccl":
         # the C ABI's replica group: RCCL all-gather on a library-owned stream, replay on ours
         from nrgpu.parallel import ReplicaGroup
 
-        cgroup = ReplicaGroup(rep, rank, world)
+        WATCH.phase = "nrg_group_join"
+        cgroup = ReplicaGroup(rep, rank, world, timeout_ms=args.group_timeout_ms)
         inputs = torch.cuda.Stream(dev_t)  # inputs exist before the timed region: gathers run ahead
         cgroup.set_input_stream(inputs.cuda_stream)
     elif world > 1:
@@ -441,8 +470,11 @@ def run_hashmap(args, env):
         return env.timed(n, step, rep, host_s)
 
     mode["n"] = args.warmup
+    WATCH.phase = "warmup rounds"
     for i in range(args.warmup):
         step(i)
+    if cgroup is not None or pgroup is not None:
+        (cgroup or pgroup).sync()  # bounded by the group's deadline
     rep.sync()
     log(f"rank {rank}: warmup {args.warmup} rounds done")
 
@@ -452,6 +484,7 @@ def run_hashmap(args, env):
     # launch (steady-state launches: round e's index plus round e-1's apply and reads, i.e. one
     # round of work each).
     host_s = [0.0]
+    WATCH.phase = "timed region"
     elapsed = run(args.steps, host_s=host_s)  # no events in the timed region
     kt = roofline_region(args, rep, run, ["hm_round", "hm_papply"])
     (k_n, k_ms), (a_n, a_ms) = kt["hm_round"], kt["hm_papply"]
@@ -594,7 +627,8 @@ def run_synthetic(args, env):
     if world > 1 and args.backend == "nccl":
         from nrgpu.parallel import ReplicaGroup
 
-        cgroup = ReplicaGroup(rep, rank, world)
+        WATCH.phase = "nrg_group_join"
+        cgroup = ReplicaGroup(rep, rank, world, timeout_ms=args.group_timeout_ms)
         inputs = torch.cuda.Stream(dev_t)
         cgroup.set_input_stream(inputs.cuda_stream)
     elif world > 1:
@@ -632,6 +666,7 @@ def run_synthetic(args, env):
         mode["n"] = n
         return env.timed(n, step, rep)
 
+    WATCH.phase = "timed region"
     elapsed = run(args.steps)  # no events in the timed region
     k_n, k_ms = roofline_region(args, rep, run, ["sy_replay"])["sy_replay"]
     rep.sync()
@@ -699,7 +734,8 @@ def run_stack(args, env):
     if world > 1 and args.backend == "nccl":
         from nrgpu.parallel import ReplicaGroup
 
-        cgroup = ReplicaGroup(rep, rank, world)
+        WATCH.phase = "nrg_group_join"
+        cgroup = ReplicaGroup(rep, rank, world, timeout_ms=args.group_timeout_ms)
         inputs = torch.cuda.Stream(dev_t)
         cgroup.set_input_stream(inputs.cuda_stream)
     elif world > 1:
@@ -737,6 +773,7 @@ def run_stack(args, env):
         mode["n"] = n
         return env.timed(n, step, rep)
 
+    WATCH.phase = "timed region"
     elapsed = run(args.steps)  # no events in the timed region
     k_n, k_ms = roofline_region(args, rep, run, ["st_replay"])["st_replay"]
     rep.sync()
@@ -815,11 +852,16 @@ def main():
     ap.add_argument("--knob", action="append", default=[], metavar="NAME=VALUE",
                     help="diagnostic/tuning knob of the replica (nrg_test_set_knob, include/nrgpu_testing.h), "
                          "e.g. K1=2; never needed for the headline")
+    ap.add_argument("--deadline", type=float, default=900.0,
+                    help="whole-process watchdog in seconds (0: off): a stalled rank exits 3 with a diagnostic")
+    ap.add_argument("--group-timeout-ms", type=int, default=120_000,
+                    help="replica group deadline for every wait on the peer ranks (nrg_group_set_timeout)")
     ap.add_argument("--pipeline", type=int, default=1,
                     help="1: a round's apply+reads ride in the next round's launch (nrg_config.pipeline); "
                          "0: every round call completes its own reads")
     args = ap.parse_args()
     args.timing_every = max(1, args.timing_every)
+    WATCH.arm(args.deadline)
     env = Env(args)
     runner = {"stack": run_stack, "synthetic": run_synthetic}.get(args.workload, run_hashmap)
     res = runner(args, env)

@@ -315,6 +315,9 @@ int nrg_synth_dump(nrg_ctx* ctx, uint64_t* words, uint64_t cap, uint64_t* n);
  * RCCL is loaded at the first group call (librccl.so.1, the process's own copy if one is
  * already loaded); without it these calls return NRG_E_COMM. */
 #define NRG_E_COMM (-9)          /* RCCL unavailable or a collective failed               */
+#define NRG_E_TIMEOUT (-10)      /* a peer rank did not take part in a collective before the
+                                    group's deadline (nrg_group_set_timeout)                 */
+#define NRG_GROUP_DEFAULT_TIMEOUT_MS 300000u
 #define NRG_GROUP_ID_BYTES 128   /* ncclUniqueId                                           */
 
 typedef struct nrg_group nrg_group;
@@ -369,6 +372,17 @@ int nrg_group_set_input_stream(nrg_group* g, int member, void* hip_stream);
 int nrg_group_round_async(nrg_group* g, const nrg_round* rounds, const uint64_t* seg_lens);
 /* Wait for all queued group work and report latched device errors of every local replica. */
 int nrg_group_sync(nrg_group* g);
+/* Deadline of every wait on the peer ranks (default NRG_GROUP_DEFAULT_TIMEOUT_MS): the host round
+ * trips of the length / count exchanges, buffer regrowth and nrg_group_sync. A rank whose peers do
+ * not post their part of a collective in time gets NRG_E_TIMEOUT instead of hanging (its
+ * communicators are aborted, so the group can still be closed). Failures that leave the ranks'
+ * replicas different -- a timeout, a failed collective, ranks that disagreed on seg_lens -- are
+ * sticky: every later round or sync of the group returns the same code; close the group.
+ * (Like RCCL, a process blocked inside ncclCommInitRank or ncclGroupEnd itself -- before the
+ * stream waits -- is not bounded here; bench.py keeps a whole-process watchdog for that.) */
+int nrg_group_set_timeout(nrg_group* g, uint32_t ms);
+/* The sticky failure's description ("nrg_group rank R of N, round E: ..."), "" if none. */
+const char* nrg_group_last_error(const nrg_group* g);
 
 /* ---- cnr-style key-partitioned NrHashMap ---------------------------------
  * cnr maps each operation to one of several logs with LogMapper::hash() (cnr/src/lib.rs:134-167);

@@ -18,6 +18,9 @@ struct Collectives {
     decltype(&ncclCommDestroy) destroy = nullptr;
     decltype(&ncclSend) send = nullptr;  // partitioned rounds only
     decltype(&ncclRecv) recv = nullptr;
+    decltype(&ncclCommAbort) abort = nullptr;  // RCCL: unblocks a collective a peer never posted
+    void (*set_timeout_ms)(uint32_t) = nullptr;  // loopback: how long this thread's collectives
+                                                 // wait for their peers (RCCL: none)
 };
 
 // loopback.cpp: every member of a group lives in this process; ncclGroupEnd turns the posted

@@ -20,9 +20,12 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <mutex>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "collectives.hpp"
@@ -56,6 +59,7 @@ const Rccl* rccl() {
             r.destroy = (decltype(r.destroy))dlsym(h, "ncclCommDestroy");
             r.send = (decltype(r.send))dlsym(h, "ncclSend");
             r.recv = (decltype(r.recv))dlsym(h, "ncclRecv");
+            r.abort = (decltype(r.abort))dlsym(h, "ncclCommAbort");
             g_rccl_ok = r.get_unique_id && r.init_rank && r.init_all && r.all_gather && r.group_start &&
                         r.group_end && r.destroy;
             if (g_rccl_ok) g_rccl = r;
@@ -240,7 +244,70 @@ struct nrg_group {
     bool owns = false;  // replicas opened by nrg_group_open
     std::vector<Member> m;
     uint64_t round = 0;
+    uint32_t timeout_ms = NRG_GROUP_DEFAULT_TIMEOUT_MS;  // deadline of every wait on the peers
+    int broken = NRG_OK;  // sticky: a timed-out collective or disagreeing ranks end the group
+    char diag[256] = {};  // what broke it (nrg_group_last_error)
 };
+
+namespace {
+
+// The group cannot go on: remember why, give up on the communicators (RCCL's abort ends a
+// collective a peer never posted, so the streams drain and close() cannot hang), and return `code`.
+int group_fail(nrg_group* g, int code, const char* what) {
+    if (g->broken == NRG_OK) {
+        g->broken = code;
+        std::snprintf(g->diag, sizeof g->diag, "nrg_group rank %d of %d, round %llu: %s", g->rank0, g->nranks,
+                      (unsigned long long)g->round, what);
+        std::fprintf(stderr, "%s\n", g->diag);
+        if (code == NRG_E_TIMEOUT && g->R && g->R->abort)
+            for (Member& m : g->m)
+                if (m.comm) {
+                    (void)g->R->abort(m.comm);
+                    m.comm = nullptr;
+                }
+    }
+    return g->broken;
+}
+
+// ncclGroupEnd with the group's deadline (the loopback blocks there until its peers post; RCCL
+// enqueues and returns, and a missing peer shows up in the stream waits below)
+int group_end(nrg_group* g, const char* phase) {
+    if (g->R->set_timeout_ms) g->R->set_timeout_ms(g->timeout_ms);
+    const ncclResult_t r = g->R->group_end();
+    if (r == ncclSuccess) return NRG_OK;
+    char what[192];
+    if (r == ncclSystemError && g->R->set_timeout_ms) {
+        std::snprintf(what, sizeof what, "%s: a peer rank did not post its part within %u ms", phase, g->timeout_ms);
+        return group_fail(g, NRG_E_TIMEOUT, what);
+    }
+    std::snprintf(what, sizeof what, "%s: collective failed (ncclResult %d)", phase, (int)r);
+    return group_fail(g, NRG_E_COMM, what);
+}
+
+// Wait until `s` drains, at most the group's deadline from now. A stream that does not drain is
+// one whose collective a peer never joined (or a hung device): the group fails with NRG_E_TIMEOUT.
+int wait_stream(nrg_group* g, hipStream_t s, const char* phase) {
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    const auto dl = t0 + std::chrono::milliseconds(g->timeout_ms);
+    for (uint32_t spin = 0;; spin++) {
+        const hipError_t e = hipStreamQuery(s);
+        if (e == hipSuccess) return NRG_OK;
+        if (e != hipErrorNotReady) return hip_rc(e);
+        const auto now = clk::now();
+        if (now >= dl) {
+            char what[192];
+            std::snprintf(what, sizeof what, "%s did not complete within %u ms (a peer rank never joined the collective?)",
+                          phase, g->timeout_ms);
+            return group_fail(g, NRG_E_TIMEOUT, what);
+        }
+        // a host round trip is short: spin for the first 200 us, then back off
+        if (now - t0 > std::chrono::microseconds(200))
+            std::this_thread::sleep_for(std::chrono::microseconds(spin < 2000 ? 20 : 500));
+    }
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -371,12 +438,13 @@ static int exchange_lengths(nrg_group* g, const nrg_round* rounds, const std::ve
     ncclResult_t res = ncclSuccess;
     for (int i = 0; i < nl && res == ncclSuccess; i++)
         res = R->all_gather(g->m[i].lx, g->m[i].glx, 2, ncclUint64, g->m[i].comm, g->m[i].cstream);
-    if (R->group_end() != ncclSuccess || res != ncclSuccess) return NRG_E_COMM;
+    RCHK(group_end(g, "length exchange"));
+    if (res != ncclSuccess) return group_fail(g, NRG_E_COMM, "length exchange: all-gather refused");
     for (int i = 0; i < nl; i++) {
         Member& m = g->m[i];
         RCHK(nrg::ctx_use_device(m.ctx));
         GCHK(hipMemcpyAsync(m.h_glx, m.glx, 2 * (uint64_t)G * 8, hipMemcpyDeviceToHost, m.cstream));
-        GCHK(hipStreamSynchronize(m.cstream));
+        RCHK(wait_stream(g, m.cstream, "length exchange"));
     }
     const uint64_t* H = g->m[0].h_glx;  // identical on every rank
     bool any_bad = false;
@@ -389,6 +457,7 @@ static int exchange_lengths(nrg_group* g, const nrg_round* rounds, const std::ve
 
 int nrg_group_round_async(nrg_group* g, const nrg_round* rounds, const uint64_t* seg_lens) {
     if (!g || !rounds) return NRG_E_INVAL;
+    if (g->broken) return g->broken;
     const Rccl* R = g->R;
     if (!R) return NRG_E_COMM;
     const int nl = (int)g->m.size(), G = g->nranks;
@@ -444,7 +513,7 @@ int nrg_group_round_async(nrg_group* g, const nrg_round* rounds, const uint64_t*
             if (!stride) continue;
             const uint64_t need = (uint64_t)G * seg_bytes;
             if (m.gbytes[b] < need) {
-                GCHK(hipStreamSynchronize(m.cstream));
+                RCHK(wait_stream(g, m.cstream, "gathered-buffer growth"));
                 if (m.gbuf[b]) GCHK(hipFree(m.gbuf[b]));
                 m.gbuf[b] = nullptr;
                 m.gbytes[b] = 0;
@@ -455,7 +524,7 @@ int nrg_group_round_async(nrg_group* g, const nrg_round* rounds, const uint64_t*
                 send[i] = x.recs;
             } else {  // pad a short segment to the common stride (a bad one sends zeros)
                 if (m.sbytes < seg_bytes) {
-                    GCHK(hipStreamSynchronize(m.cstream));
+                    RCHK(wait_stream(g, m.cstream, "send-buffer growth"));
                     if (m.sbuf) GCHK(hipFree(m.sbuf));
                     m.sbuf = nullptr;
                     m.sbytes = 0;
@@ -476,7 +545,8 @@ int nrg_group_round_async(nrg_group* g, const nrg_round* rounds, const uint64_t*
             if (stride && res == ncclSuccess)
                 res = R->all_gather(send[i], m.gbuf[b], seg_bytes / 8, ncclUint64, m.comm, m.cstream);
         }
-        if (R->group_end() != ncclSuccess || res != ncclSuccess) return NRG_E_COMM;
+        RCHK(group_end(g, "segment all-gather"));
+        if (res != ncclSuccess) return group_fail(g, NRG_E_COMM, "segment all-gather refused");
         if (given)
             for (int i = 0; i < nl; i++) {
                 Member& m = g->m[i];
@@ -492,7 +562,9 @@ int nrg_group_round_async(nrg_group* g, const nrg_round* rounds, const uint64_t*
         nrg_ctx* c = m.ctx;
         RCHK(nrg::ctx_use_device(c));
         if (bad[i]) {  // took part in the collectives, replays nothing
-            rc = NRG_E_INVAL;
+            // Its peers replay the round (with this rank's segment as zeros) and latch ERR_GROUP;
+            // the replicas now differ, so the group is over for every rank (sticky error).
+            rc = group_fail(g, NRG_E_INVAL, "this rank's segment disagreed with seg_lens: replicas diverged");
             continue;
         }
         if (stride) {
@@ -531,6 +603,7 @@ int nrg_group_round_async(nrg_group* g, const nrg_round* rounds, const uint64_t*
 
 int nrg_group_partitioned_round(nrg_group* g, const nrg_round* rounds) {
     if (!g || !rounds) return NRG_E_INVAL;
+    if (g->broken) return g->broken;
     const Rccl* R = g->R;
     if (!R || !R->send || !R->recv) return NRG_E_COMM;
     const int G = g->nranks, nl = (int)g->m.size();
@@ -580,13 +653,14 @@ int nrg_group_partitioned_round(nrg_group* g, const nrg_round* rounds) {
     ncclResult_t res = ncclSuccess;
     for (int i = 0; i < nl && res == ncclSuccess; i++)
         res = R->all_gather(g->m[i].pt[PB_CNT].p, g->m[i].pt[PB_ALLCNT].p, CW, ncclUint64, g->m[i].comm, g->m[i].cstream);
-    if (R->group_end() != ncclSuccess || res != ncclSuccess) return NRG_E_COMM;
+    RCHK(group_end(g, "partitioned count exchange"));
+    if (res != ncclSuccess) return group_fail(g, NRG_E_COMM, "partitioned count exchange refused");
     for (int i = 0; i < nl; i++) {
         Member& m = g->m[i];
         RCHK(nrg::ctx_use_device(m.ctx));
         m.hcnt.resize((size_t)G * CW);
         GCHK(hipMemcpyAsync(m.hcnt.data(), m.pt[PB_ALLCNT].p, (uint64_t)G * CW * 8, hipMemcpyDeviceToHost, m.cstream));
-        GCHK(hipStreamSynchronize(m.cstream));
+        RCHK(wait_stream(g, m.cstream, "partitioned count exchange"));
     }
     const std::vector<uint64_t>& H = g->m[0].hcnt;  // identical on every rank
     auto word = [&](int s, uint64_t k) { return H[(size_t)s * CW + 2 * G + k]; };
@@ -649,13 +723,14 @@ int nrg_group_partitioned_round(nrg_group* g, const nrg_round* rounds) {
         for (int i = 0; i < nl && res == ncclSuccess; i++)
             res = R->all_gather(g->m[i].pt[PB_ST].p, g->m[i].pt[PB_ALLST].p, 1, ncclUint64, g->m[i].comm,
                                 g->m[i].cstream);
-        if (R->group_end() != ncclSuccess || res != ncclSuccess) return NRG_E_COMM;
+        RCHK(group_end(g, "partitioned status exchange"));
+        if (res != ncclSuccess) return group_fail(g, NRG_E_COMM, "partitioned status exchange refused");
         std::vector<uint64_t> st(G);
         for (int i = 0; i < nl; i++) {
             Member& m = g->m[i];
             RCHK(nrg::ctx_use_device(m.ctx));
             GCHK(hipMemcpyAsync(st.data(), m.pt[PB_ALLST].p, (uint64_t)G * 8, hipMemcpyDeviceToHost, m.cstream));
-            GCHK(hipStreamSynchronize(m.cstream));
+            RCHK(wait_stream(g, m.cstream, "partitioned status exchange"));
         }
         for (int s = 0; s < G; s++)
             if (st[s]) return -(int)st[s];
@@ -678,7 +753,8 @@ int nrg_group_partitioned_round(nrg_group* g, const nrg_round* rounds) {
                 res = R->recv(at(m.pt[PB_RKEY], P.gfrom_off[o] * 8), P.gfrom[o], ncclUint64, o, m.comm, m.cstream);
         }
     }
-    if (R->group_end() != ncclSuccess || res != ncclSuccess) return NRG_E_COMM;
+    RCHK(group_end(g, "partitioned send/recv of Puts and Gets"));
+    if (res != ncclSuccess) return group_fail(g, NRG_E_COMM, "partitioned send/recv refused");
     // 4. each owner replays the Puts it received (rank order) and answers the Gets it received. A
     //    skewed round can hand one owner more Puts than its max_batch (or ring) takes in one
     //    replay: consecutive rounds of at most that many, the Gets answered after the last.
@@ -738,7 +814,8 @@ int nrg_group_partitioned_round(nrg_group* g, const nrg_round* rounds) {
             }
         }
     }
-    if (R->group_end() != ncclSuccess || res != ncclSuccess) return NRG_E_COMM;
+    RCHK(group_end(g, "partitioned answers back"));
+    if (res != ncclSuccess) return group_fail(g, NRG_E_COMM, "partitioned answers back refused");
     // 6. back into the caller's order
     for (int i = 0; i < nl; i++) {
         Member& m = g->m[i];
@@ -752,20 +829,38 @@ int nrg_group_partitioned_round(nrg_group* g, const nrg_round* rounds) {
             RCHK(nrg_route_back_async(c, (const uint64_t*)m.pt[PB_APREV].p, (const uint8_t*)m.pt[PB_APREVF].p,
                                       (const uint32_t*)m.pt[PB_PPOS].p, x.n, (uint64_t*)x.resp, x.some));
     }
+    g->round++;
     return NRG_OK;
 }
 
 int nrg_group_sync(nrg_group* g) {
     if (!g) return NRG_E_INVAL;
+    if (g->broken) return g->broken;
     int rc = NRG_OK;
     for (Member& m : g->m) {
         int r = nrg::ctx_use_device(m.ctx);
         if (r) return r;
-        GCHK(hipStreamSynchronize(m.cstream));
+        RCHK(wait_stream(g, m.cstream, "group sync (collectives)"));
+        RCHK(wait_stream(g, m.ctx->stream, "group sync (replay)"));
+        // disagreeing round headers (ERR_GROUP, latched by grp_check_kernel) end the group: the
+        // ranks have replayed different logs, so every later call reports it too
+        uint32_t err = 0;
+        GCHK(hipMemcpyAsync(&err, &m.ctx->d_ctl->err, sizeof err, hipMemcpyDeviceToHost, m.ctx->stream));
+        GCHK(hipStreamSynchronize(m.ctx->stream));  // drained above: returns at once
         r = nrg_sync(m.ctx);
+        if (err & nrg::ERR_GROUP)
+            r = group_fail(g, NRG_E_INVAL, "ranks disagreed on a round's segment lengths: replicas diverged");
         if (r && rc == NRG_OK) rc = r;
     }
     return rc;
 }
+
+int nrg_group_set_timeout(nrg_group* g, uint32_t ms) {
+    if (!g || ms == 0) return NRG_E_INVAL;
+    g->timeout_ms = ms;
+    return NRG_OK;
+}
+
+const char* nrg_group_last_error(const nrg_group* g) { return g ? g->diag : ""; }
 
 }  // extern "C"

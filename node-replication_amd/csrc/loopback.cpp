@@ -22,7 +22,8 @@
 // exactly at its collective's position in stream order. Mismatched all-gather sizes or p2p
 // byte counts fail on every participant (ncclInvalidArgument) instead of corrupting memory. A
 // single-thread world fails an op that cannot be matched at once (ncclInvalidUsage); a
-// threaded world gives up after LB_TIMEOUT (ncclSystemError) instead of hanging the test.
+// threaded world gives up after the group's deadline (nrg_group_set_timeout; LB_TIMEOUT before
+// one is set) with ncclSystemError instead of hanging the test.
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -89,6 +90,9 @@ std::atomic<uint64_t> g_ids{1};
 
 thread_local int t_depth = 0;
 thread_local std::vector<Op> t_pending;
+// how long this thread's collectives wait for their peers (nrg_group_set_timeout, via the
+// table's set_timeout_ms; LB_TIMEOUT until a group sets it)
+thread_local std::chrono::milliseconds t_timeout = std::chrono::duration_cast<std::chrono::milliseconds>(LB_TIMEOUT);
 
 size_t dt_bytes(ncclDataType_t t) {
     switch (t) {
@@ -118,9 +122,19 @@ hipError_t new_event(World* w, int dev, hipEvent_t* e) {
 }
 
 // Events are destroyed only once nothing can still wait on them: after every device of the
-// world has drained (callers hold the world lock, so no rank enqueues meanwhile).
+// world has drained (callers hold the world lock, so no rank enqueues meanwhile), and -- unless
+// the world is going away -- while no posted op is waiting for its match: an unmatched op's
+// `ready` event is in `spent` too, and the thread that completes the match waits on it later.
+bool any_pending(const World* w) {
+    if (!w->ag.empty()) return true;
+    for (const auto* m : {&w->snd, &w->rcv})
+        for (const auto& kv : *m)
+            if (!kv.second.empty()) return true;
+    return false;
+}
+
 void reap(World* w, bool force) {
-    if (!force && w->spent.size() < 4096) return;
+    if (!force && (w->spent.size() < 4096 || any_pending(w))) return;
     for (int d : w->devs)
         if (hipSetDevice(d) == hipSuccess) (void)hipDeviceSynchronize();
     for (hipEvent_t e : w->spent) (void)hipEventDestroy(e);
@@ -274,7 +288,7 @@ ncclResult_t execute(std::vector<Op>& ops) {
     if (res == ncclSuccess && !all_matched()) {
         w->cv.notify_all();
         if (!w->threaded) res = ncclInvalidUsage;  // nobody else can post the other half
-        else if (!w->cv.wait_for(lk, LB_TIMEOUT, all_matched)) res = ncclSystemError;
+        else if (!w->cv.wait_for(lk, t_timeout, all_matched)) res = ncclSystemError;
     } else {
         w->cv.notify_all();
     }
@@ -357,8 +371,24 @@ ncclResult_t lb_init_rank(ncclComm_t* comm, int nranks, ncclUniqueId id, int ran
         std::lock_guard<std::mutex> rl(g_reg_mu);
         g_forming.erase(key);
         w->cv.notify_all();
-    } else if (!w->cv.wait_for(lk, LB_TIMEOUT, [&] { return w->joined == w->n; })) {
-        return ncclSystemError;  // a rank never joined (the comm stays allocated: abandoned world)
+    } else if (!w->cv.wait_for(lk, t_timeout, [&] { return w->joined == w->n; })) {
+        // A rank never joined: leave the world as if this rank had never come, so a retry with
+        // the same id starts from correct counts; the last joiner to give up frees it.
+        lk.unlock();
+        std::lock_guard<std::mutex> rl(g_reg_mu);
+        std::lock_guard<std::mutex> wl(w->mu);
+        if (w->joined == w->n) {  // the last rank arrived just now: keep this rank in the world
+            *comm = reinterpret_cast<ncclComm_t>(c);
+            return ncclSuccess;
+        }
+        w->joined--;
+        const bool last = --w->alive == 0;
+        delete c;
+        if (last) {
+            g_forming.erase(key);
+            delete w;  // nobody else holds it: it was still forming, with no joiner left
+        }
+        return ncclSystemError;
     }
     *comm = reinterpret_cast<ncclComm_t>(c);
     return ncclSuccess;
@@ -431,8 +461,11 @@ ncclResult_t lb_group_end() {
     return execute(ops);
 }
 
+void lb_set_timeout_ms(uint32_t ms) { t_timeout = std::chrono::milliseconds(ms); }
+
 const nrg::Collectives g_loopback = [] {
     nrg::Collectives t;
+    t.set_timeout_ms = lb_set_timeout_ms;
     t.get_unique_id = lb_get_unique_id;
     t.init_rank = lb_init_rank;
     t.init_all = lb_init_all;

@@ -279,6 +279,7 @@ const char* nrg_strerror(int code) {
         case NRG_E_CAPACITY: return "capacity exceeded";
         case NRG_E_NODEV: return "no such HIP device";
         case NRG_E_COMM: return "RCCL unavailable or a collective failed";
+        case NRG_E_TIMEOUT: return "a peer rank missed the replica group's deadline for a collective";
         default: return "unknown error";
     }
 }
@@ -1167,6 +1168,22 @@ extern "C" int nrg_test_set_knob(nrg_ctx* c, int knob, uint64_t v) {
         case NRG_KNOB_COMB_DEPTH:
             if (v < 1 || v > 4) return NRG_E_INVAL;
             c->comb_depth = (uint32_t)v;
+            return NRG_OK;
+        case NRG_KNOB_WS:
+            if (!hm || v > 2) return NRG_E_INVAL;
+            c->ws_mode = (uint32_t)v;
+            return NRG_OK;
+        case NRG_KNOB_WS_PER:
+            if (!hm || v < 16 || v > 4096) return NRG_E_INVAL;
+            c->ws_per = (uint32_t)v;
+            return NRG_OK;
+        case NRG_KNOB_WS_EPOS:
+            if (!hm || v > 100) return NRG_E_INVAL;
+            c->ws_epos = (uint32_t)v;
+            return NRG_OK;
+        case NRG_KNOB_WS_PLAIN:
+            if (!hm || v > 1) return NRG_E_INVAL;
+            c->ws_plain = (uint32_t)v;
             return NRG_OK;
         case NRG_KNOB_PIPELINE:
             if (v > 1) return NRG_E_INVAL;

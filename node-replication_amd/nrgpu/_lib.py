@@ -29,6 +29,8 @@ NRG_E_NOT_SYNCED = -6
 NRG_E_CAPACITY = -7
 NRG_E_NODEV = -8
 NRG_E_COMM = -9
+NRG_E_TIMEOUT = -10
+NRG_GROUP_DEFAULT_TIMEOUT_MS = 300000
 NRG_GROUP_ID_BYTES = 128
 NRG_MAX_PARTS = 64
 
@@ -160,6 +162,8 @@ SIGNATURES = {
     "nrg_group_set_input_stream": (C.c_int, [vp, C.c_int, vp]),
     "nrg_group_round_async": (C.c_int, [vp, C.POINTER(Round), u64p]),
     "nrg_group_sync": (C.c_int, [vp]),
+    "nrg_group_set_timeout": (C.c_int, [vp, u32]),
+    "nrg_group_last_error": (C.c_char_p, [vp]),
     "nrg_combiner_open": (C.c_int, [vp, u32, C.POINTER(vp)]),
     "nrg_combiner_close": (C.c_int, [vp]),
     "nrg_combiner_register": (C.c_int, [vp, C.POINTER(u32)]),
@@ -189,7 +193,8 @@ TEST_SIGNATURES = {
 # nrg_test_set_knob knobs (include/nrgpu_testing.h): tuning and diagnostics of an open context
 KNOBS = {"STAMP_MAX": 1, "SKEW_EVERY": 2, "EPOCH_LIMIT": 3, "K1": 4, "EXP": 6, "SY_SORT": 7,
          "PIPELINE": 8, "COMB_SPIN": 10, "COMB_DEPTH": 11,
-         "SMALL_MAX": 12, "PART": 13, "STALL": 14, "COMB_GATHER": 15, "PA_TPB": 16}
+         "SMALL_MAX": 12, "PART": 13, "STALL": 14, "COMB_GATHER": 15, "PA_TPB": 16, "WS": 17, "WS_PER": 18,
+         "WS_EPOS": 19, "WS_PLAIN": 20}
 
 _lib = None
 

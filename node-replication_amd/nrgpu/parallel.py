@@ -51,7 +51,8 @@ class ReplicaGroup:
         return bytes(uid)
 
     def __init__(self, replica, rank: Optional[int] = None, world: Optional[int] = None,
-                 pg: Optional[dist.ProcessGroup] = None, uid: Optional[bytes] = None):
+                 pg: Optional[dist.ProcessGroup] = None, uid: Optional[bytes] = None,
+                 timeout_ms: Optional[int] = None):
         lib = L.load()
         self.replica = replica
         self.rank = dist.get_rank(pg) if rank is None else rank
@@ -70,8 +71,24 @@ class ReplicaGroup:
         L.check(lib.nrg_group_join(replica.handle, uid, self.world, self.rank, C.byref(h)), "nrg_group_join")
         self._h = h
         self._lib = lib
+        if timeout_ms is not None:
+            self.set_timeout(timeout_ms)
         self._round = L.Round()
         self._lens = None
+
+    def set_timeout(self, ms: int):
+        """nrg_group_set_timeout: deadline of every wait on the peer ranks. A round or sync whose
+        peers miss it raises NrgError(NRG_E_TIMEOUT) naming this rank and round."""
+        L.check(self._lib.nrg_group_set_timeout(self._h, int(ms)), "nrg_group_set_timeout")
+
+    def last_error(self) -> str:
+        """nrg_group_last_error: the group's sticky failure, '' if none."""
+        return (self._lib.nrg_group_last_error(self._h) or b"").decode()
+
+    def _check(self, rc: int, what: str):
+        if rc:
+            diag = self.last_error()
+            L.check(rc, f"{what} [{diag}]" if diag else what)
 
     def set_input_stream(self, stream_ptr: int):
         """All-gathers wait only for work on this stream (where the inputs are produced)."""
@@ -94,10 +111,10 @@ class ReplicaGroup:
             lens = self._lens
         rc = self._lib.nrg_group_round_async(self._h, C.byref(r), lens)
         if rc:
-            L.check(rc, "nrg_group_round_async")
+            self._check(rc, "nrg_group_round_async")
 
     def sync(self):
-        L.check(self._lib.nrg_group_sync(self._h), "nrg_group_sync")
+        self._check(self._lib.nrg_group_sync(self._h), "nrg_group_sync")
 
     def close(self):
         if getattr(self, "_h", None):
@@ -243,7 +260,7 @@ class PartitionedGroup(ReplicaGroup):
         r.get_keys, r.n_gets, r.get_vals, r.get_found = _ptr(get_keys), n_gets, _ptr(get_vals), _ptr(get_found)
         rc = self._lib.nrg_group_partitioned_round(self._h, C.byref(r))
         if rc:
-            L.check(rc, "nrg_group_partitioned_round")
+            self._check(rc, "nrg_group_partitioned_round")
 
 
 class PartitionedHashMap:

@@ -30,3 +30,19 @@ def test_cpu_baseline_record(bench):
     assert out["one_thread"]["cores"] == 1 and out["one_thread"]["value"] > 0
     host = out["host"]
     assert host["nproc"] >= 1 and "numa_nodes" in host
+
+
+def test_watchdog_ends_a_stalled_process():
+    """bench.py's whole-process deadline: a process stuck past --deadline exits with status 3 and
+    names its rank and phase (what a rank blocked in a collective whose peer never came does)."""
+    import subprocess
+    import sys
+
+    code = ("import importlib.util, time, sys; sys.path.insert(0, %r)\n"
+            "spec = importlib.util.spec_from_file_location('b', %r); b = importlib.util.module_from_spec(spec)\n"
+            "spec.loader.exec_module(b); b.WATCH.phase = 'timed region'; b.WATCH.arm(0.5); time.sleep(30)\n"
+            % (ROOT, os.path.join(ROOT, "bench.py")))
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60,
+                       env={**os.environ, "RANK": "5", "WORLD_SIZE": "8"})
+    assert p.returncode == 3, p.stderr
+    assert "rank 5 of 8 still in phase 'timed region'" in p.stderr

@@ -471,3 +471,74 @@ def test_join_rounds_with_reads_only(nrg, orc):
         np.testing.assert_array_equal(out[rank][2][0], ev1[0])
         # round 3 replays the same Puts again: contents unchanged, same answers
         np.testing.assert_array_equal(out[rank][3][0], ev1[0])
+
+
+@pytest.mark.parametrize("case", ["exchanged", "explicit", "partitioned"])
+def test_join_missing_rank_times_out(nrg, case):
+    """A rank that never posts its part of a round must not hang its peers:
+    with a 2-s group deadline (nrg_group_set_timeout) every other rank's round fails with
+    NRG_E_TIMEOUT within the deadline, the message names the rank and the round, and the failure
+    is sticky (a later sync reports it too; the group can still be closed). One full round runs
+    first, so the missing rank is absent from round 1, not from the group's formation."""
+    import time
+
+    import torch
+
+    from nrgpu import DeviceReplica, NrgError
+    from nrgpu.parallel import PartitionedGroup, ReplicaGroup
+
+    L = nrg._lib
+    G, W, R, deadline_ms = 3, 500, 300, 2000
+    missing = G - 1
+
+    def body(rank, uid):
+        rep = DeviceReplica(L.NRG_DS_HASHMAP, 0, log2_slots=14, max_batch=4096, replica_id=rank + 1)
+        cls = PartitionedGroup if case == "partitioned" else ReplicaGroup
+        grp = cls(rep, rank, G, uid=uid, timeout_ms=deadline_ms)
+        puts = torch.zeros((W, 2), dtype=torch.int64, device="cuda")
+        puts[:, 0] = torch.arange(W, device="cuda") + 1000 * rank
+        gk = torch.arange(R, dtype=torch.int64, device="cuda")
+        gv = torch.zeros(R, dtype=torch.int64, device="cuda")
+        gf = torch.zeros(R, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+
+        def one_round():
+            if case == "partitioned":
+                grp.round(puts, W, gk, R, gv, gf)
+            else:
+                grp.round_async(puts, W, None, None, gk, R, gv, gf,
+                                seg_lens=[W] * G if case == "explicit" else None)
+            grp.sync()
+
+        one_round()  # everyone
+        out = {"rank": rank}
+        if rank != missing:
+            t0 = time.monotonic()
+            try:
+                one_round()
+                out["round"] = 0
+            except NrgError as e:
+                out["round"], out["msg"] = e.code, str(e)
+            out["elapsed"] = time.monotonic() - t0
+            try:
+                grp.sync()
+                out["again"] = 0
+            except NrgError as e:
+                out["again"] = e.code
+            out["diag"] = grp.last_error()
+        else:
+            time.sleep(deadline_ms / 1000 + 3)  # keep the world alive, post nothing
+        grp.close()
+        rep.close()
+        return out
+
+    out = _run_ranks(nrg, G, body, timeout=60)
+    for o in out:
+        if o["rank"] == missing:
+            continue
+        r = o["rank"]
+        assert o["round"] == L.NRG_E_TIMEOUT, o
+        assert o["elapsed"] < deadline_ms / 1000 + 3.0, o
+        assert o["again"] == L.NRG_E_TIMEOUT, o  # sticky
+        assert f"rank {r} of {G}, round 1" in o["diag"], o
+        assert "within 2000 ms" in o["diag"], o
