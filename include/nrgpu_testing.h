@@ -66,13 +66,6 @@ int nrg_test_debug_read(nrg_ctx* ctx, uint64_t* out, uint64_t words);
                                    partition-round apply chunks, stack queries/table);
                                    2 (+1) = synthetic only, also drop the barrier that guards the
                                    bucket pass's tile map (diagnostic: results WRONG)            */
-#define NRG_KNOB_WS 17          /* hashmap: write-set rounds (one launch, no device atomic per Put): 0 never,
-                                   1 (default) rounds of <= 393216 Puts without previous values on unskewed
-                                   key streams, 2 skewed streams too                                    */
-#define NRG_KNOB_WS_PER 18      /* write-set rounds: Puts per bucket the geometry aims at (16..4096, 128)  */
-#define NRG_KNOB_WS_EPOS 19     /* write-set rounds: % of the read blocks dispatched before the set-building
-                                   workgroups (0..100, default 25)                                       */
-#define NRG_KNOB_WS_PLAIN 20    /* write-set rounds: log copy with plain (1, default) or streaming (0) stores */
 int nrg_test_set_knob(nrg_ctx* ctx, int knob, uint64_t value);
 
 /* Replica groups created after nrg_test_loopback_collectives(1) (nrg_group_open,

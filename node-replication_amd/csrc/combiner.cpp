@@ -260,7 +260,8 @@ int launch(nrg_combiner* m, Batch& x, uint32_t W, uint32_t R) {
     switch (m->kind) {
         case NRG_DS_HASHMAP:  // Put -> HashMap::insert's previous value (nr/examples/hashmap.rs:46-50)
             // a small round (one workgroup, the round's only launch) copies the error latch as its
-            // last write; any other round gets comb_err_kernel behind it
+            // last write and clears c->err_out; any other round leaves it set (only
+            // hm_small_round_kernel takes it) and gets comb_err_kernel behind it
             if (small) c->err_out = x.err;
             rc = nrg_hashmap_round_async(c, (const nrg_put*)x.recs, W, origin, (const uint64_t*)x.reads, R,
                                          (uint64_t*)x.rresp, x.rsome, (uint64_t*)x.wresp, x.wsome);

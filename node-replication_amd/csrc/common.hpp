@@ -28,9 +28,6 @@ constexpr u32 HM_BK_MAX = 1024;
 // Largest hashmap replay chunk: keeps the partition apply's per-tile LDS prefix (one u32 + one
 // u16 per tile of 2048 Puts) and 16-bit tile offsets within bounds.
 constexpr u64 HM_MAX_BATCH = 1ull << 23;
-// Write-set rounds (hashmap.hip hm_ws_kernel): largest round, and filter words per bucket (log2).
-constexpr u64 WS_MAX = 3ull << 17;  // (393216 Puts: 1024 buckets of ~384, HT 1024)
-constexpr u32 WS_BW_LOG_MAX = 8;
 
 // splitmix64 finaliser — identical constants to oracle/nr_oracle.c (orc_mix64) so that
 // device-generated workloads are reproducible by the CPU oracle.

@@ -39,7 +39,6 @@
 namespace nrg {
 
 typedef u64 u64x2 __attribute__((ext_vector_type(2)));
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 // Streaming (nt) stores for the streamed outputs (log copy, read responses) of partition-round and
 // reads-only launches: plain stores leave them dirty in the XCD's L2 for the kernel-end write-back
@@ -82,7 +81,6 @@ struct IndexJob {
                    // probe (every key new), 4 no ranking/entries
     u64* dup_acc;  // [HM_DUP_SLOTS] Puts overwritten inside their block (key skew statistic)
     bool plain;    // plain stores for the log copy (st_out)
-    u32 ent_bytes; // bytes of `ent` (write-set rounds: the buffer descriptor of its sc1 stores)
 };
 struct ReadJob {
     const u64* keys;
@@ -100,8 +98,6 @@ struct ReadJob {
     u64* s_acc;
     volatile u64* s_host;
     u64 s_seq;
-    // the replica's error latch, copied to (mapped) e_out and cleared by the same block (nrg_combiner)
-    u32* e_out;
     bool plain;  // plain stores for the responses (st_out)
 };
 
@@ -149,9 +145,7 @@ struct PartLds {
     }
 };
 
-// SC1 (write-set rounds): entries and count words are stored write-through (sc1), so a workgroup of
-// the same launch on another XCD can read them after the tile has signalled (ws_part_role).
-template <int K1, bool DEDUP, bool SC1 = false>
+template <int K1, bool DEDUP>
 __device__ __forceinline__ void part_role(const IndexJob& j, u32 blk, u32 shift, char* lds) {
     constexpr int WT = 64 * K1;
     constexpr int TILE = PartLds<K1>::TILE;
@@ -275,11 +269,7 @@ __device__ __forceinline__ void part_role(const IndexJob& j, u32 blk, u32 shift,
     for (int r = 0; r < PER; r++) {
         const u32 b = threadIdx.x * PER + r;
         if (b < nb) {
-            if constexpr (SC1)
-                __hip_atomic_store(&j.cnt[(u64)blk * nb + b], (off << 16) | tot[r], __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            else
-                j.cnt[(u64)blk * nb + b] = (off << 16) | tot[r];
+            j.cnt[(u64)blk * nb + b] = (off << 16) | tot[r];
             s_start[b] = off;
         }
         off += tot[r];
@@ -290,17 +280,11 @@ __device__ __forceinline__ void part_role(const IndexJob& j, u32 blk, u32 shift,
     for (int q = 0; q < K1; q++) {
         if (!emit[q]) continue;
         const u32 p = s_start[bkt[q]] + s_wc[w * nb + bkt[q]] + rnk[q];
-        if constexpr (SC1) {
-            const u32x4 v = {(u32)rec[q].key, (u32)(rec[q].key >> 32), (u32)rec[q].val, (u32)(rec[q].val >> 32)};
-            __builtin_amdgcn_raw_buffer_store_b128(v, __builtin_amdgcn_make_buffer_rsrc((void*)j.ent, 0, j.ent_bytes, 0x00020000),
-                                                   (u32)(((u64)blk * TILE + p) * 16), 0, 16);  // aux 16: sc1
-        } else {
-            u64x2 e;
-            e.x = rec[q].key;
-            e.y = rec[q].val;
-            ent[p] = e;
-            if (j.eidx) j.eidx[(u64)blk * TILE + p] = (u32)(base + (u64)(w * WT + q * 64 + lane));
-        }
+        u64x2 e;
+        e.x = rec[q].key;
+        e.y = rec[q].val;
+        ent[p] = e;
+        if (j.eidx) j.eidx[(u64)blk * TILE + p] = (u32)(base + (u64)(w * WT + q * 64 + lane));
     }
 }
 
@@ -606,8 +590,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_num_sgpr(80))) void hm_r
         sj.exp = 0;
     }
     u32 b = blockIdx.x;
-    if ((rj.s_seq || rj.e_out) && b == gridDim.x - 1) {  // the tail block
-        if (rj.e_out && threadIdx.x == 0) *rj.e_out = atomicExch(&ctl->err, 0u);
+    if (rj.s_seq && b == gridDim.x - 1) {  // the tail block
         // the skew sample (counters read and cleared atomically)
         if (rj.s_seq && threadIdx.x < HM_DUP_SLOTS) {
             u64 v = atomicExch((unsigned long long*)&rj.s_acc[threadIdx.x], 0ull);
@@ -1054,481 +1037,6 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(PREV ? 3 : 4)
     if (threadIdx.x == 0 && s_created) atomicAdd(&j.created_acc[b % HM_CREATED_SLOTS], (u64)s_created);
     PA_MARK(5, wall_clock64());
 #undef PA_MARK
-}
-
-// ---- write-set rounds: ONE launch per round, no device atomic per Put ----------------------------
-// Round e's launch is {P(e) | S(e-1) | R(e-1) | E(e)} on disjoint block ranges:
-//   P(e)   the records -> {key, value} entries grouped by the bucket of the key's HOME slot, log order
-//          inside a bucket (part_role, stored write-through), then the tile counts itself done;
-//   E(e)   one workgroup per bucket, dispatched after every P tile: waits until all have counted
-//          themselves done, elects each key's last entry in an LDS hash (log order) and writes the
-//          bucket's WRITE SET W(e): a linear-probing table {key, last value} and a filter word array
-//          (two bits of 64 per key). It does not touch the hash table;
-//   S(e-1) one workgroup per bucket of W(e-1): finds (or claims) each key's slot and stores its value
-//          -- one table line read and one value store per distinct key, no atomics (claims aside);
-//   R(e-1) the Gets of round e-1: a key in W(e-1) is answered from W(e-1) (S(e-1) may be storing
-//          it in this very launch), any other key from its probe chain. S(e-1) only stores values of
-//          W(e-1)'s keys and claims empty slots, which cannot end another key's probe chain, so the
-//          chain of a key outside W(e-1) reads the state after round e-1 (nr/src/replica.rs:483-497).
-// The filter word is in L2 (a few hundred KB per round); a Get whose two bits are both set reads
-// the bucket's W entry (~1-2 % of the Gets: the keys written in the round and false positives).
-// Against a stamp round this drops the 100k memory-side stamp atomics of a B1 round (5.9 us of its
-// 34.7, profiles/r04_b1_ablation.txt) and the index role's probe chain wait; against a partition
-// round the second launch. The previous round's S and R ride in the next launch, as stamp rounds'
-// apply and reads do (config.pipeline = 1), or in a flush launch {S | R}.
-// Hand-off P -> E inside the launch (MI355X_MICROARCH.md § inter-workgroup visibility, the sc1 row;
-// cdna_hip_programming.md Guideline 16 R1): P stores entries and counts write-through (sc1), every
-// storing wave drains (s_waitcnt vmcnt(0)), a workgroup barrier, then ONE lane adds to the done
-// counter; E polls it relaxed with one lane, takes ONE agent-scope acquire, drains, barrier, loads.
-// E blocks come after every P block in dispatch order, so the P tiles it waits for are placed.
-constexpr u64 WS_NONE = 0xFFull;  // dir entry of a bucket with no key in the round
-constexpr u64 WS_SALT = 0xD6E8FEB86659FD93ull;
-constexpr u32 ERR_INTERNAL = 16u;  // a bounded in-kernel wait gave up (never expected)
-
-__device__ __forceinline__ u64 ws_hash(u64 k) { return mix64(k ^ WS_SALT); }
-// the two filter bits of a key (in its bucket's word hh & (bw - 1))
-__device__ __forceinline__ u64 ws_mask(u64 hh) { return (1ull << ((hh >> 20) & 63)) | (1ull << ((hh >> 26) & 63)); }
-
-struct WsSet {  // one parity's write set, built by E(e) and read by S(e) and R(e) in the next launch
-    u64x2* pool;    // {key, value} slots; bucket b's region: a linear-probing table from (hh >> 32)
-    u64* dir;       // [nb] off << 8 | log2(cap); WS_NONE: no key
-    u64* bits;      // [nb << bw_log] filter words
-    u64* side;      // {flag, value}: the side-slot key's last value in the round
-    u32* pool_cnt;  // pool slots handed out (E), zeroed by S of the same set
-    u64 pool_slots;
-};
-
-struct WsJob {
-    IndexJob ij;     // P(e) (ij.nblocks tiles)
-    u64* done;       // P tiles published so far (monotonic)
-    u64 target;      // E waits for *done >= target
-    u32 np, ns;      // P tiles; S workgroups (buckets of the pending set, 0: none)
-    u32 ra, ne;      // R blocks dispatched before E; E workgroups (buckets of this round, 0: none)
-    u32 e_nb_log, e_bw_log;  // this round's buckets and filter words per bucket (E)
-    u32 s_bk_shift, s_bw_log;  // the pending round's (S, R)
-    u32 tile;        // Puts per P tile
-    bool e_xcd;      // E's first block is a multiple of 8: buckets dealt to XCDs in contiguous ranges
-    WsSet eset, sset;
-    u64* created_acc;
-    u64* dup_acc;    // Puts whose key an earlier Put of the round already wrote (key skew)
-    // diagnostic ablations (NRG_KNOB_EXP >> 20; RESULTS WRONG, timing only): 1 no S, 2 no E, 4 no P,
-    // 8 no R, 16 R without the set check, 32 E without the wait for P
-    u32 exp;
-};
-
-template <int K1>
-__device__ __forceinline__ void ws_part_role(const WsJob& w, u32 blk, u32 shift, char* lds) {
-    part_role<K1, false, true>(w.ij, blk, shift, lds);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave: its sc1 stores are done
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(w.done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// E(e), bucket of workgroup r. HT: LDS election entries (at most HT / 2 distinct keys take the LDS
-// path; more, and the bucket's set is built in global memory chunk by chunk).
-template <int HT>
-__device__ __forceinline__ void ws_build_role(const WsJob& w, u32 r, char* lds, DevCtl* ctl) {
-    const u32 nb = 1u << w.e_nb_log, nt = w.ij.nblocks, bw = 1u << w.e_bw_log;
-    const u32 per = nb >> 3;
-    const u32 b = (w.e_xcd && nb >= 64) ? (r & 7u) * per + (r >> 3) : r;
-    const WsSet& S = w.eset;
-    u64* s_key = (u64*)lds;                          // [HT] keys (EMPTY_KEY free)
-    u32* s_pos = (u32*)(lds + HT * 8);               // [HT] last bucket position + 1
-    u32* s_img = (u32*)(lds + HT * 12);              // [HT] the set's table: election slot + 1 (0 free)
-    u64* s_bits = (u64*)(lds + HT * 16);             // [bw] filter words
-    u32* s_pre = (u32*)(s_bits + bw);                // [nt + 1] entry prefix over tiles
-    uint16_t* s_off = (uint16_t*)(s_pre + nt + 1);   // [nt] the bucket's run offset in each tile
-    __shared__ u32 s_side, s_d, s_full, s_dup, s_cap;
-    __shared__ u64 s_base;
-    for (int h = threadIdx.x; h < HT; h += TPB) {
-        s_key[h] = EMPTY_KEY;
-        s_pos[h] = 0;
-        s_img[h] = 0;  // (the keys' entry counts during the election)
-    }
-    for (u32 i = threadIdx.x; i < bw; i += TPB) s_bits[i] = 0;
-    if (threadIdx.x == 0) {
-        s_side = s_d = s_full = s_dup = 0;
-        // every P tile of this launch has published its entries (relaxed poll, ONE acquire)
-        u32 spins = 0;
-        while (!(w.exp & 32) && __hip_atomic_load(w.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < w.target) {
-            __builtin_amdgcn_s_sleep(2);
-            if (++spins > (1u << 24)) {  // ~1 s: never expected; fail loudly instead of hanging
-                atomicOr(&ctl->err, ERR_INTERNAL);
-                break;
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    // this bucket's (offset, count) in every tile
-    const u32 K = (nt + TPB - 1) / TPB;
-    u32 loc = 0;
-    for (u32 q = 0; q < K; q++) {
-        const u32 t = threadIdx.x * K + q;
-        if (t < nt) {
-            const u32 v = w.ij.cnt[(u64)t * nb + b];
-            s_off[t] = (uint16_t)(v >> 16);
-            s_pre[t] = v & 0xFFFFu;
-            loc += v & 0xFFFFu;
-        }
-    }
-    u32 total;
-    u32 run = block_scan_excl<TPB>(loc, &total);
-    for (u32 q = 0; q < K; q++) {
-        const u32 t = threadIdx.x * K + q;
-        if (t < nt) {
-            const u32 c = s_pre[t];
-            s_pre[t] = run;
-            run += c;
-        }
-    }
-    if (threadIdx.x == 0) s_pre[nt] = total;
-    __syncthreads();
-    // entry of bucket position p: its tile is the last with s_pre[t] <= p
-    auto ent_at = [&](u32 p) -> u64 {
-        u32 lo = 0, hi = nt - 1;
-        while (lo < hi) {
-            const u32 mid = (lo + hi + 1) >> 1;
-            if (s_pre[mid] <= p) lo = mid;
-            else hi = mid - 1;
-        }
-        return (u64)lo * w.tile + s_off[lo] + (p - s_pre[lo]);
-    };
-    constexpr int PER = 2;  // entries per thread per chunk
-    constexpr u32 C = PER * TPB;
-    // Key skew statistic (skew_sample): the entries of keys written >= WS_HOT times in the round.
-    // Uniform streams have next to none (B1: at most ~3 Puts per key); Zipf 0.99 puts a large
-    // share of its Puts there.
-    constexpr u32 WS_HOT = 8;
-    u32 dup = 0;
-    // ---- LDS election over the whole bucket: the last entry of every key ----
-    for (u32 base = 0; base < total; base += C) {
-        u64x2 x[PER];
-#pragma unroll
-        for (int q = 0; q < PER; q++) {
-            const u32 p = base + q * TPB + threadIdx.x;
-            x[q].x = EMPTY_KEY;
-            x[q].y = 0;
-            if (p < total) x[q] = w.ij.ent[ent_at(p)];
-        }
-#pragma unroll
-        for (int q = 0; q < PER; q++) {
-            const u32 p = base + q * TPB + threadIdx.x;
-            if (p >= total) continue;
-            const u64 k = x[q].x;
-            if (k == EMPTY_KEY) {
-                atomicMax(&s_side, p + 1);
-                continue;
-            }
-            u32 h = (u32)(ws_hash(k) >> 40) & (HT - 1);
-            bool in = false;
-            for (int pr = 0; pr < HT; pr++) {
-                const u64 old = atomicCAS((unsigned long long*)&s_key[h], (unsigned long long)EMPTY_KEY,
-                                          (unsigned long long)k);
-                if (old == EMPTY_KEY || old == k) {
-                    if (old == EMPTY_KEY) atomicAdd(&s_d, 1u);
-                    const u32 seen = atomicAdd(&s_img[h], 1u) + 1;
-                    dup += seen == WS_HOT ? WS_HOT : seen > WS_HOT ? 1u : 0u;
-                    in = true;
-                    break;
-                }
-                h = (h + 1) & (HT - 1);
-            }
-            if (in) atomicMax(&s_pos[h], p + 1);
-            else s_full = 1;  // (benign race: every writer stores 1)
-        }
-    }
-    if (dup) atomicAdd(&s_dup, dup);
-    __syncthreads();
-    const u32 D = s_d;
-    const bool big = s_full || D > (u32)HT / 2;
-    // the set's table: >= 2x the keys (a bucket past the LDS path sizes it by its entries)
-    const u32 want = big ? 2 * total : 2 * D;
-    u32 cap = 0;
-    if (D) {
-        cap = 16;
-        while (cap < want) cap <<= 1;
-    }
-    if (threadIdx.x == 0) {
-        u64 off = 0;
-        if (cap) {
-            off = atomicAdd(S.pool_cnt, cap);
-            if (off + cap > S.pool_slots) {  // cannot happen: the pool holds 4 n + 16 nb slots
-                atomicOr(&ctl->err, ERR_INTERNAL);
-                cap = 0;
-            }
-        }
-        s_base = off;
-        s_cap = cap;
-        u32 lg = 0;
-        while ((1u << lg) < cap) lg++;
-        S.dir[b] = cap ? (off << 8) | lg : WS_NONE;
-        if (s_dup && w.dup_acc) atomicAdd(&w.dup_acc[b % HM_DUP_SLOTS], (u64)s_dup);
-        if (b == 0) {  // the side-slot key's Puts are all in bucket 0
-            const u32 sp = s_side;
-            S.side[1] = sp ? w.ij.ent[ent_at(sp - 1)].y : 0;
-            S.side[0] = sp ? 1 : 0;
-        }
-    }
-    __syncthreads();
-    const u64 off = s_base;
-    cap = s_cap;
-    if (!big) {
-        // Every key of the election table goes to its slot of the set's table: the LDS image s_img
-        // holds election slot + 1 per table slot (0 free); the election table stays intact.
-        __syncthreads();  // (the counts in s_img are no longer read)
-        for (u32 f = threadIdx.x; f < cap; f += TPB) s_img[f] = 0;
-        __syncthreads();
-        for (u32 h = threadIdx.x; h < (u32)HT && cap; h += TPB) {
-            const u64 k = s_key[h];
-            if (k == EMPTY_KEY) continue;
-            const u64 v = w.ij.ent[ent_at(s_pos[h] - 1)].y;
-            const u64 hh = ws_hash(k);
-            u32 f = (u32)(hh >> 32) & (cap - 1);
-            while (atomicCAS(&s_img[f], 0u, h + 1) != 0u) f = (f + 1) & (cap - 1);  // D <= cap / 2
-            u64x2 e;
-            e.x = k;
-            e.y = v;
-            S.pool[off + f] = e;
-            atomicOr((unsigned long long*)&s_bits[hh & (bw - 1)], (unsigned long long)ws_mask(hh));
-        }
-        __syncthreads();
-        for (u32 f = threadIdx.x; f < cap; f += TPB) {
-            if (s_img[f]) continue;
-            u64x2 e;
-            e.x = EMPTY_KEY;
-            e.y = 0;
-            S.pool[off + f] = e;
-        }
-    } else if (cap) {
-        // Many keys in one bucket (a key stream crowding one home range): the table is built in
-        // global memory, chunk by chunk in log order. Write-through stores and device atomics, and a
-        // drain before each barrier, so a later chunk's store lands after an earlier one's.
-        for (u32 f = threadIdx.x; f < cap; f += TPB) {
-            u64* slot = (u64*)&S.pool[off + f];
-            __hip_atomic_store(slot, EMPTY_KEY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(slot + 1, (u64)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        constexpr u32 CH = HT / 2;  // a chunk's keys always fit the LDS table
-        for (u32 base = 0; base < total; base += CH) {
-            for (int h = threadIdx.x; h < HT; h += TPB) {
-                s_key[h] = EMPTY_KEY;
-                s_pos[h] = 0;
-            }
-            __syncthreads();
-            constexpr int QC = CH / TPB > 0 ? CH / TPB : 1;
-            u64x2 x[QC];
-            u32 hq[QC];
-#pragma unroll
-            for (int q = 0; q < QC; q++) {
-                const u32 p = base + q * TPB + threadIdx.x;
-                x[q].x = EMPTY_KEY;
-                x[q].y = 0;
-                hq[q] = HT;
-                if (q * TPB + threadIdx.x < CH && p < total) x[q] = w.ij.ent[ent_at(p)];
-            }
-#pragma unroll
-            for (int q = 0; q < QC; q++) {
-                const u32 p = base + q * TPB + threadIdx.x;
-                if (q * TPB + threadIdx.x >= CH || p >= total || x[q].x == EMPTY_KEY) continue;
-                u32 h = (u32)(ws_hash(x[q].x) >> 40) & (HT - 1);
-                for (;;) {  // at most CH = HT / 2 keys: always found
-                    const u64 old = atomicCAS((unsigned long long*)&s_key[h], (unsigned long long)EMPTY_KEY,
-                                              (unsigned long long)x[q].x);
-                    if (old == EMPTY_KEY || old == x[q].x) break;
-                    h = (h + 1) & (HT - 1);
-                }
-                hq[q] = h;
-                atomicMax(&s_pos[h], p + 1);
-            }
-            __syncthreads();
-#pragma unroll
-            for (int q = 0; q < QC; q++) {
-                const u32 p = base + q * TPB + threadIdx.x;
-                if (hq[q] >= (u32)HT || s_pos[hq[q]] != p + 1) continue;  // not the key's last in the chunk
-                const u64 hh = ws_hash(x[q].x);
-                u32 f = (u32)(hh >> 32) & (cap - 1);
-                for (;;) {  // cap >= 2 x the bucket's entries
-                    const u64 old = atomicCAS((unsigned long long*)&S.pool[off + f], (unsigned long long)EMPTY_KEY,
-                                              (unsigned long long)x[q].x);
-                    if (old == EMPTY_KEY || old == x[q].x) break;
-                    f = (f + 1) & (cap - 1);
-                }
-                __hip_atomic_store((u64*)&S.pool[off + f] + 1, (u64)x[q].y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                atomicOr((unsigned long long*)&s_bits[hh & (bw - 1)], (unsigned long long)ws_mask(hh));
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-        }
-    }
-    __syncthreads();
-    for (u32 i = threadIdx.x; i < bw; i += TPB) S.bits[((u64)b << w.e_bw_log) + i] = s_bits[i];
-}
-
-// S(e-1): the values of W(e-1) into the table, bucket b of that set
-__device__ __forceinline__ void ws_store_role(const WsJob& w, u32 b, Slot* table, u32 shift, u64 tmask, DevCtl* ctl) {
-    const WsSet& S = w.sset;
-    __shared__ u32 s_created;
-    if (threadIdx.x == 0) s_created = 0;
-    __syncthreads();
-    u32 created = 0;
-    if (b == 0 && threadIdx.x == 0) {
-        if (S.side[0]) {
-            if (!ctl->sp_claim) {
-                ctl->sp_claim = 1;
-                ctl->sp.st[0] = ctl->sp.st[1] = STAMP_PRESENT;
-                created++;
-            }
-            ctl->sp.val = S.side[1];
-        }
-        *S.pool_cnt = 0;  // E of this set has run (an earlier launch); the next E of this parity starts over
-    }
-    const u64 d = S.dir[b];
-    if ((d & 0xFF) != WS_NONE) {
-        const u64 off = d >> 8;
-        const u32 cap = 1u << (u32)(d & 0xFF);
-        constexpr int N = 2;
-        for (u32 base = 0; base < cap; base += N * TPB) {
-            u64x2 x[N];
-            u64 k[N], vx[N];
-            bool on[N], fr[N];
-            long long sl[N];
-#pragma unroll
-            for (int q = 0; q < N; q++) {
-                const u32 f = base + q * TPB + threadIdx.x;
-                x[q].x = EMPTY_KEY;
-                x[q].y = 0;
-                if (f < cap) x[q] = S.pool[off + f];
-                k[q] = x[q].x;
-                on[q] = k[q] != EMPTY_KEY;
-            }
-            pa_resolve<N, false>(table, shift, tmask, k, on, sl, fr, vx);
-#pragma unroll
-            for (int q = 0; q < N; q++) {
-                if (!on[q]) continue;
-                if (sl[q] < 0) {
-                    atomicOr(&ctl->err, ERR_TABLE_FULL);
-                } else {
-                    table[sl[q]].val = x[q].y;
-                    created += fr[q];
-                }
-            }
-        }
-    }
-    if (created) atomicAdd(&s_created, created);
-    __syncthreads();
-    if (threadIdx.x == 0 && s_created) atomicAdd(&w.created_acc[b % HM_CREATED_SLOTS], (u64)s_created);
-}
-
-// R(e-1): a Get of a key in W(e-1) takes the set's value; any other key its probe chain (quiet:
-// nothing in this launch ends a chain early or writes a value the chain could hold)
-__device__ __forceinline__ void ws_read_role(const ReadJob& j, const WsJob& w, u32 blk, const Slot* table, u32 shift,
-                                             u64 tmask, const DevCtl* ctl) {
-    const WsSet& S = w.sset;
-    const u64 q = (u64)blk * TPB + threadIdx.x;
-    if (q >= j.R) return;
-    const u64 k = j.keys[q];
-    u64 v = 0;
-    bool f = false;
-    if (k == EMPTY_KEY) {
-        if (S.side[0]) {
-            f = true;
-            v = S.side[1];
-        } else if (ctl->sp_claim) {
-            f = true;
-            v = ctl->sp.val;
-        }
-    } else {
-        u64 sl = table_home(k, shift);
-        const u64 hh = ws_hash(k);
-        const u64 b = sl >> w.s_bk_shift;
-        const u64 wd = S.bits[(b << w.s_bw_log) | (hh & ((1ull << w.s_bw_log) - 1))];
-        u64x2 x = *(const u64x2*)&table[sl];
-        u64 kk = x.x, vv = x.y;
-        asm volatile("" : "+v"(kk), "+v"(vv));
-        for (u64 pr = 0; pr <= tmask; pr++) {
-            if (kk == k) {
-                f = true;
-                v = vv;
-                break;
-            }
-            if (kk == EMPTY_KEY) break;
-            sl = (sl + 1) & tmask;
-            x = *(const u64x2*)&table[sl];
-            kk = x.x;
-            vv = x.y;
-        }
-        const u64 m = ws_mask(hh);
-        if ((wd & m) == m && !(w.exp & 16)) {  // maybe written in the round: its set entry, if any, is the value
-            const u64 d = S.dir[b];
-            if ((d & 0xFF) != WS_NONE) {
-                const u64 off = d >> 8;
-                const u32 cmask = (1u << (u32)(d & 0xFF)) - 1;
-                for (u32 fi = (u32)(hh >> 32) & cmask, pr = 0; pr <= cmask; pr++, fi = (fi + 1) & cmask) {
-                    const u64x2 y = S.pool[off + fi];
-                    if (y.x == k) {
-                        f = true;
-                        v = y.y;
-                        break;
-                    }
-                    if (y.x == EMPTY_KEY) break;
-                }
-            }
-        }
-    }
-    st_out(&j.vals[q], f ? v : (u64)0, j.plain);
-    st_out(&j.found[q], (uint8_t)(f ? 1 : 0), j.plain);
-}
-
-// One write-set launch: [P tiles][S buckets][R blocks (ra)][E buckets][R blocks][tail block].
-template <int K1, int HT>
-__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(8))) void hm_ws_kernel(WsJob w, ReadJob rj,
-                                                                                        Slot* table, u32 shift,
-                                                                                        u64 tmask, DevCtl* ctl) {
-    extern __shared__ __attribute__((aligned(16))) char s_lds[];
-    u32 b = blockIdx.x;
-    if ((rj.s_seq || rj.e_out) && b == gridDim.x - 1) {  // the tail block (as hm_round_kernel's)
-        if (rj.e_out && threadIdx.x == 0) *rj.e_out = atomicExch(&ctl->err, 0u);
-        if (rj.s_seq && threadIdx.x < HM_DUP_SLOTS) {
-            u64 v = atomicExch((unsigned long long*)&rj.s_acc[threadIdx.x], 0ull);
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-            if (threadIdx.x == 0) {
-                rj.s_host[1] = v;
-                __threadfence_system();
-                rj.s_host[0] = rj.s_seq;
-            }
-        }
-        return;
-    }
-    if (b < w.np) {
-        if (w.exp & 4) {
-            if (threadIdx.x == 0) __hip_atomic_fetch_add(w.done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return;
-        }
-        ws_part_role<K1>(w, b, shift, s_lds);
-        return;
-    }
-    b -= w.np;
-    if (b < w.ns) {
-        if (!(w.exp & 1)) ws_store_role(w, b, table, shift, tmask, ctl);
-        return;
-    }
-    b -= w.ns;
-    if (b < w.ra) {
-        if (!(w.exp & 8)) ws_read_role(rj, w, b, table, shift, tmask, ctl);
-        return;
-    }
-    b -= w.ra;
-    if (b < w.ne) {
-        if (!(w.exp & 2)) ws_build_role<HT>(w, b, s_lds, ctl);
-        return;
-    }
-    b -= w.ne;
-    if (!(w.exp & 8)) ws_read_role(rj, w, w.ra + b, table, shift, tmask, ctl);
 }
 
 // ---- small rounds: one workgroup, one launch (the flat combiner's batches) ----------------------
@@ -2003,16 +1511,14 @@ static hipError_t launch(nrg_ctx* c, Launch& L) {
     L.rj.quiet = (L.ix != IX_STAMP || nix == 0) && L.aj.nblocks == 0;
     u32 blocks = nix + L.aj.nblocks + L.rj.nblocks;
     if (blocks == 0) return hipSuccess;
-    // a pending skew sample, or the error copy of a launch that ends a round (no index role:
-    // earlier kernels of the round, the partition apply's claims included, have latched their errors)
-    const bool err_here = c->err_out && nix == 0;
-    if (c->sample_seq || err_here) {  // the launch's last block
+    // a pending skew sample rides in the launch's last block. (The combiner's error copy,
+    // c->err_out, is taken only by hm_small_round_kernel, whose last write it is: a multi-block
+    // launch's tail block may run before its other blocks' responses land, nrg_combiner retire().)
+    if (c->sample_seq) {
         L.rj.s_acc = c->d_dup + ((c->dup_seq - 1) & 1) * HM_DUP_SLOTS;  // the window just ended
         L.rj.s_host = c->h_dup_dev;
         L.rj.s_seq = c->sample_seq;
-        L.rj.e_out = err_here ? c->err_out : nullptr;
         c->sample_seq = 0;
-        if (err_here) c->err_out = nullptr;
         blocks++;
     }
     unsigned lds = 0;
@@ -2037,176 +1543,11 @@ static hipError_t launch(nrg_ctx* c, Launch& L) {
     return hipGetLastError();
 }
 
-// ---- write-set rounds (host) ----
-static u64* ws_ctl(nrg_ctx* c) {  // {done, pool counters (2 x u32)}
-    return (u64*)((char*)c->d_ws + 2 * (c->ws_pool_slots * 16 + HM_BK_MAX * 8 + c->ws_bits_words * 8 + 16));
-}
-
-static WsSet ws_set(nrg_ctx* c, u32 par) {
-    char* base = (char*)c->d_ws + par * (c->ws_pool_slots * 16 + HM_BK_MAX * 8 + c->ws_bits_words * 8 + 16);
-    WsSet s;
-    s.pool = (u64x2*)base;
-    s.dir = (u64*)(base + c->ws_pool_slots * 16);
-    s.bits = s.dir + HM_BK_MAX;
-    s.side = s.bits + c->ws_bits_words;
-    s.pool_cnt = (u32*)(ws_ctl(c) + 1) + par;
-    s.pool_slots = c->ws_pool_slots;
-    return s;
-}
-
-struct WsLaunch {
-    WsJob w{};
-    ReadJob rj{};
-    u32 K1 = 1, ht = 512;
-    u32 rblocks = 0;
-};
-
-// the pending write set's S and R ride in this launch
-static void ws_attach(nrg_ctx* c, WsLaunch& L) {
-    const HmDeferred& p = c->pend;
-    if (p.valid && p.ws) {
-        L.w.ns = 1u << p.nb_log;
-        L.w.sset = ws_set(c, p.wpar);
-        L.w.s_bk_shift = p.bk_shift;
-        L.w.s_bw_log = p.bw_log;
-        L.rj.keys = p.keys;
-        L.rj.R = p.R;
-        L.rj.vals = p.vals;
-        L.rj.found = p.found;
-        c->pend = HmDeferred{};
-    }
-}
-
-template <int K1, int HT>
-static void ws_launch_k(nrg_ctx* c, const WsLaunch& L, u32 blocks, unsigned lds) {
-    NRG_LAUNCH(c, "hm_round", (hm_ws_kernel<K1, HT>), blocks, TPB, lds, c->stream, L.w, L.rj, c->d_table, c->slot_shift,
-               (u64)(c->slots - 1), c->d_ctl);
-}
-
-static hipError_t ws_launch(nrg_ctx* c, WsLaunch& L) {
-    WsJob& w = L.w;
-    ReadJob& rj = L.rj;
-    w.created_acc = c->d_created;
-    w.exp = c->exp >> 20;
-    rj.nblocks = (u32)((rj.R + TPB - 1) / TPB);
-    rj.quiet = true;
-    rj.plain = (c->exp >> 6) & 1;  // responses streamed (they drain while the launch runs)
-    const u32 rb = rj.nblocks;
-    // E after ws_epos % of the read blocks, its first block a multiple of 8 (buckets dealt to XCDs in
-    // contiguous ranges) when the read blocks allow it
-    w.ra = 0;
-    w.e_xcd = false;
-    if (w.ne) {
-        u32 ra = (u32)((u64)rb * c->ws_epos / 100);
-        const u32 pad = (8 - (w.np + w.ns + ra) % 8) % 8;
-        if (ra + pad <= rb) {
-            ra += pad;
-            w.e_xcd = true;
-        } else {
-            w.e_xcd = (w.np + w.ns + ra) % 8 == 0;
-        }
-        w.ra = ra;
-    }
-    u32 blocks = w.np + w.ns + rb + w.ne;
-    if (blocks == 0) return hipSuccess;
-    const bool err_here = c->err_out && w.np == 0;  // a launch that ends a round copies the error latch
-    if (c->sample_seq || err_here) {
-        rj.s_acc = c->d_dup + ((c->dup_seq - 1) & 1) * HM_DUP_SLOTS;
-        rj.s_host = c->h_dup_dev;
-        rj.s_seq = c->sample_seq;
-        rj.e_out = err_here ? c->err_out : nullptr;
-        c->sample_seq = 0;
-        if (err_here) c->err_out = nullptr;
-        blocks++;
-    }
-    unsigned lds = 0;
-    if (w.np) {
-        const u32 nb = 1u << w.ij.nb_log, nt = w.ij.nblocks, bw = 1u << w.e_bw_log;
-        const unsigned lp = 12 * nb;
-        const unsigned le = L.ht * 16 + bw * 8 + (nt + 1) * 4 + nt * 2;
-        lds = ((lp > le ? lp : le) + 15) & ~15u;
-    }
-    if (!w.np) ws_launch_k<1, 512>(c, L, blocks, 0);
-#define NRG_WK(KK, HH) else if (L.K1 == KK && L.ht == HH) ws_launch_k<KK, HH>(c, L, blocks, lds)
-    NRG_WK(1, 512); NRG_WK(4, 512); NRG_WK(1, 1024); NRG_WK(4, 1024);
-#undef NRG_WK
-    else return hipErrorInvalidValue;
-    return hipGetLastError();
-}
-
 hipError_t hm_flush(nrg_ctx* c) {
     if (!c->pend.valid) return hipSuccess;
-    if (c->pend.ws) {  // {S | R} of the pending write set
-        WsLaunch L;
-        ws_attach(c, L);
-        return ws_launch(c, L);
-    }
     Launch L;
     attach_deferred(c, L);
     return launch(c, L);
-}
-
-// One write-set round: {P(e) | E(e)} of these records, with the previous set's {S | R} beside them.
-static hipError_t ws_round(nrg_ctx* c, const nrg_put* src, u64 lo, u64 n, bool write_ring, const u64* keys, u64 R,
-                           u64* vals, uint8_t* found) {
-    hipError_t e;
-    if (c->pend.valid && !c->pend.ws && (e = hm_flush(c)) != hipSuccess) return e;  // a stamp / partition round's half
-    WsLaunch L;
-    ws_attach(c, L);
-    const u32 K1 = n <= (1u << 14) ? 1u : 4u;  // (K1 = 2 compiles with a scratch frame)
-    const u32 tile = TPB * K1;
-    const u32 log2_slots = 64 - c->slot_shift;
-    u32 nb_log = 0;
-    while (((u64)c->ws_per << nb_log) < n && (1u << nb_log) < HM_BK_MAX) nb_log++;
-    if (nb_log > log2_slots) nb_log = log2_slots;
-    const u64 per_b = (n >> nb_log) + 1;  // Puts per bucket, expected
-    u32 bw_log = 3;                       // >= 16 filter bits per expected key
-    while ((16ull << bw_log) < per_b && bw_log < WS_BW_LOG_MAX) bw_log++;
-    L.K1 = K1;
-    L.ht = per_b <= 128 ? 512u : 1024u;  // at most HT / 2 distinct keys per bucket on the LDS path
-    const u32 par = c->ws_par;
-    WsJob& w = L.w;
-    IndexJob& ij = w.ij;
-    ij.rec = ring_src(c, src, lo);
-    ij.ring_out = write_ring ? (nrg_put*)c->d_ring : nullptr;
-    ij.n = n;
-    ij.nblocks = (u32)((n + tile - 1) / tile);
-    ij.nb_log = nb_log;
-    ij.bk_shift = log2_slots - nb_log;
-    ij.ent = (u64x2*)c->d_bk_ent;
-    ij.eidx = nullptr;
-    ij.cnt = c->d_bk_cnt;
-    ij.exp = 0;
-    ij.dup_acc = nullptr;
-    ij.plain = c->ws_plain || ((c->exp >> 6) & 1);
-    ij.ent_bytes = (u32)(((c->cfg.max_batch + TPB - 1) / TPB) * TPB * 16);
-    w.np = ij.nblocks;
-    c->ws_tiles += w.np;
-    w.done = ws_ctl(c);
-    w.target = c->ws_tiles;
-    w.ne = 1u << nb_log;
-    w.e_nb_log = nb_log;
-    w.e_bw_log = bw_log;
-    w.tile = tile;
-    w.eset = ws_set(c, par);
-    w.dup_acc = c->d_dup + (c->dup_seq & 1) * HM_DUP_SLOTS;
-    if ((e = ws_launch(c, L)) != hipSuccess) return e;
-    c->ws_par ^= 1;
-    HmDeferred& p = c->pend;
-    p = HmDeferred{};
-    p.valid = true;
-    p.ws = true;
-    p.wpar = par;
-    p.nb_log = nb_log;
-    p.bw_log = bw_log;
-    p.bk_shift = log2_slots - nb_log;
-    p.lo = lo;
-    p.n = n;
-    p.keys = keys;
-    p.R = R;
-    p.vals = vals;
-    p.found = found;
-    return hipSuccess;
 }
 
 // Reads against the current state (no writes): attached to the deferred round if it has none.
@@ -2255,21 +1596,10 @@ hipError_t hm_alloc(nrg_ctx* c, u64 mb) {
     void* dp = nullptr;
     if ((e = hipHostGetDevicePointer(&dp, h, 0)) != hipSuccess) return e;
     c->h_dup_dev = (u64*)dp;
-    // write-set rounds: per parity a pool of 4 n + 16 nb {key, value} slots (every bucket's table has
-    // < 4x its keys, or its entries, and >= 16 slots), a dir word and a filter array per bucket, the
-    // side key's words; then the done counter and the two pool counters
-    c->ws_max = mb < WS_MAX ? mb : WS_MAX;
-    c->ws_pool_slots = 4 * c->ws_max + 16ull * HM_BK_MAX;
-    c->ws_bits_words = (u64)HM_BK_MAX << WS_BW_LOG_MAX;
-    const u64 ws_bytes = 2 * (c->ws_pool_slots * 16 + HM_BK_MAX * 8 + c->ws_bits_words * 8 + 16) + 64;
-    if ((e = hipMalloc(&c->d_ws, ws_bytes)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(c->d_ws, 0, ws_bytes, c->stream)) != hipSuccess) return e;
     return hipSuccess;
 }
 
 void hm_free(nrg_ctx* c) {
-    if (c->d_ws) (void)hipFree(c->d_ws);
-    c->d_ws = nullptr;
     for (int i = 0; i < 2; i++) {
         if (c->d_put_slot[i]) (void)hipFree(c->d_put_slot[i]);
         c->d_put_slot[i] = nullptr;
@@ -2332,22 +1662,9 @@ hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool
         c->rounds++;
         return e;
     }
-    hipError_t e;
-    // Write-set rounds (NRG_KNOB_WS): rounds without previous values of <= ws_max Puts on unskewed
-    // key streams (NRG_KNOB_PART = 2 keeps partition rounds for every round, for tests)
-    const bool ws = c->ws_mode && c->ws_max && !want_prev && n <= c->ws_max && c->part_mode != 2 &&
-                    (!c->skewed || c->ws_mode >= 2);
-    if (ws) {
-        if ((e = ws_round(c, src, lo, n, write_ring, d_get_keys, R, d_get_vals, d_get_found)) != hipSuccess) return e;
-        c->rounds++;
-        c->dup_puts += n;  // the round's E counts the Puts a later Put of their key overwrote
-        if (++c->dup_rounds >= c->dup_every && (e = skew_sample(c)) != hipSuccess) return e;
-        if (!c->pipeline) return hm_flush(c);
-        return hipSuccess;
-    }
-    if (c->pend.valid && c->pend.ws && (e = hm_flush(c)) != hipSuccess) return e;  // a write set's {S | R}
     // records the deferred half reads: the caller's buffer only when no ring copy is written
     const nrg_put* keep = (src && !write_ring) ? src : nullptr;
+    hipError_t e;
     u32 epoch;
     if ((e = next_epoch(c, &epoch)) != hipSuccess) return e;
     Launch L;

@@ -63,10 +63,6 @@ struct HmDeferred {
     u64 R = 0;
     u64* vals = nullptr;
     uint8_t* found = nullptr;
-    // write-set round (hm_ws_kernel): the set of parity wpar still goes into the table (S) and
-    // answers the reads; its geometry
-    bool ws = false;
-    u32 wpar = 0, nb_log = 0, bw_log = 0, bk_shift = 0;
 };
 
 // A stack chunk whose finish (cross-tile Pops, commit) has not run yet (stack.hip).
@@ -151,17 +147,6 @@ struct nrg_ctx {
     uint32_t epoch = 1;  // epoch of the last replay round (1: prefill / before any round)
     uint32_t epoch_limit = 0xFFFFFFF0u;  // renormalise stamps here (NRG_KNOB_EPOCH_LIMIT for tests)
     uint32_t* d_put_slot[2] = {nullptr, nullptr};
-    // Write-set rounds (hashmap.hip hm_ws_kernel): one launch per round, no device atomic per Put.
-    uint32_t ws_mode = 0;      // NRG_KNOB_WS: 0 never; 1 rounds of <= ws_max Puts without previous
-                               // values on unskewed streams; 2 skewed streams too
-    uint64_t ws_max = 0;       // largest write-set round (Puts); 0: scratch not allocated
-    uint32_t ws_per = 128;     // NRG_KNOB_WS_PER: Puts per bucket the round geometry aims at
-    uint32_t ws_epos = 25;     // NRG_KNOB_WS_EPOS: % of the read blocks dispatched before the E blocks
-    uint32_t ws_plain = 1;     // log copy with plain (1) or streaming (0) stores (NRG_KNOB_EXP bit 6 aside)
-    uint32_t ws_par = 0;       // parity of the next write set
-    uint64_t ws_tiles = 0;     // P tiles launched so far (E waits for the device counter to reach it)
-    void* d_ws = nullptr;      // [2] pools, [2] dirs, [2] filter arrays, [2] side words, ctl words
-    uint64_t ws_pool_slots = 0, ws_bits_words = 0;
     // Key skew (hm_dup_sample_kernel): Puts combined inside their index block, sampled every
     // dup_every rounds into mapped host memory; a skewed stream takes partition rounds.
     uint64_t* d_dup = nullptr;            // [HM_DUP_SLOTS]

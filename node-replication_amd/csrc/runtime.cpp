@@ -1169,22 +1169,6 @@ extern "C" int nrg_test_set_knob(nrg_ctx* c, int knob, uint64_t v) {
             if (v < 1 || v > 4) return NRG_E_INVAL;
             c->comb_depth = (uint32_t)v;
             return NRG_OK;
-        case NRG_KNOB_WS:
-            if (!hm || v > 2) return NRG_E_INVAL;
-            c->ws_mode = (uint32_t)v;
-            return NRG_OK;
-        case NRG_KNOB_WS_PER:
-            if (!hm || v < 16 || v > 4096) return NRG_E_INVAL;
-            c->ws_per = (uint32_t)v;
-            return NRG_OK;
-        case NRG_KNOB_WS_EPOS:
-            if (!hm || v > 100) return NRG_E_INVAL;
-            c->ws_epos = (uint32_t)v;
-            return NRG_OK;
-        case NRG_KNOB_WS_PLAIN:
-            if (!hm || v > 1) return NRG_E_INVAL;
-            c->ws_plain = (uint32_t)v;
-            return NRG_OK;
         case NRG_KNOB_PIPELINE:
             if (v > 1) return NRG_E_INVAL;
             c->pipeline = v != 0;

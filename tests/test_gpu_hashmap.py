@@ -35,7 +35,7 @@ def _check_state(dev, om):
 
 # knobs of the replay paths: default selection, partition rounds for every round, and the
 # one-launch small rounds (the combiner's) for rounds of up to 2048 Puts
-PATHS = {"default": {}, "stamp": {"WS": 0}, "ws": {"WS": 1}, "ws_fine": {"WS": 1, "WS_PER": 16}, "part": {"PART": 2}, "wide": {"PART": 2, "PA_TPB": 1024}, "w512": {"PART": 2, "PA_TPB": 512},
+PATHS = {"default": {}, "part": {"PART": 2}, "wide": {"PART": 2, "PA_TPB": 1024}, "w512": {"PART": 2, "PA_TPB": 512},
          "small": {"SMALL_MAX": 2048}}
 
 
@@ -146,27 +146,17 @@ def test_fused_round_device(nrg, orc):
     _check_state(dev, om)
 
 
-WS_PATHS = {"ws": {"WS": 1}, "ws_e0": {"WS": 1, "WS_EPOS": 0}, "ws_e100": {"WS": 1, "WS_EPOS": 100},
-            "ws_fine": {"WS": 1, "WS_PER": 16}, "ws_crowd": {"WS": 1, "WS_PER": 4096}, "ws_nt": {"WS": 1, "WS_PLAIN": 0},
-            "stamp": {"WS": 0}, "part": {"PART": 2},
-            "wide": {"PART": 2, "PA_TPB": 1024}}
-
-
-@pytest.mark.parametrize("path", list(WS_PATHS))
+@pytest.mark.parametrize("path", ["stamp", "part", "wide"])
 def test_pipelined_rounds_back_to_back(nrg, orc, path):
     """config.pipeline = 1: rounds enqueued back to back, no host sync in between. Each round's
     reads run in the next round's launch, beside its index pass (and, for stamp rounds, beside
     the apply of their own round's writes), and must see exactly their own round's state (keys
     created by later rounds invisible, values overwritten later not yet there).
     Knob PART = 2 sends every round through partition rounds instead (their reads ride in the
-    next round's partition launch); PA_TPB = 1024 applies them with 1024-thread workgroups.
-    Write-set rounds (the default below 393216 Puts): a round's set is built in its launch and goes
-    into the table in the next, beside its reads; ws_e0 / ws_e100 place the set-building workgroups
-    before / after every read block, ws_fine uses buckets of ~16 Puts, ws_crowd ~4096 (every bucket
-    past the LDS path: built in global memory chunk by chunk), ws_nt a streamed log copy."""
+    next round's partition launch); PA_TPB = 1024 applies them with 1024-thread workgroups."""
     import torch
 
-    knobs = WS_PATHS[path]
+    knobs = {"part": {"PART": 2}, "wide": {"PART": 2, "PA_TPB": 1024}}.get(path, {})
     dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, knobs=knobs, log2_slots=17, max_batch=1 << 14, pipeline=1)
     dev.use_torch_stream()
     om = orc.HashMap()
@@ -348,8 +338,8 @@ def _mix64(x):
         return x ^ (x >> np.uint64(31))
 
 
-@pytest.mark.parametrize("knobs", [{}, {"WS": 1}, {"WS": 1, "WS_PER": 16}, {"PART": 2}, {"PART": 2, "STALL": 1},
-                                   {"PART": 2, "PA_TPB": 1024, "STALL": 1}, {"PART": 2, "PA_TPB": 512, "STALL": 1}])
+@pytest.mark.parametrize("knobs", [{}, {"PART": 2}, {"PART": 2, "STALL": 1}, {"PART": 2, "PA_TPB": 1024, "STALL": 1},
+                                   {"PART": 2, "PA_TPB": 512, "STALL": 1}])
 def test_one_bucket_rounds(nrg, orc, knobs):
     """Pipelined rounds whose keys all fall into ONE slot bucket (many chunks, finer parts,
     duplicates across index tiles), with side-slot keys and a Zipf round, against the oracle.
@@ -419,7 +409,7 @@ def _bucket_rounds(nrg, orc, dev, om, rounds):
     assert dev.hm_digest() == om.digest()
 
 
-@pytest.mark.parametrize("knobs", [{"PART": 1}, {"PART": 1, "WS": 1}, {"PART": 2}, {"PART": 2, "PA_TPB": 256}])
+@pytest.mark.parametrize("knobs", [{"PART": 1}, {"PART": 2}, {"PART": 2, "PA_TPB": 256}])
 def test_large_pipelined_rounds(nrg, orc, knobs):
     """Large pipelined rounds (300k-400k Puts: 2048-Put partition tiles, 256 wide buckets, or 1024
     with PA_TPB = 256): uniform and Zipf rounds with side-slot keys and a small round in between,
@@ -438,7 +428,7 @@ def test_large_pipelined_rounds(nrg, orc, knobs):
     _bucket_rounds(nrg, orc, dev, om, rounds)
 
 
-@pytest.mark.parametrize("knobs", [{"PART": 1}, {"PART": 1, "WS": 1}, {"PART": 2}, {"PART": 2, "PA_TPB": 1024}])
+@pytest.mark.parametrize("knobs", [{"PART": 1}, {"PART": 2}, {"PART": 2, "PA_TPB": 1024}])
 def test_crowded_bucket_rounds(nrg, orc, knobs):
     """2500 new keys of a round home into the first 4096 slots of the table (one partition bucket,
     taken in several chunks; their claims crowd one region, long probe chains), repeated and
@@ -455,16 +445,15 @@ def test_crowded_bucket_rounds(nrg, orc, knobs):
     _bucket_rounds(nrg, orc, dev, om, rounds)
 
 
-@pytest.mark.parametrize("ws", [1, 0])
-def test_b1_full_size_rounds(nrg, orc, ws):
+def test_b1_full_size_rounds(nrg, orc):
     """BASELINE configs[1] at full size: 2^26-slot table, prefill [0, 2^23) -> k+1, uniform keys
-    over 10M, rounds of 100k Puts + 900k Gets (write-set rounds; ws = 0: stamp rounds), then an
-    800k-Put round (the per-GPU replay at 8 GPUs, partition round) -- every Get response and the
-    final replica digest bit-exact against the sequential oracle."""
+    over 10M, rounds of 100k Puts + 900k Gets (stamp election), then an 800k-Put round (the
+    per-GPU replay at 8 GPUs, bucket election) -- every Get response and the final replica
+    digest bit-exact against the sequential oracle."""
     import torch
 
-    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, knobs={"WS": ws}, log2_slots=26, max_batch=1 << 20,
-                            pipeline=1, log_bytes=64 * 4 * (1 << 20))
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=26, max_batch=1 << 20, pipeline=1,
+                            log_bytes=64 * 4 * (1 << 20))
     dev.use_torch_stream()
     om = orc.HashMap()
     dev.hm_prefill_range(1 << 23, 1)
