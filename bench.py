@@ -233,6 +233,7 @@ class Env:
         if args.share_gpu:
             local = 0  # rehearsal of the N > 1 path with every rank on the box's one GPU (gloo only)
         self.local = local
+        self.opening = args.opening
         torch.cuda.set_device(local)
         self.dev = torch.device("cuda", local)
         # one non-blocking stream for the replica and this process's torch work (the null
@@ -258,6 +259,16 @@ class Env:
         try:
             if self.world > 1:
                 dist.barrier()
+            if self.opening == "spin":
+                # wait for the device with the host thread awake (a blocking sync parks it, and the
+                # first calls after the wake-up ran 20-80 us slow), then keep the core busy briefly
+                ev = torch.cuda.Event()
+                ev.record()
+                while not ev.query():
+                    pass
+                t_end = time.perf_counter() + 1e-3
+                while time.perf_counter() < t_end:
+                    pass
             torch.cuda.synchronize()
             t = time.perf_counter()
             marks = [t]
@@ -841,6 +852,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-prev-variant", action="store_true")
+    ap.add_argument("--opening", choices=["sync", "spin"], default="spin",
+                    help="how the timed region's opening sync waits: polled with the host thread awake, then "
+                         "torch.cuda.synchronize (default; profiles/r05_opening_ab.txt), or the plain sync alone")
     ap.add_argument("--no-kernel-timing", action="store_true", help="diagnostic: no HIP events in the timed region")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo: CPU rehearsal)")
