@@ -249,7 +249,7 @@ class Env:
 
     first_calls = []  # host us of the first step of every timed region of the process (diagnostic)
 
-    def timed(self, n, step, rep, host_s=None):
+    def timed(self, n, step, rep, host_s=None, finish=None):
         """Barrier + sync, K steps, the replica's deferred work launched, sync + barrier; max over
         ranks of the wall time."""
         torch, dist = self.torch, self.dist
@@ -276,7 +276,12 @@ class Env:
                 step(i)
                 if i < 3:
                     marks.append(time.perf_counter())
-            rep.join()  # launches the last round's deferred apply + reads: inside the timed region
+            # launches the last round's deferred apply + reads (and completes a pipelined group
+            # round): inside the timed region
+            if finish is not None:
+                finish()
+            else:
+                rep.join()
             if host_s is not None:
                 host_s[0] = time.perf_counter() - t
                 host_s[1:] = [round((b - a) * 1e6, 2) for a, b in zip(marks, marks[1:])]
@@ -457,7 +462,7 @@ def run_hashmap(args, env):
         prev = mode["prev"]
         if pgroup is not None:
             pp, gp = ptrs[p]
-            pgroup.round(pp, W, gp, R, gv_p, gf_p, pv_p if prev else None, pf_p if prev else None)
+            pgroup.round_async(pp, W, gp, R, gv_p, gf_p, pv_p if prev else None, pf_p if prev else None)
         elif cgroup is not None:
             pp, gp = ptrs[p]
             # every rank's segment is W records: seg_lens keeps the round stream ordered (no length
@@ -476,9 +481,14 @@ def run_hashmap(args, env):
                 gathered[i + 1] = group.gather_async(puts[(i + 1) % P, :W], stride=W)
             group.replay(g, gkeys[p, :R], gvals, gfound, pvals if prev else None, pfound if prev else None)
 
+    def finish():
+        if pgroup is not None:
+            pgroup.flush()  # the last pipelined round
+        rep.join()
+
     def run(n, prev=False, host_s=None):
         mode["prev"], mode["n"] = prev, n
-        return env.timed(n, step, rep, host_s)
+        return env.timed(n, step, rep, host_s, finish=finish)
 
     mode["n"] = args.warmup
     WATCH.phase = "warmup rounds"

@@ -411,9 +411,21 @@ int nrg_hashmap_prefill_partition(nrg_ctx* ctx, uint64_t n, uint64_t off, uint32
 /* One partitioned round on every local member (group of hashmap replicas, one partition each,
  * rank = partition): rounds[i].recs / n = the member's Puts (nrg_put), get_keys / n_gets its Gets;
  * get_vals / get_found and (nullable) resp / some = the Gets' answers and the Puts' previous values,
- * in the member's order. Exchanges with ncclSend / ncclRecv; returns after the counts exchange
- * (one host round trip), the rest is stream ordered (nrg_group_sync waits). */
+ * in the member's order. A round is one fused partition launch (owner regions, no global scan), an
+ * all-gather of every rank's per-owner counts, ncclSend / ncclRecv of the Puts and Get keys to
+ * their owners (a rank's own part stays on its GPU), the owner's replay, the answers back and one
+ * route-back launch. Everything is on the replica's stream. Returns once the round is queued,
+ * after one host round trip for the counts (nrg_group_sync waits for the rest). Fails with the
+ * same code on every rank when any rank's part is bad, before any payload moves. */
 int nrg_group_partitioned_round(nrg_group* g, const nrg_round* rounds);
+/* The pipelined form: queues this round's partition and count exchange, then completes the
+ * previous round posted this way (its counts have landed by then, so the host never waits on the
+ * GPU in steady state). The caller's buffers of a round stay borrowed until the next
+ * nrg_group_partitioned_round_async / nrg_group_partitioned_flush / nrg_group_sync, which completes
+ * it; the return value is the completed round's (NRG_OK before there is one). */
+int nrg_group_partitioned_round_async(nrg_group* g, const nrg_round* rounds);
+/* Complete the round posted by nrg_group_partitioned_round_async, if any (its result). */
+int nrg_group_partitioned_flush(nrg_group* g);
 
 /* ---- device memory helpers (for callers without their own allocator) ----------------- */
 int nrg_dev_alloc(nrg_ctx* ctx, uint64_t bytes, void** d_ptr);

@@ -82,9 +82,12 @@ struct DBuf {
     uint64_t bytes = 0;
 };
 
-// Partitioned rounds (nrg_group_partitioned_round): buffers of one member.
-enum PtBuf { PB_POUT, PB_PPOS, PB_KOUT, PB_GPOS, PB_CNT, PB_ALLCNT, PB_RPUT, PB_RKEY, PB_RVAL, PB_RFOUND, PB_RPREV,
-             PB_RPREVF, PB_AVAL, PB_AFOUND, PB_APREV, PB_APREVF, PB_ST, PB_ALLST, PB_N };
+// Partitioned rounds (nrg_group_partitioned_round*): buffers of one member. A round's partition
+// output and count exchange (PtPar) alternate between two parities: round e+1 is partitioned and
+// its counts exchanged before round e's payload moves (the pipelined form), the rest is per round.
+enum PtBuf { PB_RPUT, PB_RKEY, PB_RVAL, PB_RFOUND, PB_RPREV, PB_RPREVF, PB_AVAL, PB_AFOUND, PB_APREV, PB_APREVF,
+             PB_ST, PB_ALLST, PB_DESC, PB_N };
+enum PtPar { PP_POUT, PP_PPOS, PP_KOUT, PP_GPOS, PP_CNT, PP_ALLCNT, PP_N };
 
 constexpr uint64_t GC_FROM_HEAD = 32 * 256;  // nr/src/log.rs:36 (the ring keeps this much free)
 
@@ -103,9 +106,14 @@ struct Member {
     bool used[NBUF] = {};
     void* sbuf = nullptr;  // padded send copy when a segment is shorter than the stride
     uint64_t sbytes = 0;
-    DBuf pt[PB_N];               // partitioned rounds
-    std::vector<uint64_t> hcnt;  // [nranks][2 * nranks + XW_N] counts, capacities, flags
-    uint64_t xwords[8] = {};     // this rank's host words of the exchange
+    DBuf pt[PB_N];          // partitioned rounds
+    DBuf pp[2][PP_N];       // ... by round parity
+    uint64_t* h_cnt[2] = {};  // pinned: [nranks][2 * nranks + XW_N] counts, capacities, flags (by parity)
+    hipEvent_t cnt_ev[2] = {};  // the counts of that parity are in h_cnt
+    nrg_round pr[2] = {};       // the caller's part of the round of that parity
+    uint64_t cap_p[2] = {}, cap_k[2] = {};  // its owner-region capacities (the member's n, n_gets)
+    uint32_t pt_epoch = 0;      // look-back descriptor tag of the last fused partition
+    uint64_t xwords[8] = {};    // this rank's host words of the exchange
     hipEvent_t pt_ev = nullptr;
     // Round headers and the length exchange (allocated at join, so a round cannot fail on them):
     //   hdr[b]  {n, fingerprint of seg_lens} sent with round b's segment; ghdr[b] every rank's
@@ -132,8 +140,7 @@ int hip_rc(hipError_t e) { return e == hipSuccess ? NRG_OK : (e == hipErrorOutOf
         if (_r != NRG_OK) return _r;              \
     } while (0)
 
-int grow(Member& m, PtBuf k, uint64_t bytes) {
-    DBuf& d = m.pt[k];
+int grow_buf(Member& m, DBuf& d, uint64_t bytes) {
     if (d.bytes >= bytes) return NRG_OK;
     GCHK(hipStreamSynchronize(m.cstream));
     GCHK(hipStreamSynchronize(m.ctx->stream));
@@ -145,6 +152,7 @@ int grow(Member& m, PtBuf k, uint64_t bytes) {
     d.bytes = b;
     return NRG_OK;
 }
+int grow(Member& m, PtBuf k, uint64_t bytes) { return grow_buf(m, m.pt[k], bytes); }
 
 // `to` waits for the work queued on `from` so far
 int order(Member& m, hipStream_t from, hipStream_t to) {
@@ -169,6 +177,7 @@ int member_init(Member& m, int nranks) {
     GCHK(hipStreamCreateWithFlags(&m.cstream, hipStreamNonBlocking));
     GCHK(hipEventCreateWithFlags(&m.in_ev, hipEventDisableTiming));
     GCHK(hipEventCreateWithFlags(&m.pt_ev, hipEventDisableTiming));
+    for (int q = 0; q < 2; q++) GCHK(hipEventCreateWithFlags(&m.cnt_ev[q], hipEventDisableTiming));
     for (int b = 0; b < NBUF; b++) {
         GCHK(hipEventCreateWithFlags(&m.gathered[b], hipEventDisableTiming));
         GCHK(hipEventCreateWithFlags(&m.freed[b], hipEventDisableTiming));
@@ -185,9 +194,12 @@ int member_init(Member& m, int nranks) {
     GCHK(hipHostMalloc(&m.h_glx, 2 * G * 8, hipHostMallocDefault));
     // the fixed-size buffers of a partitioned round's count and status exchanges
     const uint64_t CW = 2 * G + XW_N;
-    if ((r = grow(m, PB_CNT, CW * 8)) || (r = grow(m, PB_ALLCNT, G * CW * 8)) || (r = grow(m, PB_ST, 8)) ||
-        (r = grow(m, PB_ALLST, G * 8)))
-        return r;
+    for (int q = 0; q < 2; q++) {
+        if ((r = grow_buf(m, m.pp[q][PP_CNT], CW * 8)) || (r = grow_buf(m, m.pp[q][PP_ALLCNT], G * CW * 8))) return r;
+        // mapped: a one-rank group's partition writes its counts here directly (no exchange)
+        GCHK(hipHostMalloc(&m.h_cnt[q], G * CW * 8, hipHostMallocMapped));
+    }
+    if ((r = grow(m, PB_ST, 8)) || (r = grow(m, PB_ALLST, G * 8))) return r;
     return NRG_OK;
 }
 
@@ -229,6 +241,12 @@ void member_free(Member& m, const Rccl* R) {
     if (m.h_glx) (void)hipHostFree(m.h_glx);
     for (DBuf& d : m.pt)
         if (d.p) (void)hipFree(d.p);
+    for (int q = 0; q < 2; q++) {
+        for (DBuf& d : m.pp[q])
+            if (d.p) (void)hipFree(d.p);
+        if (m.h_cnt[q]) (void)hipHostFree(m.h_cnt[q]);
+        if (m.cnt_ev[q]) (void)hipEventDestroy(m.cnt_ev[q]);
+    }
     if (m.pt_ev) (void)hipEventDestroy(m.pt_ev);
     if (m.in_ev) (void)hipEventDestroy(m.in_ev);
     if (m.cstream) (void)hipStreamDestroy(m.cstream);
@@ -246,6 +264,8 @@ struct nrg_group {
     uint64_t round = 0;
     uint32_t timeout_ms = NRG_GROUP_DEFAULT_TIMEOUT_MS;  // deadline of every wait on the peers
     int broken = NRG_OK;  // sticky: a timed-out collective or disagreeing ranks end the group
+    int pt_pend = -1;     // parity of the partitioned round posted and not yet completed, or -1
+    int pt_next = 0;      // parity of the next partitioned round
     char diag[256] = {};  // what broke it (nrg_group_last_error)
 };
 
@@ -286,12 +306,13 @@ int group_end(nrg_group* g, const char* phase) {
 
 // Wait until `s` drains, at most the group's deadline from now. A stream that does not drain is
 // one whose collective a peer never joined (or a hung device): the group fails with NRG_E_TIMEOUT.
-int wait_stream(nrg_group* g, hipStream_t s, const char* phase) {
+template <typename Q>
+int wait_until(nrg_group* g, Q query, const char* phase) {
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
     const auto dl = t0 + std::chrono::milliseconds(g->timeout_ms);
     for (uint32_t spin = 0;; spin++) {
-        const hipError_t e = hipStreamQuery(s);
+        const hipError_t e = query();
         if (e == hipSuccess) return NRG_OK;
         if (e != hipErrorNotReady) return hip_rc(e);
         const auto now = clk::now();
@@ -305,6 +326,12 @@ int wait_stream(nrg_group* g, hipStream_t s, const char* phase) {
         if (now - t0 > std::chrono::microseconds(200))
             std::this_thread::sleep_for(std::chrono::microseconds(spin < 2000 ? 20 : 500));
     }
+}
+int wait_stream(nrg_group* g, hipStream_t s, const char* phase) {
+    return wait_until(g, [s] { return hipStreamQuery(s); }, phase);
+}
+int wait_event(nrg_group* g, hipEvent_t ev, const char* phase) {
+    return wait_until(g, [ev] { return hipEventQuery(ev); }, phase);
 }
 
 }  // namespace
@@ -601,68 +628,99 @@ int nrg_group_round_async(nrg_group* g, const nrg_round* rounds, const uint64_t*
 
 
 
-int nrg_group_partitioned_round(nrg_group* g, const nrg_round* rounds) {
-    if (!g || !rounds) return NRG_E_INVAL;
-    if (g->broken) return g->broken;
+// Post a partitioned round on every local member: the fused partition of its Puts and Gets into
+// owner regions (partition.hip pt_fused, which also writes the member's exchange words) and the
+// all-gather of every rank's counts, whose host copy lands in pinned memory (cnt_ev). Everything
+// runs on the replica's stream. Local failures travel in the XW_ERR word; nothing here waits.
+static int pt_post(nrg_group* g, const nrg_round* rounds, int par) {
     const Rccl* R = g->R;
-    if (!R || !R->send || !R->recv) return NRG_E_COMM;
     const int G = g->nranks, nl = (int)g->m.size();
-    if (G > NRG_MAX_PARTS) return NRG_E_INVAL;
     const uint64_t CW = 2 * (uint64_t)G + XW_N;
-    // Every failure from here to the send/recv plan is agreed on by all ranks before anyone
-    // posts a send or receive: a rank that returned alone would leave its peers waiting in RCCL.
-    // Local failures before the count exchange travel in its XW_ERR word; buffer growth after it
-    // is known to every rank from the exchanged capacities and confirmed by a status all-gather.
-    // What remains are HIP runtime failures of stream/event calls (and a partition kernel whose
-    // counts disagree with its input), which leave the device unusable: fatal to the group.
     for (int i = 0; i < nl; i++) {
         Member& m = g->m[i];
         const nrg_round& x = rounds[i];
+        nrg_ctx* c = m.ctx;
         int err = NRG_OK;
-        if (m.ctx->cfg.ds_kind != NRG_DS_HASHMAP || (x.n && !x.recs) ||
+        if (c->cfg.ds_kind != NRG_DS_HASHMAP || (x.n && !x.recs) ||
             (x.n_gets && (!x.get_keys || !x.get_vals || !x.get_found)))
             err = NRG_E_INVAL;
-        else if (x.n >= (1ull << 32) || x.n_gets >= (1ull << 32))
-            err = NRG_E_CAPACITY;
-        nrg_ctx* c = m.ctx;
-        // (the exchange buffers PB_CNT / PB_ALLCNT / PB_ST / PB_ALLST were sized at join)
+        else if (x.n >= (1ull << 32) || x.n_gets >= (1ull << 32) || (uint64_t)G * x.n >= (1ull << 32) ||
+                 (uint64_t)G * x.n_gets >= (1ull << 32))
+            err = NRG_E_CAPACITY;  // positions are u32 owner-region offsets
         RCHK(nrg::ctx_use_device(c));
-        if (err == NRG_OK) {
-            const PtBuf local[] = {PB_POUT, PB_PPOS, PB_KOUT, PB_GPOS, PB_AVAL, PB_AFOUND, PB_APREV, PB_APREVF};
-            const uint64_t bytes[] = {x.n * 16, x.n * 4, x.n_gets * 8, x.n_gets * 4,
-                                      x.n_gets * 8, x.n_gets, x.n * 8, x.n};
-            for (int k = 0; k < 8 && err == NRG_OK; k++) err = grow(m, local[k], bytes[k]);
-        }
         if (m.in_set && m.in_stream != c->stream) RCHK(order(m, m.in_stream, c->stream));
-        if (err == NRG_OK)
-            err = nrg_hashmap_partition_async(c, (const nrg_put*)x.recs, x.n, x.get_keys, x.n_gets, (uint32_t)G,
-                                              (nrg_put*)m.pt[PB_POUT].p, (uint32_t*)m.pt[PB_PPOS].p,
-                                              (uint64_t*)m.pt[PB_KOUT].p, (uint32_t*)m.pt[PB_GPOS].p,
-                                              (uint64_t*)m.pt[PB_CNT].p);
+        const uint64_t n = err ? 0 : x.n, k = err ? 0 : x.n_gets;
+        if (err == NRG_OK) {
+            DBuf* pp = m.pp[par];
+            const uint64_t bytes[] = {G * n * 16, n * 4, G * k * 8, k * 4};
+            const PtPar which[] = {PP_POUT, PP_PPOS, PP_KOUT, PP_GPOS};
+            for (int q = 0; q < 4 && err == NRG_OK; q++) err = grow_buf(m, pp[which[q]], bytes[q]);
+            if (err == NRG_OK) err = grow(m, PB_DESC, nrg::pt_desc_words(n, k, (uint32_t)G) * 8);
+            // owner-region answer buffers (a single rank's answers need none: they stay in RVAL)
+            if (err == NRG_OK && G > 1) {
+                const PtBuf ans[] = {PB_AVAL, PB_AFOUND, PB_APREV, PB_APREVF};
+                const uint64_t ab[] = {G * k * 8, G * k, G * n * 8, G * n};
+                for (int q = 0; q < 4 && err == NRG_OK; q++) err = grow(m, ans[q], ab[q]);
+            }
+        }
+        const bool ok = err == NRG_OK;
         uint64_t* w = m.xwords;
         w[XW_PREV] = (x.resp && x.some) ? 1 : 0;
-        w[XW_RP_CAP] = std::min(std::min(m.pt[PB_RPUT].bytes / 16, m.pt[PB_RPREV].bytes / 8), m.pt[PB_RPREVF].bytes);
-        w[XW_RK_CAP] = std::min(std::min(m.pt[PB_RKEY].bytes / 8, m.pt[PB_RVAL].bytes / 8), m.pt[PB_RFOUND].bytes);
+        // receive capacities (one rank replays straight from its partition output: no RPUT/RKEY)
+        const uint64_t rp_own = std::min(m.pt[PB_RPREV].bytes / 8, m.pt[PB_RPREVF].bytes);
+        const uint64_t rk_own = std::min(m.pt[PB_RVAL].bytes / 8, m.pt[PB_RFOUND].bytes);
+        w[XW_RP_CAP] = G == 1 ? rp_own : std::min(m.pt[PB_RPUT].bytes / 16, rp_own);
+        w[XW_RK_CAP] = G == 1 ? rk_own : std::min(m.pt[PB_RKEY].bytes / 8, rk_own);
         w[XW_ERR] = (uint64_t)(-err);
-        // host words of the exchange (pageable source: copied before hipMemcpyAsync returns)
-        GCHK(hipMemcpyAsync((uint64_t*)m.pt[PB_CNT].p + 2 * G, w, XW_N * 8, hipMemcpyHostToDevice, c->stream));
-        RCHK(order(m, c->stream, m.cstream));
+        if (++m.pt_epoch >= (1u << 22)) {  // the descriptor tag wraps: clear the stale ones once
+            m.pt_epoch = 1;
+            if (m.pt[PB_DESC].p) GCHK(hipMemsetAsync(m.pt[PB_DESC].p, 0, m.pt[PB_DESC].bytes, c->stream));
+        }
+        const hipError_t e = nrg::pt_fused(c->stream, (const uint64_t*)x.recs, ok ? n : 0, n,
+                                           (uint64_t*)m.pp[par][PP_POUT].p, (uint32_t*)m.pp[par][PP_PPOS].p,
+                                           x.get_keys, ok ? k : 0, k, (uint64_t*)m.pp[par][PP_KOUT].p,
+                                           (uint32_t*)m.pp[par][PP_GPOS].p, (uint64_t*)m.pt[PB_DESC].p, (uint32_t)G,
+                                           m.pt_epoch, G == 1 ? m.h_cnt[par] : (uint64_t*)m.pp[par][PP_CNT].p, w,
+                                           XW_N);
+        if (e != hipSuccess) return hip_rc(e);
+        m.pr[par] = x;
+        m.cap_p[par] = n;
+        m.cap_k[par] = k;
     }
-    // 2. every rank's counts, capacities and status to every rank (one host round trip)
-    if (R->group_start() != ncclSuccess) return NRG_E_COMM;
-    ncclResult_t res = ncclSuccess;
-    for (int i = 0; i < nl && res == ncclSuccess; i++)
-        res = R->all_gather(g->m[i].pt[PB_CNT].p, g->m[i].pt[PB_ALLCNT].p, CW, ncclUint64, g->m[i].comm, g->m[i].cstream);
-    RCHK(group_end(g, "partitioned count exchange"));
-    if (res != ncclSuccess) return group_fail(g, NRG_E_COMM, "partitioned count exchange refused");
+    if (G > 1) {  // (one rank's all-gather is the identity: its partition wrote h_cnt itself)
+        if (R->group_start() != ncclSuccess) return NRG_E_COMM;
+        ncclResult_t res = ncclSuccess;
+        for (int i = 0; i < nl && res == ncclSuccess; i++)
+            res = R->all_gather(g->m[i].pp[par][PP_CNT].p, g->m[i].pp[par][PP_ALLCNT].p, CW, ncclUint64,
+                                g->m[i].comm, g->m[i].ctx->stream);
+        RCHK(group_end(g, "partitioned count exchange"));
+        if (res != ncclSuccess) return group_fail(g, NRG_E_COMM, "partitioned count exchange refused");
+    }
     for (int i = 0; i < nl; i++) {
         Member& m = g->m[i];
         RCHK(nrg::ctx_use_device(m.ctx));
-        m.hcnt.resize((size_t)G * CW);
-        GCHK(hipMemcpyAsync(m.hcnt.data(), m.pt[PB_ALLCNT].p, (uint64_t)G * CW * 8, hipMemcpyDeviceToHost, m.cstream));
-        RCHK(wait_stream(g, m.cstream, "partitioned count exchange"));
+        if (G > 1)
+            GCHK(hipMemcpyAsync(m.h_cnt[par], m.pp[par][PP_ALLCNT].p, (uint64_t)G * CW * 8, hipMemcpyDeviceToHost,
+                                m.ctx->stream));
+        GCHK(hipEventRecord(m.cnt_ev[par], m.ctx->stream));
     }
-    const std::vector<uint64_t>& H = g->m[0].hcnt;  // identical on every rank
+    return NRG_OK;
+}
+
+// Complete the posted round of parity `par`: read its exchanged counts (posted a call earlier, so
+// normally long landed), move the Puts and Gets to their owners, replay, answer, send the answers
+// back and route them into the callers' order. Every failure before the first send/recv is agreed
+// on by all ranks (the same exchanged words); a rank's own part of the payload never leaves its
+// GPU (a device copy; with one rank, no copy at all).
+static int pt_complete(nrg_group* g, int par) {
+    const Rccl* R = g->R;
+    const int G = g->nranks, nl = (int)g->m.size();
+    const uint64_t CW = 2 * (uint64_t)G + XW_N;
+    for (int i = 0; i < nl; i++) {
+        RCHK(nrg::ctx_use_device(g->m[i].ctx));
+        RCHK(wait_event(g, g->m[i].cnt_ev[par], "partitioned count exchange"));
+    }
+    const uint64_t* H = g->m[0].h_cnt[par];  // identical on every rank
     auto word = [&](int s, uint64_t k) { return H[(size_t)s * CW + 2 * G + k]; };
     for (int s = 0; s < G; s++)
         if (word(s, XW_ERR)) return -(int)word(s, XW_ERR);  // the same answer on every rank
@@ -676,10 +734,10 @@ int nrg_group_partitioned_round(nrg_group* g, const nrg_round* rounds) {
         }
         any_grow |= rp > word(s, XW_RP_CAP) || rk > word(s, XW_RK_CAP);
     }
-    // 3. Puts and Get keys to their owners: member rank r sends its owner-o group to o and receives
-    //    rank s's group for r at offset sum_{s' < s} (rank order = the global log order)
+    // member rank r sends its owner-o region to o and receives rank s's group for r at offset
+    // sum_{s' < s} (rank order = the global log order)
     struct Plan {
-        std::vector<uint64_t> pto, gto, pfrom, gfrom, pto_off, gto_off, pfrom_off, gfrom_off;
+        std::vector<uint64_t> pto, gto, pfrom, gfrom, pfrom_off, gfrom_off;
         uint64_t rp = 0, rk = 0;
     };
     std::vector<Plan> plan(nl);
@@ -688,49 +746,48 @@ int nrg_group_partitioned_round(nrg_group* g, const nrg_round* rounds) {
         Member& m = g->m[i];
         Plan& P = plan[i];
         const int r = m.rank;
-        const uint64_t* h = m.hcnt.data();
         P.pto.resize(G), P.gto.resize(G), P.pfrom.resize(G), P.gfrom.resize(G);
-        P.pto_off.resize(G), P.gto_off.resize(G), P.pfrom_off.resize(G), P.gfrom_off.resize(G);
+        P.pfrom_off.resize(G), P.gfrom_off.resize(G);
         uint64_t a = 0, b = 0, cq = 0, d = 0;
         for (int o = 0; o < G; o++) {
-            P.pto[o] = h[(size_t)r * CW + o];
-            P.gto[o] = h[(size_t)r * CW + G + o];
-            P.pfrom[o] = h[(size_t)o * CW + r];
-            P.gfrom[o] = h[(size_t)o * CW + G + r];
-            P.pto_off[o] = a, a += P.pto[o];
-            P.gto_off[o] = b, b += P.gto[o];
+            P.pto[o] = H[(size_t)r * CW + o];
+            P.gto[o] = H[(size_t)r * CW + G + o];
+            P.pfrom[o] = H[(size_t)o * CW + r];
+            P.gfrom[o] = H[(size_t)o * CW + G + r];
+            a += P.pto[o], b += P.gto[o];
             P.pfrom_off[o] = cq, cq += P.pfrom[o];
             P.gfrom_off[o] = d, d += P.gfrom[o];
         }
-        if (a != rounds[i].n || b != rounds[i].n_gets) grow_err[i] = NRG_E_HIP;  // partition kernel disagrees
+        if (a != m.cap_p[par] || b != m.cap_k[par]) grow_err[i] = NRG_E_HIP;  // partition kernel disagrees
         P.rp = cq;
         P.rk = d;
         if (any_grow && grow_err[i] == NRG_OK) {
             RCHK(nrg::ctx_use_device(m.ctx));
             const PtBuf recv[] = {PB_RPUT, PB_RPREV, PB_RPREVF, PB_RKEY, PB_RVAL, PB_RFOUND};
-            const uint64_t bytes[] = {P.rp * 16, P.rp * 8, P.rp, P.rk * 8, P.rk * 8, P.rk};
+            const uint64_t bytes[] = {G > 1 ? P.rp * 16 : 0, P.rp * 8, P.rp, G > 1 ? P.rk * 8 : 0, P.rk * 8, P.rk};
             for (int k = 0; k < 6 && grow_err[i] == NRG_OK; k++) grow_err[i] = grow(m, recv[k], bytes[k]);
         }
     }
+    ncclResult_t res = ncclSuccess;
     if (any_grow) {  // every rank knows a rank had to grow: all confirm before any send/recv
         for (int i = 0; i < nl; i++) {
             Member& m = g->m[i];
             RCHK(nrg::ctx_use_device(m.ctx));
             m.xwords[0] = (uint64_t)(-grow_err[i]);
-            GCHK(hipMemcpyAsync(m.pt[PB_ST].p, m.xwords, 8, hipMemcpyHostToDevice, m.cstream));
+            GCHK(hipMemcpyAsync(m.pt[PB_ST].p, m.xwords, 8, hipMemcpyHostToDevice, m.ctx->stream));
         }
         if (R->group_start() != ncclSuccess) return NRG_E_COMM;
         for (int i = 0; i < nl && res == ncclSuccess; i++)
             res = R->all_gather(g->m[i].pt[PB_ST].p, g->m[i].pt[PB_ALLST].p, 1, ncclUint64, g->m[i].comm,
-                                g->m[i].cstream);
+                                g->m[i].ctx->stream);
         RCHK(group_end(g, "partitioned status exchange"));
         if (res != ncclSuccess) return group_fail(g, NRG_E_COMM, "partitioned status exchange refused");
         std::vector<uint64_t> st(G);
         for (int i = 0; i < nl; i++) {
             Member& m = g->m[i];
             RCHK(nrg::ctx_use_device(m.ctx));
-            GCHK(hipMemcpyAsync(st.data(), m.pt[PB_ALLST].p, (uint64_t)G * 8, hipMemcpyDeviceToHost, m.cstream));
-            RCHK(wait_stream(g, m.cstream, "partitioned status exchange"));
+            GCHK(hipMemcpyAsync(st.data(), m.pt[PB_ALLST].p, (uint64_t)G * 8, hipMemcpyDeviceToHost, m.ctx->stream));
+            RCHK(wait_stream(g, m.ctx->stream, "partitioned status exchange"));
         }
         for (int s = 0; s < G; s++)
             if (st[s]) return -(int)st[s];
@@ -738,24 +795,45 @@ int nrg_group_partitioned_round(nrg_group* g, const nrg_round* rounds) {
         for (int i = 0; i < nl; i++)
             if (grow_err[i]) return grow_err[i];  // cannot happen: the counts come from the same kernel
     }
-    auto at = [](const DBuf& d, uint64_t off) { return (void*)((char*)d.p + off); };
-    if (R->group_start() != ncclSuccess) return NRG_E_COMM;
-    for (int i = 0; i < nl && res == ncclSuccess; i++) {
-        Member& m = g->m[i];
-        const Plan& P = plan[i];
-        for (int o = 0; o < G && res == ncclSuccess; o++) {
-            if (P.pto[o]) res = R->send(at(m.pt[PB_POUT], P.pto_off[o] * 16), P.pto[o] * 2, ncclUint64, o, m.comm, m.cstream);
-            if (res == ncclSuccess && P.pfrom[o])
-                res = R->recv(at(m.pt[PB_RPUT], P.pfrom_off[o] * 16), P.pfrom[o] * 2, ncclUint64, o, m.comm, m.cstream);
-            if (res == ncclSuccess && P.gto[o])
-                res = R->send(at(m.pt[PB_KOUT], P.gto_off[o] * 8), P.gto[o], ncclUint64, o, m.comm, m.cstream);
-            if (res == ncclSuccess && P.gfrom[o])
-                res = R->recv(at(m.pt[PB_RKEY], P.gfrom_off[o] * 8), P.gfrom[o], ncclUint64, o, m.comm, m.cstream);
+    auto at = [](void* base, uint64_t off) { return (void*)((char*)base + off); };
+    // where member i's replay reads its Puts / Get keys and where its answers go back from
+    auto rput_of = [&](int i) { return G == 1 ? g->m[i].pp[par][PP_POUT].p : g->m[i].pt[PB_RPUT].p; };
+    auto rkey_of = [&](int i) { return G == 1 ? g->m[i].pp[par][PP_KOUT].p : g->m[i].pt[PB_RKEY].p; };
+    if (G > 1) {
+        // 1. Puts and Get keys to their owners (own part: a device copy)
+        if (R->group_start() != ncclSuccess) return NRG_E_COMM;
+        for (int i = 0; i < nl && res == ncclSuccess; i++) {
+            Member& m = g->m[i];
+            const Plan& P = plan[i];
+            const uint64_t cp = m.cap_p[par], ck = m.cap_k[par];
+            void *pout = m.pp[par][PP_POUT].p, *kout = m.pp[par][PP_KOUT].p;
+            hipStream_t s = m.ctx->stream;
+            for (int o = 0; o < G && res == ncclSuccess; o++) {
+                if (o == m.rank) continue;
+                if (P.pto[o]) res = R->send(at(pout, o * cp * 16), P.pto[o] * 2, ncclUint64, o, m.comm, s);
+                if (res == ncclSuccess && P.pfrom[o])
+                    res = R->recv(at(m.pt[PB_RPUT].p, P.pfrom_off[o] * 16), P.pfrom[o] * 2, ncclUint64, o, m.comm, s);
+                if (res == ncclSuccess && P.gto[o]) res = R->send(at(kout, o * ck * 8), P.gto[o], ncclUint64, o, m.comm, s);
+                if (res == ncclSuccess && P.gfrom[o])
+                    res = R->recv(at(m.pt[PB_RKEY].p, P.gfrom_off[o] * 8), P.gfrom[o], ncclUint64, o, m.comm, s);
+            }
+        }
+        RCHK(group_end(g, "partitioned send/recv of Puts and Gets"));
+        if (res != ncclSuccess) return group_fail(g, NRG_E_COMM, "partitioned send/recv refused");
+        for (int i = 0; i < nl; i++) {
+            Member& m = g->m[i];
+            const Plan& P = plan[i];
+            const int r = m.rank;
+            RCHK(nrg::ctx_use_device(m.ctx));
+            if (P.pto[r])
+                GCHK(hipMemcpyAsync(at(m.pt[PB_RPUT].p, P.pfrom_off[r] * 16), at(m.pp[par][PP_POUT].p, r * m.cap_p[par] * 16),
+                                    P.pto[r] * 16, hipMemcpyDeviceToDevice, m.ctx->stream));
+            if (P.gto[r])
+                GCHK(hipMemcpyAsync(at(m.pt[PB_RKEY].p, P.gfrom_off[r] * 8), at(m.pp[par][PP_KOUT].p, r * m.cap_k[par] * 8),
+                                    P.gto[r] * 8, hipMemcpyDeviceToDevice, m.ctx->stream));
         }
     }
-    RCHK(group_end(g, "partitioned send/recv of Puts and Gets"));
-    if (res != ncclSuccess) return group_fail(g, NRG_E_COMM, "partitioned send/recv refused");
-    // 4. each owner replays the Puts it received (rank order) and answers the Gets it received. A
+    // 2. each owner replays the Puts it received (rank order) and answers the Gets it received. A
     //    skewed round can hand one owner more Puts than its max_batch (or ring) takes in one
     //    replay: consecutive rounds of at most that many, the Gets answered after the last.
     for (int i = 0; i < nl; i++) {
@@ -763,10 +841,9 @@ int nrg_group_partitioned_round(nrg_group* g, const nrg_round* rounds) {
         const Plan& P = plan[i];
         nrg_ctx* c = m.ctx;
         RCHK(nrg::ctx_use_device(c));
-        RCHK(order(m, m.cstream, c->stream));
         const uint64_t ring_room = c->log_size > 2 * GC_FROM_HEAD ? c->log_size - GC_FROM_HEAD : GC_FROM_HEAD;
         const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(c->cfg.max_batch, ring_room));
-        const nrg_put* rput = (const nrg_put*)m.pt[PB_RPUT].p;
+        const nrg_put* rput = (const nrg_put*)rput_of(i);
         uint64_t* rprev = any_prev ? (uint64_t*)m.pt[PB_RPREV].p : nullptr;
         uint8_t* rprevf = any_prev ? (uint8_t*)m.pt[PB_RPREVF].p : nullptr;
         uint64_t off = 0;
@@ -775,68 +852,138 @@ int nrg_group_partitioned_round(nrg_group* g, const nrg_round* rounds) {
             const bool last = off + n == P.rp;
             if (n || (last && P.rk))
                 RCHK(nrg_hashmap_round_async(c, rput + off, n, (uint32_t)m.rank + 1,
-                                             last ? (const uint64_t*)m.pt[PB_RKEY].p : nullptr, last ? P.rk : 0,
+                                             last ? (const uint64_t*)rkey_of(i) : nullptr, last ? P.rk : 0,
                                              last ? (uint64_t*)m.pt[PB_RVAL].p : nullptr,
                                              last ? (uint8_t*)m.pt[PB_RFOUND].p : nullptr,
                                              rprev ? rprev + off : nullptr, rprevf ? rprevf + off : nullptr));
             off += n;
         } while (off < P.rp);
         RCHK(nrg_join(c));
-        RCHK(order(m, c->stream, m.cstream));
     }
-    // 5. answers back to the ranks that asked, into their owner-grouped order
-    if (R->group_start() != ncclSuccess) return NRG_E_COMM;
-    for (int i = 0; i < nl && res == ncclSuccess; i++) {
-        Member& m = g->m[i];
-        const Plan& P = plan[i];
-        const bool mine = rounds[i].resp && rounds[i].some;
-        for (int o = 0; o < G && res == ncclSuccess; o++) {
-            const bool theirs = word(o, XW_PREV) != 0;
-            if (P.gfrom[o]) {
-                res = R->send(at(m.pt[PB_RVAL], P.gfrom_off[o] * 8), P.gfrom[o], ncclUint64, o, m.comm, m.cstream);
-                if (res == ncclSuccess)
-                    res = R->send(at(m.pt[PB_RFOUND], P.gfrom_off[o]), P.gfrom[o], ncclUint8, o, m.comm, m.cstream);
-            }
-            if (res == ncclSuccess && P.gto[o]) {
-                res = R->recv(at(m.pt[PB_AVAL], P.gto_off[o] * 8), P.gto[o], ncclUint64, o, m.comm, m.cstream);
-                if (res == ncclSuccess)
-                    res = R->recv(at(m.pt[PB_AFOUND], P.gto_off[o]), P.gto[o], ncclUint8, o, m.comm, m.cstream);
-            }
-            if (res == ncclSuccess && theirs && P.pfrom[o]) {
-                res = R->send(at(m.pt[PB_RPREV], P.pfrom_off[o] * 8), P.pfrom[o], ncclUint64, o, m.comm, m.cstream);
-                if (res == ncclSuccess)
-                    res = R->send(at(m.pt[PB_RPREVF], P.pfrom_off[o]), P.pfrom[o], ncclUint8, o, m.comm, m.cstream);
-            }
-            if (res == ncclSuccess && mine && P.pto[o]) {
-                res = R->recv(at(m.pt[PB_APREV], P.pto_off[o] * 8), P.pto[o], ncclUint64, o, m.comm, m.cstream);
-                if (res == ncclSuccess)
-                    res = R->recv(at(m.pt[PB_APREVF], P.pto_off[o]), P.pto[o], ncclUint8, o, m.comm, m.cstream);
+    // 3. answers back to the ranks that asked, into their owner regions (own part: a device copy;
+    //    one rank routes straight from RVAL / RPREV)
+    if (G > 1) {
+        if (R->group_start() != ncclSuccess) return NRG_E_COMM;
+        for (int i = 0; i < nl && res == ncclSuccess; i++) {
+            Member& m = g->m[i];
+            const Plan& P = plan[i];
+            const bool mine = m.pr[par].resp && m.pr[par].some;
+            const uint64_t cp = m.cap_p[par], ck = m.cap_k[par];
+            hipStream_t s = m.ctx->stream;
+            for (int o = 0; o < G && res == ncclSuccess; o++) {
+                if (o == m.rank) continue;
+                const bool theirs = word(o, XW_PREV) != 0;
+                if (P.gfrom[o]) {
+                    res = R->send(at(m.pt[PB_RVAL].p, P.gfrom_off[o] * 8), P.gfrom[o], ncclUint64, o, m.comm, s);
+                    if (res == ncclSuccess)
+                        res = R->send(at(m.pt[PB_RFOUND].p, P.gfrom_off[o]), P.gfrom[o], ncclUint8, o, m.comm, s);
+                }
+                if (res == ncclSuccess && P.gto[o]) {
+                    res = R->recv(at(m.pt[PB_AVAL].p, o * ck * 8), P.gto[o], ncclUint64, o, m.comm, s);
+                    if (res == ncclSuccess) res = R->recv(at(m.pt[PB_AFOUND].p, o * ck), P.gto[o], ncclUint8, o, m.comm, s);
+                }
+                if (res == ncclSuccess && theirs && P.pfrom[o]) {
+                    res = R->send(at(m.pt[PB_RPREV].p, P.pfrom_off[o] * 8), P.pfrom[o], ncclUint64, o, m.comm, s);
+                    if (res == ncclSuccess)
+                        res = R->send(at(m.pt[PB_RPREVF].p, P.pfrom_off[o]), P.pfrom[o], ncclUint8, o, m.comm, s);
+                }
+                if (res == ncclSuccess && mine && P.pto[o]) {
+                    res = R->recv(at(m.pt[PB_APREV].p, o * cp * 8), P.pto[o], ncclUint64, o, m.comm, s);
+                    if (res == ncclSuccess) res = R->recv(at(m.pt[PB_APREVF].p, o * cp), P.pto[o], ncclUint8, o, m.comm, s);
+                }
             }
         }
+        RCHK(group_end(g, "partitioned answers back"));
+        if (res != ncclSuccess) return group_fail(g, NRG_E_COMM, "partitioned answers back refused");
     }
-    RCHK(group_end(g, "partitioned answers back"));
-    if (res != ncclSuccess) return group_fail(g, NRG_E_COMM, "partitioned answers back refused");
-    // 6. back into the caller's order
+    // 4. back into the caller's order (one launch for the Gets' answers and the previous values)
     for (int i = 0; i < nl; i++) {
         Member& m = g->m[i];
-        const nrg_round& x = rounds[i];
+        const Plan& P = plan[i];
+        const nrg_round& x = m.pr[par];
         nrg_ctx* c = m.ctx;
+        const int r = m.rank;
         RCHK(nrg::ctx_use_device(c));
-        RCHK(order(m, m.cstream, c->stream));
-        RCHK(nrg_route_back_async(c, (const uint64_t*)m.pt[PB_AVAL].p, (const uint8_t*)m.pt[PB_AFOUND].p,
-                                  (const uint32_t*)m.pt[PB_GPOS].p, x.n_gets, x.get_vals, x.get_found));
-        if (x.resp && x.some)
-            RCHK(nrg_route_back_async(c, (const uint64_t*)m.pt[PB_APREV].p, (const uint8_t*)m.pt[PB_APREVF].p,
-                                      (const uint32_t*)m.pt[PB_PPOS].p, x.n, (uint64_t*)x.resp, x.some));
+        const bool mine = x.resp && x.some;
+        const uint64_t cp = m.cap_p[par], ck = m.cap_k[par];
+        void *aval = m.pt[PB_AVAL].p, *afound = m.pt[PB_AFOUND].p, *aprev = m.pt[PB_APREV].p, *aprevf = m.pt[PB_APREVF].p;
+        if (G == 1) {
+            aval = m.pt[PB_RVAL].p, afound = m.pt[PB_RFOUND].p, aprev = m.pt[PB_RPREV].p, aprevf = m.pt[PB_RPREVF].p;
+        } else {
+            hipStream_t s = c->stream;
+            if (P.gto[r]) {
+                GCHK(hipMemcpyAsync(at(aval, r * ck * 8), at(m.pt[PB_RVAL].p, P.gfrom_off[r] * 8), P.gto[r] * 8,
+                                    hipMemcpyDeviceToDevice, s));
+                GCHK(hipMemcpyAsync(at(afound, r * ck), at(m.pt[PB_RFOUND].p, P.gfrom_off[r]), P.gto[r],
+                                    hipMemcpyDeviceToDevice, s));
+            }
+            if (mine && P.pto[r]) {
+                GCHK(hipMemcpyAsync(at(aprev, r * cp * 8), at(m.pt[PB_RPREV].p, P.pfrom_off[r] * 8), P.pto[r] * 8,
+                                    hipMemcpyDeviceToDevice, s));
+                GCHK(hipMemcpyAsync(at(aprevf, r * cp), at(m.pt[PB_RPREVF].p, P.pfrom_off[r]), P.pto[r],
+                                    hipMemcpyDeviceToDevice, s));
+            }
+        }
+        const hipError_t e = nrg::pt_route2(
+            c->stream, (const uint64_t*)aval, (const uint8_t*)afound, (const uint32_t*)m.pp[par][PP_GPOS].p, x.n_gets,
+            x.get_vals, x.get_found, (const uint64_t*)aprev, (const uint8_t*)aprevf,
+            (const uint32_t*)m.pp[par][PP_PPOS].p, mine ? x.n : 0, mine ? (uint64_t*)x.resp : nullptr, mine ? x.some : nullptr);
+        if (e != hipSuccess) return hip_rc(e);
     }
     g->round++;
     return NRG_OK;
 }
 
+// complete the pending partitioned round, if any (its error, or NRG_OK)
+static int pt_flush(nrg_group* g) {
+    if (g->pt_pend < 0) return NRG_OK;
+    const int par = g->pt_pend;
+    g->pt_pend = -1;
+    return pt_complete(g, par);
+}
+
+static int pt_check(nrg_group* g) {
+    if (!g) return NRG_E_INVAL;
+    if (g->broken) return g->broken;
+    const Rccl* R = g->R;
+    if (!R || !R->send || !R->recv) return NRG_E_COMM;
+    if (g->nranks > NRG_MAX_PARTS) return NRG_E_INVAL;
+    return NRG_OK;
+}
+
+int nrg_group_partitioned_round_async(nrg_group* g, const nrg_round* rounds) {
+    int r = pt_check(g);
+    if (r) return r;
+    if (!rounds) return NRG_E_INVAL;
+    const int par = g->pt_next;
+    if ((r = pt_post(g, rounds, par))) return r;
+    g->pt_next ^= 1;
+    const int rc = pt_flush(g);  // the previous round, whose counts have landed by now
+    g->pt_pend = par;
+    return rc;
+}
+
+int nrg_group_partitioned_flush(nrg_group* g) {
+    const int r = pt_check(g);
+    return r ? r : pt_flush(g);
+}
+
+int nrg_group_partitioned_round(nrg_group* g, const nrg_round* rounds) {
+    int r = pt_check(g);
+    if (r) return r;
+    if (!rounds) return NRG_E_INVAL;
+    if ((r = pt_flush(g))) return r;
+    const int par = g->pt_next;
+    if ((r = pt_post(g, rounds, par))) return r;
+    g->pt_next ^= 1;
+    return pt_complete(g, par);
+}
+
 int nrg_group_sync(nrg_group* g) {
     if (!g) return NRG_E_INVAL;
     if (g->broken) return g->broken;
-    int rc = NRG_OK;
+    int rc = g->pt_pend >= 0 ? pt_flush(g) : NRG_OK;  // a posted partitioned round completes first
+    if (g->broken) return g->broken;
     for (Member& m : g->m) {
         int r = nrg::ctx_use_device(m.ctx);
         if (r) return r;

@@ -227,6 +227,17 @@ hipError_t hm_prefill_range(nrg_ctx* c, u64 n, u64 off, u32 part = 0, u32 parts 
 // partition.hip: stable partition of records (key in word 0) by key owner; answers routed back
 hipError_t pt_partition(nrg_ctx* c, const u64* in, u64 n, u32 words, u32 parts, u64* out, u32* pos, u64* total);
 hipError_t pt_gather(nrg_ctx* c, const u64* src, const uint8_t* src8, const u32* pos, u64 n, u64* dst, uint8_t* dst8);
+// the replica group's partitioned rounds (partition.hip): one fused launch for the Puts and Get
+// keys into owner regions of capacity cap_p / cap_k; counts[0, parts) Puts and [parts, 2 parts)
+// Gets per owner, then the nxw host words xw; desc: pt_desc_words() look-back descriptors
+constexpr u32 PT_XW_MAX = 8;
+hipError_t pt_fused(hipStream_t s, const u64* puts, u64 W, u64 cap_p, u64* pout, u32* ppos, const u64* keys, u64 R,
+                    u64 cap_k, u64* kout, u32* gpos, u64* desc, u32 parts, u32 epoch, u64* counts, const u64* xw,
+                    u32 nxw);
+u64 pt_desc_words(u64 W, u64 R, u32 parts);
+hipError_t pt_route2(hipStream_t s, const u64* src_a, const uint8_t* src8_a, const u32* pos_a, u64 n_a, u64* dst_a,
+                     uint8_t* dst8_a, const u64* src_b, const uint8_t* src8_b, const u32* pos_b, u64 n_b, u64* dst_b,
+                     uint8_t* dst8_b);
 hipError_t hm_dump(nrg_ctx* c, u64* d_keys, u64* d_vals);
 hipError_t hm_count(nrg_ctx* c);  // DevCtl::nkeys_total = number of keys
 hipError_t hm_digest(nrg_ctx* c, u64* d_out3);

@@ -147,6 +147,217 @@ __global__ __launch_bounds__(PT_TPB) void pt_gather_kernel(const u64* __restrict
     }
 }
 
+// ---- the replica group's fused partition (nrg_group_partitioned_round) -----------------------
+// One launch partitions a round's Puts and Get keys together, in one pass: owner o's records go to
+// a region of fixed capacity (out + o * cap, cap = the job's own record count, so any owner can
+// take all of them), so no global scan of the owner totals is needed. Tiles are blockIdx-ordered
+// (Puts first, then Gets); each publishes its per-owner counts as a look-back descriptor and takes
+// its offsets from its predecessors' (decoupled look-back, relaxed agent-scope atomics; the
+// descriptor word IS the flag, epoch-tagged so no reset pass runs between rounds). The last tile
+// of a job writes the owner totals into the round's count-exchange words, and block 0 the
+// member's host words (XW_*), so the exchange needs no host copy.
+typedef u64 pt_u64x2 __attribute__((ext_vector_type(2)));
+constexpr u64 PD_CNT = (1ull << 40) - 1, PD_AGG = 1ull << 40, PD_INC = 2ull << 40, PD_ST = 3ull << 40;
+constexpr int PD_EP = 42, PD_WIN = 16;
+// fused tiles: 16 waves x 8 rounds of 64 = 8192 records, so a 1M-op round has ~123 tiles and the
+// look-back reaches an inclusive descriptor in a few windowed steps (2048-record tiles: 22 us per
+// B1 round, the look-back chain of ~490 tiles)
+constexpr int PF_TPB = 1024, PF_WAVES = PF_TPB / 64;
+constexpr u32 PF_TILE = PF_TPB * PT_ROUNDS;
+
+struct PtFJob {
+    const u64* in;
+    u64 n;
+    u64 cap;      // owner o's records at out[(o * cap + j) * words]
+    u64* out;
+    u32* pos;     // pos[i] = o * cap + j: where record i went
+    u64* desc;    // [tiles][parts] look-back descriptors
+    u64* counts;  // [parts] the job's records per owner
+    u32 tiles;
+};
+struct PtFWords {
+    u64 w[PT_XW_MAX];
+    u64* dst;
+    u32 n;
+};
+
+template <int WORDS>
+__device__ __forceinline__ void ptf_tile(const PtFJob& J, u32 tile, u32 parts, u64 ep, u32* s_wc_flat, u64* s_base) {
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    u32(*s_wc)[PT_MAX_PARTS] = (u32(*)[PT_MAX_PARTS])s_wc_flat;
+    const u64 t0 = (u64)tile * PF_TILE + (u64)w * (PT_ROUNDS * 64);
+    u64 rec[PT_ROUNDS][WORDS];
+#pragma unroll
+    for (int r = 0; r < PT_ROUNDS; r++) {
+        const u64 i = t0 + (u64)r * 64 + lane;
+        if (i < J.n) {
+            if constexpr (WORDS == 2) {
+                const pt_u64x2 v = ((const pt_u64x2*)J.in)[i];
+                rec[r][0] = v.x;
+                rec[r][1] = v.y;
+            } else {
+                rec[r][0] = J.in[i];
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < WORDS; k++) rec[r][k] = 0;
+        }
+    }
+    u32 own[PT_ROUNDS], rank[PT_ROUNDS];
+    u32 cnt = 0;  // lane p: this wave's records of owner p so far
+#pragma unroll
+    for (int r = 0; r < PT_ROUNDS; r++) {
+        const u64 i = t0 + (u64)r * 64 + lane;
+        const bool valid = i < J.n;
+        const u32 o = valid ? key_owner(rec[r][0], parts) : 0u;
+        own[r] = o;
+        rank[r] = 0;
+        u64 act = __ballot(valid);
+        while (act) {  // one ballot per distinct owner among the 64 records (wave-uniform loop)
+            const int leader = __ffsll((long long)act) - 1;
+            const u32 ol = (u32)__shfl((int)o, leader, 64);
+            const u64 m = __ballot(valid && o == ol);
+            const u32 c0 = (u32)__shfl((int)cnt, (int)ol, 64);
+            if (valid && o == ol) rank[r] = c0 + (u32)__popcll(m & ((1ull << lane) - 1));
+            if ((u32)lane == ol) cnt += (u32)__popcll(m);
+            act &= ~m;
+        }
+    }
+    if ((u32)lane < parts) s_wc[w][lane] = cnt;
+    __syncthreads();
+    if (t < (int)parts) {  // wave 0, lane = owner: tile count, wave offsets, look-back
+        u32 tc = 0;
+        for (int i = 0; i < PF_WAVES; i++) {
+            const u32 c = s_wc[i][t];
+            s_wc[i][t] = tc;
+            tc += c;
+        }
+        u64* my = J.desc + (u64)tile * parts + t;
+        __hip_atomic_store(my, ep | (tile == 0 ? PD_INC : PD_AGG) | tc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        u64 excl = 0;
+        if (tile > 0) {
+            // windowed: PD_WIN predecessor descriptors in flight per step, consumed newest-first
+            // until an inclusive one (radix_sort.hip's look-back; stale epochs read as unpublished)
+            int tt = (int)tile - 1;
+            for (;;) {
+                u64 v[PD_WIN];
+#pragma unroll
+                for (int q = 0; q < PD_WIN; q++)
+                    v[q] = tt - q >= 0 ? __hip_atomic_load(J.desc + (u64)(tt - q) * parts + t, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT)
+                                       : (ep | PD_INC);
+                int used = 0;
+                bool done = false;
+#pragma unroll
+                for (int q = 0; q < PD_WIN; q++) {
+                    if (done || used < q) continue;
+                    const u64 st = (v[q] >> PD_EP) == (ep >> PD_EP) ? (v[q] & PD_ST) : 0ull;
+                    if (st == 0) continue;  // not published yet: retry from here
+                    excl += v[q] & PD_CNT;
+                    used = q + 1;
+                    if (st == PD_INC) done = true;
+                }
+                if (done) break;
+                tt -= used;
+                if (used < PD_WIN) __builtin_amdgcn_s_sleep(1);
+            }
+            __hip_atomic_store(my, ep | PD_INC | (excl + tc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_base[t] = (u64)t * J.cap + excl;
+        if (tile + 1 == J.tiles) J.counts[t] = excl + tc;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < PT_ROUNDS; r++) {
+        const u64 i = t0 + (u64)r * 64 + lane;
+        if (i >= J.n) continue;
+        const u32 o = own[r];
+        const u64 dest = s_base[o] + s_wc[w][o] + rank[r];
+        if constexpr (WORDS == 2) {
+            pt_u64x2 v;
+            v.x = rec[r][0];
+            v.y = rec[r][1];
+            ((pt_u64x2*)J.out)[dest] = v;
+        } else {
+            J.out[dest] = rec[r][0];
+        }
+        J.pos[i] = (u32)dest;
+    }
+}
+
+__global__ __launch_bounds__(PF_TPB) void pt_fused_kernel(PtFJob P, PtFJob K, u32 parts, u64 ep, PtFWords xw) {
+    __shared__ u32 s_wc[PF_WAVES * PT_MAX_PARTS];
+    __shared__ u64 s_base[PT_MAX_PARTS];
+    const u32 b = blockIdx.x;
+    if (b == 0) {
+        if (threadIdx.x == 0) {  // (constant indices: a lane-indexed argument array goes to scratch)
+#pragma unroll
+            for (u32 k = 0; k < PT_XW_MAX; k++)
+                if (k < xw.n) xw.dst[k] = xw.w[k];
+        }
+        if (threadIdx.x < parts) {  // a job without tiles has no owner records
+            if (P.tiles == 0) P.counts[threadIdx.x] = 0;
+            if (K.tiles == 0) K.counts[threadIdx.x] = 0;
+        }
+    }
+    if (b < P.tiles) ptf_tile<2>(P, b, parts, ep, s_wc, s_base);
+    else if (b - P.tiles < K.tiles) ptf_tile<1>(K, b - P.tiles, parts, ep, s_wc, s_base);
+}
+
+struct PtRoute {
+    const u64* src;
+    const uint8_t* src8;
+    const u32* pos;
+    u64 n;
+    u64* dst;
+    uint8_t* dst8;
+};
+// answers back to the caller's order, both routes of a round in one launch: dst[i] = src[pos[i]]
+__global__ __launch_bounds__(PT_TPB) void pt_route2_kernel(PtRoute a, PtRoute b) {
+    const u64 N = a.n + b.n;
+    for (u64 i = blockIdx.x * (u64)PT_TPB + threadIdx.x; i < N; i += (u64)gridDim.x * PT_TPB) {
+        const bool first = i < a.n;
+        const PtRoute& r = first ? a : b;
+        const u64 j = first ? i : i - a.n;
+        const u32 p = r.pos[j];
+        if (r.dst) r.dst[j] = r.src[p];
+        if (r.dst8) r.dst8[j] = r.src8[p];
+    }
+}
+
+hipError_t pt_fused(hipStream_t s, const u64* puts, u64 W, u64 cap_p, u64* pout, u32* ppos, const u64* keys, u64 R,
+                    u64 cap_k, u64* kout, u32* gpos, u64* desc, u32 parts, u32 epoch, u64* counts, const u64* xw,
+                    u32 nxw) {
+    if (parts == 0 || parts > PT_MAX_PARTS || nxw > PT_XW_MAX) return hipErrorInvalidValue;
+    if (W && (W > cap_p || (u64)parts * cap_p > 0xFFFFFFFFull)) return hipErrorInvalidValue;
+    if (R && (R > cap_k || (u64)parts * cap_k > 0xFFFFFFFFull)) return hipErrorInvalidValue;
+    PtFJob P{(const u64*)puts, W, cap_p, pout, ppos, desc, counts, (u32)((W + PF_TILE - 1) / PF_TILE)};
+    PtFJob K{keys, R, cap_k, kout, gpos, desc + (u64)P.tiles * parts, counts + parts,
+             (u32)((R + PF_TILE - 1) / PF_TILE)};
+    PtFWords x{};
+    for (u32 k = 0; k < nxw; k++) x.w[k] = xw[k];
+    x.dst = counts + 2 * parts;
+    x.n = nxw;
+    const u32 blocks = P.tiles + K.tiles;
+    pt_fused_kernel<<<blocks ? blocks : 1u, PF_TPB, 0, s>>>(P, K, parts, (u64)(epoch & ((1u << 22) - 1)) << PD_EP, x);
+    return hipGetLastError();
+}
+
+hipError_t pt_route2(hipStream_t s, const u64* src_a, const uint8_t* src8_a, const u32* pos_a, u64 n_a, u64* dst_a,
+                     uint8_t* dst8_a, const u64* src_b, const uint8_t* src8_b, const u32* pos_b, u64 n_b, u64* dst_b,
+                     uint8_t* dst8_b) {
+    const u64 n = n_a + n_b;
+    if (n == 0) return hipSuccess;
+    const u64 blocks = (n + PT_TPB - 1) / PT_TPB;
+    pt_route2_kernel<<<(unsigned)(blocks < 4096 ? blocks : 4096), PT_TPB, 0, s>>>(
+        PtRoute{src_a, src8_a, pos_a, n_a, dst_a, dst8_a}, PtRoute{src_b, src8_b, pos_b, n_b, dst_b, dst8_b});
+    return hipGetLastError();
+}
+
+u64 pt_desc_words(u64 W, u64 R, u32 parts) {
+    return ((W + PF_TILE - 1) / PF_TILE + (R + PF_TILE - 1) / PF_TILE) * parts;
+}
+
 // Scratch for the tile counts and offsets, grown on demand (the replica's stream is drained
 // before a reallocation).
 static hipError_t pt_scratch(nrg_ctx* c, u64 words) {

@@ -177,6 +177,8 @@ SIGNATURES = {
     "nrg_route_back_async": (C.c_int, [vp, vp, vp, vp, u64, vp, vp]),
     "nrg_hashmap_prefill_partition": (C.c_int, [vp, u64, u64, C.c_uint32, C.c_uint32]),
     "nrg_group_partitioned_round": (C.c_int, [vp, C.POINTER(Round)]),
+    "nrg_group_partitioned_round_async": (C.c_int, [vp, C.POINTER(Round)]),
+    "nrg_group_partitioned_flush": (C.c_int, [vp]),
 }
 
 # include/nrgpu_testing.h (kernel unit-test hooks)

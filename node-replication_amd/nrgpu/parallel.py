@@ -255,12 +255,29 @@ class PartitionedGroup(ReplicaGroup):
     send/recv): nrg_group_partitioned_round."""
 
     def round(self, puts, n: int, get_keys, n_gets: int, get_vals, get_found, prev=None, prev_found=None):
+        """One round, queued once its counts are exchanged (nrg_group_partitioned_round)."""
         r = self._round
         r.recs, r.n, r.resp, r.some = _ptr(puts), n, _ptr(prev), _ptr(prev_found)
         r.get_keys, r.n_gets, r.get_vals, r.get_found = _ptr(get_keys), n_gets, _ptr(get_vals), _ptr(get_found)
         rc = self._lib.nrg_group_partitioned_round(self._h, C.byref(r))
         if rc:
             self._check(rc, "nrg_group_partitioned_round")
+
+    def round_async(self, puts, n: int, get_keys, n_gets: int, get_vals, get_found, prev=None, prev_found=None):
+        """Pipelined: queue this round and complete the previous one (nrg_group_partitioned_round_async).
+        This round's buffers stay borrowed until the next round_async / flush / sync."""
+        r = self._round
+        r.recs, r.n, r.resp, r.some = _ptr(puts), n, _ptr(prev), _ptr(prev_found)
+        r.get_keys, r.n_gets, r.get_vals, r.get_found = _ptr(get_keys), n_gets, _ptr(get_vals), _ptr(get_found)
+        rc = self._lib.nrg_group_partitioned_round_async(self._h, C.byref(r))
+        if rc:
+            self._check(rc, "nrg_group_partitioned_round_async (the previous round)")
+
+    def flush(self):
+        """Complete the round queued by round_async, if any."""
+        rc = self._lib.nrg_group_partitioned_flush(self._h)
+        if rc:
+            self._check(rc, "nrg_group_partitioned_flush")
 
 
 class PartitionedHashMap:

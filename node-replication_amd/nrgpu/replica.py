@@ -157,7 +157,8 @@ class DeviceReplica:
 
     @_stream_ordered
     def join(self):
-        """Order outstanding side-stream reads (pipeline=1) on this replica's stream."""
+        """Order outstanding side-stream reads (pipeline=1) on this replica's stream.
+        Ordered after torch's current stream, and torch's stream after it (_stream_ordered)."""
         L.check(self._lib.nrg_join(self._h), "nrg_join")
 
     # -- log -----------------------------------------------------------------------
@@ -174,12 +175,14 @@ class DeviceReplica:
 
     @_stream_ordered
     def log_append_device(self, d_recs, n: int, origin: int) -> int:
+        """Ordered after torch's current stream, and torch's stream after it (_stream_ordered)."""
         first = C.c_uint64()
         L.check(self._lib.nrg_log_append_async(self._h, _dptr(d_recs), n, origin, C.byref(first)), "append")
         return first.value
 
     @_stream_ordered
     def log_append_segments(self, d_base, seg_stride: int, lens: Sequence[int], origins: Sequence[int]):
+        """Ordered after torch's current stream, and torch's stream after it (_stream_ordered)."""
         key = (tuple(lens), tuple(origins))
         if getattr(self, "_seg_key", None) != key:  # marshalled once per distinct round shape
             nseg = len(lens)
@@ -206,18 +209,21 @@ class DeviceReplica:
 
     @_stream_ordered
     def log_exec_device(self, resp_lo=0, resp_hi=0, d_resp=None, d_some=None):
+        """Ordered after torch's current stream, and torch's stream after it (_stream_ordered)."""
         L.check(self._lib.nrg_log_exec_async(self._h, resp_lo, resp_hi, _dptr(d_resp), _dptr(d_some)), "exec")
 
     @_stream_ordered
     def st_round_device(self, d_ops, n: int, origin: int, d_resp=None, d_some=None):
         """Replica::combine for one stack batch on device buffers: append + exec in one replay
-        pass (nrg_stack_round_async); Pop responses for these ops into d_resp / d_some."""
+        pass (nrg_stack_round_async); Pop responses for these ops into d_resp / d_some.
+        Ordered after torch's current stream, and torch's stream after it (_stream_ordered)."""
         L.check(self._lib.nrg_stack_round_async(self._h, _dptr(d_ops), n, origin, _dptr(d_resp), _dptr(d_some)),
                 "stack_round")
 
     @_stream_ordered
     def sy_round_device(self, d_ops, n: int, origin: int, d_resp=None, d_some=None):
-        """Replica::combine for one synthetic batch on device buffers (nrg_synth_round_async)."""
+        """Replica::combine for one synthetic batch on device buffers (nrg_synth_round_async).
+        Ordered after torch's current stream, and torch's stream after it (_stream_ordered)."""
         L.check(self._lib.nrg_synth_round_async(self._h, _dptr(d_ops), n, origin, _dptr(d_resp), _dptr(d_some)),
                 "synth_round")
 
@@ -235,11 +241,13 @@ class DeviceReplica:
 
     @_stream_ordered
     def hm_get_device(self, d_keys, n, d_vals, d_found):
+        """Ordered after torch's current stream, and torch's stream after it (_stream_ordered)."""
         L.check(self._lib.nrg_hashmap_get_async(self._h, _dptr(d_keys), n, _dptr(d_vals), _dptr(d_found)), "get")
 
     @_stream_ordered
     def hm_round_device(self, d_puts, W, origin, d_get_keys, R, d_get_vals, d_get_found, d_prev=None,
                         d_prev_found=None):
+        """Ordered after torch's current stream, and torch's stream after it (_stream_ordered)."""
         L.check(self._lib.nrg_hashmap_round_async(self._h, _dptr(d_puts), W, origin, _dptr(d_get_keys), R,
                                                   _dptr(d_get_vals), _dptr(d_get_found), _dptr(d_prev),
                                                   _dptr(d_prev_found)), "round")
@@ -247,6 +255,7 @@ class DeviceReplica:
     @_stream_ordered
     def hm_round_segments_device(self, d_base, seg_stride, lens, origins, resp_seg, d_get_keys, R, d_get_vals,
                                  d_get_found, d_prev=None, d_prev_found=None):
+        """Ordered after torch's current stream, and torch's stream after it (_stream_ordered)."""
         key = (tuple(lens), tuple(origins))
         if getattr(self, "_seg_key", None) != key:  # marshalled once per distinct round shape
             nseg = len(lens)
@@ -271,13 +280,15 @@ class DeviceReplica:
 
     @_stream_ordered
     def hm_partition_device(self, d_puts, W, d_keys, R, parts, d_puts_out, d_put_pos, d_keys_out, d_get_pos, d_counts):
-        """Stable partition of a round's Puts and Get keys by owner (nrg_hashmap_partition_async)."""
+        """Stable partition of a round's Puts and Get keys by owner (nrg_hashmap_partition_async).
+        Ordered after torch's current stream, and torch's stream after it (_stream_ordered)."""
         L.check(self._lib.nrg_hashmap_partition_async(self._h, _dptr(d_puts), W, _dptr(d_keys), R, parts,
                                                       _dptr(d_puts_out), _dptr(d_put_pos), _dptr(d_keys_out),
                                                       _dptr(d_get_pos), _dptr(d_counts)), "partition")
 
     @_stream_ordered
     def route_back_device(self, d_src, d_src8, d_pos, n, d_dst, d_dst8):
+        """Ordered after torch's current stream, and torch's stream after it (_stream_ordered)."""
         L.check(self._lib.nrg_route_back_async(self._h, _dptr(d_src), _dptr(d_src8), _dptr(d_pos), n, _dptr(d_dst),
                                                _dptr(d_dst8)), "route_back")
 
@@ -361,22 +372,27 @@ class DeviceReplica:
     # -- generators / timing -------------------------------------------------------
     @_stream_ordered
     def gen_uniform_device(self, d_out, n, seed, span):
+        """Ordered after torch's current stream, and torch's stream after it (_stream_ordered)."""
         L.check(self._lib.nrg_gen_uniform_async(self._h, _dptr(d_out), n, seed, span))
 
     @_stream_ordered
     def gen_raw_device(self, d_out, n, seed):
+        """Ordered after torch's current stream, and torch's stream after it (_stream_ordered)."""
         L.check(self._lib.nrg_gen_raw_async(self._h, _dptr(d_out), n, seed))
 
     @_stream_ordered
     def gen_zipf_device(self, d_out, n, seed, N, theta=0.99, scramble=False):
+        """Ordered after torch's current stream, and torch's stream after it (_stream_ordered)."""
         L.check(self._lib.nrg_gen_zipf_async(self._h, _dptr(d_out), n, seed, N, float(theta), int(scramble)), "zipf")
 
     @_stream_ordered
     def gen_stack_ops_device(self, d_out, n, seed):
+        """Ordered after torch's current stream, and torch's stream after it (_stream_ordered)."""
         L.check(self._lib.nrg_gen_stack_ops_async(self._h, _dptr(d_out), n, seed), "stack ops")
 
     @_stream_ordered
     def gen_puts_device(self, d_out, d_keys, d_vals, n):
+        """Ordered after torch's current stream, and torch's stream after it (_stream_ordered)."""
         L.check(self._lib.nrg_gen_puts_async(self._h, _dptr(d_out), _dptr(d_keys), _dptr(d_vals), n))
 
     def kernel_timing(self, enable: bool = True, only: Optional[str] = None, every: int = 1):

@@ -136,4 +136,6 @@ def test_key_owner_matches_the_python_mirror(lib):
     from nrgpu import _lib as L
 
     assert lib.nrg_group_partitioned_round(None, None) == L.NRG_E_INVAL
+    assert lib.nrg_group_partitioned_round_async(None, None) == L.NRG_E_INVAL
+    assert lib.nrg_group_partitioned_flush(None) == L.NRG_E_INVAL
     assert lib.nrg_hashmap_partition_async(None, None, 0, None, 0, 2, None, None, None, None, None) == L.NRG_E_INVAL

@@ -261,12 +261,15 @@ def _digest_sum(digs):
     return tot
 
 
-@pytest.mark.parametrize("G,skew", [(3, False), (8, False), (3, True)])
-def test_group_partitioned_members(nrg, orc, G, skew):
+@pytest.mark.parametrize("G,skew,pipelined", [(3, False, False), (8, False, False), (3, True, False), (1, False, True),
+                                              (3, False, True), (8, False, True), (3, True, True)])
+def test_group_partitioned_members(nrg, orc, G, skew, pipelined):
     """cnr-style partitioned rounds (nrg_group_partitioned_round) over G partitions: every
     member's Gets and previous values equal the NR replay of the global log, and the partitions'
     digests add up to the NR replica's. skew: every Put of every member belongs to partition 0,
-    which then receives G times its max_batch in one round and replays it in chunks."""
+    which then receives G times its max_batch in one round and replays it in chunks. pipelined:
+    the rounds go through nrg_group_partitioned_round_async back to back (each call completes the
+    round before it) and one flush; checked afterwards, round by round."""
     import torch
 
     from nrgpu.parallel import key_owner
@@ -283,7 +286,8 @@ def test_group_partitioned_members(nrg, orc, G, skew):
     om.prefill_range(prefill, 1)
     pool = orc.gen_uniform(200_000, 99, span)
     owned0 = pool[key_owner(pool, G) == 0]
-    for r in range(4):
+    posted = []
+    for r in range(5 if pipelined else 4):
         rd = (L.Round * G)()
         keep = []
         for i in range(G):
@@ -310,8 +314,17 @@ def test_group_partitioned_members(nrg, orc, G, skew):
             rd[i].get_vals, rd[i].get_found = d["gv"].data_ptr(), d["gf"].data_ptr()
             keep.append((d, k, v, gk, w_prev))
         torch.cuda.synchronize()
+        if pipelined:
+            L.check(lib.nrg_group_partitioned_round_async(g, rd), f"partitioned round {r} (completes round {r - 1})")
+            posted.append((rd, keep))
+            continue
         L.check(lib.nrg_group_partitioned_round(g, rd), f"partitioned round {r}")
         L.check(lib.nrg_group_sync(g))
+        posted.append((rd, keep))
+    if pipelined:
+        L.check(lib.nrg_group_partitioned_flush(g), "flush")
+        L.check(lib.nrg_group_sync(g))
+    for r, (rd, keep) in enumerate(posted):
         exp = [om.replay(k, v) for (_, k, v, _, _) in keep]
         for i, (d, k, v, gk, w_prev) in enumerate(keep):
             msg = f"G={G} round {r} member {i}"

@@ -292,12 +292,14 @@ def _digest_sum(digs):
     return tot
 
 
-@pytest.mark.parametrize("G,skew", [(2, False), (3, False), (8, False), (3, True)])
-def test_join_partitioned_rounds(nrg, orc, G, skew):
+@pytest.mark.parametrize("G,skew,pipelined", [(2, False, False), (3, False, False), (8, False, False),
+                                              (3, True, False), (3, False, True), (8, True, True)])
+def test_join_partitioned_rounds(nrg, orc, G, skew, pipelined):
     """cnr-style partitioned rounds through PartitionedGroup, one rank per thread: the count
     exchange, the send/recv plan and the answers back between separate callers. Every rank's
     Gets and previous values equal the NR replay; the partitions' digests add up to the NR
-    replica's. skew: every Put belongs to partition 0 (replayed there in max_batch chunks)."""
+    replica's. skew: every Put belongs to partition 0 (replayed there in max_batch chunks).
+    pipelined: round_async back to back, one flush, answers read afterwards."""
     import torch
 
     from nrgpu import DeviceReplica
@@ -333,7 +335,7 @@ def test_join_partitioned_rounds(nrg, orc, G, skew):
         rep = DeviceReplica(L.NRG_DS_HASHMAP, 0, log2_slots=17, max_batch=4096, replica_id=rank + 1)
         rep.hm_prefill_partition(prefill, 1, rank, G)
         grp = PartitionedGroup(rep, rank, G, uid=uid)
-        res = []
+        res, bufs = [], []
         for parts, _, _ in plan:
             k, v, gk, w_prev = parts[rank]
             W, R = len(k), len(gk)
@@ -344,9 +346,18 @@ def test_join_partitioned_rounds(nrg, orc, G, skew):
             pv = torch.full((max(W, 1),), -1, dtype=torch.int64, device="cuda")
             pf = torch.full((max(W, 1),), 7, dtype=torch.uint8, device="cuda")
             torch.cuda.synchronize()
+            if pipelined:
+                grp.round_async(p, W, g, R, gv, gf, pv if w_prev else None, pf if w_prev else None)
+                bufs.append((p, g, gv, gf, pv, pf, R, W))
+                continue
             grp.round(p, W, g, R, gv, gf, pv if w_prev else None, pf if w_prev else None)
             grp.sync()
             res.append((_u64(gv[:R]), gf[:R].cpu().numpy(), _u64(pv[:W]), pf[:W].cpu().numpy()))
+        if pipelined:
+            grp.flush()
+            grp.sync()
+            res = [(_u64(gv[:R]), gf[:R].cpu().numpy(), _u64(pv[:W]), pf[:W].cpu().numpy())
+                   for (_, _, gv, gf, pv, pf, R, W) in bufs]
         dig = rep.hm_digest()
         grp.close()
         rep.close()
