@@ -52,6 +52,10 @@ int nrg_test_debug_read(nrg_ctx* ctx, uint64_t* out, uint64_t words);
                                    for rounds of >= 2^16 Puts, else 256: the default) */
 #define NRG_KNOB_COMB_GATHER 15 /* combiner: us an idle combiner waits for as many posts as the last
                                    round carried before sealing (0..1000, default 20; 0 = seal at once) */
+#define NRG_KNOB_COMB_SERVE 17 /* combiner (hashmap): 1 (default) = small rounds go to the resident round
+                                   server (hm_serve_kernel) instead of a launch each; 0 = launched;
+                                   v >= 2 (tests) = only rounds of at most v ops are served, so
+                                   served and launched rounds alternate                          */
 #define NRG_KNOB_SMALL_MAX 12   /* hashmap: rounds of at most this many Puts (<= 2048, and <= 8192
                                    Gets) replay in one one-workgroup launch (0: never; the
                                    combiner sets 2048 while it is open)                          */
@@ -67,6 +71,12 @@ int nrg_test_debug_read(nrg_ctx* ctx, uint64_t* out, uint64_t words);
                                    2 (+1) = synthetic only, also drop the barrier that guards the
                                    bucket pass's tile map (diagnostic: results WRONG)            */
 int nrg_test_set_knob(nrg_ctx* ctx, int knob, uint64_t value);
+/* The combiner's round-server words and round counters: out = {posted, served, exited,
+ * session, server running, rounds completed, rounds launched, open round}. */
+int nrg_test_combiner_probe(nrg_combiner* m, uint64_t out[8]);
+/* The combiner's round phases, summed over its rounds (ns): out = {rounds, batch open -> sealed,
+ * sealed -> enqueued, enqueued -> completion seen}. */
+int nrg_test_combiner_times(nrg_combiner* m, uint64_t out[4]);
 
 /* Replica groups created after nrg_test_loopback_collectives(1) (nrg_group_open,
  * nrg_group_unique_id / nrg_group_join) use an in-process stand-in for RCCL instead of RCCL:

@@ -51,6 +51,8 @@ static int run(int threads, int batch, double secs, bool stack, int spin, int de
         if (int r = nrg_test_set_knob(ctx, NRG_KNOB_COMB_DEPTH, (uint64_t)depth)) return r;
     if (const char* g = std::getenv("CB_GATHER"))  // (this tool's own setting: the gather window, us)
         if (int r = nrg_test_set_knob(ctx, NRG_KNOB_COMB_GATHER, std::strtoull(g, nullptr, 10))) return r;
+    if (const char* g = std::getenv("CB_SERVE"))  // (this tool's own setting: the round server on / off)
+        if (int r = nrg_test_set_knob(ctx, NRG_KNOB_COMB_SERVE, std::strtoull(g, nullptr, 10))) return r;
     nrg_combiner* comb = nullptr;
     if (int r = nrg_combiner_open(ctx, (uint32_t)threads, &comb)) return r;
     std::atomic<bool> stop{false};
@@ -110,6 +112,10 @@ static int run(int threads, int batch, double secs, bool stack, int spin, int de
                 stack ? "stack  " : "hashmap", threads, batch, spin, depth, tot / dt / 1e6, (unsigned long long)rounds,
                 rounds ? (double)ops / rounds : 0.0, rounds / dt / 1e3, err ? "  ERROR" : "");
     std::printf("        clients' CPU: user %.2f s, system %.2f s\n", usr_us.load() / 1e6, sys_us.load() / 1e6);
+    uint64_t tm[4] = {0, 0, 0, 0};
+    if (nrg_test_combiner_times(comb, tm) == 0 && tm[0])
+        std::printf("        per round (us): gather %.2f  seal->enqueued %.2f  enqueued->done %.2f\n", tm[1] / 1e3 / tm[0],
+                    tm[2] / 1e3 / tm[0], tm[3] / 1e3 / tm[0]);
     std::fflush(stdout);
     nrg_combiner_close(comb);
     nrg_close(ctx);

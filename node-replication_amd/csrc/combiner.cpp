@@ -53,6 +53,7 @@ constexpr uint32_t WAKE_FAN = 2;  // children each woken waiter wakes (a binary 
                                   // 16 threads 16.2-16.8 vs 18.0-19.0 M ops/s, 256 threads 31 vs 43,
                                   // 64 threads 40.4 vs 37.6; profiles/r04_combiner.txt E)
 constexpr int NB = 6;                 // batch slots
+static_assert(NB <= (int)nrg::SERVE_SLOTS, "a doorbell per batch slot");
 constexpr uint64_t DEPTH = 2;         // default rounds in flight (NRG_KNOB_COMB_DEPTH, <= NB - 2: a
                                       // slot's clients copy their responses out while later rounds run)
 // With a round in flight, the open batch is sealed into a second one only once it holds this
@@ -92,8 +93,8 @@ uint64_t now_ns() {
 
 enum : uint32_t { FREE = 0, OPEN = 1, SEALED = 2, DONE = 3 };
 
-void futex_wait(std::atomic<uint32_t>* w, uint32_t seen) {
-    const timespec ts{0, 2000000};  // a lost wake-up costs at most 2 ms
+void futex_wait(std::atomic<uint32_t>* w, uint32_t seen, long ns = 2000000) {
+    const timespec ts{0, ns};  // a lost wake-up costs at most 2 ms
     syscall(SYS_futex, (uint32_t*)w, FUTEX_WAIT_PRIVATE, seen, &ts, nullptr, 0);
 }
 void futex_wake_all(std::atomic<uint32_t>* w) { syscall(SYS_futex, (uint32_t*)w, FUTEX_WAKE_PRIVATE, INT32_MAX, nullptr, nullptr, 0); }
@@ -128,6 +129,9 @@ struct alignas(64) Batch {
     uint8_t* rsome = nullptr;
     uint32_t* err = nullptr;  // the replica's error latch after the round (ERR_PENDING until then)
     uint32_t polls = 0;       // retire's polls of the word (the event is queried every 256th)
+    uint64_t t_open = 0, t_seal = 0, t_post = 0;  // (stats) when the batch opened, was sealed, went out
+    bool served = false;      // the round went to the round server (no launch, no event)
+    uint64_t lo = 0;          // its first log position (a relaunched server starts there)
     hipEvent_t done = nullptr;
 };
 
@@ -188,6 +192,7 @@ struct nrg_combiner {
     alignas(64) std::atomic<uint64_t> completed{0};  // rounds < completed are done
     std::atomic<uint64_t> launched{0};               // rounds < launched are enqueued (combiner thread)
     std::atomic<uint64_t> rounds{0}, ops{0};
+    uint64_t t_n = 0, t_gather = 0, t_enqueue = 0, t_gpu = 0;  // (combiner thread) round phase sums, ns
     int32_t spin_cap = 0;                            // clients that may spin at once
     uint64_t depth = DEPTH;                          // rounds in flight
     bool depth_auto = true;                          // a second round only for a batch of SECOND_MIN ops
@@ -195,6 +200,14 @@ struct nrg_combiner {
     uint32_t last_posts = 0;                         // posts of the last sealed batch
     uint64_t gather_k = ~0ull, gather_t0 = 0;        // the batch being gathered, its first sight
     alignas(64) std::atomic<int32_t> spinning{0};
+    // the round server (hashmap.hip hm_serve_kernel): small hashmap rounds without a launch each
+    nrg::ServeCtl* sc = nullptr;     // mapped host memory
+    nrg::SmallJobBlob* hdr = nullptr;  // [NB] the jobs, by batch slot (mapped host memory)
+    bool serve = false;              // policy (NRG_KNOB_COMB_SERVE)
+    uint32_t serve_max = 0;          // (tests) serve only rounds of at most this many ops (0: any)
+    bool srv_running = false;        // a server of session `session` is launched and not seen to exit
+    uint64_t session = 0;
+    uint64_t idle_t0 = 0;            // (combiner thread) when it went idle with the server running
     // the combiner thread
     std::thread worker;
     std::atomic<bool> stop{false};
@@ -212,6 +225,8 @@ void* host_alloc(uint64_t bytes) {
 
 void comb_free(nrg_combiner* m) {
     if (!m) return;
+    if (m->sc) (void)hipHostFree(m->sc);
+    if (m->hdr) (void)hipHostFree(m->hdr);
     for (Batch& x : m->b) {
         void* ps[] = {x.recs, x.reads, x.wresp, x.wsome, x.rresp, x.rsome, x.err};
         for (void* p : ps)
@@ -221,6 +236,49 @@ void comb_free(nrg_combiner* m) {
     }
     delete[] m->tok;
     delete m;
+}
+
+// ---- the round server ----------------------------------------------------------------------------
+// A resident workgroup (hm_serve_kernel) serves the small hashmap rounds: the combiner thread
+// writes a round's job into its slot's header and bumps `posted`; the round's error word is its
+// completion as before. Any launch on the replica's stream would queue behind the server, so the
+// server is stopped first (it drains every posted round, then exits); it is also stopped when the
+// combiner has been idle for SERVE_IDLE_NS and at close, and exits by itself after SERVE_IDLE_TICKS
+// without a post (a host that died or stalled never leaves it running).
+constexpr uint64_t SERVE_IDLE_NS = 1000000;      // 1 ms idle: stop the server
+constexpr uint64_t SERVE_IDLE_TICKS = 10000000;  // 100 ms of the 100-MHz wall clock: it stops itself
+
+uint64_t vload(const uint64_t* p) { return __atomic_load_n(p, __ATOMIC_SEQ_CST); }
+
+int serve_start(nrg_combiner* m, uint64_t first, uint64_t first_lo) {
+    nrg_ctx* c = m->ctx;
+    m->session++;
+    __atomic_store_n(&m->sc->stop, 0u, __ATOMIC_SEQ_CST);
+    if (nrg::hm_serve_launch(c, m->sc, m->hdr, NB, first, first_lo, m->session, SERVE_IDLE_TICKS) != hipSuccess)
+        return NRG_E_HIP;
+    m->srv_running = true;
+    return NRG_OK;
+}
+
+// stop the server once every posted round is served (combiner thread)
+int serve_stop(nrg_combiner* m) {
+    if (!m->srv_running) return NRG_OK;
+    __atomic_store_n(&m->sc->stop, 1u, __ATOMIC_SEQ_CST);
+    hipStream_t st = (hipStream_t)nrg_get_stream(m->ctx);
+    int rc = NRG_OK;
+    for (uint32_t i = 0; vload(&m->sc->exited) != m->session; i++) {
+        if ((i & 255) == 255) {  // a server that faulted never writes `exited`
+            const hipError_t q = hipStreamQuery(st);
+            if (q != hipErrorNotReady) {
+                if (q != hipSuccess) rc = NRG_E_HIP;
+                break;
+            }
+        }
+        _mm_pause();
+    }
+    __atomic_store_n(&m->sc->stop, 0u, __ATOMIC_SEQ_CST);
+    m->srv_running = false;
+    return rc;
 }
 
 // Retire completed rounds in order and wake their clients (combiner thread). A round is complete
@@ -233,20 +291,38 @@ void retire(nrg_combiner* m) {
         const uint32_t ew = *(volatile uint32_t*)x.err;
         if (ew == ERR_PENDING && x.rc == NRG_OK) {
             if ((++x.polls & 255) != 0) break;
-            const hipError_t q = hipEventQuery(x.done);
-            if (q == hipErrorNotReady) break;
-            if (*(volatile uint32_t*)x.err == ERR_PENDING) x.rc = NRG_E_HIP;  // done, and the word never came
+            if (x.served) {
+                // a server that exited by itself (idle bound) before this round was posted never
+                // reads `posted` again: serve the rest from `served` with a new one
+                if (m->srv_running && vload(&m->sc->exited) == m->session && vload(&m->sc->served) <= k) {
+                    m->srv_running = false;
+                    const uint64_t s0 = vload(&m->sc->served);
+                    if (serve_start(m, s0, m->b[s0 % NB].lo) != NRG_OK) x.rc = NRG_E_HIP;
+                }
+                const hipError_t q = hipStreamQuery((hipStream_t)nrg_get_stream(m->ctx));
+                if (q != hipSuccess && q != hipErrorNotReady) x.rc = NRG_E_HIP;  // the server faulted
+                if (x.rc == NRG_OK) break;
+            } else {
+                const hipError_t q = hipEventQuery(x.done);
+                if (q == hipErrorNotReady) break;
+                if (*(volatile uint32_t*)x.err == ERR_PENDING) x.rc = NRG_E_HIP;  // done, and the word never came
+            }
         }
         std::atomic_thread_fence(std::memory_order_acquire);  // responses after the word
         if (x.rc == NRG_OK) x.rc = err_code(*(volatile uint32_t*)x.err);
         x.state.store(DONE, std::memory_order_release);
+        const uint64_t t_done = now_ns();
+        m->t_n++;
+        m->t_gather += x.t_seal - x.t_open;
+        m->t_enqueue += x.t_post - x.t_seal;
+        m->t_gpu += t_done - x.t_post;
         m->completed.store(++k, std::memory_order_seq_cst);
         if (x.nwait.load(std::memory_order_seq_cst)) wake_one(&x.wk[0]);  // the root of the wake tree
     }
 }
 
-// Enqueue the round of sealed batch x (combiner thread): the replica's writes, then its reads.
-int launch(nrg_combiner* m, Batch& x, uint32_t W, uint32_t R) {
+// Enqueue the round k of sealed batch x (combiner thread): the replica's writes, then its reads.
+int launch(nrg_combiner* m, Batch& x, uint64_t k, uint32_t W, uint32_t R) {
     nrg_ctx* c = m->ctx;
     int rc = nrg::ctx_use_device(c);
     if (rc) return rc;
@@ -254,6 +330,23 @@ int launch(nrg_combiner* m, Batch& x, uint32_t W, uint32_t R) {
     const uint32_t origin = c->cfg.replica_id;
     *(volatile uint32_t*)x.err = ERR_PENDING;
     x.polls = 0;
+    x.served = false;
+    if (m->serve && W <= 2048 && R <= nrg::SERVE_R && (m->serve_max == 0 || W + R <= m->serve_max)) {
+        // the round server takes it: the log bookkeeping here, then the slot's doorbell with the
+        // round's counts (the slot's buffers are fixed: the server read them when it started)
+        uint64_t lo = 0;
+        rc = nrg::hm_small_job(c, (const nrg_put*)x.recs, W, origin, (const uint64_t*)x.reads, R, (uint64_t*)x.rresp,
+                               x.rsome, (uint64_t*)x.wresp, x.wsome, x.err, nullptr, &lo);
+        if (rc == NRG_OK) {
+            x.lo = lo;
+            if (!m->srv_running && (rc = serve_start(m, k, lo)) != NRG_OK) return rc;
+            __atomic_store_n(&m->sc->door[k % NB], ((k + 1) << 32) | ((uint64_t)W << 16) | R, __ATOMIC_SEQ_CST);
+            x.served = true;
+            return NRG_OK;
+        }
+        rc = NRG_OK;  // not a small round of a caught-up replica: launched below
+    }
+    if (m->srv_running && (rc = serve_stop(m)) != NRG_OK) return rc;  // launches queue behind the server
     // hashmap rounds of <= 2048 Puts (>= 1) and <= 8192 Gets run as ONE small-round workgroup
     // (hashmap.hip small_round), whose last write can be the error copy
     const bool small = m->kind == NRG_DS_HASHMAP && W > 0 && W <= c->small_max && W <= 2048 && R <= 8192;
@@ -310,6 +403,7 @@ bool advance(nrg_combiner* m) {
         }
         if (t - m->gather_t0 < m->gather_ns) return false;
     }
+    x.t_seal = now_ns();
     x.state.store(SEALED, std::memory_order_seq_cst);
     while (x.writers.load(std::memory_order_seq_cst)) _mm_pause();
     m->last_posts = x.readers.load(std::memory_order_relaxed);  // (no client has left a sealed batch)
@@ -323,13 +417,15 @@ bool advance(nrg_combiner* m) {
     y.rc = NRG_OK;
     y.nwait.store(0, std::memory_order_relaxed);
     y.round.store(k + 1, std::memory_order_relaxed);
+    y.t_open = now_ns();
     y.state.store(OPEN, std::memory_order_seq_cst);
     m->open.store(k + 1, std::memory_order_seq_cst);
     m->opened.fetch_add(1, std::memory_order_seq_cst);
     if (m->open_sleepers.load(std::memory_order_seq_cst)) futex_wake_all(&m->opened);
-    x.rc = launch(m, x, W, R);
+    x.rc = launch(m, x, k, W, R);
+    x.t_post = now_ns();
     hipStream_t st = (hipStream_t)nrg_get_stream(m->ctx);
-    if (hipEventRecord(x.done, st) != hipSuccess && x.rc == NRG_OK) x.rc = NRG_E_HIP;
+    if (!x.served && hipEventRecord(x.done, st) != hipSuccess && x.rc == NRG_OK) x.rc = NRG_E_HIP;
     if (x.rc != NRG_OK) *(volatile uint32_t*)x.err = 0;  // nothing will write it: retire at once
     m->launched.store(k + 1, std::memory_order_release);
     m->rounds.fetch_add(1, std::memory_order_relaxed);
@@ -344,19 +440,28 @@ void combiner_main(nrg_combiner* m) {
         const uint64_t done0 = m->completed.load(std::memory_order_relaxed);
         retire(m);
         const bool launched = advance(m);
+        if (launched) m->idle_t0 = 0;
         if (launched || m->completed.load(std::memory_order_relaxed) != done0) continue;
         const bool busy = m->launched.load(std::memory_order_relaxed) != m->completed.load(std::memory_order_relaxed);
         if (busy) {  // a round is in flight: poll again shortly
             for (int i = 0; i < 16; i++) _mm_pause();
             continue;
         }
-        // idle: park until a post (or close) bumps `work`
+        // idle: park until a post (or close) bumps `work`; a server idle for SERVE_IDLE_NS is stopped
+        if (m->srv_running) {
+            const uint64_t t = now_ns();
+            if (!m->idle_t0) m->idle_t0 = t;
+            if (t - m->idle_t0 >= SERVE_IDLE_NS) {
+                (void)serve_stop(m);  // (a fault shows up in the next round's launch)
+                m->idle_t0 = 0;
+            }
+        }
         const uint32_t seen = m->work.load(std::memory_order_seq_cst);
         m->parked.store(1, std::memory_order_seq_cst);
         const Batch& o = m->b[m->open.load(std::memory_order_seq_cst) % NB];
         if (!o.nw.load(std::memory_order_seq_cst) && !o.nr.load(std::memory_order_seq_cst) &&
             !m->stop.load(std::memory_order_seq_cst))
-            futex_wait(&m->work, seen);
+            futex_wait(&m->work, seen, m->srv_running ? 250000 : 2000000);
         m->parked.store(0, std::memory_order_seq_cst);
     }
 }
@@ -476,6 +581,27 @@ extern "C" int nrg_combiner_open(nrg_ctx* ctx, uint32_t max_threads, nrg_combine
         comb_free(m);
         return NRG_E_NOMEM;
     }
+    if (kind == NRG_DS_HASHMAP && ctx->comb_serve != 0) {
+        ok = (m->sc = (nrg::ServeCtl*)host_alloc(sizeof(nrg::ServeCtl))) &&
+             (m->hdr = (nrg::SmallJobBlob*)host_alloc(NB * sizeof(nrg::SmallJobBlob)));
+        if (!ok) {
+            comb_free(m);
+            return NRG_E_NOMEM;
+        }
+        std::memset((void*)m->sc, 0, sizeof(nrg::ServeCtl));
+        // each slot's fixed job fields (its batch buffers), read by a server when it starts
+        for (int i = 0; i < NB && ok; i++) {
+            Batch& x = m->b[i];
+            ok = nrg::hm_small_fill(ctx, (const nrg_put*)x.recs, 0, 1, (const uint64_t*)x.reads, 1, (uint64_t*)x.rresp,
+                                    x.rsome, (uint64_t*)x.wresp, x.wsome, x.err, &m->hdr[i]);
+        }
+        if (!ok) {
+            comb_free(m);
+            return NRG_E_INVAL;
+        }
+        m->serve = true;
+        if (ctx->comb_serve >= 2) m->serve_max = (uint32_t)ctx->comb_serve;
+    }
     m->saved_pipeline = ctx->pipeline;
     ctx->pipeline = false;
     // hashmap rounds of up to 2048 Puts in one launch (hashmap.hip hm_small_round_kernel)
@@ -498,6 +624,7 @@ extern "C" int nrg_combiner_open(nrg_ctx* ctx, uint32_t max_threads, nrg_combine
         m->depth_auto = false;
     }
     m->b[0].round.store(0);
+    m->b[0].t_open = now_ns();
     m->b[0].state.store(OPEN);
     try {
         m->worker = std::thread(combiner_main, m);
@@ -520,6 +647,7 @@ extern "C" int nrg_combiner_close(nrg_combiner* m) {
     syscall(SYS_futex, (uint32_t*)&m->work, FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
     if (m->worker.joinable()) m->worker.join();  // the combiner thread touches nothing after this
     (void)nrg::ctx_use_device(m->ctx);
+    if (serve_stop(m) != NRG_OK) rc = NRG_E_HIP;
     if (hipStreamSynchronize((hipStream_t)nrg_get_stream(m->ctx)) != hipSuccess) rc = NRG_E_HIP;
     m->ctx->pipeline = m->saved_pipeline;
     m->ctx->small_max = m->saved_small;
@@ -566,6 +694,38 @@ extern "C" int nrg_combiner_get(nrg_combiner* m, uint32_t token, const uint64_t*
                                 uint8_t* found) {
     if (!m || m->kind != NRG_DS_HASHMAP) return NRG_E_INVAL;
     return post_and_wait(m, token, false, keys, n, vals, found);
+}
+
+// (tests) the round server's words and the combiner's round counters
+extern "C" int nrg_test_combiner_probe(nrg_combiner* m, uint64_t out[8]) {
+    if (!m || !out) return NRG_E_INVAL;
+    if (m->sc)
+        std::fprintf(stderr, "serve trace: served %llu; last poll: round %llu posted-seen %llu polls %llu\n",
+                     (unsigned long long)vload(&m->sc->served),
+                     (unsigned long long)vload(&m->sc->trace[1]), (unsigned long long)vload(&m->sc->trace[2]),
+                     (unsigned long long)vload(&m->sc->trace[3]));
+    uint64_t rung = 0;  // the last rung round + 1
+    for (int i = 0; m->sc && i < NB; i++) rung = std::max<uint64_t>(rung, vload(&m->sc->door[i]) >> 32);
+    out[0] = rung;
+    out[1] = m->sc ? vload(&m->sc->served) : 0;
+    out[2] = m->sc ? vload(&m->sc->exited) : 0;
+    out[3] = m->session;
+    out[4] = m->srv_running ? 1 : 0;
+    out[5] = m->completed.load();
+    out[6] = m->launched.load();
+    out[7] = m->open.load();
+    return NRG_OK;
+}
+
+// (tests) round phase sums: {rounds, ns open -> sealed, ns sealed -> posted/launched, ns posted ->
+// completion seen by the combiner thread}
+extern "C" int nrg_test_combiner_times(nrg_combiner* m, uint64_t out[4]) {
+    if (!m || !out) return NRG_E_INVAL;
+    out[0] = m->t_n;
+    out[1] = m->t_gather;
+    out[2] = m->t_enqueue;
+    out[3] = m->t_gpu;
+    return NRG_OK;
 }
 
 // GPU rounds combined so far and the ops they carried.

@@ -34,6 +34,8 @@
 //   chunk resolves. It runs at the memory-side request floor (profiles/r04_papply_phases.txt).
 //   With previous values every Put keeps its entry and one wave walks each chunk in log order:
 //   a Put's previous value is its predecessor's, else the key's value before the chunk, else None.
+#include <cstring>
+
 #include "internal.hpp"
 
 namespace nrg {
@@ -1073,16 +1075,34 @@ struct SmallJob {
 
 __device__ __forceinline__ u32 sm_hash(u64 k) { return (u32)(mix64(k) >> 40) & (SM_HT - 1); }
 
-__global__ __launch_bounds__(SM_TPB) void hm_small_round_kernel(SmallJob j, Slot* table, u32 shift, u64 tmask,
-                                                                DevCtl* ctl) {
-    __shared__ u64 s_val[SM_W];
-    __shared__ uint16_t s_ent[SM_W];    // hash entry of each Put
-    __shared__ u64 s_hk[SM_HT];
-    __shared__ u32 s_cnt[SM_HT + 1];    // Puts of the key; [SM_HT]: the side key
-    __shared__ u32 s_last[SM_HT + 1];   // its last Put + 1
-    __shared__ u32 s_created;
+struct SmallLds {
+    u64 val[SM_W];
+    uint16_t ent[SM_W];    // hash entry of each Put
+    u64 hk[SM_HT];
+    u32 cnt[SM_HT + 1];    // Puts of the key; [SM_HT]: the side key
+    u32 last[SM_HT + 1];   // its last Put + 1
+    u32 created;
+};
+
+// a word for the host, stored write-through (system scope: the line leaves the L2), so the host
+// sees it now and not at the next L2 writeback (the resident server has no kernel end to flush it)
+__device__ __forceinline__ void host_put(u64* p, u64 v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// RQ Gets per thread (RQ * SM_TPB <= SM_R per round); FLUSH: the responses and the error word are
+// made visible to the host at once (the resident server's rounds)
+template <int RQ, bool FLUSH>
+__device__ __forceinline__ void small_body(const SmallJob& j, Slot* table, u32 shift, u64 tmask, DevCtl* ctl,
+                                           SmallLds& L) {
+    u64* s_val = L.val;
+    uint16_t* s_ent = L.ent;
+    u64* s_hk = L.hk;
+    u32* s_cnt = L.cnt;
+    u32* s_last = L.last;
+    u32& s_created = L.created;
     const int tid = threadIdx.x;
-    constexpr int WQ = (int)(SM_W / SM_TPB), RQ = (int)(SM_R / SM_TPB);
+    constexpr int WQ = (int)(SM_W / SM_TPB);
     // every Put record, every Get key and every Get's first probe in flight together
     nrg_put r[WQ];
 #pragma unroll
@@ -1237,12 +1257,140 @@ __global__ __launch_bounds__(SM_TPB) void hm_small_round_kernel(SmallJob j, Slot
         j.found[i] = f ? 1 : 0;
     }
     if (j.e_out) {  // the round's last write: the host (nrg_combiner) polls it as the round's completion
+        // every wave's response stores issued before the barrier (the barrier alone does not wait
+        // for them), then one lane's system release and the word (MI355X_MICROARCH.md, producer form)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) {
             const u32 e = atomicExch(&ctl->err, 0u);
-            __threadfence_system();
-            *(volatile u32*)j.e_out = e;
+            if constexpr (FLUSH) {
+                // the responses (plain stores, every wave waited for them above) written back
+                // from the L2 by one system release, then the word itself write-through: the
+                // resident server has no kernel end to write its L2 back (write-through stores
+                // of every response, bytes included, measured slower: 18.8 vs 15.2 us a round)
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+                __hip_atomic_store(j.e_out, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            } else {
+                __threadfence_system();
+                *(volatile u32*)j.e_out = e;
+            }
         }
+    }
+}
+
+__global__ __launch_bounds__(SM_TPB) void hm_small_round_kernel(SmallJob j, Slot* table, u32 shift, u64 tmask,
+                                                                DevCtl* ctl) {
+    __shared__ SmallLds L;
+    small_body<(int)(SM_R / SM_TPB), false>(j, table, shift, tmask, ctl, L);
+}
+
+// ---- the combiner's round server: small rounds without a launch per round -----------------------
+// One resident workgroup serves the flat combiner's hashmap batches (nrg_combiner) from mapped
+// host memory. It reads every batch slot's fixed job fields (its buffers) once, then per round k
+// polls slot k's doorbell, `(k + 1) << 32 | Puts << 16 | Gets`, runs the round as
+// hm_small_round_kernel would (its log position tracked here: each round starts where the last
+// ended) and ends it with the batch's error word, as there, and `served`. The host's launch and the
+// dispatch from an idle queue leave the round's critical path. It exits when the host asks
+// (`stop`, every rung round served) or after idle_ticks of the 100-MHz wall clock without a round,
+// and then writes its session number to `exited`: every wave reaches that exit, so a host that
+// stops posting (or dies) never leaves it running. A host that finds `exited` at its session with
+// rounds still unserved relaunches from `served` (the old server never reads a doorbell again).
+static_assert(sizeof(SmallJob) <= sizeof(SmallJobBlob), "a server slot holds one SmallJob");
+static_assert(SERVE_R <= SM_R && SERVE_R % SM_TPB == 0, "server rounds are small rounds");
+__device__ __forceinline__ u64 sgpr64(u64 v) {
+    // (readfirstlane returns int: through u32, or a set bit 31 sign-extends over the high word)
+    return ((u64)(u32)__builtin_amdgcn_readfirstlane((u32)(v >> 32)) << 32) |
+           (u64)(u32)__builtin_amdgcn_readfirstlane((u32)v);
+}
+__global__ __launch_bounds__(SM_TPB) void hm_serve_kernel(ServeCtl* sc, const SmallJobBlob* hdr, u32 nslots, u64 first,
+                                                          u64 first_lo, u64 session, u64 idle_ticks, Slot* table,
+                                                          u32 shift, u64 tmask, DevCtl* ctl) {
+    __shared__ SmallLds L;
+    __shared__ SmallJob s_job[SERVE_SLOTS];  // the slots' fixed job fields, read once
+    __shared__ int s_cmd;
+    __shared__ u32 s_n, s_r;
+    __shared__ u64 s_k, s_lo;  // (in LDS: nothing of the loop stays live in registers across a round)
+    constexpr u32 JW = (u32)(sizeof(SmallJob) / 8);
+    static_assert(sizeof(SmallJob) % 8 == 0, "job copied in words");
+    for (u32 t = threadIdx.x; t < nslots * JW; t += SM_TPB)
+        ((u64*)s_job)[t] = __hip_atomic_load((const u64*)hdr[t / JW].b + t % JW, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_SYSTEM);
+    if (threadIdx.x == 0) {
+        s_k = first;
+        s_lo = first_lo;
+    }
+    __syncthreads();
+    // wave 0 polls the round's doorbell, as a whole wave in uniform control flow (readfirstlane'd
+    // values, scalar branches): a loop run by lane 0 alone under an exec mask never saw the host's
+    // next post (microbench/serve_mech.hip)
+    const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (;;) {
+        if (wave == 0) {
+            const u64 k = sgpr64(s_k);
+            const u64* door = &sc->door[k % nslots];
+            const u64 t0 = wall_clock64();
+            u64 d = 0;
+            int cmd = 0;
+            for (u64 polls = 0;; polls++) {
+                d = sgpr64(__hip_atomic_load(door, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM));
+                if ((polls & 4095) == 0 && threadIdx.x == 0) {  // (diagnostic trace, Combiner.probe)
+                    host_put(&sc->trace[1], k);
+                    host_put(&sc->trace[2], d >> 32);
+                    host_put(&sc->trace[3], polls);
+                }
+                if ((d >> 32) == k + 1) {
+                    cmd = 1;
+                    break;
+                }
+                if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&sc->stop, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM))) {
+                    // the host rings every doorbell before it asks to stop: look once more
+                    d = sgpr64(__hip_atomic_load(door, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM));
+                    cmd = (d >> 32) == k + 1 ? 1 : 0;
+                    break;
+                }
+                if (wall_clock64() - t0 > idle_ticks) break;
+                __builtin_amdgcn_s_sleep(2);
+            }
+            if (threadIdx.x == 0) {
+                s_cmd = cmd;
+                s_n = (u32)(d >> 16) & 0xFFFFu;
+                s_r = (u32)d & 0xFFFFu;
+            }
+        }
+        __syncthreads();  // (also: every wave is done with the previous round's LDS)
+        if (!s_cmd) break;
+        // the round's job: the slot's fixed fields, the round's counts, its log position
+        const SmallJob& h = s_job[s_k % nslots];
+        const u64 lo = sgpr64(s_lo);
+        const u32 n = (u32)__builtin_amdgcn_readfirstlane(s_n), R = (u32)__builtin_amdgcn_readfirstlane(s_r);
+        SmallJob j;
+        j.rec.src = (const nrg_put*)sgpr64((u64)h.rec.src);
+        j.rec.ring = (const nrg_put*)sgpr64((u64)h.rec.ring);
+        j.rec.mask = sgpr64(h.rec.mask);
+        j.rec.lo = lo;
+        j.ring_out = (nrg_put*)sgpr64((u64)h.ring_out);
+        j.n = n;
+        j.lo = lo;
+        j.resp_lo = lo;
+        j.resp_hi = lo + n;
+        j.prev = n ? (u64*)sgpr64((u64)h.prev) : nullptr;
+        j.prevf = n ? (uint8_t*)sgpr64((u64)h.prevf) : nullptr;
+        j.keys = R ? (const u64*)sgpr64((u64)h.keys) : nullptr;
+        j.R = R;
+        j.vals = (u64*)sgpr64((u64)h.vals);
+        j.found = (uint8_t*)sgpr64((u64)h.found);
+        j.e_out = (u32*)sgpr64((u64)h.e_out);
+        j.created_acc = (u64*)sgpr64((u64)h.created_acc);
+        small_body<(int)(SERVE_R / SM_TPB), true>(j, table, shift, tmask, ctl, L);  // ends with the error word
+        if (threadIdx.x == 0) {
+            s_k = s_k + 1;
+            s_lo = s_lo + n;
+            host_put(&sc->served, s_k);
+        }
+    }
+    if (threadIdx.x == 0) {
+        __threadfence_system();
+        host_put(&sc->exited, session);
     }
 }
 
@@ -1271,6 +1419,40 @@ static hipError_t small_round(nrg_ctx* c, const nrg_put* src, u64 lo, u64 n, boo
     j.created_acc = c->d_created;
     NRG_LAUNCH(c, "hm_small", hm_small_round_kernel, 1, SM_TPB, 0, c->stream, j, c->d_table, c->slot_shift,
                (u64)(c->slots - 1), c->d_ctl);
+    return hipGetLastError();
+}
+
+// The job of a small round of records [lo, lo + W) (hm_small_round_kernel's, as small_round would
+// launch it with the log copy written) into `blob`, for hm_serve_kernel; runtime.cpp hm_small_job
+// does the replica's log bookkeeping around it.
+bool hm_small_fill(nrg_ctx* c, const nrg_put* recs, u64 lo, u64 W, const u64* keys, u64 R, u64* vals, uint8_t* found,
+                   u64* prev, uint8_t* prevf, u32* e_out, SmallJobBlob* blob) {
+    if (W > SM_W || R > SERVE_R || c->pend.valid) return false;
+    if (!blob) return true;  // (the server's slots hold the fixed fields; only the checks)
+    SmallJob j;
+    j.rec = ring_src(c, recs, lo);
+    j.ring_out = (nrg_put*)c->d_ring;
+    j.n = (u32)W;
+    j.lo = lo;
+    j.resp_lo = lo;
+    j.resp_hi = lo + W;
+    j.prev = (prev && prevf && W) ? prev : nullptr;
+    j.prevf = j.prev ? prevf : nullptr;
+    j.keys = R ? keys : nullptr;
+    j.R = R ? (u32)R : 0u;
+    j.vals = vals;
+    j.found = found;
+    j.e_out = e_out;
+    j.created_acc = c->d_created;
+    std::memcpy(blob->b, &j, sizeof j);
+    return true;
+}
+
+hipError_t hm_serve_launch(nrg_ctx* c, ServeCtl* sc, const SmallJobBlob* hdr, u32 nslots, u64 first, u64 first_lo,
+                           u64 session, u64 idle_ticks) {
+    if (nslots > SERVE_SLOTS) return hipErrorInvalidValue;
+    NRG_LAUNCH(c, "hm_serve", hm_serve_kernel, 1, SM_TPB, 0, c->stream, sc, hdr, nslots, first, first_lo, session,
+               idle_ticks, c->d_table, c->slot_shift, (u64)(c->slots - 1), c->d_ctl);
     return hipGetLastError();
 }
 

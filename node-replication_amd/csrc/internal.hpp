@@ -130,6 +130,7 @@ struct nrg_ctx {
     uint64_t small_max = 0;   // hashmap: rounds of <= small_max Puts take the one-launch small round
     uint32_t comb_depth = 0;
     int32_t comb_gather = -1;  // NRG_KNOB_COMB_GATHER (us; -1 = default)
+    int32_t comb_serve = -1;   // NRG_KNOB_COMB_SERVE (-1 = default: on)
     uint32_t stall = 0;       // NRG_KNOB_STALL (tests): 1 odd waves sleep at LDS reuse points, 2 (synthetic,
                               // diagnostic: wrong results) without the bucket pass's tile-map barrier
     uint64_t* d_created = nullptr;  // [HM_CREATED_SLOTS] keys created by replay rounds
@@ -227,6 +228,33 @@ hipError_t hm_prefill_range(nrg_ctx* c, u64 n, u64 off, u32 part = 0, u32 parts 
 // partition.hip: stable partition of records (key in word 0) by key owner; answers routed back
 hipError_t pt_partition(nrg_ctx* c, const u64* in, u64 n, u32 words, u32 parts, u64* out, u32* pos, u64* total);
 hipError_t pt_gather(nrg_ctx* c, const u64* src, const uint8_t* src8, const u32* pos, u64 n, u64* dst, uint8_t* dst8);
+// the flat combiner's round server (hashmap.hip hm_serve_kernel), in mapped host memory
+// The host's words and the device's sit on separate 128-B lines: the GPU's L2 keeps host memory
+// lines it has written, and a poll of a word on a line the server itself dirtied read that stale
+// line (its buffer_inv keeps dirty lines), so the server never saw the next round.
+constexpr uint32_t SERVE_SLOTS = 8;
+struct ServeCtl {
+    alignas(128) uint64_t door[SERVE_SLOTS];  // (host) slot k % NB: (k + 1) << 32 | Puts << 16 | Gets
+    uint32_t stop;                            // (host) exit once every rung round is served
+    alignas(128) uint64_t served;             // rounds served (device)
+    uint64_t exited;                          // session of the last server that exited (device)
+    uint64_t trace[4];                        // (diagnostic) -, round, doorbell seen, polls
+};
+// Gets per served round (4 per thread of the 1024: the resident loop's registers; the combiner
+// launches rounds with more)
+constexpr uint32_t SERVE_R = 4096;
+struct SmallJobBlob {  // one small round's job (hashmap.hip SmallJob)
+    alignas(16) unsigned char b[192];
+};
+bool hm_small_fill(nrg_ctx* c, const nrg_put* recs, u64 lo, u64 W, const u64* keys, u64 R, u64* vals, uint8_t* found,
+                   u64* prev, uint8_t* prevf, u32* e_out, SmallJobBlob* blob);
+// runtime.cpp: a round as nrg_hashmap_round_async would run it as a small round, its log bookkeeping
+// done and nothing launched (the server runs it); *lo = its first log position. NRG_E_INVAL: not a
+// small round of a caught-up replica. blob (optional): the round's whole job.
+int hm_small_job(nrg_ctx* c, const nrg_put* recs, u64 W, u32 origin, const u64* keys, u64 R, u64* vals,
+                 uint8_t* found, u64* prev, uint8_t* prevf, u32* e_out, SmallJobBlob* blob, u64* lo);
+hipError_t hm_serve_launch(nrg_ctx* c, ServeCtl* sc, const SmallJobBlob* hdr, u32 nslots, u64 first, u64 first_lo,
+                           u64 session, u64 idle_ticks);
 // the replica group's partitioned rounds (partition.hip): one fused launch for the Puts and Get
 // keys into owner regions of capacity cap_p / cap_k; counts[0, parts) Puts and [parts, 2 parts)
 // Gets per owner, then the nxw host words xw; desc: pt_desc_words() look-back descriptors

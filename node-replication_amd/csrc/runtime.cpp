@@ -193,6 +193,24 @@ int staging(nrg_ctx* c, Staging& st, uint64_t bytes) {
 
 namespace nrg {
 int ctx_use_device(nrg_ctx* c) { return use_device(c); }
+
+int hm_small_job(nrg_ctx* c, const nrg_put* recs, u64 W, u32 origin, const u64* keys, u64 R, u64* vals,
+                 uint8_t* found, u64* prev, uint8_t* prevf, u32* e_out, SmallJobBlob* blob, u64* lo_out) {
+    if (!c || c->cfg.ds_kind != NRG_DS_HASHMAP || W > c->cfg.max_batch || c->ltail != c->tail) return NRG_E_INVAL;
+    if ((W && !recs) || (R && (!keys || !vals || !found))) return NRG_E_INVAL;
+    if (W > c->log_size - GC_FROM_HEAD) return NRG_E_INVAL;
+    int r = reserve(c, W);  // (caught up and nothing deferred: only moves head, launches nothing)
+    if (r) return r;
+    const uint64_t lo = c->tail;
+    if (!hm_small_fill(c, recs, lo, W, keys, R, vals, found, prev, prevf, e_out, blob)) return NRG_E_INVAL;
+    if (lo_out) *lo_out = lo;
+    c->rounds++;
+    if (W) note_origin(c, lo, W, origin);
+    c->tail = lo + W;
+    c->ltail = c->tail;
+    if (c->ctail < c->tail) c->ctail = c->tail;
+    return NRG_OK;
+}
 // c->timing_only: empty (time every kernel) or a comma-separated list of kernel names
 static bool timer_match(const nrg_ctx* c, const char* name) {
     if (c->timing_only.empty()) return true;
@@ -1164,6 +1182,10 @@ extern "C" int nrg_test_set_knob(nrg_ctx* c, int knob, uint64_t v) {
         case NRG_KNOB_COMB_GATHER:
             if (v > 1000) return NRG_E_INVAL;
             c->comb_gather = (int32_t)v;
+            return NRG_OK;
+        case NRG_KNOB_COMB_SERVE:
+            if (v > (1u << 20)) return NRG_E_INVAL;
+            c->comb_serve = (int32_t)v;
             return NRG_OK;
         case NRG_KNOB_COMB_DEPTH:
             if (v < 1 || v > 4) return NRG_E_INVAL;

@@ -183,6 +183,8 @@ SIGNATURES = {
 
 # include/nrgpu_testing.h (kernel unit-test hooks)
 TEST_SIGNATURES = {
+    "nrg_test_combiner_probe": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
+    "nrg_test_combiner_times": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
     "nrg_test_sort_pairs": (C.c_int, [vp, vp, vp, u64, C.c_int, vp, vp]),
     "nrg_test_maxscan": (C.c_int, [vp, vp, vp, u64, vp]),
     "nrg_test_ring_read": (C.c_int, [vp, u64, vp]),
@@ -195,8 +197,7 @@ TEST_SIGNATURES = {
 # nrg_test_set_knob knobs (include/nrgpu_testing.h): tuning and diagnostics of an open context
 KNOBS = {"STAMP_MAX": 1, "SKEW_EVERY": 2, "EPOCH_LIMIT": 3, "K1": 4, "EXP": 6, "SY_SORT": 7,
          "PIPELINE": 8, "COMB_SPIN": 10, "COMB_DEPTH": 11,
-         "SMALL_MAX": 12, "PART": 13, "STALL": 14, "COMB_GATHER": 15, "PA_TPB": 16, "WS": 17, "WS_PER": 18,
-         "WS_EPOS": 19, "WS_PLAIN": 20}
+         "SMALL_MAX": 12, "PART": 13, "STALL": 14, "COMB_GATHER": 15, "PA_TPB": 16, "COMB_SERVE": 17}
 
 _lib = None
 

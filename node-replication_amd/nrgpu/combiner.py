@@ -35,6 +35,13 @@ class Combiner:
         self.replica = replica
         self.kind = replica.kind
 
+    def probe(self) -> dict:
+        """(tests) the round server's words and the round counters (nrg_test_combiner_probe)."""
+        out = (C.c_uint64 * 8)()
+        L.check(self._lib.nrg_test_combiner_probe(self._h, out), "nrg_test_combiner_probe")
+        keys = ("posted", "served", "exited", "session", "running", "completed", "launched", "open")
+        return dict(zip(keys, (int(x) for x in out)))
+
     def register(self) -> int:
         """Replica::register: a thread token (NrgError NRG_E_CAPACITY past max_threads)."""
         t = C.c_uint32()

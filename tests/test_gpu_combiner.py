@@ -18,16 +18,21 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("T,ITERS", [(8, 40), (64, 12), (256, 5)])
-def test_combiner_threads(nrg, orc, T, ITERS):
+@pytest.mark.parametrize("T,ITERS,serve", [(8, 40, 1), (64, 12, 1), (256, 5, 1), (8, 40, 0), (64, 12, 0),
+                                           (256, 5, 0), (8, 40, 40), (64, 12, 200)])
+def test_combiner_threads(nrg, orc, T, ITERS, serve):
     """T client threads; at 64 the rounds are larger, waiters wake through the futex tree and
     rounds of up to 2048 Puts take the one-launch small rounds; at 256 batches pass 512 ops and
-    two rounds run in flight, the larger ones as full (not small) rounds."""
+    two rounds run in flight, the larger ones as full (not small) rounds. serve: small rounds go
+    to the resident round server (NRG_KNOB_COMB_SERVE, the default) or are launched one by one;
+    40 / 200: only rounds of at most that many ops are served, so the server is stopped for every
+    larger round and restarted after it."""
     SPAN = 5000
     cap = max(1 << 12, T * 32)
     dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=20, max_batch=cap, max_reads=cap,
                             log_bytes=64 * (1 << 16))
     dev.hm_prefill_range(1000, 1)  # keys 0..999 -> k + 1: thread 0's range starts with them
+    dev.set_knob("COMB_SERVE", serve)
     comb = nrg.Combiner(dev, T)
     errors, finals = [], {}
 
@@ -81,6 +86,65 @@ def test_combiner_threads(nrg, orc, T, ITERS):
     dev.close()
 
 
+def test_combiner_server_stops_and_restarts(nrg, orc):
+    """The round server around idle gaps and launched rounds: clients pause together (the
+    combiner stops the idle server after 1 ms, the next round starts a new one), and a round of
+    more Gets than a served round holds (5120 > SERVE_R 4096: 160 clients post 32 Gets at once)
+    is launched between served rounds (the server drains and exits first). Every answer follows
+    the per-thread models; the table equals the oracle's replay."""
+    import time
+
+    T, SPAN = 160, 4000
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=20, max_batch=8192, max_reads=8192,
+                            log_bytes=64 * (1 << 16))
+    comb = nrg.Combiner(dev, T)
+    bar = threading.Barrier(T)
+    errors, finals = [], {}
+
+    def client(seed):
+        try:
+            tok = comb.register()
+            rng = np.random.default_rng(seed)
+            lo = tok * SPAN
+            model = {}
+            for it in range(6):
+                n = 32
+                keys = rng.integers(lo, lo + SPAN, n, dtype=np.uint64)
+                vals = rng.integers(0, 2**63, n, dtype=np.uint64)
+                prev, some = comb.put(tok, keys, vals)
+                for i in range(n):
+                    want = model.get(int(keys[i]))
+                    assert bool(some[i]) == (want is not None) and (want is None or int(prev[i]) == want)
+                    model[int(keys[i])] = int(vals[i])
+                bar.wait()
+                if it % 2 == 0:
+                    time.sleep(0.005)  # everyone idle: the server is stopped
+                bar.wait()
+                q = rng.integers(lo, lo + SPAN, 32, dtype=np.uint64)  # all 160 at once: one big round
+                got, found = comb.get(tok, q)
+                for i, k in enumerate(q):
+                    want = model.get(int(k))
+                    assert bool(found[i]) == (want is not None) and (want is None or int(got[i]) == want)
+            finals[tok] = model
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+            bar.abort()
+
+    th = [threading.Thread(target=client, args=(500 + i,)) for i in range(T)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors[0]
+    comb.close()
+    om = orc.HashMap()
+    keys = np.array([k for m in finals.values() for k in m], np.uint64)
+    vals = np.array([v for m in finals.values() for v in m.values()], np.uint64)
+    om.replay(keys, vals)
+    assert dev.hm_digest() == om.digest()
+    dev.close()
+
+
 def test_combiner_limits(nrg):
     dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=12, max_batch=64, max_reads=64)
     with pytest.raises(nrg.NrgError):  # 4 threads x 32 ops exceed max_batch
@@ -117,10 +181,16 @@ def test_combiner_token_in_use(nrg):
 
     def client(who):
         rng = np.random.default_rng(40 + who)
+        # batches made up front, so the two threads' calls follow each other as closely as
+        # Python allows; at least 300 calls each, then on until the threads have collided (a
+        # round of the resident server takes ~15 us, so a collision can take a while)
+        K = rng.integers(0, 3000, (20000, 32), dtype=np.uint64)
+        V = rng.integers(0, 2**63, (20000, 32), dtype=np.uint64)
         try:
-            for _ in range(300):
-                keys = rng.integers(0, 3000, 32, dtype=np.uint64)
-                vals = rng.integers(0, 2**63, 32, dtype=np.uint64)
+            for it in range(20000):
+                if it >= 300 and refused[0] + refused[1] > 0:
+                    break
+                keys, vals = K[it], V[it]
                 try:
                     comb.put(tok, keys, vals)
                     accepted[who].append((keys, vals))
