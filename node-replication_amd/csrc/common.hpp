@@ -8,6 +8,7 @@ namespace nrg {
 
 typedef uint64_t u64;
 typedef unsigned int u32;
+typedef unsigned short u16;
 
 // Empty-slot marker of the open-addressing tables. Keys span all of u64 (key 0 is used by
 // benches/hashmap.rs:95-96,150), so the one key equal to the marker lives in a side slot

@@ -289,6 +289,11 @@ __device__ __forceinline__ u32 ent_make(u32 xl, bool set, u32 k, u32 opl) {
 __device__ __forceinline__ u32 ent_word(u32 e) { return e & (SYB_WORDS - 1); }
 __device__ __forceinline__ bool ent_set(u32 e) { return (e >> 9) & 1u; }
 __device__ __forceinline__ u32 ent_op(u32 e) { return e >> 13; }
+// In HBM a touch is two 2-B records in parallel arrays: Ew {word in bucket, SET} for the bucket
+// pass and Eo {op in tile} for the sums (and the bucket pass's SET passes): each pass reads only
+// the half it needs (round 4 kept the 4-B entry: both passes read all 4 B).
+__device__ __forceinline__ u16 ent_w(u32 e) { return (u16)(e & 0x3FFu); }
+__device__ __forceinline__ u16 ent_o(u32 e) { return (u16)(e >> 13); }
 
 // x mod d for d < 2^32 with m = floor((2^64 - 1) / d): the quotient estimate is at most two low
 // (a software 64-bit division costs ~10x more: 10 us of a 1M-op partition pass)
@@ -396,7 +401,8 @@ struct SyPartArgs {
     u32 HW, NB, W;
     u64 wm;
     u32 ntiles;
-    u32* E;
+    u16* Ew;  // [tile][entry] {word, SET} records
+    u16* Eo;  // [tile][entry] op-in-tile records
     u32* cnt_tb;
     SyHot* hot;
     SyFlags* fl;
@@ -410,7 +416,7 @@ struct SyPartArgs {
 constexpr u32 SY_DBG_PART = 1024, SY_DBG_SUM = 2048, SY_DBG_ROWS = 3072;
 struct SySumArgs {
     u32 blocks;  // workgroups of the sum role (0: none)
-    const u32* E;
+    const u16* Eo;
     const u64* V;
     u64 n, lo, resp_lo, resp_hi;
     u64* resp;
@@ -450,7 +456,8 @@ __device__ __forceinline__ void sy_part_role(const SyPartArgs& A, u32 tile, SyPa
     const u64 ring_mask = A.ring_mask, lo = A.lo, n = A.n, span = A.span, span_m = A.span_m, hr_m = A.hr_m, wm = A.wm;
     const u32 w64 = A.w64;
     const u32 HR = A.HR, HW = A.HW, NB = A.NB, W = A.W;
-    u32* __restrict__ E = A.E;
+    u16* __restrict__ Ew = A.Ew;
+    u16* __restrict__ Eo = A.Eo;
     u32* __restrict__ cnt_tb = A.cnt_tb;
     SyHot* __restrict__ hot = A.hot;
     auto& s_wcnt = L.wcnt;
@@ -607,8 +614,15 @@ __device__ __forceinline__ void sy_part_role(const SyPartArgs& A, u32 tile, SyPa
     __syncthreads();
     SYP_MARK(3);
     const u32 nops = (u32)(n - op0 < SYA_OPS ? n - op0 : SYA_OPS);
-    u32* Et = E + (u64)tile * (SYA_OPS * CW);
-    for (u32 i = tid; i < nops * CW; i += SYA_TPB) st_out(&Et[i], s_u.stage[i], A.plain_e);
+    // two records per thread: 4-B stores into each array
+    u32* Ewt = (u32*)(Ew + (u64)tile * (SYA_OPS * CW));
+    u32* Eot = (u32*)(Eo + (u64)tile * (SYA_OPS * CW));
+    const u32 ne = nops * CW;
+    for (u32 i = tid; 2 * i < ne; i += SYA_TPB) {
+        const u32 a = s_u.stage[2 * i], b = 2 * i + 1 < ne ? s_u.stage[2 * i + 1] : 0u;
+        st_out(&Ewt[i], (u32)ent_w(a) | ((u32)ent_w(b) << 16), A.plain_e);
+        st_out(&Eot[i], (u32)ent_o(a) | ((u32)ent_o(b) << 16), A.plain_e);
+    }
     if (dbg) {
         dbg[4] = wall_clock64();
         dbg[9] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
@@ -622,7 +636,7 @@ __device__ __forceinline__ void sy_part_role(const SyPartArgs& A, u32 tile, SyPa
 // touches without barriers, then per-word prefixes over the waves place them. A pass with a
 // WriteOnly in it is applied wave by wave instead (values depend on the last SET).
 // (<= 128 VGPRs: two 8-wave workgroups per CU)
-__global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) void sy_bucket_kernel(const u32* __restrict__ E, const u32* __restrict__ cnt_tb,
+__global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) void sy_bucket_kernel(const u16* __restrict__ Ew, const u16* __restrict__ Eo, const u32* __restrict__ cnt_tb,
                                                             u32 ntiles, u32 tile_entries, u64* __restrict__ V,
                                                             u64* __restrict__ words, u64 N, u32 HR, u32 W,
                                                             const nrg_synth_op* __restrict__ ring, u64 ring_mask, u64 lo,
@@ -724,7 +738,7 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
 #pragma unroll
         for (int q = 0; q < SYB_PER; q++) {
             const u32 i = base + (u32)w * (SYB_PER * 64) + q * 64 + lane;
-            nent[q] = i < total ? E[gpos_of(base, map, i)] : 0u;
+            nent[q] = i < total ? (u32)Ew[gpos_of(base, map, i)] : 0u;
         }
     };
     if (total) {
@@ -800,7 +814,8 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
             for (int q = 0; q < SYB_PER; q++) {
                 const bool isset = ent_set(ent[q]);  // 0 for touches past the end
                 const u32 iq = base + (u32)w * (SYB_PER * 64) + q * 64 + lane;
-                const u64 op = iq < total ? (u64)cmap[iq - base] * SYA_OPS + ent_op(ent[q]) : 0ull;
+                // (the op of a SET touch: its Eo record, read only in passes with a WriteOnly)
+                const u64 op = isset && iq < total ? (u64)cmap[iq - base] * SYA_OPS + Eo[gpos_of(base, cmap, iq)] : 0ull;
                 sv[q] = isset ? ring[(lo + op) & ring_mask].tid : 0ull;
             }
             for (int ww = 0; ww < SYB_WAVES; ww++) {
@@ -883,7 +898,7 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
 // Per-op sums of chunk S (one workgroup per 2048-op tile of the response window), then, in
 // workgroup 0, the ordered fold of the tiles' hot-word summaries into the hot words.
 __device__ __forceinline__ void sy_sum_role(const SySumArgs& S, u32 blk, u64* s_sum) {
-    const u32* __restrict__ E = S.E;
+    const u16* __restrict__ Eo = S.Eo;
     const u64* __restrict__ V = S.V;
     const u64 n = S.n, lo = S.lo, resp_lo = S.resp_lo, resp_hi = S.resp_hi;
     u64* __restrict__ resp = S.resp;
@@ -905,7 +920,7 @@ __device__ __forceinline__ void sy_sum_role(const SySumArgs& S, u32 blk, u64* s_
         for (u32 i = tid; i < SYS_T * SYA_OPS; i += SYC_TPB) s_sum[i] = 0;
         __syncthreads();
         const u32 TE = SYA_OPS * CW;
-        const u32* Et = E + (u64)t0 * TE;
+        const u16* Et = Eo + (u64)t0 * TE;
         // the run's entries: whole tiles of TE, then the last tile's nops % SYA_OPS ops
         const u32 ne = (u32)(nops / SYA_OPS) * TE + (u32)(nops % SYA_OPS) * CW;
         // SYS_U entries per thread in flight before their LDS adds (one at a time, every add
@@ -924,7 +939,7 @@ __device__ __forceinline__ void sy_sum_role(const SySumArgs& S, u32 blk, u64* s_
                 for (int q = 0; q < SYS_U; q++) {
                     const u32 e = e0 + q * SYC_TPB;
                     const u32 j = SYS_T == 1 ? 0u : SYS_T == 2 ? (u32)(e >= TE) : e / TE;
-                    if (e < ne) atomicAdd((unsigned long long*)&s_sum[j * SYA_OPS + ent_op(ee[q])], (unsigned long long)vv[q]);
+                    if (e < ne) atomicAdd((unsigned long long*)&s_sum[j * SYA_OPS + ee[q]], (unsigned long long)vv[q]);
                 }
             }
         };
@@ -1011,7 +1026,7 @@ static SyAux sy_aux(void* base, const nrg_config& cf) {
     const u64 te = tiles * SYA_OPS * cf.synth_cold_writes;
     SyAux x;
     x.V = (u64*)base;
-    x.E[0] = (u32*)(x.V + te);
+    x.E[0] = (u32*)(x.V + te);  // per parity: Ew (te u16) then Eo (te u16)
     x.E[1] = x.E[0] + te;
     x.cnt = x.E[1] + te;
     x.hot[0] = (SyHot*)(((uintptr_t)(x.cnt + sy_nb(cf) * tiles) + 15) & ~(uintptr_t)15);
@@ -1041,7 +1056,7 @@ static SySumArgs sy_sum_args(nrg_ctx* c, const SyDeferred& d) {
     SyAux x = sy_aux(c->d_sy_aux, cf);
     SySumArgs S{};
     S.blocks = (d.t1 - d.t0 + SYS_T - 1) / SYS_T;
-    S.E = x.E[d.par];
+    S.Eo = (const u16*)x.E[d.par] + (x.cnt - x.E[1]);  // Eo: the parity's second half
     S.V = x.V;
     S.n = d.n;
     S.lo = d.lo;
@@ -1113,7 +1128,8 @@ static hipError_t sy_bucket_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 re
     A.W = W;
     A.wm = ((1ull << 40) + W - 1) / W;
     A.ntiles = ntiles;
-    A.E = x.E[par];
+    A.Ew = (u16*)x.E[par];
+    A.Eo = (u16*)x.E[par] + (x.cnt - x.E[1]);
     A.cnt_tb = x.cnt;
     A.hot = x.hot[par];
     A.fl = x.fl;
@@ -1128,7 +1144,7 @@ static hipError_t sy_bucket_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 re
     hipError_t e = sy_launch_part(c, A, S);
     if (e != hipSuccess) return e;
     const size_t dyn = (size_t)(ntiles + 1) * 4 + (size_t)ntiles * 2;
-    sy_bucket_kernel<<<NB, SYB_TPB, dyn, st>>>(x.E[par], x.cnt, ntiles, SYA_OPS * CW, x.V, c->d_words, cf.synth_n, HR,
+    sy_bucket_kernel<<<NB, SYB_TPB, dyn, st>>>((const u16*)x.E[par], (const u16*)x.E[par] + (x.cnt - x.E[1]), x.cnt, ntiles, SYA_OPS * CW, x.V, c->d_words, cf.synth_n, HR,
                                                W, A.ring, A.ring_mask, lo, x.fl, A.epoch, par,
                                                (c->exp & 2) ? c->d_dbg : nullptr, c->stall, !((c->exp >> 8) & 1));
     timer_end(c, "sy_replay");
