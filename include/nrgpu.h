@@ -418,11 +418,13 @@ int nrg_hashmap_prefill_partition(nrg_ctx* ctx, uint64_t n, uint64_t off, uint32
  * after one host round trip for the counts (nrg_group_sync waits for the rest). Fails with the
  * same code on every rank when any rank's part is bad, before any payload moves. */
 int nrg_group_partitioned_round(nrg_group* g, const nrg_round* rounds);
-/* The pipelined form: queues this round's partition and count exchange, then completes the
- * previous round posted this way (its counts have landed by then, so the host never waits on the
- * GPU in steady state). The caller's buffers of a round stay borrowed until the next
- * nrg_group_partitioned_round_async / nrg_group_partitioned_flush / nrg_group_sync, which completes
- * it; the return value is the completed round's (NRG_OK before there is one). */
+/* The pipelined form, three calls deep: queues this round's partition and count exchange, moves
+ * the previous round's Puts and Gets to their owners and replays it (its counts have landed by
+ * then, so the host never waits on the GPU in steady state; its reads ride in the next round's
+ * first launch), and sends the round before that back into its caller's order. The caller's
+ * buffers of a round stay borrowed for the next two calls, or until nrg_group_partitioned_flush /
+ * nrg_group_sync completes every posted round. A round dropped on an agreed error (a rank's bad
+ * part) returns that error from the call that moved it (NRG_OK otherwise). */
 int nrg_group_partitioned_round_async(nrg_group* g, const nrg_round* rounds);
 /* Complete the round posted by nrg_group_partitioned_round_async, if any (its result). */
 int nrg_group_partitioned_flush(nrg_group* g);

@@ -83,11 +83,19 @@ struct DBuf {
 };
 
 // Partitioned rounds (nrg_group_partitioned_round*): buffers of one member. A round's partition
-// output and count exchange (PtPar) alternate between two parities: round e+1 is partitioned and
-// its counts exchanged before round e's payload moves (the pipelined form), the rest is per round.
-enum PtBuf { PB_RPUT, PB_RKEY, PB_RVAL, PB_RFOUND, PB_RPREV, PB_RPREVF, PB_AVAL, PB_AFOUND, PB_APREV, PB_APREVF,
-             PB_ST, PB_ALLST, PB_DESC, PB_N };
+// A round lives over three calls in the pipelined form (post, stage A, stage B: see pt_post), so its
+// partition output and count exchange (PtPar) rotate over PT_DEPTH slots and what the owner
+// received and answered (PtRecv) over two.
+enum PtBuf { PB_AVAL, PB_AFOUND, PB_APREV, PB_APREVF, PB_ST, PB_ALLST, PB_DESC, PB_N };
 enum PtPar { PP_POUT, PP_PPOS, PP_KOUT, PP_GPOS, PP_CNT, PP_ALLCNT, PP_N };
+enum PtRecv { PR_RPUT, PR_RKEY, PR_RVAL, PR_RFOUND, PR_RPREV, PR_RPREVF, PR_N };
+constexpr int PT_DEPTH = 3;
+
+// A round's send/recv plan (stage A), kept for its answers (stage B).
+struct PtPlan {
+    std::vector<uint64_t> pto, gto, pfrom, gfrom, pfrom_off, gfrom_off;
+    uint64_t rp = 0, rk = 0;
+};
 
 constexpr uint64_t GC_FROM_HEAD = 32 * 256;  // nr/src/log.rs:36 (the ring keeps this much free)
 
@@ -106,12 +114,14 @@ struct Member {
     bool used[NBUF] = {};
     void* sbuf = nullptr;  // padded send copy when a segment is shorter than the stride
     uint64_t sbytes = 0;
-    DBuf pt[PB_N];          // partitioned rounds
-    DBuf pp[2][PP_N];       // ... by round parity
-    uint64_t* h_cnt[2] = {};  // pinned: [nranks][2 * nranks + XW_N] counts, capacities, flags (by parity)
-    hipEvent_t cnt_ev[2] = {};  // the counts of that parity are in h_cnt
-    nrg_round pr[2] = {};       // the caller's part of the round of that parity
-    uint64_t cap_p[2] = {}, cap_k[2] = {};  // its owner-region capacities (the member's n, n_gets)
+    DBuf pt[PB_N];                  // partitioned rounds
+    DBuf pp[PT_DEPTH][PP_N];        // ... by round slot (round % PT_DEPTH)
+    DBuf rv[2][PR_N];               // ... by round parity
+    uint64_t* h_cnt[PT_DEPTH] = {};  // pinned: [nranks][2 * nranks + XW_N] counts, capacities, flags
+    hipEvent_t cnt_ev[PT_DEPTH] = {};  // the counts of that slot are in h_cnt
+    nrg_round pr[PT_DEPTH] = {};       // the caller's part of the round of that slot
+    uint64_t cap_p[PT_DEPTH] = {}, cap_k[PT_DEPTH] = {};  // its owner-region capacities (n, n_gets)
+    PtPlan plan[PT_DEPTH];
     uint32_t pt_epoch = 0;      // look-back descriptor tag of the last fused partition
     uint64_t xwords[8] = {};    // this rank's host words of the exchange
     hipEvent_t pt_ev = nullptr;
@@ -177,7 +187,7 @@ int member_init(Member& m, int nranks) {
     GCHK(hipStreamCreateWithFlags(&m.cstream, hipStreamNonBlocking));
     GCHK(hipEventCreateWithFlags(&m.in_ev, hipEventDisableTiming));
     GCHK(hipEventCreateWithFlags(&m.pt_ev, hipEventDisableTiming));
-    for (int q = 0; q < 2; q++) GCHK(hipEventCreateWithFlags(&m.cnt_ev[q], hipEventDisableTiming));
+    for (int q = 0; q < PT_DEPTH; q++) GCHK(hipEventCreateWithFlags(&m.cnt_ev[q], hipEventDisableTiming));
     for (int b = 0; b < NBUF; b++) {
         GCHK(hipEventCreateWithFlags(&m.gathered[b], hipEventDisableTiming));
         GCHK(hipEventCreateWithFlags(&m.freed[b], hipEventDisableTiming));
@@ -194,7 +204,7 @@ int member_init(Member& m, int nranks) {
     GCHK(hipHostMalloc(&m.h_glx, 2 * G * 8, hipHostMallocDefault));
     // the fixed-size buffers of a partitioned round's count and status exchanges
     const uint64_t CW = 2 * G + XW_N;
-    for (int q = 0; q < 2; q++) {
+    for (int q = 0; q < PT_DEPTH; q++) {
         if ((r = grow_buf(m, m.pp[q][PP_CNT], CW * 8)) || (r = grow_buf(m, m.pp[q][PP_ALLCNT], G * CW * 8))) return r;
         // mapped: a one-rank group's partition writes its counts here directly (no exchange)
         GCHK(hipHostMalloc(&m.h_cnt[q], G * CW * 8, hipHostMallocMapped));
@@ -241,12 +251,15 @@ void member_free(Member& m, const Rccl* R) {
     if (m.h_glx) (void)hipHostFree(m.h_glx);
     for (DBuf& d : m.pt)
         if (d.p) (void)hipFree(d.p);
-    for (int q = 0; q < 2; q++) {
+    for (int q = 0; q < PT_DEPTH; q++) {
         for (DBuf& d : m.pp[q])
             if (d.p) (void)hipFree(d.p);
         if (m.h_cnt[q]) (void)hipHostFree(m.h_cnt[q]);
         if (m.cnt_ev[q]) (void)hipEventDestroy(m.cnt_ev[q]);
     }
+    for (int q = 0; q < 2; q++)
+        for (DBuf& d : m.rv[q])
+            if (d.p) (void)hipFree(d.p);
     if (m.pt_ev) (void)hipEventDestroy(m.pt_ev);
     if (m.in_ev) (void)hipEventDestroy(m.in_ev);
     if (m.cstream) (void)hipStreamDestroy(m.cstream);
@@ -264,8 +277,10 @@ struct nrg_group {
     uint64_t round = 0;
     uint32_t timeout_ms = NRG_GROUP_DEFAULT_TIMEOUT_MS;  // deadline of every wait on the peers
     int broken = NRG_OK;  // sticky: a timed-out collective or disagreeing ranks end the group
-    int pt_pend = -1;     // parity of the partitioned round posted and not yet completed, or -1
-    int pt_next = 0;      // parity of the next partitioned round
+    // partitioned rounds: posted (partition + count exchange), through stage A (payload to the
+    // owners, replay with its reads deferred), through stage B (answers back, route-back)
+    uint64_t pt_posted = 0, pt_a = 0, pt_b = 0;
+    bool pt_drop[PT_DEPTH] = {};  // the round failed in stage A (an agreed error): no stage B
     char diag[256] = {};  // what broke it (nrg_group_last_error)
 };
 
@@ -628,13 +643,26 @@ int nrg_group_round_async(nrg_group* g, const nrg_round* rounds, const uint64_t*
 
 
 
-// Post a partitioned round on every local member: the fused partition of its Puts and Gets into
-// owner regions (partition.hip pt_fused, which also writes the member's exchange words) and the
-// all-gather of every rank's counts, whose host copy lands in pinned memory (cnt_ev). Everything
-// runs on the replica's stream. Local failures travel in the XW_ERR word; nothing here waits.
-static int pt_post(nrg_group* g, const nrg_round* rounds, int par) {
+// Partitioned rounds, pipelined over three calls (nrg_group_partitioned_round_async):
+//   call e     post(e):    the fused partition of round e's Puts and Gets into owner regions
+//                          (partition.hip pt_fused, which also writes the member's exchange words)
+//                          and the all-gather of every rank's counts, copied to pinned host memory
+//                          behind an event;
+//   call e+1   stage A(e): its counts (landed long ago: no host wait in steady state), the plan,
+//                          Puts and Get keys to their owners (RCCL send/recv; a rank's own part is a
+//                          device copy, or none with one rank), the owner's replay with the reads
+//                          deferred: they ride in round e+1's index launch (the replicated
+//                          pipeline's overlap);
+//   call e+2   stage B(e): (round e's reads were launched in stage A(e+1)) answers and previous
+//                          values back to the ranks that asked, one route-back launch into the
+//                          caller's order.
+// Everything runs on the replica's stream. Every failure before a round's first send/recv is
+// agreed on by all ranks (the same exchanged words): the round is dropped everywhere and the call
+// that ran its stage A returns the error.
+static int pt_post(nrg_group* g, const nrg_round* rounds, uint64_t e) {
     const Rccl* R = g->R;
     const int G = g->nranks, nl = (int)g->m.size();
+    const int sl = (int)(e % PT_DEPTH), par = (int)(e & 1);
     const uint64_t CW = 2 * (uint64_t)G + XW_N;
     for (int i = 0; i < nl; i++) {
         Member& m = g->m[i];
@@ -651,7 +679,7 @@ static int pt_post(nrg_group* g, const nrg_round* rounds, int par) {
         if (m.in_set && m.in_stream != c->stream) RCHK(order(m, m.in_stream, c->stream));
         const uint64_t n = err ? 0 : x.n, k = err ? 0 : x.n_gets;
         if (err == NRG_OK) {
-            DBuf* pp = m.pp[par];
+            DBuf* pp = m.pp[sl];
             const uint64_t bytes[] = {G * n * 16, n * 4, G * k * 8, k * 4};
             const PtPar which[] = {PP_POUT, PP_PPOS, PP_KOUT, PP_GPOS};
             for (int q = 0; q < 4 && err == NRG_OK; q++) err = grow_buf(m, pp[which[q]], bytes[q]);
@@ -663,35 +691,37 @@ static int pt_post(nrg_group* g, const nrg_round* rounds, int par) {
                 for (int q = 0; q < 4 && err == NRG_OK; q++) err = grow(m, ans[q], ab[q]);
             }
         }
-        const bool ok = err == NRG_OK;
         uint64_t* w = m.xwords;
         w[XW_PREV] = (x.resp && x.some) ? 1 : 0;
-        // receive capacities (one rank replays straight from its partition output: no RPUT/RKEY)
-        const uint64_t rp_own = std::min(m.pt[PB_RPREV].bytes / 8, m.pt[PB_RPREVF].bytes);
-        const uint64_t rk_own = std::min(m.pt[PB_RVAL].bytes / 8, m.pt[PB_RFOUND].bytes);
-        w[XW_RP_CAP] = G == 1 ? rp_own : std::min(m.pt[PB_RPUT].bytes / 16, rp_own);
-        w[XW_RK_CAP] = G == 1 ? rk_own : std::min(m.pt[PB_RKEY].bytes / 8, rk_own);
+        // receive capacities of the round's parity (one rank replays straight from its partition
+        // output: no RPUT / RKEY)
+        const DBuf* rv = m.rv[par];
+        const uint64_t rp_own = std::min(rv[PR_RPREV].bytes / 8, rv[PR_RPREVF].bytes);
+        const uint64_t rk_own = std::min(rv[PR_RVAL].bytes / 8, rv[PR_RFOUND].bytes);
+        w[XW_RP_CAP] = G == 1 ? rp_own : std::min(rv[PR_RPUT].bytes / 16, rp_own);
+        w[XW_RK_CAP] = G == 1 ? rk_own : std::min(rv[PR_RKEY].bytes / 8, rk_own);
         w[XW_ERR] = (uint64_t)(-err);
         if (++m.pt_epoch >= (1u << 22)) {  // the descriptor tag wraps: clear the stale ones once
             m.pt_epoch = 1;
             if (m.pt[PB_DESC].p) GCHK(hipMemsetAsync(m.pt[PB_DESC].p, 0, m.pt[PB_DESC].bytes, c->stream));
         }
-        const hipError_t e = nrg::pt_fused(c->stream, (const uint64_t*)x.recs, ok ? n : 0, n,
-                                           (uint64_t*)m.pp[par][PP_POUT].p, (uint32_t*)m.pp[par][PP_PPOS].p,
-                                           x.get_keys, ok ? k : 0, k, (uint64_t*)m.pp[par][PP_KOUT].p,
-                                           (uint32_t*)m.pp[par][PP_GPOS].p, (uint64_t*)m.pt[PB_DESC].p, (uint32_t)G,
-                                           m.pt_epoch, G == 1 ? m.h_cnt[par] : (uint64_t*)m.pp[par][PP_CNT].p, w,
-                                           XW_N);
-        if (e != hipSuccess) return hip_rc(e);
-        m.pr[par] = x;
-        m.cap_p[par] = n;
-        m.cap_k[par] = k;
+        const bool ok = err == NRG_OK;
+        const hipError_t he = nrg::pt_fused(c->stream, (const uint64_t*)x.recs, ok ? n : 0, n,
+                                            (uint64_t*)m.pp[sl][PP_POUT].p, (uint32_t*)m.pp[sl][PP_PPOS].p,
+                                            x.get_keys, ok ? k : 0, k, (uint64_t*)m.pp[sl][PP_KOUT].p,
+                                            (uint32_t*)m.pp[sl][PP_GPOS].p, (uint64_t*)m.pt[PB_DESC].p, (uint32_t)G,
+                                            m.pt_epoch, G == 1 ? m.h_cnt[sl] : (uint64_t*)m.pp[sl][PP_CNT].p, w,
+                                            XW_N);
+        if (he != hipSuccess) return hip_rc(he);
+        m.pr[sl] = x;
+        m.cap_p[sl] = n;
+        m.cap_k[sl] = k;
     }
     if (G > 1) {  // (one rank's all-gather is the identity: its partition wrote h_cnt itself)
         if (R->group_start() != ncclSuccess) return NRG_E_COMM;
         ncclResult_t res = ncclSuccess;
         for (int i = 0; i < nl && res == ncclSuccess; i++)
-            res = R->all_gather(g->m[i].pp[par][PP_CNT].p, g->m[i].pp[par][PP_ALLCNT].p, CW, ncclUint64,
+            res = R->all_gather(g->m[i].pp[sl][PP_CNT].p, g->m[i].pp[sl][PP_ALLCNT].p, CW, ncclUint64,
                                 g->m[i].comm, g->m[i].ctx->stream);
         RCHK(group_end(g, "partitioned count exchange"));
         if (res != ncclSuccess) return group_fail(g, NRG_E_COMM, "partitioned count exchange refused");
@@ -700,27 +730,26 @@ static int pt_post(nrg_group* g, const nrg_round* rounds, int par) {
         Member& m = g->m[i];
         RCHK(nrg::ctx_use_device(m.ctx));
         if (G > 1)
-            GCHK(hipMemcpyAsync(m.h_cnt[par], m.pp[par][PP_ALLCNT].p, (uint64_t)G * CW * 8, hipMemcpyDeviceToHost,
+            GCHK(hipMemcpyAsync(m.h_cnt[sl], m.pp[sl][PP_ALLCNT].p, (uint64_t)G * CW * 8, hipMemcpyDeviceToHost,
                                 m.ctx->stream));
-        GCHK(hipEventRecord(m.cnt_ev[par], m.ctx->stream));
+        GCHK(hipEventRecord(m.cnt_ev[sl], m.ctx->stream));
     }
     return NRG_OK;
 }
 
-// Complete the posted round of parity `par`: read its exchanged counts (posted a call earlier, so
-// normally long landed), move the Puts and Gets to their owners, replay, answer, send the answers
-// back and route them into the callers' order. Every failure before the first send/recv is agreed
-// on by all ranks (the same exchanged words); a rank's own part of the payload never leaves its
-// GPU (a device copy; with one rank, no copy at all).
-static int pt_complete(nrg_group* g, int par) {
+static void* at(void* base, uint64_t off) { return (void*)((char*)base + off); }
+
+static int pt_stage_a(nrg_group* g, uint64_t e) {
     const Rccl* R = g->R;
     const int G = g->nranks, nl = (int)g->m.size();
+    const int sl = (int)(e % PT_DEPTH), par = (int)(e & 1);
     const uint64_t CW = 2 * (uint64_t)G + XW_N;
+    g->pt_drop[sl] = true;  // until the round's payload has moved
     for (int i = 0; i < nl; i++) {
         RCHK(nrg::ctx_use_device(g->m[i].ctx));
-        RCHK(wait_event(g, g->m[i].cnt_ev[par], "partitioned count exchange"));
+        RCHK(wait_event(g, g->m[i].cnt_ev[sl], "partitioned count exchange"));
     }
-    const uint64_t* H = g->m[0].h_cnt[par];  // identical on every rank
+    const uint64_t* H = g->m[0].h_cnt[sl];  // identical on every rank
     auto word = [&](int s, uint64_t k) { return H[(size_t)s * CW + 2 * G + k]; };
     for (int s = 0; s < G; s++)
         if (word(s, XW_ERR)) return -(int)word(s, XW_ERR);  // the same answer on every rank
@@ -736,18 +765,13 @@ static int pt_complete(nrg_group* g, int par) {
     }
     // member rank r sends its owner-o region to o and receives rank s's group for r at offset
     // sum_{s' < s} (rank order = the global log order)
-    struct Plan {
-        std::vector<uint64_t> pto, gto, pfrom, gfrom, pfrom_off, gfrom_off;
-        uint64_t rp = 0, rk = 0;
-    };
-    std::vector<Plan> plan(nl);
     std::vector<int> grow_err(nl, NRG_OK);
     for (int i = 0; i < nl; i++) {
         Member& m = g->m[i];
-        Plan& P = plan[i];
+        PtPlan& P = m.plan[sl];
         const int r = m.rank;
-        P.pto.resize(G), P.gto.resize(G), P.pfrom.resize(G), P.gfrom.resize(G);
-        P.pfrom_off.resize(G), P.gfrom_off.resize(G);
+        P.pto.assign(G, 0), P.gto.assign(G, 0), P.pfrom.assign(G, 0), P.gfrom.assign(G, 0);
+        P.pfrom_off.assign(G, 0), P.gfrom_off.assign(G, 0);
         uint64_t a = 0, b = 0, cq = 0, d = 0;
         for (int o = 0; o < G; o++) {
             P.pto[o] = H[(size_t)r * CW + o];
@@ -758,14 +782,14 @@ static int pt_complete(nrg_group* g, int par) {
             P.pfrom_off[o] = cq, cq += P.pfrom[o];
             P.gfrom_off[o] = d, d += P.gfrom[o];
         }
-        if (a != m.cap_p[par] || b != m.cap_k[par]) grow_err[i] = NRG_E_HIP;  // partition kernel disagrees
+        if (a != m.cap_p[sl] || b != m.cap_k[sl]) grow_err[i] = NRG_E_HIP;  // partition kernel disagrees
         P.rp = cq;
         P.rk = d;
         if (any_grow && grow_err[i] == NRG_OK) {
             RCHK(nrg::ctx_use_device(m.ctx));
-            const PtBuf recv[] = {PB_RPUT, PB_RPREV, PB_RPREVF, PB_RKEY, PB_RVAL, PB_RFOUND};
+            const PtRecv recv[] = {PR_RPUT, PR_RPREV, PR_RPREVF, PR_RKEY, PR_RVAL, PR_RFOUND};
             const uint64_t bytes[] = {G > 1 ? P.rp * 16 : 0, P.rp * 8, P.rp, G > 1 ? P.rk * 8 : 0, P.rk * 8, P.rk};
-            for (int k = 0; k < 6 && grow_err[i] == NRG_OK; k++) grow_err[i] = grow(m, recv[k], bytes[k]);
+            for (int k = 0; k < 6 && grow_err[i] == NRG_OK; k++) grow_err[i] = grow_buf(m, m.rv[par][recv[k]], bytes[k]);
         }
     }
     ncclResult_t res = ncclSuccess;
@@ -795,57 +819,61 @@ static int pt_complete(nrg_group* g, int par) {
         for (int i = 0; i < nl; i++)
             if (grow_err[i]) return grow_err[i];  // cannot happen: the counts come from the same kernel
     }
-    auto at = [](void* base, uint64_t off) { return (void*)((char*)base + off); };
-    // where member i's replay reads its Puts / Get keys and where its answers go back from
-    auto rput_of = [&](int i) { return G == 1 ? g->m[i].pp[par][PP_POUT].p : g->m[i].pt[PB_RPUT].p; };
-    auto rkey_of = [&](int i) { return G == 1 ? g->m[i].pp[par][PP_KOUT].p : g->m[i].pt[PB_RKEY].p; };
+    g->pt_drop[sl] = false;
+    // where member i's replay reads its Puts / Get keys
+    auto rput_of = [&](int i) { return G == 1 ? g->m[i].pp[sl][PP_POUT].p : g->m[i].rv[par][PR_RPUT].p; };
+    auto rkey_of = [&](int i) { return G == 1 ? g->m[i].pp[sl][PP_KOUT].p : g->m[i].rv[par][PR_RKEY].p; };
     if (G > 1) {
-        // 1. Puts and Get keys to their owners (own part: a device copy)
+        // Puts and Get keys to their owners (own part: a device copy)
         if (R->group_start() != ncclSuccess) return NRG_E_COMM;
         for (int i = 0; i < nl && res == ncclSuccess; i++) {
             Member& m = g->m[i];
-            const Plan& P = plan[i];
-            const uint64_t cp = m.cap_p[par], ck = m.cap_k[par];
-            void *pout = m.pp[par][PP_POUT].p, *kout = m.pp[par][PP_KOUT].p;
+            const PtPlan& P = m.plan[sl];
+            const uint64_t cp = m.cap_p[sl], ck = m.cap_k[sl];
+            void *pout = m.pp[sl][PP_POUT].p, *kout = m.pp[sl][PP_KOUT].p;
             hipStream_t s = m.ctx->stream;
             for (int o = 0; o < G && res == ncclSuccess; o++) {
                 if (o == m.rank) continue;
                 if (P.pto[o]) res = R->send(at(pout, o * cp * 16), P.pto[o] * 2, ncclUint64, o, m.comm, s);
                 if (res == ncclSuccess && P.pfrom[o])
-                    res = R->recv(at(m.pt[PB_RPUT].p, P.pfrom_off[o] * 16), P.pfrom[o] * 2, ncclUint64, o, m.comm, s);
+                    res = R->recv(at(m.rv[par][PR_RPUT].p, P.pfrom_off[o] * 16), P.pfrom[o] * 2, ncclUint64, o,
+                                  m.comm, s);
                 if (res == ncclSuccess && P.gto[o]) res = R->send(at(kout, o * ck * 8), P.gto[o], ncclUint64, o, m.comm, s);
                 if (res == ncclSuccess && P.gfrom[o])
-                    res = R->recv(at(m.pt[PB_RKEY].p, P.gfrom_off[o] * 8), P.gfrom[o], ncclUint64, o, m.comm, s);
+                    res = R->recv(at(m.rv[par][PR_RKEY].p, P.gfrom_off[o] * 8), P.gfrom[o], ncclUint64, o, m.comm, s);
             }
         }
         RCHK(group_end(g, "partitioned send/recv of Puts and Gets"));
         if (res != ncclSuccess) return group_fail(g, NRG_E_COMM, "partitioned send/recv refused");
         for (int i = 0; i < nl; i++) {
             Member& m = g->m[i];
-            const Plan& P = plan[i];
+            const PtPlan& P = m.plan[sl];
             const int r = m.rank;
             RCHK(nrg::ctx_use_device(m.ctx));
             if (P.pto[r])
-                GCHK(hipMemcpyAsync(at(m.pt[PB_RPUT].p, P.pfrom_off[r] * 16), at(m.pp[par][PP_POUT].p, r * m.cap_p[par] * 16),
-                                    P.pto[r] * 16, hipMemcpyDeviceToDevice, m.ctx->stream));
+                GCHK(hipMemcpyAsync(at(m.rv[par][PR_RPUT].p, P.pfrom_off[r] * 16),
+                                    at(m.pp[sl][PP_POUT].p, r * m.cap_p[sl] * 16), P.pto[r] * 16,
+                                    hipMemcpyDeviceToDevice, m.ctx->stream));
             if (P.gto[r])
-                GCHK(hipMemcpyAsync(at(m.pt[PB_RKEY].p, P.gfrom_off[r] * 8), at(m.pp[par][PP_KOUT].p, r * m.cap_k[par] * 8),
-                                    P.gto[r] * 8, hipMemcpyDeviceToDevice, m.ctx->stream));
+                GCHK(hipMemcpyAsync(at(m.rv[par][PR_RKEY].p, P.gfrom_off[r] * 8),
+                                    at(m.pp[sl][PP_KOUT].p, r * m.cap_k[sl] * 8), P.gto[r] * 8,
+                                    hipMemcpyDeviceToDevice, m.ctx->stream));
         }
     }
-    // 2. each owner replays the Puts it received (rank order) and answers the Gets it received. A
-    //    skewed round can hand one owner more Puts than its max_batch (or ring) takes in one
-    //    replay: consecutive rounds of at most that many, the Gets answered after the last.
+    // each owner replays the Puts it received (rank order) and answers the Gets it received; the
+    // reads (and a stamp round's apply) are deferred into the next round's first launch. A skewed
+    // round can hand one owner more Puts than its max_batch (or ring) takes in one replay:
+    // consecutive rounds of at most that many, the Gets answered after the last.
     for (int i = 0; i < nl; i++) {
         Member& m = g->m[i];
-        const Plan& P = plan[i];
+        const PtPlan& P = m.plan[sl];
         nrg_ctx* c = m.ctx;
         RCHK(nrg::ctx_use_device(c));
         const uint64_t ring_room = c->log_size > 2 * GC_FROM_HEAD ? c->log_size - GC_FROM_HEAD : GC_FROM_HEAD;
         const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(c->cfg.max_batch, ring_room));
         const nrg_put* rput = (const nrg_put*)rput_of(i);
-        uint64_t* rprev = any_prev ? (uint64_t*)m.pt[PB_RPREV].p : nullptr;
-        uint8_t* rprevf = any_prev ? (uint8_t*)m.pt[PB_RPREVF].p : nullptr;
+        uint64_t* rprev = any_prev ? (uint64_t*)m.rv[par][PR_RPREV].p : nullptr;
+        uint8_t* rprevf = any_prev ? (uint8_t*)m.rv[par][PR_RPREVF].p : nullptr;
         uint64_t off = 0;
         do {
             const uint64_t n = std::min(chunk, P.rp - off);
@@ -853,39 +881,51 @@ static int pt_complete(nrg_group* g, int par) {
             if (n || (last && P.rk))
                 RCHK(nrg_hashmap_round_async(c, rput + off, n, (uint32_t)m.rank + 1,
                                              last ? (const uint64_t*)rkey_of(i) : nullptr, last ? P.rk : 0,
-                                             last ? (uint64_t*)m.pt[PB_RVAL].p : nullptr,
-                                             last ? (uint8_t*)m.pt[PB_RFOUND].p : nullptr,
+                                             last ? (uint64_t*)m.rv[par][PR_RVAL].p : nullptr,
+                                             last ? (uint8_t*)m.rv[par][PR_RFOUND].p : nullptr,
                                              rprev ? rprev + off : nullptr, rprevf ? rprevf + off : nullptr));
             off += n;
         } while (off < P.rp);
-        RCHK(nrg_join(c));
     }
-    // 3. answers back to the ranks that asked, into their owner regions (own part: a device copy;
-    //    one rank routes straight from RVAL / RPREV)
-    if (G > 1) {
+    return NRG_OK;
+}
+
+// Stage B of round e: its reads and previous values are queued (launched with the next round's
+// replay, or by the flush's join).
+static int pt_stage_b(nrg_group* g, uint64_t e) {
+    const Rccl* R = g->R;
+    const int G = g->nranks, nl = (int)g->m.size();
+    const int sl = (int)(e % PT_DEPTH), par = (int)(e & 1);
+    if (g->pt_drop[sl]) return NRG_OK;  // dropped in stage A (its error was returned there)
+    const uint64_t CW = 2 * (uint64_t)G + XW_N;
+    const uint64_t* H = g->m[0].h_cnt[sl];
+    auto word = [&](int s, uint64_t k) { return H[(size_t)s * CW + 2 * G + k]; };
+    ncclResult_t res = ncclSuccess;
+    if (G > 1) {  // answers back to the ranks that asked, into their owner regions
         if (R->group_start() != ncclSuccess) return NRG_E_COMM;
         for (int i = 0; i < nl && res == ncclSuccess; i++) {
             Member& m = g->m[i];
-            const Plan& P = plan[i];
-            const bool mine = m.pr[par].resp && m.pr[par].some;
-            const uint64_t cp = m.cap_p[par], ck = m.cap_k[par];
+            const PtPlan& P = m.plan[sl];
+            const bool mine = m.pr[sl].resp && m.pr[sl].some;
+            const uint64_t cp = m.cap_p[sl], ck = m.cap_k[sl];
+            const DBuf* rv = m.rv[par];
             hipStream_t s = m.ctx->stream;
             for (int o = 0; o < G && res == ncclSuccess; o++) {
                 if (o == m.rank) continue;
                 const bool theirs = word(o, XW_PREV) != 0;
                 if (P.gfrom[o]) {
-                    res = R->send(at(m.pt[PB_RVAL].p, P.gfrom_off[o] * 8), P.gfrom[o], ncclUint64, o, m.comm, s);
+                    res = R->send(at(rv[PR_RVAL].p, P.gfrom_off[o] * 8), P.gfrom[o], ncclUint64, o, m.comm, s);
                     if (res == ncclSuccess)
-                        res = R->send(at(m.pt[PB_RFOUND].p, P.gfrom_off[o]), P.gfrom[o], ncclUint8, o, m.comm, s);
+                        res = R->send(at(rv[PR_RFOUND].p, P.gfrom_off[o]), P.gfrom[o], ncclUint8, o, m.comm, s);
                 }
                 if (res == ncclSuccess && P.gto[o]) {
                     res = R->recv(at(m.pt[PB_AVAL].p, o * ck * 8), P.gto[o], ncclUint64, o, m.comm, s);
                     if (res == ncclSuccess) res = R->recv(at(m.pt[PB_AFOUND].p, o * ck), P.gto[o], ncclUint8, o, m.comm, s);
                 }
                 if (res == ncclSuccess && theirs && P.pfrom[o]) {
-                    res = R->send(at(m.pt[PB_RPREV].p, P.pfrom_off[o] * 8), P.pfrom[o], ncclUint64, o, m.comm, s);
+                    res = R->send(at(rv[PR_RPREV].p, P.pfrom_off[o] * 8), P.pfrom[o], ncclUint64, o, m.comm, s);
                     if (res == ncclSuccess)
-                        res = R->send(at(m.pt[PB_RPREVF].p, P.pfrom_off[o]), P.pfrom[o], ncclUint8, o, m.comm, s);
+                        res = R->send(at(rv[PR_RPREVF].p, P.pfrom_off[o]), P.pfrom[o], ncclUint8, o, m.comm, s);
                 }
                 if (res == ncclSuccess && mine && P.pto[o]) {
                     res = R->recv(at(m.pt[PB_APREV].p, o * cp * 8), P.pto[o], ncclUint64, o, m.comm, s);
@@ -896,50 +936,65 @@ static int pt_complete(nrg_group* g, int par) {
         RCHK(group_end(g, "partitioned answers back"));
         if (res != ncclSuccess) return group_fail(g, NRG_E_COMM, "partitioned answers back refused");
     }
-    // 4. back into the caller's order (one launch for the Gets' answers and the previous values)
+    // back into the caller's order (one launch for the Gets' answers and the previous values)
     for (int i = 0; i < nl; i++) {
         Member& m = g->m[i];
-        const Plan& P = plan[i];
-        const nrg_round& x = m.pr[par];
+        const PtPlan& P = m.plan[sl];
+        const nrg_round& x = m.pr[sl];
         nrg_ctx* c = m.ctx;
         const int r = m.rank;
         RCHK(nrg::ctx_use_device(c));
         const bool mine = x.resp && x.some;
-        const uint64_t cp = m.cap_p[par], ck = m.cap_k[par];
+        const uint64_t cp = m.cap_p[sl], ck = m.cap_k[sl];
+        const DBuf* rv = m.rv[par];
         void *aval = m.pt[PB_AVAL].p, *afound = m.pt[PB_AFOUND].p, *aprev = m.pt[PB_APREV].p, *aprevf = m.pt[PB_APREVF].p;
         if (G == 1) {
-            aval = m.pt[PB_RVAL].p, afound = m.pt[PB_RFOUND].p, aprev = m.pt[PB_RPREV].p, aprevf = m.pt[PB_RPREVF].p;
+            aval = rv[PR_RVAL].p, afound = rv[PR_RFOUND].p, aprev = rv[PR_RPREV].p, aprevf = rv[PR_RPREVF].p;
         } else {
             hipStream_t s = c->stream;
             if (P.gto[r]) {
-                GCHK(hipMemcpyAsync(at(aval, r * ck * 8), at(m.pt[PB_RVAL].p, P.gfrom_off[r] * 8), P.gto[r] * 8,
+                GCHK(hipMemcpyAsync(at(aval, r * ck * 8), at(rv[PR_RVAL].p, P.gfrom_off[r] * 8), P.gto[r] * 8,
                                     hipMemcpyDeviceToDevice, s));
-                GCHK(hipMemcpyAsync(at(afound, r * ck), at(m.pt[PB_RFOUND].p, P.gfrom_off[r]), P.gto[r],
+                GCHK(hipMemcpyAsync(at(afound, r * ck), at(rv[PR_RFOUND].p, P.gfrom_off[r]), P.gto[r],
                                     hipMemcpyDeviceToDevice, s));
             }
             if (mine && P.pto[r]) {
-                GCHK(hipMemcpyAsync(at(aprev, r * cp * 8), at(m.pt[PB_RPREV].p, P.pfrom_off[r] * 8), P.pto[r] * 8,
+                GCHK(hipMemcpyAsync(at(aprev, r * cp * 8), at(rv[PR_RPREV].p, P.pfrom_off[r] * 8), P.pto[r] * 8,
                                     hipMemcpyDeviceToDevice, s));
-                GCHK(hipMemcpyAsync(at(aprevf, r * cp), at(m.pt[PB_RPREVF].p, P.pfrom_off[r]), P.pto[r],
+                GCHK(hipMemcpyAsync(at(aprevf, r * cp), at(rv[PR_RPREVF].p, P.pfrom_off[r]), P.pto[r],
                                     hipMemcpyDeviceToDevice, s));
             }
         }
-        const hipError_t e = nrg::pt_route2(
-            c->stream, (const uint64_t*)aval, (const uint8_t*)afound, (const uint32_t*)m.pp[par][PP_GPOS].p, x.n_gets,
+        const hipError_t he = nrg::pt_route2(
+            c->stream, (const uint64_t*)aval, (const uint8_t*)afound, (const uint32_t*)m.pp[sl][PP_GPOS].p, x.n_gets,
             x.get_vals, x.get_found, (const uint64_t*)aprev, (const uint8_t*)aprevf,
-            (const uint32_t*)m.pp[par][PP_PPOS].p, mine ? x.n : 0, mine ? (uint64_t*)x.resp : nullptr, mine ? x.some : nullptr);
-        if (e != hipSuccess) return hip_rc(e);
+            (const uint32_t*)m.pp[sl][PP_PPOS].p, mine ? x.n : 0, mine ? (uint64_t*)x.resp : nullptr, mine ? x.some : nullptr);
+        if (he != hipSuccess) return hip_rc(he);
     }
     g->round++;
     return NRG_OK;
 }
 
-// complete the pending partitioned round, if any (its error, or NRG_OK)
+// every posted round through stage B (its result: the first error)
 static int pt_flush(nrg_group* g) {
-    if (g->pt_pend < 0) return NRG_OK;
-    const int par = g->pt_pend;
-    g->pt_pend = -1;
-    return pt_complete(g, par);
+    int rc = NRG_OK;
+    while (g->pt_a < g->pt_posted) {
+        const int r = pt_stage_a(g, g->pt_a++);
+        if (g->broken) return g->broken;
+        if (r && rc == NRG_OK) rc = r;
+    }
+    if (g->pt_b < g->pt_a) {
+        for (Member& m : g->m) {  // the last round's deferred reads
+            RCHK(nrg::ctx_use_device(m.ctx));
+            RCHK(nrg_join(m.ctx));
+        }
+    }
+    while (g->pt_b < g->pt_a) {
+        const int r = pt_stage_b(g, g->pt_b++);
+        if (g->broken) return g->broken;
+        if (r && rc == NRG_OK) rc = r;
+    }
+    return rc;
 }
 
 static int pt_check(nrg_group* g) {
@@ -955,11 +1010,23 @@ int nrg_group_partitioned_round_async(nrg_group* g, const nrg_round* rounds) {
     int r = pt_check(g);
     if (r) return r;
     if (!rounds) return NRG_E_INVAL;
-    const int par = g->pt_next;
-    if ((r = pt_post(g, rounds, par))) return r;
-    g->pt_next ^= 1;
-    const int rc = pt_flush(g);  // the previous round, whose counts have landed by now
-    g->pt_pend = par;
+    if ((r = pt_post(g, rounds, g->pt_posted))) return r;
+    g->pt_posted++;
+    int rc = NRG_OK;
+    if (g->pt_posted - g->pt_a >= 2) {  // the previous round: its counts have landed by now
+        rc = pt_stage_a(g, g->pt_a++);
+        if (g->broken) return g->broken;
+    }
+    if (g->pt_a - g->pt_b >= 2) {  // the round before: its reads rode in the launch just queued
+        if (rc != NRG_OK)  // (that round was dropped, so nothing launched them: now)
+            for (Member& m : g->m) {
+                RCHK(nrg::ctx_use_device(m.ctx));
+                RCHK(nrg_join(m.ctx));
+            }
+        const int r2 = pt_stage_b(g, g->pt_b++);
+        if (g->broken) return g->broken;
+        if (r2 && rc == NRG_OK) rc = r2;
+    }
     return rc;
 }
 
@@ -973,16 +1040,15 @@ int nrg_group_partitioned_round(nrg_group* g, const nrg_round* rounds) {
     if (r) return r;
     if (!rounds) return NRG_E_INVAL;
     if ((r = pt_flush(g))) return r;
-    const int par = g->pt_next;
-    if ((r = pt_post(g, rounds, par))) return r;
-    g->pt_next ^= 1;
-    return pt_complete(g, par);
+    if ((r = pt_post(g, rounds, g->pt_posted))) return r;
+    g->pt_posted++;
+    return pt_flush(g);
 }
 
 int nrg_group_sync(nrg_group* g) {
     if (!g) return NRG_E_INVAL;
     if (g->broken) return g->broken;
-    int rc = g->pt_pend >= 0 ? pt_flush(g) : NRG_OK;  // a posted partitioned round completes first
+    int rc = g->pt_b < g->pt_posted ? pt_flush(g) : NRG_OK;  // posted partitioned rounds complete first
     if (g->broken) return g->broken;
     for (Member& m : g->m) {
         int r = nrg::ctx_use_device(m.ctx);

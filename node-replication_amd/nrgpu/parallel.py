@@ -264,8 +264,9 @@ class PartitionedGroup(ReplicaGroup):
             self._check(rc, "nrg_group_partitioned_round")
 
     def round_async(self, puts, n: int, get_keys, n_gets: int, get_vals, get_found, prev=None, prev_found=None):
-        """Pipelined: queue this round and complete the previous one (nrg_group_partitioned_round_async).
-        This round's buffers stay borrowed until the next round_async / flush / sync."""
+        """Pipelined: queue this round, move the previous one to its owners and replay it, and send
+        the one before back (nrg_group_partitioned_round_async). A round's buffers stay borrowed
+        for the next two round_async calls, or until flush / sync."""
         r = self._round
         r.recs, r.n, r.resp, r.some = _ptr(puts), n, _ptr(prev), _ptr(prev_found)
         r.get_keys, r.n_gets, r.get_vals, r.get_found = _ptr(get_keys), n_gets, _ptr(get_vals), _ptr(get_found)

@@ -278,6 +278,7 @@ def test_group_partitioned_members(nrg, orc, G, skew, pipelined):
     lib = L.load()
     cfg = L.default_config(L.NRG_DS_HASHMAP)
     cfg.log2_slots, cfg.max_batch = 17, 4096
+    cfg.pipeline = 1 if pipelined else 0  # pipelined: each round's reads ride in the next round's launch
     g, ctxs = _open(L, lib, G, cfg)
     prefill, span = 6000, 30_000
     for p, c in enumerate(ctxs):
@@ -336,6 +337,59 @@ def test_group_partitioned_members(nrg, orc, G, skew, pipelined):
                 ev, ef = om.get_batch(gk)
                 np.testing.assert_array_equal(_u64(d["gv"][:R]), ev, err_msg=msg + " gets")
                 np.testing.assert_array_equal(d["gf"][:R].cpu().numpy(), ef.astype(np.uint8), err_msg=msg)
+    assert _digest_sum([list(_digest(lib, L, c)) for c in ctxs]) == [int(x) for x in om.digest()]
+    L.check(lib.nrg_group_close(g))
+
+
+@pytest.mark.parametrize("G", [1, 3])
+def test_group_partitioned_pipelined_drops_a_bad_round(nrg, orc, G):
+    """Pipelined partitioned rounds (three calls deep) with one bad round in the middle: member 0
+    posts Puts without records in round 2. Every member's call that moves round 2 (the call of
+    round 3) returns NRG_E_INVAL, the round is dropped everywhere, and rounds 0, 1, 3, 4 answer as
+    the NR replay of the log without round 2."""
+    import torch
+
+    L = nrg._lib
+    lib = L.load()
+    cfg = L.default_config(L.NRG_DS_HASHMAP)
+    cfg.log2_slots, cfg.max_batch, cfg.pipeline = 17, 4096, 1
+    g, ctxs = _open(L, lib, G, cfg)
+    for p, c in enumerate(ctxs):
+        L.check(lib.nrg_hashmap_prefill_partition(c, 3000, 1, p, G))
+    om = orc.HashMap()
+    om.prefill_range(3000, 1)
+    posted = []
+    for r in range(5):
+        rd = (L.Round * G)()
+        keep = []
+        for i in range(G):
+            W, R = 700 + 50 * i, 900
+            k = orc.gen_uniform(W, 40 * r + i, 12_000)
+            v = orc.gen_raw(W, 40 * r + i + 7)
+            gk = orc.gen_uniform(R, 40 * r + i + 13, 12_000)
+            d = dict(p=_cuda(np.stack([k, v], 1).astype(np.uint64)), gk=_cuda(gk),
+                     gv=torch.full((R,), -1, dtype=torch.int64, device="cuda"),
+                     gf=torch.full((R,), 7, dtype=torch.uint8, device="cuda"))
+            rd[i].recs, rd[i].n = (0 if (r == 2 and i == 0) else d["p"].data_ptr()), W
+            rd[i].resp = rd[i].some = 0
+            rd[i].get_keys, rd[i].n_gets = d["gk"].data_ptr(), R
+            rd[i].get_vals, rd[i].get_found = d["gv"].data_ptr(), d["gf"].data_ptr()
+            keep.append((d, k, v, gk))
+        torch.cuda.synchronize()
+        rc = lib.nrg_group_partitioned_round_async(g, rd)
+        assert rc == (L.NRG_E_INVAL if r == 3 else L.NRG_OK), (r, rc)
+        posted.append(keep)
+    L.check(lib.nrg_group_partitioned_flush(g), "flush")
+    L.check(lib.nrg_group_sync(g))
+    for r, keep in enumerate(posted):
+        if r == 2:
+            continue
+        for (_, k, v, _) in keep:
+            om.replay(k, v)
+        for i, (d, k, v, gk) in enumerate(keep):
+            ev, ef = om.get_batch(gk)
+            np.testing.assert_array_equal(_u64(d["gv"]), ev, err_msg=f"round {r} member {i}")
+            np.testing.assert_array_equal(d["gf"].cpu().numpy(), ef.astype(np.uint8))
     assert _digest_sum([list(_digest(lib, L, c)) for c in ctxs]) == [int(x) for x in om.digest()]
     L.check(lib.nrg_group_close(g))
 
