@@ -123,6 +123,8 @@ struct Member {
     uint64_t cap_p[PT_DEPTH] = {}, cap_k[PT_DEPTH] = {};  // its owner-region capacities (n, n_gets)
     PtPlan plan[PT_DEPTH];
     uint32_t pt_epoch = 0;      // look-back descriptor tag of the last fused partition
+    hipStream_t pstream = nullptr;  // a one-rank group's partitions, beside the replay
+    hipEvent_t pin_ev = nullptr;    // the replica stream's work up to a post (inputs, older rounds)
     uint64_t xwords[8] = {};    // this rank's host words of the exchange
     hipEvent_t pt_ev = nullptr;
     // Round headers and the length exchange (allocated at join, so a round cannot fail on them):
@@ -188,6 +190,8 @@ int member_init(Member& m, int nranks) {
     GCHK(hipEventCreateWithFlags(&m.in_ev, hipEventDisableTiming));
     GCHK(hipEventCreateWithFlags(&m.pt_ev, hipEventDisableTiming));
     for (int q = 0; q < PT_DEPTH; q++) GCHK(hipEventCreateWithFlags(&m.cnt_ev[q], hipEventDisableTiming));
+    GCHK(hipEventCreateWithFlags(&m.pin_ev, hipEventDisableTiming));
+    GCHK(hipStreamCreateWithFlags(&m.pstream, hipStreamNonBlocking));
     for (int b = 0; b < NBUF; b++) {
         GCHK(hipEventCreateWithFlags(&m.gathered[b], hipEventDisableTiming));
         GCHK(hipEventCreateWithFlags(&m.freed[b], hipEventDisableTiming));
@@ -261,6 +265,9 @@ void member_free(Member& m, const Rccl* R) {
         for (DBuf& d : m.rv[q])
             if (d.p) (void)hipFree(d.p);
     if (m.pt_ev) (void)hipEventDestroy(m.pt_ev);
+    if (m.pstream) (void)hipStreamSynchronize(m.pstream);
+    if (m.pstream) (void)hipStreamDestroy(m.pstream);
+    if (m.pin_ev) (void)hipEventDestroy(m.pin_ev);
     if (m.in_ev) (void)hipEventDestroy(m.in_ev);
     if (m.cstream) (void)hipStreamDestroy(m.cstream);
     m = Member{};
@@ -701,12 +708,22 @@ static int pt_post(nrg_group* g, const nrg_round* rounds, uint64_t e) {
         w[XW_RP_CAP] = G == 1 ? rp_own : std::min(rv[PR_RPUT].bytes / 16, rp_own);
         w[XW_RK_CAP] = G == 1 ? rk_own : std::min(rv[PR_RKEY].bytes / 8, rk_own);
         w[XW_ERR] = (uint64_t)(-err);
+        // A one-rank group partitions on a side stream, after everything queued on the replica's
+        // stream so far (the inputs, the slot's previous round), beside the previous round's
+        // replay queued next (with RCCL the partition stays in line: the count exchange must keep
+        // its place among the communicator's operations)
+        hipStream_t ps = c->stream;
+        if (G == 1) {
+            ps = m.pstream;
+            GCHK(hipEventRecord(m.pin_ev, c->stream));
+            GCHK(hipStreamWaitEvent(ps, m.pin_ev, 0));
+        }
         if (++m.pt_epoch >= (1u << 22)) {  // the descriptor tag wraps: clear the stale ones once
             m.pt_epoch = 1;
-            if (m.pt[PB_DESC].p) GCHK(hipMemsetAsync(m.pt[PB_DESC].p, 0, m.pt[PB_DESC].bytes, c->stream));
+            if (m.pt[PB_DESC].p) GCHK(hipMemsetAsync(m.pt[PB_DESC].p, 0, m.pt[PB_DESC].bytes, ps));
         }
         const bool ok = err == NRG_OK;
-        const hipError_t he = nrg::pt_fused(c->stream, (const uint64_t*)x.recs, ok ? n : 0, n,
+        const hipError_t he = nrg::pt_fused(ps, (const uint64_t*)x.recs, ok ? n : 0, n,
                                             (uint64_t*)m.pp[sl][PP_POUT].p, (uint32_t*)m.pp[sl][PP_PPOS].p,
                                             x.get_keys, ok ? k : 0, k, (uint64_t*)m.pp[sl][PP_KOUT].p,
                                             (uint32_t*)m.pp[sl][PP_GPOS].p, (uint64_t*)m.pt[PB_DESC].p, (uint32_t)G,
@@ -732,7 +749,7 @@ static int pt_post(nrg_group* g, const nrg_round* rounds, uint64_t e) {
         if (G > 1)
             GCHK(hipMemcpyAsync(m.h_cnt[sl], m.pp[sl][PP_ALLCNT].p, (uint64_t)G * CW * 8, hipMemcpyDeviceToHost,
                                 m.ctx->stream));
-        GCHK(hipEventRecord(m.cnt_ev[sl], m.ctx->stream));
+        GCHK(hipEventRecord(m.cnt_ev[sl], G == 1 ? m.pstream : m.ctx->stream));
     }
     return NRG_OK;
 }
@@ -748,6 +765,7 @@ static int pt_stage_a(nrg_group* g, uint64_t e) {
     for (int i = 0; i < nl; i++) {
         RCHK(nrg::ctx_use_device(g->m[i].ctx));
         RCHK(wait_event(g, g->m[i].cnt_ev[sl], "partitioned count exchange"));
+        if (G == 1) GCHK(hipStreamWaitEvent(g->m[i].ctx->stream, g->m[i].cnt_ev[sl], 0));  // (side stream)
     }
     const uint64_t* H = g->m[0].h_cnt[sl];  // identical on every rank
     auto word = [&](int s, uint64_t k) { return H[(size_t)s * CW + 2 * G + k]; };
@@ -1054,6 +1072,7 @@ int nrg_group_sync(nrg_group* g) {
         int r = nrg::ctx_use_device(m.ctx);
         if (r) return r;
         RCHK(wait_stream(g, m.cstream, "group sync (collectives)"));
+        RCHK(wait_stream(g, m.pstream, "group sync (partitions)"));
         RCHK(wait_stream(g, m.ctx->stream, "group sync (replay)"));
         // disagreeing round headers (ERR_GROUP, latched by grp_check_kernel) end the group: the
         // ranks have replayed different logs, so every later call reports it too
