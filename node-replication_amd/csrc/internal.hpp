@@ -293,4 +293,5 @@ bool sy_bucket_eligible(const nrg_config& cf);  // configs the sort-free bucket 
 u64 sy_bucket_aux_bytes(const nrg_config& cf);  // size of nrg_ctx::d_sy_aux
 hipError_t sy_aux_init(nrg_ctx* c);              // after (re)allocating d_sy_aux
 hipError_t sy_maxscan(nrg_ctx* c, const u32* sk, const u32* sv, u64 n, u32* M);
+hipError_t sy_lds_add_order(nrg_ctx* c, u32 K, u32 trials, u32 blocks, u64* d_out);
 }  // namespace nrg

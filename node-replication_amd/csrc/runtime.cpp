@@ -1079,6 +1079,21 @@ extern "C" int nrg_test_maxscan(nrg_ctx* c, const uint32_t* d_keys, const uint32
     return NRG_OK;
 }
 
+extern "C" int nrg_test_lds_add_order(nrg_ctx* c, uint32_t keys, uint32_t trials, uint32_t blocks,
+                                      uint64_t out[2]) {
+    if (!c || !out || keys < 1 || keys > 512 || blocks < 1 || blocks > 65536) return NRG_E_INVAL;
+    int r = use_device(c);
+    if (r) return r;
+    u64* d = nullptr;
+    HIPCHK(hipMallocAsync((void**)&d, 16, c->stream));
+    HIPCHK(hipMemsetAsync(d, 0, 16, c->stream));
+    HIPCHK(sy_lds_add_order(c, keys, trials, blocks, d));
+    HIPCHK(hipMemcpyAsync(out, d, 16, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipFreeAsync(d, c->stream));
+    HIPCHK(sync_all(c));
+    return NRG_OK;
+}
+
 extern "C" int nrg_test_ring_read(nrg_ctx* c, uint64_t phys, void* out) {
     if (!c || !out || phys >= c->log_size) return NRG_E_INVAL;
     int r = use_device(c);

@@ -252,6 +252,15 @@ constexpr u32 SY_MAX_NB = 512, SY_MAX_HOT = 16, SY_MAX_TILES = 4096, SY_MAX_CW =
 #define NRG_SYB_PER 10  // 1M-op rounds: 8 -> 57.2 us, 10 -> 56.4 (two passes per bucket, not three; E positions
                         // recomputed, not kept per touch); 12 spills (profiles/r03_synth_pass_size.txt)
 #endif
+#ifndef NRG_SYP_ADD
+// 1: the partition and the bucket pass's SET-free passes rank a wave's touches with one returning
+// LDS add per touch on a wave-private count. A returning LDS add hands the lanes of one
+// instruction that hit the same count their old values in lane order (checked on the hardware:
+// microbench/lds_add_order.hip, 2.1 G lanes; nrg_test_lds_add_order in the GPU suite), so the
+// ranks follow log order. 0: the peer-mask ranking (OR, read back, leader update: three LDS
+// round trips). 55.5 -> 51.8 us per 1M-op round (profiles/r05_synth_lds_add.txt)
+#define NRG_SYP_ADD 1
+#endif
 #ifndef NRG_SYP_PD
 #define NRG_SYP_PD 1  // partition: wave rounds of op records in flight ahead of the one ranked
 #endif
@@ -561,8 +570,17 @@ __device__ __forceinline__ void sy_part_role(const SyPartArgs& A, u32 tile, SyPa
         for (int r = 0; r < CW; r++) bw[r] = vw[r] != NOTOUCH ? bucket_of((vw[r] & ~SETBIT) - HR, wm) : 0u;
 #pragma unroll
         for (int r = 0; r < CW; r++) {
+#if NRG_SYP_ADD
+            // one returning LDS add per touch on the wave's packed u16 count pair
+            u32 rank = 0;
+            if (vw[r] != NOTOUCH) {
+                const u32 sh = (bw[r] & 1u) * 16u;
+                rank = (atomicAdd((u32*)&s_wcnt[w][bw[r] & ~1u], 1u << sh) >> sh) & 0xFFFFu;
+            }
+#else
             u64 peers;
             const u32 rank = wave_rank_mask(vw[r] != NOTOUCH, bw[r], lane, s_u.r.mask[w], s_wcnt[w], &peers);
+#endif
             const u32 xl = word_in_bucket((vw[r] & ~SETBIT) - HR, bw[r], W);
             pk[orr * CW + r] = vw[r] == NOTOUCH ? 0u
                                                 : (1u << 31) | ((vw[r] & SETBIT) ? 1u << 29 : 0u) | (xl << 20) | (bw[r] << 11) | rank;
@@ -783,8 +801,12 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
 #pragma unroll
                 for (int q = 0; q < SYB_PER; q++) {
                     const u32 i = base + (u32)w * (SYB_PER * 64) + q * 64 + lane;
+#if NRG_SYP_ADD
+                    sv[q] = i < total ? atomicAdd(&s_wc[w][ent_word(ent[q])], 1u) : 0u;
+#else
                     u64 peers;
                     sv[q] = wave_rank_mask(i < total, ent_word(ent[q]), lane, s_mk[w], s_wc[w], &peers);
+#endif
                 }
             }
             __syncthreads();
@@ -1172,6 +1194,43 @@ static hipError_t sy_bucket_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 re
     c->sy_pend = d;
     c->sy_par ^= 1;
     return c->pipeline ? hipSuccess : sy_flush(c);
+}
+
+// nrg_test_lds_add_order: the property NRG_SYP_ADD ranks by. Each wave, per trial, issues five
+// returning adds over K packed u16 counts (as the partition does) with keys from a hash, and
+// compares every lane's old value with the count before the instruction plus the lower lanes of
+// the same key. out[0] += lanes checked, out[1] += lanes out of lane order.
+__global__ __launch_bounds__(512) void sy_lds_add_order_kernel(u32 K, u32 trials, u64* out) {
+    __shared__ unsigned short cnt[8][512];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    u64 nbad = 0, nchk = 0;
+    for (u32 t = 0; t < trials; t++) {
+        for (int i = lane; i < 512; i += 64) cnt[w][i] = 0;
+        wave_lds_sync();
+        for (int r = 0; r < 5; r++) {
+            const u32 key = (u32)(mix64(((u64)blockIdx.x << 40) ^ ((u64)t << 20) ^ (u64)(r * 4096 + w * 64 + lane)) % K);
+            u32 before = 0;
+            for (int l = 0; l < 64; l++) {
+                const u32 kl = (u32)__shfl((int)key, l, 64);  // every lane takes part (a source lane must be active)
+                before += (l < lane && kl == key) ? 1u : 0u;
+            }
+            const u32 prior = cnt[w][key];
+            wave_lds_sync();
+            const u32 sh = (key & 1u) * 16u;
+            const u32 old = (atomicAdd((u32*)&cnt[w][key & ~1u], 1u << sh) >> sh) & 0xFFFFu;
+            wave_lds_sync();
+            nbad += old != prior + before ? 1u : 0u;
+            nchk++;
+        }
+    }
+    atomicAdd((unsigned long long*)&out[0], (unsigned long long)nchk);
+    atomicAdd((unsigned long long*)&out[1], (unsigned long long)nbad);
+}
+
+hipError_t sy_lds_add_order(nrg_ctx* c, u32 K, u32 trials, u32 blocks, u64* d_out) {
+    if (K < 1 || K > 512) return hipErrorInvalidValue;
+    sy_lds_add_order_kernel<<<blocks, 512, 0, c->stream>>>(K, trials, d_out);
+    return hipGetLastError();
 }
 
 hipError_t sy_init(nrg_ctx* c) {

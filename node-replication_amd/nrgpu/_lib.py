@@ -187,6 +187,7 @@ TEST_SIGNATURES = {
     "nrg_test_combiner_times": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
     "nrg_test_sort_pairs": (C.c_int, [vp, vp, vp, u64, C.c_int, vp, vp]),
     "nrg_test_maxscan": (C.c_int, [vp, vp, vp, u64, vp]),
+    "nrg_test_lds_add_order": (C.c_int, [vp, u32, u32, u32, vp]),
     "nrg_test_ring_read": (C.c_int, [vp, u64, vp]),
     "nrg_test_debug_read": (C.c_int, [vp, vp, u64]),
     "nrg_test_hm_skewed": (C.c_int, [vp, vp]),

@@ -79,6 +79,20 @@ def test_maxscan(nrg, orc, n, span, setfrac):
     np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), want)
 
 
+@pytest.mark.parametrize("keys", [1, 2, 8, 64, 512])
+def test_lds_add_lane_order(nrg, keys):
+    """The hardware property the synthetic replay's rankings rest on (synthetic.hip NRG_SYP_ADD):
+    the lanes of one returning LDS add that hit the same count get their old values in lane
+    order, so a wave's ranks follow log order."""
+    import ctypes as C
+
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_SYNTHETIC, 0, max_batch=1 << 12)
+    out = (C.c_uint64 * 2)()
+    nrg._lib.check(nrg.load().nrg_test_lds_add_order(dev.handle, keys, 40, 512, out), "nrg_test_lds_add_order")
+    assert out[0] == 512 * 8 * 64 * 40 * 5
+    assert out[1] == 0, f"{out[1]} of {out[0]} lanes out of lane order"
+
+
 def test_device_stack_and_zipf_generators(nrg, orc):
     """Device generators used by bench.py: stack ops bit-exact with the oracle; Zipf keys equal
     to the oracle's except where device pow and glibc pow round differently (rare, +-1 rank)."""
