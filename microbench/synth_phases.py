@@ -30,8 +30,8 @@ ops[:, 3] = 1
 resp = torch.empty(N, dtype=torch.int64, device="cuda")
 some = torch.empty(N, dtype=torch.uint8, device="cuda")
 SPAN = 200_000 - 2  # hot_reads = 2
-W = -(-(SPAN - 1) // 511)
-NB = 1 + -(-(SPAN - 1) // W)  # bucket 0: cold word 0 alone
+W = -(-(SPAN - 1) // 508)  # synthetic.hip SY_MAX_NB - SY_B0_PARTS
+NB = 1 + -(-(SPAN - 1) // W) + 3  # workgroups: bucket 0 (cold word 0) in 4 parts, then the buckets
 R = 20
 acc = np.zeros((NB, 9))
 T = -(-N // 2048)  # partition tiles (synthetic.hip SYA_OPS)

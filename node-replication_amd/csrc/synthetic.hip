@@ -248,6 +248,14 @@ constexpr u32 SYB_WORDS = 1u << SYB_SHIFT;  // LDS words per bucket (a bucket ho
 constexpr int SYA_TPB = 512, SYA_WAVES = SYA_TPB / 64, SYA_OROUNDS = 4;
 constexpr u32 SYA_OPS = SYA_WAVES * SYA_OROUNDS * 64;  // ops per tile (11 bits)
 constexpr u32 SY_MAX_NB = 512, SY_MAX_HOT = 16, SY_MAX_TILES = 4096, SY_MAX_CW = 8;
+// Cold word 0 (bucket 0) is replayed by SY_B0_PARTS workgroups when the chunk holds no WriteOnly:
+// its seen values are then its value plus the touch's rank, so each part takes a contiguous
+// range of the touches. The bucket pass launches SY_MAX_NB workgroups in all (two per CU), so
+// words 1.. go to SY_MAX_NB - SY_B0_PARTS buckets.
+#ifndef NRG_SY_B0_PARTS
+#define NRG_SY_B0_PARTS 4
+#endif
+constexpr u32 SY_B0_PARTS = NRG_SY_B0_PARTS;
 #ifndef NRG_SYB_PER
 #define NRG_SYB_PER 10  // 1M-op rounds: 8 -> 57.2 us, 10 -> 56.4 (two passes per bucket, not three; E positions
                         // recomputed, not kept per touch); 12 spills (profiles/r03_synth_pass_size.txt)
@@ -397,6 +405,7 @@ struct SyFlags {
     u32 big[2];
     u32 set_epoch;
     u32 v32[2];
+    u32 wo_epoch;  // = e: chunk e holds a WriteOnly (bucket 0 then runs in one workgroup)
 };
 
 // Arguments of the partition pass of chunk e and of the sums of chunk e-1, which share a launch.
@@ -481,7 +490,8 @@ __device__ __forceinline__ void sy_part_role(const SyPartArgs& A, u32 tile, SyPa
     if (dbg) dbg[K] = wall_clock64()
     SYP_MARK(0);
     for (u32 i = tid; i < SYA_WAVES * SY_MAX_NB / 2; i += SYA_TPB) ((u32*)&s_wcnt[0][0])[i] = 0;
-    for (u32 i = tid; i < SYA_WAVES * SY_MAX_NB; i += SYA_TPB) (&s_u.r.mask[0][0])[i] = 0;
+    if (!NRG_SYP_ADD)
+        for (u32 i = tid; i < SYA_WAVES * SY_MAX_NB; i += SYA_TPB) (&s_u.r.mask[0][0])[i] = 0;
     if (lane < SY_MAX_HOT) s_hot[w][lane] = SyHot{0, 0, 0};
     __syncthreads();
     // a ranked cold touch: valid (bit 31), SET (29), word in bucket (20..28), bucket (11..19),
@@ -506,6 +516,7 @@ __device__ __forceinline__ void sy_part_role(const SyPartArgs& A, u32 tile, SyPa
         if (src && valid) st_op(&ring[(lo + op0 + opw + orr * 64) & ring_mask], o, A.plain);
         const bool set = valid && o.op == NRG_SYNTH_WRITE_ONLY;
         if (set && (o.tid >> 31)) A.fl->set_epoch = A.epoch;  // this chunk's seen values may pass 2^32
+        if (set) A.fl->wo_epoch = A.epoch;                     // this chunk holds a WriteOnly
         // hot touches (r2 + j) % HR, j < HW, skipped when r2 + HW wraps; ordered (lane, j)
         const bool hot_ok = valid && (o.r2 + HW >= o.r2);
         const u32 h0 = hot_ok ? (u32)mod_recip(o.r2, HR, hr_m) : 0u;
@@ -655,7 +666,7 @@ __device__ __forceinline__ void sy_part_role(const SyPartArgs& A, u32 tile, SyPa
 // WriteOnly in it is applied wave by wave instead (values depend on the last SET).
 // (<= 128 VGPRs: two 8-wave workgroups per CU)
 __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) void sy_bucket_kernel(const u16* __restrict__ Ew, const u16* __restrict__ Eo, const u32* __restrict__ cnt_tb,
-                                                            u32 ntiles, u32 tile_entries, u64* __restrict__ V,
+                                                            u32 NB, u32 ntiles, u32 tile_entries, u64* __restrict__ V,
                                                             u64* __restrict__ words, u64 N, u32 HR, u32 W,
                                                             const nrg_synth_op* __restrict__ ring, u64 ring_mask, u64 lo,
                                                             SyFlags* __restrict__ fl, u32 epoch, u32 par,
@@ -686,7 +697,12 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
     // buckets in contiguous runs per XCD (workgroups go to XCDs round-robin): neighbouring
     // buckets share the lines at their segments' edges in E and V, and those stay in one L2
     const u32 nxcd = 8, q = gridDim.x / nxcd, rem = gridDim.x % nxcd, xcd = blockIdx.x % nxcd;
-    const u32 b = xcd * q + (xcd < rem ? xcd : rem) + blockIdx.x / nxcd;
+    const u32 v = xcd * q + (xcd < rem ? xcd : rem) + blockIdx.x / nxcd;
+    // v = 0..H: the parts of bucket 0 (H = gridDim.x - NB helpers beside its own workgroup)
+    const u32 H = gridDim.x - NB;
+    const u32 b = v <= H ? 0u : v - H, part = v <= H ? v : 0u;
+    const bool split = b == 0 && H && fl->wo_epoch != epoch;
+    if (b == 0 && part && !split) return;  // a WriteOnly in the chunk: bucket 0 in one workgroup
     const u64 w0 = b ? (u64)HR + 1 + (u64)(b - 1) * W : (u64)HR;  // bucket 0: cold word 0 alone
     const u32 nw = b ? W : 1u;
     // 4-B seen values this chunk (SyFlags): decided alike by every workgroup
@@ -694,7 +710,7 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
     for (u32 t = tid; t < ntiles; t += SYB_TPB) {
         // [tile][bucket]: a tile's word for bucket b shares its line with the neighbouring buckets,
         // which run on this XCD (the contiguous runs above), so the line is fetched once per XCD
-        const u32 p = cnt_tb[(u64)t * gridDim.x + b];
+        const u32 p = cnt_tb[(u64)t * NB + b];
         s_off[t] = (unsigned short)(p >> 16);
         s_pre[t] = p & 0xFFFFu;
     }
@@ -732,6 +748,11 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
         }
     }
     if (tid == 0) s_pre[ntiles] = total;
+    // this workgroup's touches [start, end): all of its bucket's, or a part of bucket 0's, whose
+    // word starts the part at its value plus the touches before it
+    const u32 start = split ? (u32)((u64)total * part / (H + 1)) : 0u;
+    const u32 end = split ? (u32)((u64)total * (part + 1) / (H + 1)) : total;
+    if (split && tid == 0) s_cur[0] += start;
     __syncthreads();
     SY_MARK(2);
     // The pass starting at `base`: the tile of each of its touches, then this thread's entries.
@@ -756,17 +777,17 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
 #pragma unroll
         for (int q = 0; q < SYB_PER; q++) {
             const u32 i = base + (u32)w * (SYB_PER * 64) + q * 64 + lane;
-            nent[q] = i < total ? (u32)Ew[gpos_of(base, map, i)] : 0u;
+            nent[q] = i < end ? (u32)Ew[gpos_of(base, map, i)] : 0u;
         }
     };
-    if (total) {
-        map_pass(0, s_tile[0]);
+    if (start < end) {
+        map_pass(start, s_tile[0]);
         __syncthreads();
-        load_pass(0, s_tile[0]);
+        load_pass(start, s_tile[0]);
     }
     // Software pipelined: the next pass's entries are in flight while this pass is ranked.
     const u32 late = blockIdx.x >= gridDim.x / 2 ? 1u : 0u;  // the second workgroup on its CU
-    for (u32 base = 0, pb = 0; base < total; base += SYB_PASS, pb ^= 1) {
+    for (u32 base = start, pb = 0; base < end; base += SYB_PASS, pb ^= 1) {
         // alternate which of a CU's two workgroups the SIMDs prefer, pass by pass: oldest-first
         // arbitration otherwise favours the first-dispatched one all the way through, and the
         // second ones ended 3.6 us later (profiles/r04_stack_synth_phases.txt; 55.97-56.83 vs
@@ -784,9 +805,9 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
         }
         SY_ACC(1);
         const u32 nb = base + SYB_PASS;
-        if (nb < total) map_pass(nb, s_tile[pb ^ 1]);
+        if (nb < end) map_pass(nb, s_tile[pb ^ 1]);
         const int anyset = __syncthreads_or(myset);  // also publishes the next pass's tile map
-        if (nb < total) load_pass(nb, s_tile[pb ^ 1]);
+        if (nb < end) load_pass(nb, s_tile[pb ^ 1]);
         SY_ACC(0);
         if (!anyset) {
             if (b == 0) {  // one word: a touch's rank in its wave is its position there
@@ -796,16 +817,16 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
 #pragma unroll
                 for (int q = 0; q < SYB_PER; q++) sv[q] = (u64)(q * 64 + l);
                 if (lane == 0)
-                    s_wc[w][0] = total > w0i ? (total - w0i < SYB_PER * 64 ? total - w0i : SYB_PER * 64) : 0u;
+                    s_wc[w][0] = end > w0i ? (end - w0i < SYB_PER * 64 ? end - w0i : SYB_PER * 64) : 0u;
             } else {
 #pragma unroll
                 for (int q = 0; q < SYB_PER; q++) {
                     const u32 i = base + (u32)w * (SYB_PER * 64) + q * 64 + lane;
 #if NRG_SYP_ADD
-                    sv[q] = i < total ? atomicAdd(&s_wc[w][ent_word(ent[q])], 1u) : 0u;
+                    sv[q] = i < end ? atomicAdd(&s_wc[w][ent_word(ent[q])], 1u) : 0u;
 #else
                     u64 peers;
-                    sv[q] = wave_rank_mask(i < total, ent_word(ent[q]), lane, s_mk[w], s_wc[w], &peers);
+                    sv[q] = wave_rank_mask(i < end, ent_word(ent[q]), lane, s_mk[w], s_wc[w], &peers);
 #endif
                 }
             }
@@ -837,7 +858,7 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
                 const bool isset = ent_set(ent[q]);  // 0 for touches past the end
                 const u32 iq = base + (u32)w * (SYB_PER * 64) + q * 64 + lane;
                 // (the op of a SET touch: its Eo record, read only in passes with a WriteOnly)
-                const u64 op = isset && iq < total ? (u64)cmap[iq - base] * SYA_OPS + Eo[gpos_of(base, cmap, iq)] : 0ull;
+                const u64 op = isset && iq < end ? (u64)cmap[iq - base] * SYA_OPS + Eo[gpos_of(base, cmap, iq)] : 0ull;
                 sv[q] = isset ? ring[(lo + op) & ring_mask].tid : 0ull;
             }
             for (int ww = 0; ww < SYB_WAVES; ww++) {
@@ -845,7 +866,7 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
 #pragma unroll
                     for (int q = 0; q < SYB_PER; q++) {
                         const u32 i = base + (u32)w * (SYB_PER * 64) + q * 64 + lane;
-                        const bool valid = i < total;
+                        const bool valid = i < end;
                         const u32 xl = ent_word(ent[q]);
                         const bool isset = valid && ent_set(ent[q]);
                         u64 peers;
@@ -877,14 +898,14 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
         if (v32) {
 #pragma unroll
             for (int q = 0; q < SYB_PER; q++)
-                if (base + (u32)w * (SYB_PER * 64) + q * 64 + lane < total) {
+                if (base + (u32)w * (SYB_PER * 64) + q * 64 + lane < end) {
                     const u32 gp = gpos_of(base, cmap, base + (u32)w * (SYB_PER * 64) + q * 64 + lane);
                     if (gp < vcap) st_out(&((u32*)V)[gp], (u32)sv[q], plain);
                 }
         } else {
 #pragma unroll
             for (int q = 0; q < SYB_PER; q++)
-                if (base + (u32)w * (SYB_PER * 64) + q * 64 + lane < total) {
+                if (base + (u32)w * (SYB_PER * 64) + q * 64 + lane < end) {
                     const u32 gp = gpos_of(base, cmap, base + (u32)w * (SYB_PER * 64) + q * 64 + lane);
                     if (gp < vcap) st_out(&V[gp], sv[q], plain);
                 }
@@ -896,7 +917,8 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
         SY_ACC(3);
     }
     bool big = false;
-    for (u32 i = tid; i < nw; i += SYB_TPB)
+    const bool owner = !split || part == H;  // bucket 0's last part ends at the word's value
+    for (u32 i = tid; owner && i < nw; i += SYB_TPB)
         if (w0 + i < N) {
             words[w0 + i] = s_cur[i];
             big |= (s_cur[i] >> 31) != 0;
@@ -1022,10 +1044,15 @@ __global__ __launch_bounds__(SYA_TPB) void sy_part_kernel(SyPartArgs A, SySumArg
         sy_sum_role(S, blockIdx.x - A.ntiles, L.u.sum);
 }
 
+// buckets: 0 = cold word 0, then W words each over at most SY_MAX_NB - SY_B0_PARTS buckets
+static u64 sy_bucket_words(u64 span) {
+    const u64 nbw = SY_MAX_NB - SY_B0_PARTS;
+    return span > 1 ? (span - 1 + nbw - 1) / nbw : 1;
+}
 bool sy_bucket_eligible(const nrg_config& cf) {
     const u64 span = cf.synth_n - cf.synth_hot_reads;
     return cf.synth_cold_writes >= 1 && cf.synth_cold_writes <= SY_MAX_CW && cf.synth_hot_reads <= SY_MAX_HOT &&
-           span <= 1 + (u64)(SY_MAX_NB - 1) * SYB_WORDS && cf.max_batch <= (u64)SY_MAX_TILES * SYA_OPS;
+           span <= 1 + (u64)(SY_MAX_NB - SY_B0_PARTS) * SYB_WORDS && cf.max_batch <= (u64)SY_MAX_TILES * SYA_OPS;
 }
 
 // scratch: V (seen values, u64 per touch), then per buffer parity: E (touch entries), the
@@ -1040,7 +1067,7 @@ struct SyAux {
 };
 static u64 sy_nb(const nrg_config& cf) {
     const u64 span = cf.synth_n - cf.synth_hot_reads;
-    const u64 W = span > 1 ? (span - 1 + SY_MAX_NB - 2) / (SY_MAX_NB - 1) : 1;
+    const u64 W = sy_bucket_words(span);
     return 1 + (span - 1 + W - 1) / W;
 }
 static SyAux sy_aux(void* base, const nrg_config& cf) {
@@ -1129,7 +1156,7 @@ static hipError_t sy_bucket_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 re
     const u32 HW = cf.synth_hot_writes, CW = cf.synth_cold_writes, HR = cf.synth_hot_reads;
     const u64 span = cf.synth_n - HR;
     // bucket 0: cold word 0 alone; buckets 1..: W words each (<= 512, sy_bucket_eligible)
-    const u32 W = span > 1 ? (u32)((span - 1 + SY_MAX_NB - 2) / (SY_MAX_NB - 1)) : 1u;
+    const u32 W = (u32)sy_bucket_words(span);
     const u32 NB = 1 + (u32)((span - 1 + W - 1) / W);
     const u32 ntiles = (u32)((n + SYA_OPS - 1) / SYA_OPS);
     SyAux x = sy_aux(c->d_sy_aux, cf);
@@ -1166,7 +1193,7 @@ static hipError_t sy_bucket_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 re
     hipError_t e = sy_launch_part(c, A, S);
     if (e != hipSuccess) return e;
     const size_t dyn = (size_t)(ntiles + 1) * 4 + (size_t)ntiles * 2;
-    sy_bucket_kernel<<<NB, SYB_TPB, dyn, st>>>((const u16*)x.E[par], (const u16*)x.E[par] + (x.cnt - x.E[1]), x.cnt, ntiles, SYA_OPS * CW, x.V, c->d_words, cf.synth_n, HR,
+    sy_bucket_kernel<<<NB + SY_B0_PARTS - 1, SYB_TPB, dyn, st>>>((const u16*)x.E[par], (const u16*)x.E[par] + (x.cnt - x.E[1]), x.cnt, NB, ntiles, SYA_OPS * CW, x.V, c->d_words, cf.synth_n, HR,
                                                W, A.ring, A.ring_mask, lo, x.fl, A.epoch, par,
                                                (c->exp & 2) ? c->d_dbg : nullptr, c->stall, !((c->exp >> 8) & 1));
     timer_end(c, "sy_replay");
