@@ -17,7 +17,7 @@ int nrg_test_sort_pairs(nrg_ctx* ctx, const uint32_t* d_keys, const uint32_t* d_
 /* M[p] = max{q <= p : q == 0 || keys[q-1] != keys[q] || (vals[q] & 0x80000000)} */
 int nrg_test_maxscan(nrg_ctx* ctx, const uint32_t* d_keys, const uint32_t* d_vals, uint64_t n,
                      uint32_t* d_out);
-/* The hardware property the synthetic replay's rankings rest on (synthetic.hip NRG_SYP_ADD): a
+/* The hardware property the synthetic replay's rankings rest on (synthetic.hip): a
  * returning LDS add gives the lanes of one instruction that hit the same count their old values
  * in lane order. `blocks` workgroups of 8 waves run `trials` x 5 adds over `keys` (1..512)
  * counts; out[0] = lanes checked, out[1] = lanes out of lane order (0 expected). */

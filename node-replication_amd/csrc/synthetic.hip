@@ -260,15 +260,12 @@ constexpr u32 SY_B0_PARTS = NRG_SY_B0_PARTS;
 #define NRG_SYB_PER 10  // 1M-op rounds: 8 -> 57.2 us, 10 -> 56.4 (two passes per bucket, not three; E positions
                         // recomputed, not kept per touch); 12 spills (profiles/r03_synth_pass_size.txt)
 #endif
-#ifndef NRG_SYP_ADD
-// 1: the partition and the bucket pass's SET-free passes rank a wave's touches with one returning
-// LDS add per touch on a wave-private count. A returning LDS add hands the lanes of one
+// Rankings: the partition and the bucket pass's SET-free passes rank a wave's touches with one
+// returning LDS add per touch on a wave-private count. A returning LDS add hands the lanes of one
 // instruction that hit the same count their old values in lane order (checked on the hardware:
 // microbench/lds_add_order.hip, 2.1 G lanes; nrg_test_lds_add_order in the GPU suite), so the
-// ranks follow log order. 0: the peer-mask ranking (OR, read back, leader update: three LDS
-// round trips). 55.5 -> 51.8 us per 1M-op round (profiles/r05_synth_lds_add.txt)
-#define NRG_SYP_ADD 1
-#endif
+// ranks follow log order. Round 4's peer masks (OR, read back, leader update: three LDS round
+// trips per touch) ran 55.5 us per 1M-op round against 51.8 (profiles/r05_synth_lds_add.txt).
 #ifndef NRG_SYP_PD
 #define NRG_SYP_PD 1  // partition: wave rounds of op records in flight ahead of the one ranked
 #endif
@@ -347,32 +344,10 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Stable ranking by ballots: the lanes holding the same BITS-bit key are found by matching the
-// key bit by bit (BITS ballots and no LDS round trip), then one read of the wave-private
-// count[key] and one write by the highest such lane (one wave's LDS accesses stay in order).
-// Returns count[key] + the number of lower lanes with the key; *peers_out = those lanes.
-template <int BITS, typename CNT>
-__device__ __forceinline__ u32 wave_rank_bits(bool on, u32 key, int lane, CNT* count, u64* peers_out) {
-    u64 peers = __ballot(on);
-#pragma unroll
-    for (int b = 0; b < BITS; b++) {
-        const bool bit = (key >> b) & 1u;
-        const u64 bal = __ballot(bit);
-        peers &= bit ? bal : ~bal;
-    }
-    if (!on) peers = 0;
-    const u32 c0 = on ? (u32)count[key] : 0u;
-    __builtin_amdgcn_wave_barrier();
-    if (on && 63 - __clzll(peers) == lane) count[key] = (CNT)(c0 + (u32)__popcll(peers));
-    __builtin_amdgcn_wave_barrier();
-    *peers_out = peers;
-    return c0 + (u32)__popcll(peers & ((1ull << lane) - 1));
-}
-
-// Stable ranking of one wave round in a wave-private (mask, count) table: every lane with a
-// key ORs its bit into mask[key]; the mask read back is the set of lanes with that key. Returns
-// count[key] + the number of lower lanes with the same key; the highest such lane advances count
-// and clears mask (three LDS round trips per ranking).
+// Stable ranking of one wave round in a (mask, count) table: every lane with a key ORs its bit
+// into mask[key]; the mask read back is the set of lanes with that key. Returns count[key] + the
+// number of lower lanes with the same key; the highest such lane advances count and clears mask
+// (three LDS round trips; the bucket pass's passes with a WriteOnly, which need the peers).
 template <typename CNT>
 __device__ __forceinline__ u32 wave_rank_mask(bool on, u32 key, int lane, u64* mask, CNT* count, u64* peers_out) {
     if (on) atomicOr((unsigned long long*)&mask[key], 1ull << lane);
@@ -455,7 +430,6 @@ struct SyPartLds {
     unsigned short wcnt[SYA_WAVES][SY_MAX_NB];
     union {
         struct {
-            u64 mask[SYA_WAVES][SY_MAX_NB];
             u32 words[SYA_WAVES][64 * CW];
         } r;
         u32 stage[SYA_OPS * CW];
@@ -490,8 +464,6 @@ __device__ __forceinline__ void sy_part_role(const SyPartArgs& A, u32 tile, SyPa
     if (dbg) dbg[K] = wall_clock64()
     SYP_MARK(0);
     for (u32 i = tid; i < SYA_WAVES * SY_MAX_NB / 2; i += SYA_TPB) ((u32*)&s_wcnt[0][0])[i] = 0;
-    if (!NRG_SYP_ADD)
-        for (u32 i = tid; i < SYA_WAVES * SY_MAX_NB; i += SYA_TPB) (&s_u.r.mask[0][0])[i] = 0;
     if (lane < SY_MAX_HOT) s_hot[w][lane] = SyHot{0, 0, 0};
     __syncthreads();
     // a ranked cold touch: valid (bit 31), SET (29), word in bucket (20..28), bucket (11..19),
@@ -581,17 +553,12 @@ __device__ __forceinline__ void sy_part_role(const SyPartArgs& A, u32 tile, SyPa
         for (int r = 0; r < CW; r++) bw[r] = vw[r] != NOTOUCH ? bucket_of((vw[r] & ~SETBIT) - HR, wm) : 0u;
 #pragma unroll
         for (int r = 0; r < CW; r++) {
-#if NRG_SYP_ADD
             // one returning LDS add per touch on the wave's packed u16 count pair
             u32 rank = 0;
             if (vw[r] != NOTOUCH) {
                 const u32 sh = (bw[r] & 1u) * 16u;
                 rank = (atomicAdd((u32*)&s_wcnt[w][bw[r] & ~1u], 1u << sh) >> sh) & 0xFFFFu;
             }
-#else
-            u64 peers;
-            const u32 rank = wave_rank_mask(vw[r] != NOTOUCH, bw[r], lane, s_u.r.mask[w], s_wcnt[w], &peers);
-#endif
             const u32 xl = word_in_bucket((vw[r] & ~SETBIT) - HR, bw[r], W);
             pk[orr * CW + r] = vw[r] == NOTOUCH ? 0u
                                                 : (1u << 31) | ((vw[r] & SETBIT) ? 1u << 29 : 0u) | (xl << 20) | (bw[r] << 11) | rank;
@@ -687,7 +654,7 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
     extern __shared__ u32 s_dyn[];  // s_pre[ntiles + 1], s_off[ntiles] (u16)
     __shared__ u64 s_cur[SYB_WORDS];
     __shared__ u32 s_wc[SYB_WAVES][SYB_WORDS];
-    __shared__ u64 s_mk[SYB_WAVES][SYB_WORDS];
+    __shared__ u64 s_mk[SYB_WORDS];  // peer masks of the passes with a WriteOnly (one wave at a time)
     __shared__ unsigned short s_tile[2][SYB_PASS];  // tile of every touch of a pass (double buffered)
     __shared__ u32 s_part[SYB_WAVES];
     __shared__ u32 s_big;  // a word ends the chunk >= 2^31 (SyFlags)
@@ -716,8 +683,8 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
     }
     for (u32 i = tid; i < SYB_WORDS; i += SYB_TPB) s_cur[i] = i < nw && w0 + i < N ? words[w0 + i] : 0ull;
     if (tid == 0) s_big = 0;
+    for (u32 i = tid; i < SYB_WORDS; i += SYB_TPB) s_mk[i] = 0;
     for (u32 i = tid; i < SYB_WAVES * SYB_WORDS; i += SYB_TPB) (&s_wc[0][0])[i] = 0;
-    for (u32 i = tid; i < SYB_WAVES * SYB_WORDS; i += SYB_TPB) (&s_mk[0][0])[i] = 0;
     __syncthreads();
     SY_MARK(1);
     // exclusive scan of the per-tile counts: thread owns tiles [tid*K, tid*K + K)
@@ -822,12 +789,7 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
 #pragma unroll
                 for (int q = 0; q < SYB_PER; q++) {
                     const u32 i = base + (u32)w * (SYB_PER * 64) + q * 64 + lane;
-#if NRG_SYP_ADD
                     sv[q] = i < end ? atomicAdd(&s_wc[w][ent_word(ent[q])], 1u) : 0u;
-#else
-                    u64 peers;
-                    sv[q] = wave_rank_mask(i < end, ent_word(ent[q]), lane, s_mk[w], s_wc[w], &peers);
-#endif
                 }
             }
             __syncthreads();
@@ -870,7 +832,7 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) vo
                         const u32 xl = ent_word(ent[q]);
                         const bool isset = valid && ent_set(ent[q]);
                         u64 peers;
-                        (void)wave_rank_mask(valid, xl, lane, s_mk[w], s_wc[w], &peers);
+                        (void)wave_rank_mask(valid, xl, lane, s_mk, s_wc[w], &peers);
                         const u64 P = peers & ((1ull << lane) - 1);
                         const u64 S = __ballot(isset) & P;
                         const int sl = S ? 63 - __clzll(S) : lane;
@@ -1223,7 +1185,7 @@ static hipError_t sy_bucket_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 re
     return c->pipeline ? hipSuccess : sy_flush(c);
 }
 
-// nrg_test_lds_add_order: the property NRG_SYP_ADD ranks by. Each wave, per trial, issues five
+// nrg_test_lds_add_order: the property the synthetic rankings rest on. Each wave, per trial, issues five
 // returning adds over K packed u16 counts (as the partition does) with keys from a hash, and
 // compares every lane's old value with the count before the instruction plus the lower lanes of
 // the same key. out[0] += lanes checked, out[1] += lanes out of lane order.

@@ -81,7 +81,7 @@ def test_maxscan(nrg, orc, n, span, setfrac):
 
 @pytest.mark.parametrize("keys", [1, 2, 8, 64, 512])
 def test_lds_add_lane_order(nrg, keys):
-    """The hardware property the synthetic replay's rankings rest on (synthetic.hip NRG_SYP_ADD):
+    """The hardware property the synthetic replay's rankings rest on (synthetic.hip):
     the lanes of one returning LDS add that hit the same count get their old values in lane
     order, so a wave's ranks follow log order."""
     import ctypes as C
