@@ -233,18 +233,11 @@ __device__ __forceinline__ void part_role(const IndexJob& j, u32 blk, u32 shift,
     u32 rnk[K1];
 #pragma unroll
     for (int q = 0; q < K1; q++) {
-        const u32 b = emit[q] ? bkt[q] : 0u;
-        u64 peers = __ballot(emit[q]);
-        for (u32 bit = 0; bit < j.nb_log; bit++) {
-            const bool one = (b >> bit) & 1u;
-            const u64 bal = __ballot(one);
-            peers &= one ? bal : ~bal;
-        }
+        // one returning LDS add per Put on the wave's packed u16 count (lanes of one instruction
+        // get their old values in lane order: synthetic.hip's rankings, nrg_test_lds_add_order)
         if (emit[q]) {
-            const u64 below = peers & ((1ull << lane) - 1);
-            const u32 cur = s_wc[w * nb + b];
-            rnk[q] = cur + (u32)__popcll(below);
-            if (below == 0) s_wc[w * nb + b] = (uint16_t)(cur + (u32)__popcll(peers));
+            const u32 ix = w * nb + bkt[q], sh = (ix & 1u) * 16u;
+            rnk[q] = (atomicAdd((u32*)s_wc + (ix >> 1), 1u << sh) >> sh) & 0xFFFFu;
         }
     }
     __syncthreads();
