@@ -39,7 +39,10 @@ pacc = np.zeros((T, 5))
 sacc = np.zeros((T, 3))
 hw = None
 for r in range(R + 3):
-    dev.sy_round_device(ops, N, 1, resp, some)
+    if os.environ.get("SY_NORESP"):  # (diagnostic: no responses -> the sum role only folds the hot words)
+        dev.sy_round_device(ops, N, 1)
+    else:
+        dev.sy_round_device(ops, N, 1, resp, some)
     torch.cuda.synchronize()
     buf = np.zeros(3072 * 16, np.uint64)  # synthetic.hip SY_DBG_ROWS
     L.check(L.load().nrg_test_debug_read(dev.handle, buf.ctypes.data_as(C.c_void_p), buf.size))

@@ -156,6 +156,7 @@ int grow_buf(Member& m, DBuf& d, uint64_t bytes) {
     if (d.bytes >= bytes) return NRG_OK;
     GCHK(hipStreamSynchronize(m.cstream));
     GCHK(hipStreamSynchronize(m.ctx->stream));
+    if (m.pstream) GCHK(hipStreamSynchronize(m.pstream));  // a one-rank group's partitions
     if (d.p) GCHK(hipFree(d.p));
     d.p = nullptr;
     d.bytes = 0;
