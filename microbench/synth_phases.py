@@ -39,10 +39,14 @@ pacc = np.zeros((T, 5))
 sacc = np.zeros((T, 3))
 hw = None
 for r in range(R + 3):
-    if os.environ.get("SY_NORESP"):  # (diagnostic: no responses -> the sum role only folds the hot words)
-        dev.sy_round_device(ops, N, 1)
-    else:
-        dev.sy_round_device(ops, N, 1, resp, some)
+    # two rounds back to back, the second's stamps read: its partition launch follows the first
+    # round's bucket pass on a busy queue, as in the bench (a launch from an idle GPU starts its
+    # XCDs up to 3 us apart)
+    for _ in range(2):
+        if os.environ.get("SY_NORESP"):  # (diagnostic: no responses -> the sum role only folds the hot words)
+            dev.sy_round_device(ops, N, 1)
+        else:
+            dev.sy_round_device(ops, N, 1, resp, some)
     torch.cuda.synchronize()
     buf = np.zeros(3072 * 16, np.uint64)  # synthetic.hip SY_DBG_ROWS
     L.check(L.load().nrg_test_debug_read(dev.handle, buf.ctypes.data_as(C.c_void_p), buf.size))
@@ -61,6 +65,7 @@ for r in range(R + 3):
         sacc += st
     if r == R + 2:
         hw = rows[:NB, 9:12].astype(np.int64)
+        phw = rows[1024:1024 + T, 9:11].astype(np.int64)  # the tiles' HW_ID, XCC_ID
 acc /= R
 pacc /= R
 sacc /= R
@@ -68,6 +73,11 @@ print(f"partition tiles {T}: start {pacc[:, 0].min() / 100:.2f}..{pacc[:, 0].max
 for nm, d in [("load+rank", pacc[:, 1] - pacc[:, 0]), ("offsets", pacc[:, 2] - pacc[:, 1]), ("stage LDS", pacc[:, 3] - pacc[:, 2]),
               ("E stores", pacc[:, 4] - pacc[:, 3]), ("tile span", pacc[:, 4] - pacc[:, 0])]:
     print(f"  {nm:12s} mean {d.mean() / 100:7.2f} us  max {d.max() / 100:7.2f} us")
+pst = pacc[:, 0] / 100
+xcc = phw[:, 1] & 0xF
+print("  tile start by XCC (mean / max us): " + "  ".join(f"{x}: {pst[xcc == x].mean():.2f}/{pst[xcc == x].max():.2f}" for x in range(8) if (xcc == x).any()))
+print("  tile start by tile index eighth (mean us): " + " ".join(f"{pst[k * T // 8:(k + 1) * T // 8].mean():.2f}" for k in range(8)))
+print("  tile end by XCC (mean / max us): " + "  ".join(f"{x}: {pacc[xcc == x, 4].mean() / 100:.2f}/{pacc[xcc == x, 4].max() / 100:.2f}" for x in range(8) if (xcc == x).any()))
 print(f"sum workgroups (previous round) start {sacc[:, 0].min() / 100:.2f}..{sacc[:, 0].max() / 100:.2f} us, last end {sacc[:, 2].max() / 100:.2f} us")
 for nm, d in [("atomics", sacc[:, 1] - sacc[:, 0]), ("responses", sacc[:, 2] - sacc[:, 1])]:
     print(f"  {nm:12s} mean {d.mean() / 100:7.2f} us  max {d.max() / 100:7.2f} us")

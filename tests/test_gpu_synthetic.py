@@ -87,6 +87,23 @@ def test_synth_one_word(nrg, orc, path, wo):
     dev.close()
 
 
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 4099])
+def test_synth_word0_parts(nrg, orc, n):
+    """Cold word 0 (every op's first cold touch for tid 0) is replayed by four workgroups in a
+    chunk without a WriteOnly, each from the word's value plus the touches before its part
+    (synthetic.hip SY_B0_PARTS): chunks of 1-3 touches leave parts empty, and a chunk with one
+    WriteOnly goes back to one workgroup; words and responses against the oracle."""
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_SYNTHETIC, 0, max_batch=1 << 13)
+    os_ = orc.Synthetic()
+
+    def one_wo(ops):
+        ops["op"][len(ops) // 2] = 0  # WriteOnly
+    _check_rounds(nrg, orc, dev, os_, 2, n, 600 + n, [0], 0)
+    _check_rounds(nrg, orc, dev, os_, 1, n, 700 + n, [0], 0, one_wo)
+    _check_rounds(nrg, orc, dev, os_, 1, n, 800 + n, [0, 0, 0, 9], 0)
+    dev.close()
+
+
 def test_synth_wide_values(nrg, orc, path):
     """Seen values past 2^32. The bucket pass stores 4-B seen values only while every word is
     < 2^31 and no WriteOnly of the chunk writes a tid >= 2^31 (synthetic.hip SyFlags): a chunk
