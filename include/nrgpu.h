@@ -424,7 +424,9 @@ int nrg_group_partitioned_round(nrg_group* g, const nrg_round* rounds);
  * first launch), and sends the round before that back into its caller's order. The caller's
  * buffers of a round stay borrowed for the next two calls, or until nrg_group_partitioned_flush /
  * nrg_group_sync completes every posted round. A round dropped on an agreed error (a rank's bad
- * part) returns that error from the call that moved it (NRG_OK otherwise). */
+ * part) returns that error from the call that moved it (NRG_OK otherwise). A one-rank group
+ * partitions on a library-owned side stream, after the work queued on the replica's stream and
+ * beside the previous round's replay; the replica's stream waits for it before moving the round. */
 int nrg_group_partitioned_round_async(nrg_group* g, const nrg_round* rounds);
 /* Complete the round posted by nrg_group_partitioned_round_async, if any (its result). */
 int nrg_group_partitioned_flush(nrg_group* g);
