@@ -632,7 +632,10 @@ __device__ __forceinline__ void sy_part_role(const SyPartArgs& A, u32 tile, SyPa
 // touches without barriers, then per-word prefixes over the waves place them. A pass with a
 // WriteOnly in it is applied wave by wave instead (values depend on the last SET).
 // (<= 128 VGPRs: two 8-wave workgroups per CU)
-__global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(4))) void sy_bucket_kernel(const u16* __restrict__ Ew, const u16* __restrict__ Eo, const u32* __restrict__ cnt_tb,
+#ifndef NRG_SYB_WPE
+#define NRG_SYB_WPE 4  // waves per SIMD the bucket pass is compiled for (4: 128 VGPRs, two workgroups per CU)
+#endif
+__global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(NRG_SYB_WPE))) void sy_bucket_kernel(const u16* __restrict__ Ew, const u16* __restrict__ Eo, const u32* __restrict__ cnt_tb,
                                                             u32 NB, u32 ntiles, u32 tile_entries, u64* __restrict__ V,
                                                             u64* __restrict__ words, u64 N, u32 HR, u32 W,
                                                             const nrg_synth_op* __restrict__ ring, u64 ring_mask, u64 lo,
