@@ -905,6 +905,9 @@ static int pt_stage_a(nrg_group* g, uint64_t e) {
                                              rprev ? rprev + off : nullptr, rprevf ? rprevf + off : nullptr));
             off += n;
         } while (off < P.rp);
+        // a round with nothing for this owner launches nothing, and the previous round's reads
+        // would wait for a later launch while its answers go back in this call's stage B: now
+        if (P.rp == 0 && P.rk == 0) RCHK(nrg_join(c));
     }
     return NRG_OK;
 }

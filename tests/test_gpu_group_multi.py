@@ -262,14 +262,18 @@ def _digest_sum(digs):
 
 
 @pytest.mark.parametrize("G,skew,pipelined", [(3, False, False), (8, False, False), (3, True, False), (1, False, True),
-                                              (3, False, True), (8, False, True), (3, True, True)])
+                                              (1, False, "instream"), (3, False, True), (8, False, True),
+                                              (3, True, True)])
 def test_group_partitioned_members(nrg, orc, G, skew, pipelined):
     """cnr-style partitioned rounds (nrg_group_partitioned_round) over G partitions: every
     member's Gets and previous values equal the NR replay of the global log, and the partitions'
     digests add up to the NR replica's. skew: every Put of every member belongs to partition 0,
     which then receives G times its max_batch in one round and replays it in chunks. pipelined:
     the rounds go through nrg_group_partitioned_round_async back to back (each call completes the
-    round before it) and one flush; checked afterwards, round by round."""
+    round before it) and one flush; checked afterwards, round by round. "instream": the inputs'
+    stream set (nrg_group_set_input_stream) and 7 rounds, so round 4 -- empty for the only rank --
+    comes between round 3's replay and round 3's answers going back: round 3's reads, which ride
+    in the next replay launch, must launch anyway."""
     import torch
 
     from nrgpu.parallel import key_owner
@@ -280,6 +284,9 @@ def test_group_partitioned_members(nrg, orc, G, skew, pipelined):
     cfg.log2_slots, cfg.max_batch = 17, 4096
     cfg.pipeline = 1 if pipelined else 0  # pipelined: each round's reads ride in the next round's launch
     g, ctxs = _open(L, lib, G, cfg)
+    if pipelined == "instream":
+        in_stream = torch.cuda.Stream()
+        L.check(lib.nrg_group_set_input_stream(g, 0, C.c_void_p(in_stream.cuda_stream)))
     prefill, span = 6000, 30_000
     for p, c in enumerate(ctxs):
         L.check(lib.nrg_hashmap_prefill_partition(c, prefill, 1, p, G))
@@ -288,7 +295,7 @@ def test_group_partitioned_members(nrg, orc, G, skew, pipelined):
     pool = orc.gen_uniform(200_000, 99, span)
     owned0 = pool[key_owner(pool, G) == 0]
     posted = []
-    for r in range(5 if pipelined else 4):
+    for r in range(7 if pipelined == "instream" else 5 if pipelined else 4):
         rd = (L.Round * G)()
         keep = []
         for i in range(G):
