@@ -19,7 +19,7 @@ int nrg_test_maxscan(nrg_ctx* ctx, const uint32_t* d_keys, const uint32_t* d_val
                      uint32_t* d_out);
 /* The hardware property the synthetic replay's rankings rest on (synthetic.hip): a
  * returning LDS add gives the lanes of one instruction that hit the same count their old values
- * in lane order. `blocks` workgroups of 8 waves run `trials` x 5 adds over `keys` (1..512)
+ * in lane order. `blocks` (<= 65536) workgroups of 8 waves run `trials` (<= 4096) x 5 adds over `keys` (1..512)
  * counts; out[0] = lanes checked, out[1] = lanes out of lane order (0 expected). */
 int nrg_test_lds_add_order(nrg_ctx* ctx, uint32_t keys, uint32_t trials, uint32_t blocks, uint64_t out[2]);
 /* copy the record stored at PHYSICAL ring position `phys` (< log size) to host memory `out`

@@ -1081,7 +1081,7 @@ extern "C" int nrg_test_maxscan(nrg_ctx* c, const uint32_t* d_keys, const uint32
 
 extern "C" int nrg_test_lds_add_order(nrg_ctx* c, uint32_t keys, uint32_t trials, uint32_t blocks,
                                       uint64_t out[2]) {
-    if (!c || !out || keys < 1 || keys > 512 || blocks < 1 || blocks > 65536) return NRG_E_INVAL;
+    if (!c || !out || keys < 1 || keys > 512 || blocks < 1 || blocks > 65536 || trials > 4096) return NRG_E_INVAL;
     int r = use_device(c);
     if (r) return r;
     u64* d = nullptr;
