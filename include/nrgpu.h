@@ -123,7 +123,7 @@ typedef struct {
                                  stack: the Pops answered from earlier tiles and the commit;
                                  synthetic: the per-op sums and the hot-word fold. Those outputs
                                  (and the buffers they read) are complete only after nrg_join(),
-                                 the next call that replays writes on this context, or
+                                 the next round call on this context (an empty one included), or
                                  nrg_sync(); give back-to-back rounds distinct response buffers.
                                  Synchronous calls are unaffected (their outputs are complete on
                                  return). */

@@ -1827,7 +1827,8 @@ static hipError_t next_epoch(nrg_ctx* c, u32* e) {
 hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool write_ring, const u64* d_get_keys,
                            u64 R, u64* d_get_vals, uint8_t* d_get_found, u64 resp_lo, u64 resp_hi, u64* d_prev,
                            uint8_t* d_prev_found) {
-    if (n == 0) return hm_reads(c, d_get_keys, R, d_get_vals, d_get_found);
+    // (an empty round still completes the last round's deferred half: "the next call" does)
+    if (n == 0) return R ? hm_reads(c, d_get_keys, R, d_get_vals, d_get_found) : hm_flush(c);
     if (n > HM_MAX_BATCH) return hipErrorInvalidValue;
     const nrg_put* src = (const nrg_put*)src_recs;
     const bool want_prev = d_prev && resp_lo < lo + n && resp_hi > lo;

@@ -895,7 +895,7 @@ hipError_t st_flush(nrg_ctx* c) {
 // or right away.
 hipError_t st_replay_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 resp_hi, uint32_t* d_resp, uint8_t* d_some,
                            const nrg_stack_op* src) {
-    if (n == 0) return hipSuccess;
+    if (n == 0) return st_flush(c);  // an empty round still completes the last round's deferred finish
     StPass A = st_pass(c, c->st_par);
     A.src = src;
     A.lo = lo;

@@ -1232,7 +1232,7 @@ hipError_t sy_init(nrg_ctx* c) {
 
 hipError_t sy_replay_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 resp_hi, u64* d_resp, uint8_t* d_some,
                            const nrg_synth_op* src) {
-    if (n == 0) return hipSuccess;
+    if (n == 0) return sy_flush(c);  // an empty round still completes the last round's deferred sums
     if (c->d_sy_aux) return sy_bucket_chunk(c, lo, n, resp_lo, resp_hi, d_resp, d_some, src);
     if (src) {  // the sort path replays from the ring: append the ops first (wrapping)
         const u64 mask = c->log_size - 1, first = std::min<u64>(n, c->log_size - (lo & mask));

@@ -187,6 +187,52 @@ def test_pipelined_rounds_back_to_back(nrg, orc, path):
     _check_state(dev, om)
 
 
+def test_pipelined_empty_round_completes_the_last(nrg, orc):
+    """config.pipeline = 1: an empty round (no Puts, no Gets) is "the next call" too -- it
+    launches the last round's deferred apply and reads, for every data structure, so their
+    outputs are complete once the stream passes it (no join)."""
+    import torch
+
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=17, max_batch=1 << 14, pipeline=1)
+    dev.use_torch_stream()
+    om = orc.HashMap()
+    W, R = 6000, 20000
+    keys, vals = orc.gen_uniform(W, 170, 9000), orc.gen_raw(W, 171)
+    gk = orc.gen_uniform(R, 172, 9500)
+    d_puts = torch.from_numpy(_puts(keys, vals).view(np.int64).copy()).cuda()
+    d_gk = torch.from_numpy(gk.view(np.int64)).cuda()
+    d_gv = torch.full((R,), -1, dtype=torch.int64, device="cuda")
+    d_gf = torch.full((R,), 7, dtype=torch.uint8, device="cuda")
+    dev.hm_round_device(d_puts, W, 1, d_gk, R, d_gv, d_gf, None, None)
+    dev.hm_round_device(None, 0, 1, None, 0, None, None, None, None)  # the empty round
+    torch.cuda.synchronize()
+    om.replay(keys, vals)
+    ev, ef = om.get_batch(gk)
+    np.testing.assert_array_equal(d_gf.cpu().numpy(), ef.astype(np.uint8))
+    np.testing.assert_array_equal(d_gv.cpu().numpy().view(np.uint64), ev)
+    dev.sync()
+    _check_state(dev, om)
+
+    for kind, rnd in ((nrg._lib.NRG_DS_STACK, "st_round_device"), (nrg._lib.NRG_DS_SYNTHETIC, "sy_round_device")):
+        d = nrg.DeviceReplica(kind, 0, max_batch=1 << 14, pipeline=1)
+        d.use_torch_stream()
+        n = 10_000
+        if kind == nrg._lib.NRG_DS_STACK:
+            ops = torch.from_numpy((orc.gen_raw(n, 173) & 0x1FFFFFFFF).astype(np.int64)).cuda()
+            resp = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+        else:
+            raw = orc.gen_raw(4 * n, 174)
+            o = np.stack([raw[0::4] % 64, raw[1::4], raw[2::4], np.ones(n, np.uint64)], 1).astype(np.uint64)
+            ops = torch.from_numpy(o.view(np.int64)).cuda()
+            resp = torch.full((n,), -1, dtype=torch.int64, device="cuda")
+        some = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+        getattr(d, rnd)(ops, n, 1, resp, some)
+        getattr(d, rnd)(ops, 0, 1, None, None)  # the empty round
+        torch.cuda.synchronize()
+        assert np.all(some.cpu().numpy() != 7), f"{rnd}: the last round's deferred outputs did not complete"
+        d.close()
+
+
 @pytest.mark.parametrize("span", [40, 3000, 1 << 40])
 def test_small_rounds_device(nrg, orc, span):
     """One-launch small rounds (hashmap.hip hm_small_round_kernel, the combiner's path):
