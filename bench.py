@@ -228,8 +228,8 @@ class Env:
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         local = int(os.environ.get("LOCAL_RANK", "0"))
-        if self.world != args.gpus:
-            log(f"WORLD_SIZE={self.world} but --gpus={args.gpus}; using WORLD_SIZE")
+        # main() refuses a WORLD_SIZE that disagrees with --gpus before any GPU call
+        assert self.world == args.gpus, (self.world, args.gpus)
         if args.share_gpu:
             local = 0  # rehearsal of the N > 1 path with every rank on the box's one GPU (gloo only)
         self.local = local
@@ -563,6 +563,12 @@ def run_hashmap(args, env):
         "distinct_get_keys": int(u_r),
         "distinct_put_keys": int(u_w),
     }
+    if not args.partitioned:
+        s = amdahl_speedup(world, args.write_ratio)
+        res["amdahl"] = {"predicted_speedup_vs_1gpu": round(s, 3), "write_pct": args.write_ratio,
+                         "c_w_over_c_r": 2.0,
+                         "model": "SURVEY.md 8(e): S(G) = G(w c_w + (1-w) c_r) / (w c_w G + (1-w) c_r), "
+                                  "all-gather time ignored; every replica replays every Put"}
     if prev_value is not None:
         res["variants"] = {"prev_value_responses_Mops": round(prev_value, 3)}
     if not args.no_cpu_baseline and world == 1 and args.dist == "uniform" and not args.partitioned:
@@ -841,6 +847,83 @@ def write_scaleout_csv(path, name, world, ops_per_rank_per_round, steps, elapsed
                         int(ops_per_rank_per_round * steps / elapsed)])
 
 
+def _free_port():
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args, argv, script=None):
+    """`python3 bench.py --gpus N` without a launcher: start N rank processes of this script, one
+    per GPU (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set as torch.distributed.run sets them),
+    relay rank 0's JSON line, and return non-zero if any rank fails or the deadline passes. The
+    reference's harness likewise spawns its own workers per replica (benches/mkbench.rs:611-700,
+    benches/hashmap.rs:226-259). This parent process makes no GPU call: no torch, no libnrgpu."""
+    import subprocess
+
+    n = args.gpus
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL across processes)
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    log(f"launched {n} ranks (pids {[p.pid for p in procs]}), rendezvous 127.0.0.1:{port}")
+    lines = []
+    reader = threading.Thread(target=lambda: lines.extend(procs[0].stdout.read().decode().splitlines()),
+                              daemon=True)
+    reader.start()
+    deadline = time.monotonic() + (args.deadline if args.deadline > 0 else float("inf")) + 30.0
+    status = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        failed = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+        if failed:
+            r, c = failed[0]
+            log(f"rank {r} exited with status {c}; stopping the other ranks")
+            status = c if c > 0 else 1
+            break
+        if all(c == 0 for c in codes):
+            break
+        if time.monotonic() > deadline:
+            log(f"ranks {[r for r, c in enumerate(codes) if c is None]} still running past the deadline; stopping")
+            status = 3
+            break
+        time.sleep(0.05)
+    if status:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=20)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    reader.join(timeout=10)
+    if status == 0:
+        out = [ln for ln in lines if ln.startswith("{")]
+        if not out:
+            log("rank 0 printed no result line")
+            return 1
+        print(out[-1], flush=True)
+    return status
+
+
+def amdahl_speedup(n, write_pct, cw_over_cr=2.0):
+    """whole-node speedup of full replication over one replica,
+    S(G) = G (w c_w + (1-w) c_r) / (w c_w G + (1-w) c_r), the all-gather ignored. c_w / c_r = 2
+    is calibrated from the per-GPU emulated rounds (100k Puts + 900k Gets in 34.3 us,
+    800k + 900k in 79 us)."""
+    w = write_pct / 100.0
+    a = cw_over_cr
+    return n * (w * a + (1 - w)) / (w * a * n + (1 - w))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -885,6 +968,15 @@ def main():
                          "0: every round call completes its own reads")
     args = ap.parse_args()
     args.timing_every = max(1, args.timing_every)
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is None and args.gpus > 1:
+        # no launcher around us: start the N ranks ourselves (this process never touches the GPU)
+        sys.exit(launch_ranks(args, sys.argv[1:]))
+    if ws is not None and int(ws) != args.gpus:
+        log(f"WORLD_SIZE={ws} but --gpus={args.gpus}: refusing to measure a different GPU count than asked")
+        sys.exit(2)
     WATCH.arm(args.deadline)
     env = Env(args)
     runner = {"stack": run_stack, "synthetic": run_synthetic}.get(args.workload, run_hashmap)

@@ -376,16 +376,21 @@ ncclResult_t lb_init_rank(ncclComm_t* comm, int nranks, ncclUniqueId id, int ran
         // the same id starts from correct counts; the last joiner to give up frees it.
         lk.unlock();
         std::lock_guard<std::mutex> rl(g_reg_mu);
-        std::lock_guard<std::mutex> wl(w->mu);
-        if (w->joined == w->n) {  // the last rank arrived just now: keep this rank in the world
-            *comm = reinterpret_cast<ncclComm_t>(c);
-            return ncclSuccess;
+        bool last = false;
+        {
+            // the world's lock is released before the world may be freed below
+            std::lock_guard<std::mutex> wl(w->mu);
+            if (w->joined == w->n) {  // the last rank arrived just now: keep this rank in the world
+                *comm = reinterpret_cast<ncclComm_t>(c);
+                return ncclSuccess;
+            }
+            w->joined--;
+            last = --w->alive == 0;
         }
-        w->joined--;
-        const bool last = --w->alive == 0;
         delete c;
         if (last) {
-            g_forming.erase(key);
+            auto it = g_forming.find(key);
+            if (it != g_forming.end() && it->second == w) g_forming.erase(it);
             delete w;  // nobody else holds it: it was still forming, with no joiner left
         }
         return ncclSystemError;

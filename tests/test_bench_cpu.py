@@ -46,3 +46,76 @@ def test_watchdog_ends_a_stalled_process():
                        env={**os.environ, "RANK": "5", "WORLD_SIZE": "8"})
     assert p.returncode == 3, p.stderr
     assert "rank 5 of 8 still in phase 'timed region'" in p.stderr
+
+
+def _run_bench(args, env_extra=None, timeout=120):
+    import subprocess
+    import sys
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                          timeout=timeout, env=env)
+
+
+def test_world_size_mismatch_refused():
+    """A launcher's WORLD_SIZE that disagrees with --gpus exits non-zero before any GPU call
+    (the run used to log and bench WORLD_SIZE ranks under a --gpus N command)."""
+    p = _run_bench(["--gpus", "8", "--steps", "1", "--warmup", "0"], {"WORLD_SIZE": "1", "RANK": "0"})
+    assert p.returncode == 2, p.stderr
+    assert "WORLD_SIZE=1 but --gpus=8" in p.stderr
+    assert not p.stdout.strip()
+
+
+def test_launcher_spawns_ranks_and_relays_rank0(bench, tmp_path):
+    """`bench.py --gpus N` with no launcher starts N ranks with torch.distributed.run's env and
+    relays rank 0's JSON line (a stand-in rank script, so no GPU is needed)."""
+    script = tmp_path / "rank.py"
+    script.write_text(
+        "import json, os, sys\n"
+        "if os.environ['RANK'] == '0':\n"
+        "    print('noise'); print(json.dumps({k: os.environ[k] for k in\n"
+        "        ('RANK', 'LOCAL_RANK', 'WORLD_SIZE', 'MASTER_ADDR', 'MASTER_PORT')} | {'argv': sys.argv[1:]}))\n")
+    import argparse
+    import contextlib
+    import io
+
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        rc = bench.launch_ranks(argparse.Namespace(gpus=3, deadline=60.0), ["--gpus", "3", "--x"], script=str(script))
+    assert rc == 0
+    line = json.loads(buf.getvalue().strip())
+    assert line["RANK"] == "0" and line["WORLD_SIZE"] == "3" and line["MASTER_ADDR"] == "127.0.0.1"
+    assert line["argv"] == ["--gpus", "3", "--x"]
+
+
+def test_launcher_fails_when_a_rank_fails(bench, tmp_path):
+    """One failing rank ends the run non-zero and stops the others (which would otherwise wait in
+    a collective for it)."""
+    script = tmp_path / "rank.py"
+    script.write_text("import os, sys, time\n"
+                      "if os.environ['RANK'] == '1': sys.exit(7)\n"
+                      "time.sleep(60)\n")
+    import argparse
+    import time
+
+    t = time.monotonic()
+    rc = bench.launch_ranks(argparse.Namespace(gpus=2, deadline=120.0), [], script=str(script))
+    assert rc == 7
+    assert time.monotonic() - t < 40
+
+
+def test_launcher_without_gpu_exits_nonzero():
+    """The real bench through its own launcher on a host without a GPU: every rank fails, so
+    the run must fail rather than print a line."""
+    p = _run_bench(["--gpus", "2", "--backend", "gloo", "--share-gpu", "--steps", "2", "--warmup", "1",
+                    "--no-cpu-baseline", "--deadline", "100"], timeout=200)
+    assert p.returncode != 0
+    assert "exited with status" in p.stderr
+    assert not p.stdout.strip()
+
+
+def test_amdahl_model(bench):
+    assert bench.amdahl_speedup(1, 10) == pytest.approx(1.0)
+    assert bench.amdahl_speedup(8, 10) == pytest.approx(8 * 1.1 / 2.5)
+    assert bench.amdahl_speedup(8, 100) == pytest.approx(1.0)
