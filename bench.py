@@ -141,17 +141,9 @@ def _nr_cpu_run(seconds, write_ratio, key_space, prefill, threads=None):
     one Replica per NUMA node over the threads used (oracle/nr_cpu.cpp)."""
     import oracle
 
-    cpus = sorted(os.sched_getaffinity(0))
-    budget = cpu_budget(len(cpus)) if threads is None else threads
-    nodes = numa_groups(cpus)
-    # spread the thread budget evenly over the NUMA nodes (lowest-numbered CPUs of each node are
+    # the thread budget spread evenly over the NUMA nodes (lowest-numbered CPUs of each node are
     # physical cores; their SMT siblings come later), one Replica per node
-    per = max(1, budget // len(nodes))
-    groups = [g[:per] for g in nodes][: max(1, min(len(nodes), budget))]
-    cpu_list, rep = [], []
-    for r, g in enumerate(groups):
-        cpu_list += g
-        rep += [r] * len(g)
+    cpu_list, rep, groups = _nr_groups(threads)
     res = oracle.nr_hashmap_bench(cpu_list, rep, seconds, write_ratio, key_space, prefill, 2_500_000, 0xC0FFEE)
     return res, cpu_list, groups
 
@@ -581,43 +573,87 @@ def run_hashmap(args, env):
 
 
 # ---------------------------------------------------------------------------------------------
+def _nr_groups(threads=None):
+    """The thread budget spread over the NUMA nodes, one Replica per node (as _nr_cpu_run)."""
+    cpus = sorted(os.sched_getaffinity(0))
+    budget = cpu_budget(len(cpus)) if threads is None else threads
+    nodes = numa_groups(cpus)
+    per = max(1, budget // len(nodes))
+    groups = [g[:per] for g in nodes][: max(1, min(len(nodes), budget))]
+    cpu_list, rep = [], []
+    for r, g in enumerate(groups):
+        cpu_list += g
+        rep += [r] * len(g)
+    return cpu_list, rep, groups
+
+
 def stack_cpu_baseline(seconds, n_ops, init):
-    """The sequential oracle Stack (Vec::push/pop, benches/stack.rs:36-84) on one host core over
-    a bounded sample of the same op stream."""
+    """The stack scale-out (benches/stack.rs:115-134) through the C++ restatement of nr: pinned
+    threads on the job's CPU budget, one Replica per NUMA node, execute_mut(Push/Pop) from a
+    shared 10,000-op stream, Stack::default (0..50000) per replica. Beside it, the sequential
+    oracle Stack (a Vec in a loop, no log) on one core, labelled as such."""
     import numpy as np
     import oracle
 
+    cpu_list, rep, groups = _nr_groups()
+    r = oracle.nr_stack_bench(cpu_list, rep, seconds, 10_000, 0x5AC)
+    out = {"value": round(r.ops / r.seconds / 1e6, 3), "unit": "Mops/s", "cores": len(cpu_list), "kind": "port",
+           "sample": ("%.1f s of the stack scale-out (benches/stack.rs:115-134: 10,000-op 50/50 Push/Pop stream, "
+                      "seeded) through the C++ restatement of nr (log + flat combining) on %d threads, %d replica(s) "
+                      "(one per NUMA node); %d ops" % (r.seconds, len(cpu_list), len(groups), r.ops)),
+           "host": host_topology()}
+    side = min(3.0, seconds)
+    t1 = oracle.nr_stack_bench(cpu_list[:1], [0], side, 10_000, 0x5AC)
+    out["one_thread_nr"] = {"value": round(t1.ops / t1.seconds / 1e6, 3), "unit": "Mops/s", "cores": 1,
+                            "sample": "the same stream through nr on 1 thread, 1 replica, %.1f s" % t1.seconds}
     st = oracle.Stack(np.arange(init, dtype=np.uint32))
     vals, ops = oracle.gen_stack_ops(n_ops, 0x5AC)
     t0 = time.perf_counter()
     done = 0
-    while time.perf_counter() - t0 < seconds:
+    while time.perf_counter() - t0 < side:
         st.replay(vals, ops)
         done += n_ops
     el = time.perf_counter() - t0
-    return {"value": round(done / el / 1e6, 3), "unit": "Mops/s", "cores": 1, "kind": "port",
-            "sample": "%.1f s of %d-op push/pop batches (50/50, seeded) replayed by the sequential oracle Stack" % (
-                el, n_ops)}
+    out["one_thread_sequential"] = {
+        "value": round(done / el / 1e6, 3), "unit": "Mops/s", "cores": 1,
+        "sample": "%.1f s of %d-op batches replayed by the sequential oracle Stack (no log, no combining)" % (el, n_ops)}
+    return out
 
 
 def synth_cpu_baseline(seconds, n_ops):
-    """The sequential oracle AbstractDataStructure (benches/synthetic.rs:112-195) on one host
-    core over a bounded sample of the same kind of ReadWrite stream."""
+    """The synthetic scale-out (benches/synthetic.rs:296-335) through the C++ restatement of nr:
+    ReadWrite ops from a shared 10,000-op stream, tid = the issuing thread's core id, 200,000
+    CachePadded words per replica, one Replica per NUMA node. Beside it, the sequential oracle
+    AbstractDataStructure on one core, labelled as such."""
     import numpy as np
     import oracle
 
+    cpu_list, rep, groups = _nr_groups()
+    r = oracle.nr_synth_bench(cpu_list, rep, seconds, 10_000, 0x5E7)
+    out = {"value": round(r.ops / r.seconds / 1e6, 3), "unit": "Mops/s", "cores": len(cpu_list), "kind": "port",
+           "sample": ("%.1f s of the synthetic scale-out (benches/synthetic.rs:296-335: 10,000 ReadWrite ops, tid = "
+                      "core id, seeded r1/r2) through the C++ restatement of nr (log + flat combining) on %d "
+                      "threads, %d replica(s) (one per NUMA node); %d ops" % (r.seconds, len(cpu_list), len(groups),
+                                                                             r.ops)),
+           "host": host_topology()}
+    side = min(3.0, seconds)
+    t1 = oracle.nr_synth_bench(cpu_list[:1], [0], side, 10_000, 0x5E7)
+    out["one_thread_nr"] = {"value": round(t1.ops / t1.seconds / 1e6, 3), "unit": "Mops/s", "cores": 1,
+                            "sample": "the same stream through nr on 1 thread, 1 replica, %.1f s" % t1.seconds}
     sy = oracle.Synthetic()
     raw = oracle.gen_raw(3 * n_ops, 0x5E7)
     ops = np.stack([raw[0::3] % 64, raw[1::3], raw[2::3], np.ones(n_ops, np.uint64)], axis=1)
     t0 = time.perf_counter()
     done = 0
-    while time.perf_counter() - t0 < seconds:
+    while time.perf_counter() - t0 < side:
         sy.replay(ops)
         done += n_ops
     el = time.perf_counter() - t0
-    return {"value": round(done / el / 1e6, 3), "unit": "Mops/s", "cores": 1, "kind": "port",
-            "sample": "%.1f s of %d-op ReadWrite batches (tid < 64, seeded) replayed by the sequential oracle "
-                      "AbstractDataStructure (200,000 words)" % (el, n_ops)}
+    out["one_thread_sequential"] = {
+        "value": round(done / el / 1e6, 3), "unit": "Mops/s", "cores": 1,
+        "sample": "%.1f s of %d-op ReadWrite batches replayed by the sequential oracle (no log, no combining)" % (
+            el, n_ops)}
+    return out
 
 
 def run_synthetic(args, env):

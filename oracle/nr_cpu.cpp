@@ -449,6 +449,161 @@ struct JunkD {
     uint64_t dispatch(const uint64_t&) const { return junk; }
 };
 
+
+// Stack (benches/stack.rs:36-84): a Vec<u32>, Push -> None, Pop -> Vec::pop. Stack::default
+// holds 0..50000 (:50-63). Op encoding: bit 32 = Push, low 32 bits = the value.
+struct StackD {
+    using W = uint64_t;
+    using Rd = uint64_t;  // OpRd is empty in the reference (:29-30); never dispatched
+    using Resp = uint64_t;  // Option<u32>: bit 32 = Some
+    std::vector<uint32_t> storage;
+    uint64_t dispatch_mut(const uint64_t& op) {
+        if ((op >> 32) & 1) {
+            storage.push_back((uint32_t)op);
+            return 0;
+        }
+        if (storage.empty()) return 0;
+        uint32_t v = storage.back();
+        storage.pop_back();
+        return (1ull << 32) | v;
+    }
+    uint64_t dispatch(const uint64_t&) const { return 0; }
+};
+
+// AbstractDataStructure (benches/synthetic.rs:60-195) with the bench's default
+// new(200_000, 20, 5, 2, 1) (:75-79) and its CachePadded<usize> words (:72). Wrapping usize
+// arithmetic as a release build; the hot loop is empty when rnd2 + hot_writes wraps.
+struct SyOp {
+    uint64_t tid, r1, r2, kind;  // kind 1 = ReadWrite, 0 = WriteOnly
+};
+struct SynthD {
+    using W = SyOp;
+    using Rd = SyOp;
+    using Resp = uint64_t;
+    struct alignas(128) Word {
+        uint64_t v;
+    };
+    uint64_t n = 200000, cold_reads = 20, cold_writes = 5, hot_reads = 2, hot_writes = 1;
+    std::vector<Word> storage;
+    void init() {
+        storage.resize(n);
+        for (uint64_t i = 0; i < n; i++) storage[i].v = i;  // :97-100
+    }
+    uint64_t hot_count(uint64_t b) const { return b + hot_writes < b ? 0 : hot_writes; }
+    uint64_t dispatch_mut(const SyOp& o) {
+        uint64_t hc = hot_count(o.r2), begin = o.r1 * o.tid, sum = 0;
+        if (o.kind) {  // read_write (:154-174)
+            for (uint64_t j = 0; j < hc; j++) storage[(o.r2 + j) % hot_reads].v += 1;
+            for (uint64_t k = 0; k < cold_writes; k++) {
+                uint64_t idx = begin % (n - hot_reads) + hot_reads;
+                begin += o.r2;
+                sum += storage[idx].v;
+                storage[idx].v += 1;
+            }
+            return sum;
+        }
+        for (uint64_t j = 0; j < hc; j++) storage[(o.r2 + j) % hot_reads].v = o.tid;  // write (:134-152)
+        for (uint64_t k = 0; k < cold_writes; k++) {
+            uint64_t idx = begin % (n - hot_reads) + hot_reads;
+            begin += o.r2;
+            storage[idx].v = o.tid;
+        }
+        return 0;
+    }
+    uint64_t dispatch(const SyOp& o) const {  // read (:112-132)
+        uint64_t hc = hot_count(o.r2), begin = o.r1 * o.tid, sum = 0;
+        for (uint64_t j = 0; j < hc; j++) sum += storage[(o.r2 + j) % hot_reads].v;
+        for (uint64_t k = 0; k < cold_reads; k++) {
+            sum += storage[begin % (n - hot_reads) + hot_reads].v;
+            begin += o.r2;
+        }
+        return sum;
+    }
+};
+
+// The scale-out harness (benches/mkbench.rs:611-831) over any D: one Replica per CPU group,
+// each replica's D built by a thread pinned to its first core (node-local memory, :611-629),
+// pinned worker threads that each walk their own shuffled copy of the op stream (:705-706),
+// 128 ops per clock check (:737-773), and a final sync so finished replicas keep combining
+// for the others' GC (:799-821). init(D&) builds a replica's data; run(rep, tok, i, cpu)
+// issues op i of the shared stream and returns 1 for a write.
+static inline void pin_to(int cpu) {
+    if (cpu < 0) return;
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    CPU_SET(cpu, &set);
+    pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+}
+
+template <typename D, typename Init, typename Run, typename Fini>
+static void scale_out(uint32_t nreplicas, const int* cpus, const uint32_t* cpu_replica, uint32_t nthreads,
+                      double duration_s, uint64_t nop, uint64_t seed, uint64_t log_bytes, Init&& init,
+                      Run&& run, Fini&& fini, double* seconds, uint64_t* ops, uint64_t* writes) {
+    Log<typename D::W> log(log_bytes ? log_bytes : DEFAULT_LOG_BYTES);
+    std::vector<D> ds(nreplicas);
+    std::vector<std::unique_ptr<Replica<D>>> reps;
+    for (uint32_t r = 0; r < nreplicas; r++) {
+        int cpu = -1;
+        for (uint32_t t = 0; t < nthreads; t++)
+            if (cpu_replica[t] == r) {
+                cpu = cpus[t];
+                break;
+            }
+        std::thread b([&, r, cpu] {
+            pin_to(cpu);
+            init(ds[r]);
+        });
+        b.join();
+        reps.emplace_back(new Replica<D>(&log, &ds[r]));
+    }
+    std::atomic<int> ready{0};
+    std::atomic<bool> go{false}, stop{false};
+    std::vector<uint64_t> cnt(nthreads * 8, 0), wcnt(nthreads * 8, 0);
+    std::vector<std::thread> th;
+    for (uint32_t t = 0; t < nthreads; t++) {
+        th.emplace_back([&, t] {
+            pin_to(cpus[t]);
+            Replica<D>* rep = reps[cpu_replica[t]].get();
+            long tok = rep->reg();
+            std::vector<uint32_t> order(nop);
+            for (uint64_t i = 0; i < nop; i++) order[i] = (uint32_t)i;
+            for (uint64_t i = nop; i > 1; i--) {
+                uint64_t j = (uint64_t)(((unsigned __int128)orc_sm64_at(seed + 1000 + t, nop - i) * i) >> 64);
+                std::swap(order[i - 1], order[j]);
+            }
+            ready.fetch_add(1);
+            while (!go.load()) spin_pause();
+            uint64_t n = 0, w = 0, pos = 0;
+            while (!stop.load(std::memory_order_relaxed)) {
+                for (int b = 0; b < 128; b++) {
+                    w += run(rep, (size_t)tok, order[pos], cpus[t]);
+                    pos = pos + 1 == nop ? 0 : pos + 1;
+                }
+                n += 128;
+            }
+            cnt[t * 8] = n;
+            wcnt[t * 8] = w;
+            rep->sync((size_t)tok);
+        });
+    }
+    while (ready.load() < (int)nthreads) std::this_thread::yield();
+    auto t0 = std::chrono::steady_clock::now();
+    go.store(true);
+    std::this_thread::sleep_for(std::chrono::duration<double>(duration_s));
+    stop.store(true);
+    auto t1 = std::chrono::steady_clock::now();
+    for (auto& x : th) x.join();
+    uint64_t tot = 0, wt = 0;
+    for (uint32_t t = 0; t < nthreads; t++) {
+        tot += cnt[t * 8];
+        wt += wcnt[t * 8];
+    }
+    *seconds = std::chrono::duration<double>(t1 - t0).count();
+    *ops = tot;
+    *writes = wt;
+    for (auto& d : ds) fini(d);
+}
+
 }  // namespace nrcpu
 
 using namespace nrcpu;
@@ -618,96 +773,104 @@ int orc_nr_hashmap_bench(uint32_t nreplicas, const int* cpus, const uint32_t* cp
                          uint64_t key_space, uint64_t prefill, uint64_t nop, uint64_t seed,
                          uint64_t log_bytes, BenchResult* out) {
     if (nreplicas == 0 || nthreads == 0) return -1;
-    Log<HmOp> log(log_bytes ? log_bytes : DEFAULT_LOG_BYTES);
-    std::vector<HashMapD> ds(nreplicas);
-    std::vector<std::unique_ptr<Replica<HashMapD>>> reps;
-    // Each replica's D is built by a thread pinned to the replica's first core so that its
-    // memory is node-local (benches/mkbench.rs:611-629).
-    for (uint32_t r = 0; r < nreplicas; r++) {
-        int cpu = -1;
-        for (uint32_t t = 0; t < nthreads; t++)
-            if (cpu_replica[t] == r) { cpu = cpus[t]; break; }
-        std::thread b([&, r, cpu] {
-            if (cpu >= 0) {
-                cpu_set_t set;
-                CPU_ZERO(&set);
-                CPU_SET(cpu, &set);
-                pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
-            }
-            ds[r].m = orc_hm_new(prefill);
-            orc_hm_prefill_range(ds[r].m, prefill, 1);
-        });
-        b.join();
-        reps.emplace_back(new Replica<HashMapD>(&log, &ds[r]));
-    }
     std::vector<uint8_t> isput(nop);
     std::vector<uint64_t> keys(nop), vals(nop);
     orc_gen_hashmap_ops(isput.data(), keys.data(), vals.data(), nop, seed, key_space, write_ratio);
-
-    std::atomic<int> ready{0};
-    std::atomic<bool> go{false}, stop{false};
-    std::vector<uint64_t> cnt(nthreads * 8, 0), wcnt(nthreads * 8, 0);
-    std::vector<std::thread> th;
-    for (uint32_t t = 0; t < nthreads; t++) {
-        th.emplace_back([&, t] {
-            int cpu = cpus[t];
-            if (cpu >= 0) {
-                cpu_set_t set;
-                CPU_ZERO(&set);
-                CPU_SET(cpu, &set);
-                pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+    volatile uint64_t sink = 0;
+    scale_out<HashMapD>(
+        nreplicas, cpus, cpu_replica, nthreads, duration_s, nop, seed, log_bytes,
+        [&](HashMapD& d) {
+            d.m = orc_hm_new(prefill);
+            orc_hm_prefill_range(d.m, prefill, 1);
+        },
+        [&](Replica<HashMapD>* rep, size_t tok, uint32_t i, int) -> uint64_t {
+            if (isput[i]) {  // benches/hashmap.rs:226-259
+                sink += rep->execute_mut(HmOp{keys[i], vals[i]}, tok).some;
+                return 1;
             }
-            Replica<HashMapD>* rep = reps[cpu_replica[t]].get();
-            long tok = rep->reg();
-            // each thread shuffles its own copy (benches/mkbench.rs:705-706)
-            std::vector<uint32_t> order(nop);
-            for (uint64_t i = 0; i < nop; i++) order[i] = (uint32_t)i;
-            for (uint64_t i = nop; i > 1; i--) {
-                uint64_t j = (uint64_t)(((unsigned __int128)orc_sm64_at(seed + 1000 + t, nop - i) * i) >> 64);
-                std::swap(order[i - 1], order[j]);
-            }
-            ready.fetch_add(1);
-            while (!go.load()) spin_pause();
-            uint64_t n = 0, w = 0, pos = 0;
-            volatile uint64_t sink = 0;
-            while (!stop.load(std::memory_order_relaxed)) {
-                for (int b = 0; b < 128; b++) {  // 128 ops per clock check (mkbench.rs:737-773)
-                    uint32_t i = order[pos];
-                    pos = pos + 1 == nop ? 0 : pos + 1;
-                    if (isput[i]) {
-                        sink += rep->execute_mut(HmOp{keys[i], vals[i]}, (size_t)tok).some;
-                        w++;
-                    } else {
-                        sink += rep->execute(keys[i], (size_t)tok).val;
-                    }
-                }
-                n += 128;
-            }
-            (void)sink;
-            cnt[t * 8] = n;
-            wcnt[t * 8] = w;
-            // keep combining so finished replicas do not starve others' GC (mkbench.rs:799-821)
-            rep->sync((size_t)tok);
-        });
-    }
-    while (ready.load() < (int)nthreads) std::this_thread::yield();
-    auto t0 = std::chrono::steady_clock::now();
-    go.store(true);
-    std::this_thread::sleep_for(std::chrono::duration<double>(duration_s));
-    stop.store(true);
-    auto t1 = std::chrono::steady_clock::now();
-    for (auto& x : th) x.join();
-    uint64_t tot = 0, wt = 0;
-    for (uint32_t t = 0; t < nthreads; t++) {
-        tot += cnt[t * 8];
-        wt += wcnt[t * 8];
-    }
-    out->seconds = std::chrono::duration<double>(t1 - t0).count();
-    out->ops = tot;
-    out->writes = wt;
-    out->reads = tot - wt;
-    for (auto& d : ds) orc_hm_free(d.m);
+            sink += rep->execute(keys[i], tok).val;
+            return 0;
+        },
+        [](HashMapD& d) { orc_hm_free(d.m); }, &out->seconds, &out->ops, &out->writes);
+    out->reads = out->ops - out->writes;
     return 0;
+}
+
+// Stack scale-out (benches/stack.rs:115-134): every op an execute_mut of Push/Pop from the
+// shared stream (orc_gen_stack_ops, 50/50), Stack::default (0..50000) per replica.
+int orc_nr_stack_bench(uint32_t nreplicas, const int* cpus, const uint32_t* cpu_replica, uint32_t nthreads,
+                       double duration_s, uint64_t nop, uint64_t seed, uint64_t log_bytes, BenchResult* out) {
+    if (nreplicas == 0 || nthreads == 0) return -1;
+    std::vector<uint32_t> v(nop), o(nop);
+    orc_gen_stack_ops(v.data(), o.data(), nop, seed);
+    std::vector<uint64_t> ops(nop);
+    for (uint64_t i = 0; i < nop; i++) ops[i] = ((uint64_t)(o[i] & 1) << 32) | v[i];
+    volatile uint64_t sink = 0;
+    scale_out<StackD>(
+        nreplicas, cpus, cpu_replica, nthreads, duration_s, nop, seed, log_bytes,
+        [](StackD& d) {
+            d.storage.reserve(1 << 20);
+            for (uint32_t e = 0; e < 50000; e++) d.storage.push_back(e);
+        },
+        [&](Replica<StackD>* rep, size_t tok, uint32_t i, int) -> uint64_t {
+            sink += rep->execute_mut(ops[i], tok);
+            return 1;
+        },
+        [](StackD&) {}, &out->seconds, &out->ops, &out->writes);
+    out->reads = 0;
+    return 0;
+}
+
+// Synthetic scale-out (benches/synthetic.rs:296-335): ReadWrite ops only
+// (generate_operations(NOP, 0, false, false, true)), tid set to the issuing thread's core id
+// (o.set_tid(cid)), r1/r2 from the seeded stream.
+int orc_nr_synth_bench(uint32_t nreplicas, const int* cpus, const uint32_t* cpu_replica, uint32_t nthreads,
+                       double duration_s, uint64_t nop, uint64_t seed, uint64_t log_bytes, BenchResult* out) {
+    if (nreplicas == 0 || nthreads == 0) return -1;
+    std::vector<uint64_t> raw(2 * nop);
+    orc_gen_raw(raw.data(), 2 * nop, seed);
+    volatile uint64_t sink = 0;
+    scale_out<SynthD>(
+        nreplicas, cpus, cpu_replica, nthreads, duration_s, nop, seed, log_bytes, [](SynthD& d) { d.init(); },
+        [&](Replica<SynthD>* rep, size_t tok, uint32_t i, int cpu) -> uint64_t {
+            SyOp o{(uint64_t)(cpu < 0 ? 0 : cpu), raw[2 * i], raw[2 * i + 1], 1};
+            sink += rep->execute_mut(o, tok);
+            return 1;
+        },
+        [](SynthD&) {}, &out->seconds, &out->ops, &out->writes);
+    out->reads = 0;
+    return 0;
+}
+
+// Parity hooks for the two D's above (tests/test_control_plane.py): one thread replays a
+// given op stream through Replica<D> (append + exec + responses) and returns every response
+// and the final state, to be compared with the sequential oracle.
+uint64_t orc_nr_stack_run(const uint32_t* init, uint64_t ninit, const uint32_t* vals, const uint32_t* kinds,
+                          uint64_t n, uint64_t* resp, uint32_t* final_out, uint64_t cap) {
+    Log<uint64_t> log(2 * 1024 * 1024);
+    StackD d;
+    d.storage.assign(init, init + ninit);
+    Replica<StackD> rep(&log, &d);
+    long tok = rep.reg();
+    for (uint64_t i = 0; i < n; i++) resp[i] = rep.execute_mut(((uint64_t)(kinds[i] & 1) << 32) | vals[i], (size_t)tok);
+    rep.sync((size_t)tok);
+    uint64_t len = d.storage.size();
+    for (uint64_t i = 0; i < len && i < cap; i++) final_out[i] = d.storage[i];
+    return len;
+}
+
+void orc_nr_synth_run(const uint64_t* ops4, uint64_t n, const uint64_t* reads3, uint64_t nr, uint64_t* resp,
+                      uint64_t* rresp, uint64_t* final_out) {
+    Log<SyOp> log(2 * 1024 * 1024);
+    SynthD d;
+    d.init();
+    Replica<SynthD> rep(&log, &d);
+    long tok = rep.reg();
+    for (uint64_t i = 0; i < n; i++)
+        resp[i] = rep.execute_mut(SyOp{ops4[4 * i], ops4[4 * i + 1], ops4[4 * i + 2], ops4[4 * i + 3]}, (size_t)tok);
+    for (uint64_t i = 0; i < nr; i++)
+        rresp[i] = rep.execute(SyOp{reads3[3 * i], reads3[3 * i + 1], reads3[3 * i + 2], 0}, (size_t)tok);
+    for (uint64_t i = 0; i < d.n; i++) final_out[i] = d.storage[i].v;
 }
 
 }  // extern "C"

@@ -106,6 +106,12 @@ def lib():
             "orc_nr_hashmap_bench": (C.c_int, [C.c_uint32, C.POINTER(C.c_int), u32p, C.c_uint32, C.c_double,
                                                 C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
                                                 C.c_uint64, C.c_void_p]),
+            "orc_nr_stack_bench": (C.c_int, [C.c_uint32, C.POINTER(C.c_int), u32p, C.c_uint32, C.c_double,
+                                              C.c_uint64, C.c_uint64, C.c_uint64, C.c_void_p]),
+            "orc_nr_synth_bench": (C.c_int, [C.c_uint32, C.POINTER(C.c_int), u32p, C.c_uint32, C.c_double,
+                                              C.c_uint64, C.c_uint64, C.c_uint64, C.c_void_p]),
+            "orc_nr_stack_run": (C.c_uint64, [u32p, C.c_uint64, u32p, u32p, C.c_uint64, u64p, u32p, C.c_uint64]),
+            "orc_nr_synth_run": (None, [u64p, C.c_uint64, u64p, C.c_uint64, u64p, u64p, u64p]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -306,3 +312,52 @@ def nr_hashmap_bench(cpus, cpu_replica, duration_s, write_ratio, key_space, pref
     if rc != 0:
         raise RuntimeError("orc_nr_hashmap_bench failed")
     return res
+
+
+def _scale_out(fn, cpus, cpu_replica, duration_s, *args):
+    n = len(cpus)
+    ca = (C.c_int * n)(*cpus)
+    ra = (C.c_uint32 * n)(*cpu_replica)
+    res = BenchResult()
+    rc = getattr(lib(), fn)(max(cpu_replica) + 1, ca, ra, n, duration_s, *args, C.byref(res))
+    if rc != 0:
+        raise RuntimeError(fn + " failed")
+    return res
+
+
+def nr_stack_bench(cpus, cpu_replica, duration_s, nop, seed, log_bytes=32 << 20):
+    """Stack scale-out through the C++ restatement of nr (benches/stack.rs:115-134)."""
+    return _scale_out("orc_nr_stack_bench", cpus, cpu_replica, duration_s, nop, seed, log_bytes)
+
+
+def nr_synth_bench(cpus, cpu_replica, duration_s, nop, seed, log_bytes=32 << 20):
+    """Synthetic scale-out through the C++ restatement of nr (benches/synthetic.rs:296-335)."""
+    return _scale_out("orc_nr_synth_bench", cpus, cpu_replica, duration_s, nop, seed, log_bytes)
+
+
+def nr_stack_run(init, vals, kinds):
+    """One thread's execute_mut stream through Replica<Stack> of the nr restatement: returns
+    (responses as Option<u32> with bit 32 = Some, final storage)."""
+    init = np.ascontiguousarray(init, np.uint32)
+    vals = np.ascontiguousarray(vals, np.uint32)
+    kinds = np.ascontiguousarray(kinds, np.uint32)
+    n = vals.shape[0]
+    resp = np.zeros(n, np.uint64)
+    cap = init.shape[0] + n
+    fin = np.zeros(max(cap, 1), np.uint32)
+    ln = lib().orc_nr_stack_run(_p(init, u32p), init.shape[0], _p(vals, u32p), _p(kinds, u32p), n,
+                                _p(resp, u64p), _p(fin, u32p), cap)
+    return resp, fin[:ln]
+
+
+def nr_synth_run(ops4, reads3):
+    """One thread's execute_mut stream then execute reads through Replica<AbstractDataStructure>
+    of the nr restatement: (write responses, read responses, final storage)."""
+    ops4 = np.ascontiguousarray(ops4, np.uint64)
+    reads3 = np.ascontiguousarray(reads3, np.uint64).reshape(-1, 3)
+    resp = np.zeros(ops4.shape[0], np.uint64)
+    rresp = np.zeros(max(reads3.shape[0], 1), np.uint64)
+    fin = np.zeros(200_000, np.uint64)
+    lib().orc_nr_synth_run(_p(ops4, u64p), ops4.shape[0], _p(reads3, u64p), reads3.shape[0], _p(resp, u64p),
+                           _p(rresp, u64p), _p(fin, u64p))
+    return resp, rresp[:reads3.shape[0]], fin

@@ -119,3 +119,12 @@ def test_amdahl_model(bench):
     assert bench.amdahl_speedup(1, 10) == pytest.approx(1.0)
     assert bench.amdahl_speedup(8, 10) == pytest.approx(8 * 1.1 / 2.5)
     assert bench.amdahl_speedup(8, 100) == pytest.approx(1.0)
+
+
+def test_stack_and_synth_cpu_baselines_go_through_nr(bench):
+    """the stack and synthetic lines' cpu_baseline is the nr restatement (log + flat
+    combining, one replica per NUMA node), with the sequential oracle only as a labelled point."""
+    for out in (bench.stack_cpu_baseline(0.3, 20_000, 50_000), bench.synth_cpu_baseline(0.3, 20_000)):
+        json.dumps(out)
+        assert out["kind"] == "port" and out["value"] > 0 and "restatement of nr" in out["sample"]
+        assert out["one_thread_nr"]["cores"] == 1 and out["one_thread_sequential"]["value"] > 0

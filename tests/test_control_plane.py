@@ -589,3 +589,46 @@ def test_replica_execute_not_synced(orc):
     r.L.orc_rep_log_append_exec(r.h, ops.ctypes.data_as(C.POINTER(C.c_uint64)), 2, 2)
     t1 = r.register()
     assert int(r.L.orc_rep_execute(r.h, 11, t1)) == 2
+
+
+# ---- the Stack and AbstractDataStructure plugged into the nr restatement (bench.py's CPU
+# baselines for the stack and synthetic lines, benches/stack.rs:115-134,
+# benches/synthetic.rs:296-335): one thread's stream through Replica<D> must give exactly the
+# sequential oracle's responses and final state ---------------------------------------------
+def test_nr_stack_replica_matches_oracle(orc):
+    import numpy as np
+
+    vals, kinds = orc.gen_stack_ops(20_000, 0xAB)
+    kinds = kinds.copy()
+    kinds[:3000] = 0  # drain past empty: Pop on an empty Vec is None
+    init = np.arange(1000, dtype=np.uint32)
+    resp, fin = orc.nr_stack_run(init, vals, kinds)
+    st = orc.Stack(init)
+    r_o, s_o = st.replay(vals, kinds)
+    assert np.array_equal((resp >> 32).astype(np.uint8), s_o)
+    assert np.array_equal((resp & 0xFFFFFFFF).astype(np.uint32)[s_o == 1], r_o[s_o == 1])
+    assert np.array_equal(fin, st.dump()[:len(st)])
+
+
+def test_nr_synth_replica_matches_oracle(orc):
+    import numpy as np
+
+    n = 6000
+    raw = orc.gen_raw(3 * n, 0x77)
+    ops = np.stack([raw[0::3] % 64, raw[1::3], raw[2::3], (raw[0::3] >> 40) & 1], axis=1).astype(np.uint64)
+    ops[:50, 2] = np.uint64(2**64 - 1)  # r2 + hot_writes wraps: the hot loop is empty
+    reads = np.stack([raw[1::3][:500] % 64, raw[2::3][:500], raw[0::3][:500]], axis=1).astype(np.uint64)
+    resp, rresp, fin = orc.nr_synth_run(ops, reads)
+    sy = orc.Synthetic()
+    assert np.array_equal(resp, sy.replay(ops))
+    assert np.array_equal(rresp, sy.read(reads))
+    assert np.array_equal(fin, sy.dump())
+
+
+def test_nr_stack_and_synth_scale_out_run(orc):
+    import os
+
+    cpus = sorted(os.sched_getaffinity(0))[:2]
+    for fn in (orc.nr_stack_bench, orc.nr_synth_bench):
+        r = fn(cpus, [0] * len(cpus), 0.2, 10_000, 0x5A)
+        assert r.ops > 0 and r.writes == r.ops and r.seconds > 0.1
