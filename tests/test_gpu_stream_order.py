@@ -122,8 +122,14 @@ def test_hashmap_round_ordered_after_torch_fill(nrg, orc):
 
 
 def test_unordered_call_does_race(nrg, orc):
-    """Control: the same sleep + sentinel fill around a RAW C-ABI call (no ordering) leaves the
-    sentinel on top of the round's responses -- the race the helpers close is real on this stack."""
+    """NON-GATING DIAGNOSTIC (not coverage): the same sleep + sentinel fill around a RAW C-ABI
+    call (no ordering) leaves the sentinel on top of the round's responses when the replica's
+    stream and torch's run on different hardware queues -- the race the helpers close. The
+    process has GPU_MAX_HW_QUEUES = 4 hardware queues, so once it has created more streams than
+    that (earlier tests in the same run), HIP may map the replica's stream onto the queue of
+    torch's, where the two are serialised in enqueue order and no race can happen; the control
+    then skips. The gating tests above do not depend on the race showing: they check bit-exact
+    responses with the sentinel fill enqueued before the round either way."""
     import ctypes as C
 
     import torch
@@ -146,4 +152,4 @@ def test_unordered_call_does_race(nrg, orc):
     left = int(np.count_nonzero(some.cpu().numpy() == 7))
     dev.close()
     if left == 0:
-        pytest.skip("the unordered call happened to run after the fill on this box")
+        pytest.skip("non-gating diagnostic: the unordered call ran after the fill (streams sharing a hardware queue)")
