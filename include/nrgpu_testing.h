@@ -47,6 +47,9 @@ int nrg_test_debug_read(nrg_ctx* ctx, uint64_t* out, uint64_t words);
                                   apply, no index, no reads) -- measurement only                   */
 #define NRG_KNOB_SY_SORT 7     /* synthetic: 1 = sort-based replay instead of the bucket path      */
 #define NRG_KNOB_PIPELINE 8    /* overrides nrg_config.pipeline                                    */
+#define NRG_KNOB_SY_FUSED 18   /* synthetic bucket path: 1 (default) = one launch per round (chunk e's
+                                  partition, e-1's bucket pass and e-2's sums side by side), 0 = two
+                                  launches (partition + previous sums, then the bucket pass)       */
 #define NRG_KNOB_COMB_SPIN 10   /* combiner (read by nrg_combiner_open): client threads that may spin
                                    while their round runs (default: max_threads - 1 when every
                                    client fits the CPUs the process may use, else 0 -- parked on

@@ -75,10 +75,11 @@ struct StDeferred {
     uint8_t* some = nullptr;
 };
 
-// A synthetic chunk whose per-op sums and hot-word fold have not run yet (synthetic.hip).
+// A synthetic chunk whose bucket pass or per-op sums and hot-word fold have not run yet
+// (synthetic.hip); its scratch slots follow from its epoch.
 struct SyDeferred {
     bool valid = false;
-    u32 par = 0;
+    u32 epoch = 0;
     u64 lo = 0, n = 0;
     u32 ntiles = 0, want = 0, t0 = 0, t1 = 1;
     u64 rlo = 0, rhi = 0;
@@ -123,9 +124,10 @@ struct nrg_ctx {
     nrg::HmDeferred pend;
     nrg::StDeferred st_pend;  // stack: the last chunk's finish, if deferred
     uint32_t st_par = 0;      // stack: buffer parity of the next chunk
-    nrg::SyDeferred sy_pend;  // synthetic: the last chunk's sums, if deferred
-    uint32_t sy_par = 0;      // synthetic: buffer parity of the next chunk
-    uint32_t sy_round = 0;    // synthetic: chunks replayed (the epoch of the 32-bit seen-value test)
+    nrg::SyDeferred sy_pend;    // synthetic: the chunk whose sums are deferred, if any
+    nrg::SyDeferred sy_pend_b;  // synthetic, one launch per round: the chunk whose bucket pass is deferred
+    bool sy_fused = true;       // synthetic: one launch per round, chunks three deep (NRG_KNOB_SY_FUSED)
+    uint32_t sy_round = 0;      // synthetic: chunks replayed (the chunk epoch: scratch slots, 32-bit seen values)
     int32_t comb_spin = -1;   // combiner knobs (NRG_KNOB_COMB_SPIN / _DEPTH): -1 / 0 = defaults
     uint64_t small_max = 0;   // hashmap: rounds of <= small_max Puts take the one-launch small round
     uint32_t comb_depth = 0;

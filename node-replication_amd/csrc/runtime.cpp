@@ -1206,6 +1206,10 @@ extern "C" int nrg_test_set_knob(nrg_ctx* c, int knob, uint64_t v) {
             if (v < 1 || v > 4) return NRG_E_INVAL;
             c->comb_depth = (uint32_t)v;
             return NRG_OK;
+        case NRG_KNOB_SY_FUSED:
+            if (!sy || v > 1) return NRG_E_INVAL;
+            c->sy_fused = v != 0;
+            return NRG_OK;
         case NRG_KNOB_PIPELINE:
             if (v > 1) return NRG_E_INVAL;
             c->pipeline = v != 0;

@@ -271,7 +271,6 @@ constexpr u32 SY_B0_PARTS = NRG_SY_B0_PARTS;
 #endif
 constexpr int SYP_PD = NRG_SYP_PD;
 constexpr int SYB_TPB = 512, SYB_WAVES = SYB_TPB / 64, SYB_PER = NRG_SYB_PER;
-constexpr u32 SYB_PASS = SYB_TPB * SYB_PER;  // touches per pass of a bucket workgroup
 constexpr int SYC_TPB = 512;
 #ifndef NRG_SYS_T
 // tiles per sum workgroup (A/B builds). With 1 the 489 sum workgroups of a 1M-op chunk queue
@@ -373,14 +372,14 @@ __device__ __forceinline__ u32 wave_rank_mask(bool on, u32 key, int lane, u64* m
 // a SET's value plus fewer than 2^31 touches). The bucket pass then stores 4-B seen values (half
 // the V traffic of the bucket pass and of the sums). Device-side, per chunk epoch e:
 //   big[e & 1] = e   written by any bucket workgroup whose words end chunk e with a value >= 2^31
-//   set_epoch = e    written by any partition tile holding such a WriteOnly
-//   v32[par]         the bucket pass's decision, read by the chunk's sums
-// Every bucket workgroup decides alike: v32 = big[(e-1) & 1] != e-1 && set_epoch != e.
+//   set_epoch[e & 1] = e   written by any partition tile holding such a WriteOnly
+//   v32[slot]        the bucket pass's decision, read by the chunk's sums
+// Every bucket workgroup decides alike: v32 = big[(e-1) & 1] != e-1 && set_epoch[e & 1] != e.
 struct SyFlags {
     u32 big[2];
-    u32 set_epoch;
+    u32 set_epoch[2];  // by epoch parity: chunk e's partition and chunk e-1's bucket pass may share a launch
     u32 v32[2];
-    u32 wo_epoch;  // = e: chunk e holds a WriteOnly (bucket 0 then runs in one workgroup)
+    u32 wo_epoch[2];  // [e & 1] = e: chunk e holds a WriteOnly (bucket 0 then runs in one workgroup)
 };
 
 // Arguments of the partition pass of chunk e and of the sums of chunk e-1, which share a launch.
@@ -487,8 +486,8 @@ __device__ __forceinline__ void sy_part_role(const SyPartArgs& A, u32 tile, SyPa
                                    : ring[(lo + op0 + opw + (orr + SYP_PD) * 64) & ring_mask];
         if (src && valid) st_op(&ring[(lo + op0 + opw + orr * 64) & ring_mask], o, A.plain);
         const bool set = valid && o.op == NRG_SYNTH_WRITE_ONLY;
-        if (set && (o.tid >> 31)) A.fl->set_epoch = A.epoch;  // this chunk's seen values may pass 2^32
-        if (set) A.fl->wo_epoch = A.epoch;                     // this chunk holds a WriteOnly
+        if (set && (o.tid >> 31)) A.fl->set_epoch[A.epoch & 1] = A.epoch;  // this chunk's seen values may pass 2^32
+        if (set) A.fl->wo_epoch[A.epoch & 1] = A.epoch;                    // this chunk holds a WriteOnly
         // hot touches (r2 + j) % HR, j < HW, skipped when r2 + HW wraps; ordered (lane, j)
         const bool hot_ok = valid && (o.r2 + HW >= o.r2);
         const u32 h0 = hot_ok ? (u32)mod_recip(o.r2, HR, hr_m) : 0u;
@@ -635,18 +634,59 @@ __device__ __forceinline__ void sy_part_role(const SyPartArgs& A, u32 tile, SyPa
 #ifndef NRG_SYB_WPE
 #define NRG_SYB_WPE 4  // waves per SIMD the bucket pass is compiled for (4: 128 VGPRs, two workgroups per CU)
 #endif
-__global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(NRG_SYB_WPE))) void sy_bucket_kernel(const u16* __restrict__ Ew, const u16* __restrict__ Eo, const u32* __restrict__ cnt_tb,
-                                                            u32 NB, u32 ntiles, u32 tile_entries, u64* __restrict__ V,
-                                                            u64* __restrict__ words, u64 N, u32 HR, u32 W,
-                                                            const nrg_synth_op* __restrict__ ring, u64 ring_mask, u64 lo,
-                                                            SyFlags* __restrict__ fl, u32 epoch, u32 par,
-                                                            u64* __restrict__ dbg, u32 stall, bool plain) {
+// Arguments of the bucket pass of one chunk.
+struct SyBucketArgs {
+    const u16* Ew;
+    const u16* Eo;
+    const u32* cnt_tb;
+    u32 NB, ntiles, tile_entries;
+    u64* V;
+    u64* words;
+    u64 N;
+    u32 HR, W;
+    const nrg_synth_op* ring;
+    u64 ring_mask, lo;
+    SyFlags* fl;
+    u32 epoch, vslot;  // the chunk's epoch; its seen values' slot (SyFlags::v32[vslot])
+    u64* dbg;
+    u32 stall;
+    bool plain;
+};
+// LDS of a bucket workgroup; its dynamic part (s_pre[ntiles + 1], s_off[ntiles] u16) follows
+template <int PER>
+struct SyBucketLds {
+    u64 cur[SYB_WORDS];
+    u32 wc[SYB_WAVES][SYB_WORDS];
+    u64 mk[SYB_WORDS];  // peer masks of the passes with a WriteOnly (one wave at a time)
+    unsigned short tile[2][SYB_TPB * PER];  // tile of every touch of a pass (double buffered)
+    u32 part[SYB_WAVES];
+    u32 big;  // a word ends the chunk >= 2^31 (SyFlags)
+};
+__host__ __device__ constexpr size_t sy_bucket_dyn_bytes(u32 ntiles) { return (size_t)(ntiles + 1) * 4 + (size_t)ntiles * 2; }
+
+// Workgroup `blk` of the pass's `nblk` (two per CU): its bucket, or a part of bucket 0.
+template <int PER>
+__device__ __forceinline__ void sy_bucket_role(const SyBucketArgs& B, u32 blk, u32 nblk, SyBucketLds<PER>& L, u32* s_dyn) {
+    constexpr u32 SYB_PASS = SYB_TPB * PER;  // touches per pass
+    constexpr int SYB_PER = PER;
+    const u16* __restrict__ Ew = B.Ew;
+    const u16* __restrict__ Eo = B.Eo;
+    const u32* __restrict__ cnt_tb = B.cnt_tb;
+    const u32 NB = B.NB, ntiles = B.ntiles, tile_entries = B.tile_entries, HR = B.HR, W = B.W, epoch = B.epoch;
+    u64* __restrict__ V = B.V;
+    u64* __restrict__ words = B.words;
+    const u64 N = B.N, ring_mask = B.ring_mask, lo = B.lo;
+    const nrg_synth_op* __restrict__ ring = B.ring;
+    SyFlags* __restrict__ fl = B.fl;
+    u64* __restrict__ dbg = B.dbg;
+    const u32 stall = B.stall;
+    const bool plain = B.plain;
     // dbg (NRG_EXP & 2, diagnostic): per block, thread 0's wall clock at the phase edges
     // [0] start [1] prologue loaded [2] scanned, then summed over passes [3] tile map [4] gather
     // [5] rank + place [6] stores, [7] end, [8] passes
     u64 tm_acc[4] = {0, 0, 0, 0}, tm_last = 0;
 #define SY_MARK(K) \
-    if (dbg && threadIdx.x == 0) dbg[(u64)blockIdx.x * 16 + (K)] = tm_last = wall_clock64()
+    if (dbg && threadIdx.x == 0) dbg[(u64)blk * 16 + (K)] = tm_last = wall_clock64()
 #define SY_ACC(K)                                  \
     if (dbg && threadIdx.x == 0) {                 \
         const u64 now_ = wall_clock64();           \
@@ -654,29 +694,28 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(NRG_SYB
         tm_last = now_;                            \
     }
     SY_MARK(0);
-    extern __shared__ u32 s_dyn[];  // s_pre[ntiles + 1], s_off[ntiles] (u16)
-    __shared__ u64 s_cur[SYB_WORDS];
-    __shared__ u32 s_wc[SYB_WAVES][SYB_WORDS];
-    __shared__ u64 s_mk[SYB_WORDS];  // peer masks of the passes with a WriteOnly (one wave at a time)
-    __shared__ unsigned short s_tile[2][SYB_PASS];  // tile of every touch of a pass (double buffered)
-    __shared__ u32 s_part[SYB_WAVES];
-    __shared__ u32 s_big;  // a word ends the chunk >= 2^31 (SyFlags)
+    auto& s_cur = L.cur;
+    auto& s_wc = L.wc;
+    auto& s_mk = L.mk;
+    auto& s_tile = L.tile;
+    auto& s_part = L.part;
+    auto& s_big = L.big;
     u32* s_pre = s_dyn;
     unsigned short* s_off = (unsigned short*)(s_dyn + ntiles + 1);
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     // buckets in contiguous runs per XCD (workgroups go to XCDs round-robin): neighbouring
     // buckets share the lines at their segments' edges in E and V, and those stay in one L2
-    const u32 nxcd = 8, q = gridDim.x / nxcd, rem = gridDim.x % nxcd, xcd = blockIdx.x % nxcd;
-    const u32 v = xcd * q + (xcd < rem ? xcd : rem) + blockIdx.x / nxcd;
-    // v = 0..H: the parts of bucket 0 (H = gridDim.x - NB helpers beside its own workgroup)
-    const u32 H = gridDim.x - NB;
+    const u32 nxcd = 8, q = nblk / nxcd, rem = nblk % nxcd, xcd = blk % nxcd;
+    const u32 v = xcd * q + (xcd < rem ? xcd : rem) + blk / nxcd;
+    // v = 0..H: the parts of bucket 0 (H = nblk - NB helpers beside its own workgroup)
+    const u32 H = nblk - NB;
     const u32 b = v <= H ? 0u : v - H, part = v <= H ? v : 0u;
-    const bool split = b == 0 && H && fl->wo_epoch != epoch;
+    const bool split = b == 0 && H && fl->wo_epoch[epoch & 1] != epoch;
     if (b == 0 && part && !split) return;  // a WriteOnly in the chunk: bucket 0 in one workgroup
     const u64 w0 = b ? (u64)HR + 1 + (u64)(b - 1) * W : (u64)HR;  // bucket 0: cold word 0 alone
     const u32 nw = b ? W : 1u;
     // 4-B seen values this chunk (SyFlags): decided alike by every workgroup
-    const bool v32 = fl->big[(epoch - 1) & 1] != epoch - 1 && fl->set_epoch != epoch;
+    const bool v32 = fl->big[(epoch - 1) & 1] != epoch - 1 && fl->set_epoch[epoch & 1] != epoch;
     for (u32 t = tid; t < ntiles; t += SYB_TPB) {
         // [tile][bucket]: a tile's word for bucket b shares its line with the neighbouring buckets,
         // which run on this XCD (the contiguous runs above), so the line is fetched once per XCD
@@ -756,7 +795,7 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(NRG_SYB
         load_pass(start, s_tile[0]);
     }
     // Software pipelined: the next pass's entries are in flight while this pass is ranked.
-    const u32 late = blockIdx.x >= gridDim.x / 2 ? 1u : 0u;  // the second workgroup on its CU
+    const u32 late = blk >= nblk / 2 ? 1u : 0u;  // the second workgroup on its CU
     for (u32 base = start, pb = 0; base < end; base += SYB_PASS, pb ^= 1) {
         // alternate which of a CU's two workgroups the SIMDs prefer, pass by pass: oldest-first
         // arbitration otherwise favours the first-dispatched one all the way through, and the
@@ -891,17 +930,23 @@ __global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(NRG_SYB
     if (big) s_big = 1u;  // (an LDS flag: __syncthreads_or here kept the thread-id math live and spilled)
     __syncthreads();
     if (s_big && tid == 0) fl->big[epoch & 1] = epoch;
-    if (blockIdx.x == 0 && tid == 0) fl->v32[par] = v32 ? 1u : 0u;
+    if (blk == 0 && tid == 0) fl->v32[B.vslot] = v32 ? 1u : 0u;
     if (dbg && threadIdx.x == 0) {
-        for (int k = 0; k < 4; k++) dbg[(u64)blockIdx.x * 16 + 3 + k] = tm_acc[k];
-        dbg[(u64)blockIdx.x * 16 + 8] = (total + SYB_PASS - 1) / SYB_PASS;
-        dbg[(u64)blockIdx.x * 16 + 9] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
-        dbg[(u64)blockIdx.x * 16 + 10] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
-        dbg[(u64)blockIdx.x * 16 + 11] = total;
+        for (int k = 0; k < 4; k++) dbg[(u64)blk * 16 + 3 + k] = tm_acc[k];
+        dbg[(u64)blk * 16 + 8] = (total + SYB_PASS - 1) / SYB_PASS;
+        dbg[(u64)blk * 16 + 9] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+        dbg[(u64)blk * 16 + 10] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+        dbg[(u64)blk * 16 + 11] = total;
     }
     SY_MARK(7);
 #undef SY_MARK
 #undef SY_ACC
+}
+
+__global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(NRG_SYB_WPE))) void sy_bucket_kernel(SyBucketArgs B) {
+    extern __shared__ u32 s_dyn[];  // s_pre[ntiles + 1], s_off[ntiles] (u16)
+    __shared__ SyBucketLds<SYB_PER> L;
+    sy_bucket_role<SYB_PER>(B, blockIdx.x, gridDim.x, L, s_dyn);
 }
 
 // Per-op sums of chunk S (one workgroup per 2048-op tile of the response window), then, in
@@ -1020,14 +1065,17 @@ bool sy_bucket_eligible(const nrg_config& cf) {
            span <= 1 + (u64)(SY_MAX_NB - SY_B0_PARTS) * SYB_WORDS && cf.max_batch <= (u64)SY_MAX_TILES * SYA_OPS;
 }
 
-// scratch: V (seen values, u64 per touch), then per buffer parity: E (touch entries), the
-// [bucket][tile] counts and the hot summaries; a chunk's sums may run in the next chunk's
-// partition launch, so E and the hot summaries alternate between two parities
+// Scratch: seen values V in two slots (chunk epoch & 1), touch records E in three (epoch % 3:
+// Ew then Eo), [tile][bucket] counts in two (epoch & 1), hot summaries in three (epoch % 3).
+// With one launch per round (NRG_KNOB_SY_FUSED) the partition of chunk e, the bucket pass of
+// e-1 and the sums of e-2 share a launch: E and the hot summaries are live for three chunks,
+// the counts and V for two. (The two-launch round needs two slots of E and one of counts and V.)
 struct SyAux {
-    u64* V;  // u64 seen values, or u32 ones (SyFlags) in the same bytes
-    u32* E[2];
-    u32* cnt;
-    SyHot* hot[2];
+    u64 te;  // touch records per slot
+    u64* V[2];  // u64 seen values, or u32 ones (SyFlags) in the same bytes
+    u32* E[3];
+    u32* cnt[2];
+    SyHot* hot[3];
     SyFlags* fl;
 };
 static u64 sy_nb(const nrg_config& cf) {
@@ -1038,22 +1086,30 @@ static u64 sy_nb(const nrg_config& cf) {
 static SyAux sy_aux(void* base, const nrg_config& cf) {
     const u64 tiles = (cf.max_batch + SYA_OPS - 1) / SYA_OPS;
     const u64 te = tiles * SYA_OPS * cf.synth_cold_writes;
+    const u64 nbt = sy_nb(cf) * tiles, ht = tiles * cf.synth_hot_reads;
     SyAux x;
-    x.V = (u64*)base;
-    x.E[0] = (u32*)(x.V + te);  // per parity: Ew (te u16) then Eo (te u16)
+    x.te = te;
+    x.V[0] = (u64*)base;
+    x.V[1] = x.V[0] + te;
+    x.E[0] = (u32*)(x.V[1] + te);  // per slot: Ew (te u16) then Eo (te u16)
     x.E[1] = x.E[0] + te;
-    x.cnt = x.E[1] + te;
-    x.hot[0] = (SyHot*)(((uintptr_t)(x.cnt + sy_nb(cf) * tiles) + 15) & ~(uintptr_t)15);
-    x.hot[1] = x.hot[0] + tiles * cf.synth_hot_reads;
-    x.fl = (SyFlags*)(((uintptr_t)(x.hot[1] + tiles * cf.synth_hot_reads) + 15) & ~(uintptr_t)15);
+    x.E[2] = x.E[1] + te;
+    x.cnt[0] = x.E[2] + te;
+    x.cnt[1] = x.cnt[0] + nbt;
+    x.hot[0] = (SyHot*)(((uintptr_t)(x.cnt[1] + nbt) + 15) & ~(uintptr_t)15);
+    x.hot[1] = x.hot[0] + ht;
+    x.hot[2] = x.hot[1] + ht;
+    x.fl = (SyFlags*)(((uintptr_t)(x.hot[2] + ht) + 15) & ~(uintptr_t)15);
     return x;
 }
+static u16* sy_ew(const SyAux& x, u32 epoch) { return (u16*)x.E[epoch % 3]; }
+static u16* sy_eo(const SyAux& x, u32 epoch) { return (u16*)x.E[epoch % 3] + x.te; }
 
 u64 sy_bucket_aux_bytes(const nrg_config& cf) {
     const u64 tiles = (cf.max_batch + SYA_OPS - 1) / SYA_OPS;
     const u64 te = tiles * SYA_OPS * cf.synth_cold_writes;
-    return te * (8 + 4 + 4) + sy_nb(cf) * tiles * 4 + 2 * tiles * cf.synth_hot_reads * sizeof(SyHot) + 256 +
-           sizeof(SyFlags) + 16;
+    return te * (2 * 8 + 3 * 4) + 2 * sy_nb(cf) * tiles * 4 + 3 * tiles * cf.synth_hot_reads * sizeof(SyHot) + 256 +
+           sizeof(SyFlags) + 32;
 }
 
 // Fresh scratch: the words may hold anything (sort-path chunks ran before), so the next chunk
@@ -1069,9 +1125,10 @@ static SySumArgs sy_sum_args(nrg_ctx* c, const SyDeferred& d) {
     const nrg_config& cf = c->cfg;
     SyAux x = sy_aux(c->d_sy_aux, cf);
     SySumArgs S{};
+    if (!d.valid) return S;
     S.blocks = (d.t1 - d.t0 + SYS_T - 1) / SYS_T;
-    S.Eo = (const u16*)x.E[d.par] + (x.cnt - x.E[1]);  // Eo: the parity's second half
-    S.V = x.V;
+    S.Eo = sy_eo(x, d.epoch);
+    S.V = x.V[d.epoch & 1];
     S.n = d.n;
     S.lo = d.lo;
     S.resp_lo = d.rlo;
@@ -1081,15 +1138,83 @@ static SySumArgs sy_sum_args(nrg_ctx* c, const SyDeferred& d) {
     S.tile0 = d.t0;
     S.tile1 = d.t1;
     S.want = d.want;
-    S.hot = x.hot[d.par];
+    S.hot = x.hot[d.epoch % 3];
     S.ntiles = d.ntiles;
     S.HR = cf.synth_hot_reads;
     S.CW = cf.synth_cold_writes;
     S.words = c->d_words;
-    S.v32 = &x.fl->v32[d.par];
+    S.v32 = &x.fl->v32[d.epoch & 1];
     S.dbg = (c->exp & 2) ? c->d_dbg : nullptr;
     S.plain = !((c->exp >> 9) & 1);
     return S;
+}
+
+// bucket 0: cold word 0 alone; buckets 1..: W words each (<= 512, sy_bucket_eligible)
+static u32 sy_W(const nrg_config& cf) { return (u32)sy_bucket_words(cf.synth_n - cf.synth_hot_reads); }
+static u32 sy_NB(const nrg_config& cf) {
+    const u64 span = cf.synth_n - cf.synth_hot_reads;
+    const u32 W = sy_W(cf);
+    return 1 + (u32)((span - 1 + W - 1) / W);
+}
+
+static SyBucketArgs sy_bucket_args(nrg_ctx* c, const SyDeferred& d) {
+    const nrg_config& cf = c->cfg;
+    SyAux x = sy_aux(c->d_sy_aux, cf);
+    SyBucketArgs B{};
+    B.Ew = sy_ew(x, d.epoch);
+    B.Eo = sy_eo(x, d.epoch);
+    B.cnt_tb = x.cnt[d.epoch & 1];
+    B.NB = sy_NB(cf);
+    B.ntiles = d.ntiles;
+    B.tile_entries = SYA_OPS * cf.synth_cold_writes;
+    B.V = x.V[d.epoch & 1];
+    B.words = c->d_words;
+    B.N = cf.synth_n;
+    B.HR = cf.synth_hot_reads;
+    B.W = sy_W(cf);
+    B.ring = (const nrg_synth_op*)c->d_ring;
+    B.ring_mask = c->log_size - 1;
+    B.lo = d.lo;
+    B.fl = x.fl;
+    B.epoch = d.epoch;
+    B.vslot = d.epoch & 1;
+    B.dbg = (c->exp & 2) ? c->d_dbg : nullptr;
+    B.stall = c->stall;
+    B.plain = !((c->exp >> 8) & 1);
+    return B;
+}
+
+static SyPartArgs sy_part_args(nrg_ctx* c, u64 lo, u64 n, const nrg_synth_op* src, u32 epoch) {
+    const nrg_config& cf = c->cfg;
+    const u32 HR = cf.synth_hot_reads;
+    const u64 span = cf.synth_n - HR;
+    SyAux x = sy_aux(c->d_sy_aux, cf);
+    SyPartArgs A;
+    A.src = src;
+    A.ring = (nrg_synth_op*)c->d_ring;
+    A.ring_mask = c->log_size - 1;
+    A.lo = lo;
+    A.n = n;
+    A.span = span;
+    A.span_m = ~0ull / span;
+    A.w64 = (u32)((~0ull % span + 1) % span);
+    A.HR = HR;
+    A.hr_m = ~0ull / HR;
+    A.HW = cf.synth_hot_writes;
+    A.NB = sy_NB(cf);
+    A.W = sy_W(cf);
+    A.wm = ((1ull << 40) + A.W - 1) / A.W;
+    A.ntiles = (u32)((n + SYA_OPS - 1) / SYA_OPS);
+    A.Ew = sy_ew(x, epoch);
+    A.Eo = sy_eo(x, epoch);
+    A.cnt_tb = x.cnt[epoch & 1];
+    A.hot = x.hot[epoch % 3];
+    A.fl = x.fl;
+    A.epoch = epoch;
+    A.dbg = (c->exp & 2) ? c->d_dbg : nullptr;
+    A.plain = !((c->exp >> 6) & 1);
+    A.plain_e = !((c->exp >> 7) & 1);
+    return A;
 }
 
 static hipError_t sy_launch_part(nrg_ctx* c, const SyPartArgs& A, const SySumArgs& S) {
@@ -1105,8 +1230,121 @@ static hipError_t sy_launch_part(nrg_ctx* c, const SyPartArgs& A, const SySumArg
     return hipGetLastError();
 }
 
-// The sums (and hot-word fold) of the last replayed chunk, if still pending.
+// One launch per round (NRG_KNOB_SY_FUSED): the partition of chunk e (A), the bucket pass of
+// chunk e-1 (B, when bvalid) and the sums of chunk e-2 (S) in SY_FUSED_WG workgroups, two per CU,
+// all resident at once. Workgroup w takes partition tile w, bucket workgroup w and sum workgroup
+// w (and w + SY_FUSED_WG, ... for larger chunks); the first of a CU's two workgroups partitions
+// first, the second replays its bucket first, so each CU runs one of each side by side (the
+// partition streams records at memory bandwidth, the bucket pass is LDS- and latency-bound),
+// and the sums follow. No role waits on another in the launch: the three chunks share no buffer.
+constexpr u32 SY_FUSED_WG = SY_MAX_NB;  // = the bucket pass's workgroups: 2 per CU on 256 CUs
+#ifndef NRG_SYF_PER
+#define NRG_SYF_PER 10  // bucket-pass touches per thread per pass in the fused kernel
+#endif
+constexpr int SYF_PER = NRG_SYF_PER;
+// The roles read their arguments through a laundered kernarg pointer at their point of use:
+// the compiler cannot then keep the fields of the roles that run later live in registers across
+// the roles that run first (kept live, they pushed the bucket role from 125 VGPRs into scratch).
+// Kernarg layout of sy_round_kernel: A, B, S at their natural alignments, in order.
+constexpr size_t sy_al(size_t x, size_t a) { return (x + a - 1) / a * a; }
+constexpr size_t SY_KA_B = sy_al(sizeof(SyPartArgs), alignof(SyBucketArgs));
+constexpr size_t SY_KA_S = sy_al(SY_KA_B + sizeof(SyBucketArgs), alignof(SySumArgs));
+template <typename T>
+__device__ __forceinline__ const T* sy_karg(size_t off) {
+    const char __attribute__((address_space(4)))* k =
+        (const char __attribute__((address_space(4)))*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(k));
+    return (const T*)(const T __attribute__((address_space(4)))*)(k + off);
+}
+template <int CW>
+__device__ __forceinline__ void sy_round_part(u32 w, unsigned char* s_raw) {
+    const SyPartArgs* a = sy_karg<SyPartArgs>(0);
+    for (u32 t = w; t < a->ntiles; t += SY_FUSED_WG) {
+        sy_part_role<CW>(*a, t, *reinterpret_cast<SyPartLds<CW>*>(s_raw));
+        __syncthreads();
+    }
+}
+template <int CW>
+__global__ __launch_bounds__(SYB_TPB) __attribute__((amdgpu_waves_per_eu(NRG_SYB_WPE))) void sy_round_kernel(
+    SyPartArgs A, SyBucketArgs B, SySumArgs S, u32 nblk_b, u32 part_first_below) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char s_raw[];
+    const u32 w = blockIdx.x;
+    (void)A;
+    (void)B;
+    (void)S;
+    // the CU's first workgroup partitions, then replays its bucket; the second the other way
+    // round (straight-line code: a loop over the two phases had the compiler hoist each role's
+    // lane constants across the other role, and spill)
+    if (w < part_first_below) sy_round_part<CW>(w, s_raw);
+    {
+        const SyBucketArgs* b = sy_karg<SyBucketArgs>(SY_KA_B);
+        // (nblk_b <= SY_MAX_NB = SY_FUSED_WG: at most one bucket workgroup each)
+        if (w < nblk_b) {
+            sy_bucket_role<SYF_PER>(*b, w, nblk_b, *reinterpret_cast<SyBucketLds<SYF_PER>*>(s_raw),
+                                    reinterpret_cast<u32*>(s_raw + ((sizeof(SyBucketLds<SYF_PER>) + 15) & ~(size_t)15)));
+            __syncthreads();
+        }
+    }
+    if (w >= part_first_below) sy_round_part<CW>(w, s_raw);
+    const SySumArgs* sa = sy_karg<SySumArgs>(SY_KA_S);
+    for (u32 k = w; k < sa->blocks; k += SY_FUSED_WG) {
+        sy_sum_role(*sa, k, reinterpret_cast<SyPartLds<CW>*>(s_raw)->u.sum);
+        __syncthreads();
+    }
+}
+
+static hipError_t sy_launch_fused(nrg_ctx* c, const SyPartArgs& A, const SyDeferred& bd, const SySumArgs& S) {
+    const nrg_config& cf = c->cfg;
+    SyBucketArgs B{};
+    u32 nblk_b = 0;
+    size_t dyn_b = 0;
+    if (bd.valid) {
+        B = sy_bucket_args(c, bd);
+        nblk_b = B.NB + SY_B0_PARTS - 1;
+        dyn_b = ((sizeof(SyBucketLds<SYF_PER>) + 15) & ~(size_t)15) + sy_bucket_dyn_bytes(B.ntiles);
+    }
+    hipStream_t st = c->stream;
+    // the first of each CU's two workgroups (0 .. 255, one per CU) partitions first
+    const u32 pfb = SY_FUSED_WG / 2;
+#define SY_FUSED(CWV)                                                                                      \
+    case CWV: {                                                                                            \
+        const size_t dyn = std::max(sizeof(SyPartLds<CWV>), dyn_b);                                        \
+        if (dyn > 65536) {                                                                                 \
+            hipError_t e_ = hipFuncSetAttribute((const void*)sy_round_kernel<CWV>,                         \
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);     \
+            if (e_ != hipSuccess) return e_;                                                               \
+        }                                                                                                  \
+        sy_round_kernel<CWV><<<SY_FUSED_WG, SYB_TPB, dyn, st>>>(A, B, S, nblk_b, pfb);                     \
+        break;                                                                                             \
+    }
+    switch (cf.synth_cold_writes) {
+        SY_FUSED(1); SY_FUSED(2); SY_FUSED(3); SY_FUSED(4); SY_FUSED(5); SY_FUSED(6); SY_FUSED(7); SY_FUSED(8);
+        default: return hipErrorInvalidValue;
+    }
+#undef SY_FUSED
+    return hipGetLastError();
+}
+
+static hipError_t sy_launch_bucket(nrg_ctx* c, const SyDeferred& d) {
+    const SyBucketArgs B = sy_bucket_args(c, d);
+    sy_bucket_kernel<<<B.NB + SY_B0_PARTS - 1, SYB_TPB, sy_bucket_dyn_bytes(B.ntiles), c->stream>>>(B);
+    return hipGetLastError();
+}
+
+// The deferred work of the last replayed chunks, if any: the sums (and hot-word fold) of the
+// last chunk; with one launch per round also the bucket pass of the last chunk, then its sums.
 hipError_t sy_flush(nrg_ctx* c) {
+    if (c->sy_fused) {
+        while (c->sy_pend_b.valid || c->sy_pend.valid) {
+            const SySumArgs S = sy_sum_args(c, c->sy_pend);
+            SyPartArgs A{};
+            hipError_t e = sy_launch_fused(c, A, c->sy_pend_b, S);
+            if (e != hipSuccess) return e;
+            c->sy_pend = c->sy_pend_b;  // its sums next
+            c->sy_pend_b.valid = false;
+        }
+        return hipSuccess;
+    }
     if (!c->sy_pend.valid) return hipSuccess;
     const SySumArgs S = sy_sum_args(c, c->sy_pend);
     c->sy_pend.valid = false;
@@ -1116,60 +1354,14 @@ hipError_t sy_flush(nrg_ctx* c) {
 
 static hipError_t sy_bucket_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 resp_hi, u64* d_resp, uint8_t* d_some,
                                   const nrg_synth_op* src) {
-    hipStream_t st = c->stream;
-    const nrg_config& cf = c->cfg;
-    const u32 HW = cf.synth_hot_writes, CW = cf.synth_cold_writes, HR = cf.synth_hot_reads;
-    const u64 span = cf.synth_n - HR;
-    // bucket 0: cold word 0 alone; buckets 1..: W words each (<= 512, sy_bucket_eligible)
-    const u32 W = (u32)sy_bucket_words(span);
-    const u32 NB = 1 + (u32)((span - 1 + W - 1) / W);
-    const u32 ntiles = (u32)((n + SYA_OPS - 1) / SYA_OPS);
-    SyAux x = sy_aux(c->d_sy_aux, cf);
-    const u32 par = c->sy_par;
-    SyPartArgs A;
-    A.src = src;
-    A.ring = (nrg_synth_op*)c->d_ring;
-    A.ring_mask = c->log_size - 1;
-    A.lo = lo;
-    A.n = n;
-    A.span = span;
-    A.span_m = ~0ull / span;
-    A.w64 = (u32)((~0ull % span + 1) % span);
-    A.HR = HR;
-    A.hr_m = ~0ull / HR;
-    A.HW = HW;
-    A.NB = NB;
-    A.W = W;
-    A.wm = ((1ull << 40) + W - 1) / W;
-    A.ntiles = ntiles;
-    A.Ew = (u16*)x.E[par];
-    A.Eo = (u16*)x.E[par] + (x.cnt - x.E[1]);
-    A.cnt_tb = x.cnt;
-    A.hot = x.hot[par];
-    A.fl = x.fl;
-    A.epoch = ++c->sy_round;
-    A.dbg = (c->exp & 2) ? c->d_dbg : nullptr;
-    A.plain = !((c->exp >> 6) & 1);
-    A.plain_e = !((c->exp >> 7) & 1);
-    SySumArgs S{};
-    if (c->sy_pend.valid) S = sy_sum_args(c, c->sy_pend);
-    c->sy_pend.valid = false;
-    timer_begin(c, "sy_replay");
-    hipError_t e = sy_launch_part(c, A, S);
-    if (e != hipSuccess) return e;
-    const size_t dyn = (size_t)(ntiles + 1) * 4 + (size_t)ntiles * 2;
-    sy_bucket_kernel<<<NB + SY_B0_PARTS - 1, SYB_TPB, dyn, st>>>((const u16*)x.E[par], (const u16*)x.E[par] + (x.cnt - x.E[1]), x.cnt, NB, ntiles, SYA_OPS * CW, x.V, c->d_words, cf.synth_n, HR,
-                                               W, A.ring, A.ring_mask, lo, x.fl, A.epoch, par,
-                                               (c->exp & 2) ? c->d_dbg : nullptr, c->stall, !((c->exp >> 8) & 1));
-    timer_end(c, "sy_replay");
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    // this chunk's sums: in the next chunk's partition launch (pipeline = 1) or now
+    const u32 epoch = ++c->sy_round;
+    const SyPartArgs A = sy_part_args(c, lo, n, src, epoch);
     SyDeferred d;
     d.valid = true;
-    d.par = par;
+    d.epoch = epoch;
     d.lo = lo;
     d.n = n;
-    d.ntiles = ntiles;
+    d.ntiles = A.ntiles;
     d.want = d_resp != nullptr && resp_lo < lo + n && resp_hi > lo;
     d.t0 = 0;
     d.t1 = 1;
@@ -1183,8 +1375,24 @@ static hipError_t sy_bucket_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 re
     d.rhi = resp_hi;
     d.resp = d.want ? d_resp : nullptr;
     d.some = d.want ? d_some : nullptr;
-    c->sy_pend = d;
-    c->sy_par ^= 1;
+    const SySumArgs S = sy_sum_args(c, c->sy_pend);
+    hipError_t e;
+    timer_begin(c, "sy_replay");
+    if (c->sy_fused) {
+        // one launch: this chunk's partition, the last chunk's bucket pass, the one before's sums
+        e = sy_launch_fused(c, A, c->sy_pend_b, S);
+        timer_end(c, "sy_replay");
+        if (e != hipSuccess) return e;
+        c->sy_pend = c->sy_pend_b;
+        c->sy_pend_b = d;
+    } else {
+        // two launches: this chunk's partition beside the last chunk's sums, then its bucket pass
+        e = sy_launch_part(c, A, S);
+        if (e == hipSuccess) e = sy_launch_bucket(c, d);
+        timer_end(c, "sy_replay");
+        if (e != hipSuccess) return e;
+        c->sy_pend = d;
+    }
     return c->pipeline ? hipSuccess : sy_flush(c);
 }
 
@@ -1229,6 +1437,7 @@ hipError_t sy_init(nrg_ctx* c) {
     sy_init_kernel<<<1024, 256, 0, c->stream>>>(c->d_words, c->cfg.synth_n);
     return hipGetLastError();
 }
+
 
 hipError_t sy_replay_chunk(nrg_ctx* c, u64 lo, u64 n, u64 resp_lo, u64 resp_hi, u64* d_resp, uint8_t* d_some,
                            const nrg_synth_op* src) {

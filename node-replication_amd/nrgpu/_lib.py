@@ -198,7 +198,7 @@ TEST_SIGNATURES = {
 # nrg_test_set_knob knobs (include/nrgpu_testing.h): tuning and diagnostics of an open context
 KNOBS = {"STAMP_MAX": 1, "SKEW_EVERY": 2, "EPOCH_LIMIT": 3, "K1": 4, "EXP": 6, "SY_SORT": 7,
          "PIPELINE": 8, "COMB_SPIN": 10, "COMB_DEPTH": 11,
-         "SMALL_MAX": 12, "PART": 13, "STALL": 14, "COMB_GATHER": 15, "PA_TPB": 16, "COMB_SERVE": 17}
+         "SMALL_MAX": 12, "PART": 13, "STALL": 14, "COMB_GATHER": 15, "PA_TPB": 16, "COMB_SERVE": 17, "SY_FUSED": 18}
 
 _lib = None
 

@@ -1,7 +1,8 @@
 """AbstractDataStructure parity (benches/synthetic.rs): HIP replay vs oracle.
 
-Both replay paths are covered: the default sort-free bucket replay and the sort-based one
-(knob NRG_KNOB_SY_SORT = 1, kept for configurations the bucket path does not take).
+Both replay paths are covered: the default sort-free bucket replay (one launch per round, and
+the two-launch form, knob NRG_KNOB_SY_FUSED = 0) and the sort-based one (knob NRG_KNOB_SY_SORT =
+1, kept for configurations the bucket path does not take).
 
 The bench uses ReadWrite only with tid = core id (:296-335); WriteOnly and ReadOnly are
 part of the data structure's Dispatch (:177-195) and are covered too, including the
@@ -25,10 +26,12 @@ def _ops(orc, n, seed, tids, wo_frac):
     return r
 
 
-@pytest.fixture(params=["bucket", "sort"])
+@pytest.fixture(params=["bucket", "bucket2", "sort"])
 def path(request):
-    """the replay path's knobs (nrg_test_set_knob)"""
-    return {"SY_SORT": 1} if request.param == "sort" else {}
+    """the replay path's knobs (nrg_test_set_knob): the bucket path in one launch per round
+    (default: chunk e's partition, e-1's bucket pass and e-2's sums side by side), in two launches
+    per round (SY_FUSED = 0), and the sort path"""
+    return {"sort": {"SY_SORT": 1}, "bucket2": {"SY_FUSED": 0}, "bucket": {}}[request.param]
 
 
 def _check_rounds(nrg, orc, dev, os_, rounds, n, seed, tids, wo, tweak=None):
@@ -168,13 +171,15 @@ def test_synth_round_fused(nrg, orc, path, n, wo, tids):
     np.testing.assert_array_equal(dev.sy_dump(), os_.dump())
 
 
-def test_synth_bench_size_rounds(nrg, orc):
+@pytest.mark.parametrize("fused", [1, 0])
+def test_synth_bench_size_rounds(nrg, orc, fused):
     """The bench's synthetic rounds at full size: 1M ReadWrite ops (tid < 64) against the
     200,000-word storage, every sum and the final storage bit-exact against the oracle."""
     import torch
 
     n = 1_000_000
-    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_SYNTHETIC, 0, max_batch=n, log_bytes=64 * 4 * n)
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_SYNTHETIC, 0, knobs={"SY_FUSED": fused}, max_batch=n,
+                            log_bytes=64 * 4 * n)
     os_ = orc.Synthetic()
     resp = torch.zeros(n, dtype=torch.int64, device="cuda")
     some = torch.zeros(n, dtype=torch.uint8, device="cuda")
@@ -193,27 +198,29 @@ def _heavy(ops):
     ops["r2"][::20] = 0
 
 
+@pytest.mark.parametrize("fused", [1, 0])
 @pytest.mark.parametrize("stall", [0, 1])
 @pytest.mark.parametrize("wo", [0, 40])
-def test_synth_heavy_buckets(nrg, orc, wo, stall):
+def test_synth_heavy_buckets(nrg, orc, wo, stall, fused):
     """Skewed rounds: tid 0 (whose cold touches start at word hot_reads) on 30 % of the ops and
     r2 = 0 (all of an op's cold touches on one word) on 5 %, so a few buckets carry several times
     the mean and take many passes; WriteOnly ops make the values depend on each word's last SET.
     stall = 1 (NRG_KNOB_STALL): odd waves of every bucket workgroup sleep before each pass's value
     stores, which read the pass's tile map while the next-but-one pass rebuilds it."""
     tweak = _heavy
-    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_SYNTHETIC, 0, knobs={"STALL": stall}, max_batch=1 << 18)
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_SYNTHETIC, 0, knobs={"STALL": stall, "SY_FUSED": fused}, max_batch=1 << 18)
     _check_rounds(nrg, orc, dev, orc.Synthetic(), 4, 200_000, 0x4EA + wo, list(range(64)), wo, tweak)
     dev.close()
 
 
-def test_stall_exposes_a_missing_barrier(nrg, orc):
+@pytest.mark.parametrize("fused", [1, 0])
+def test_stall_exposes_a_missing_barrier(nrg, orc, fused):
     """The stall knob makes the race that 2a46f39's barrier closes deterministic: with the barrier
     after each pass's value stores dropped (STALL = 3, diagnostic only) the slow waves store
     through a tile map the fast waves have already rebuilt for a later pass, and the heavy rounds
     come out wrong every time; test_synth_heavy_buckets[stall=1] is the same stall with the
     barrier in place. (Stores the broken map would send outside V are dropped.)"""
-    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_SYNTHETIC, 0, knobs={"STALL": 3}, max_batch=1 << 18)
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_SYNTHETIC, 0, knobs={"STALL": 3, "SY_FUSED": fused}, max_batch=1 << 18)
     os_ = orc.Synthetic()
     ops = _ops(orc, 200_000, 0x4EA, list(range(64)), 0)
     _heavy(ops)
@@ -224,15 +231,18 @@ def test_stall_exposes_a_missing_barrier(nrg, orc):
     dev.close()
 
 
-def test_synth_pipelined_rounds(nrg, orc):
-    """pipeline=1: a chunk's per-op sums and hot-word fold ride in the next chunk's partition
-    launch; every round answers into its own buffers, complete after nrg_join. Then reads
+@pytest.mark.parametrize("fused", [1, 0])
+def test_synth_pipelined_rounds(nrg, orc, fused):
+    """pipeline=1: with one launch per round a chunk's bucket pass rides in the next chunk's launch
+    and its sums in the one after (two launches per round: its sums in the next chunk's
+    partition launch); every round answers into its own buffers, complete after nrg_join. Then reads
     (ReadOnly, which see the folded hot words), a multi-chunk exec and the final storage, all
     against the oracle (benches/synthetic.rs:112-195)."""
     import torch
 
     n = 100_000
-    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_SYNTHETIC, 0, max_batch=1 << 17, log_bytes=64 * 4 * (1 << 19), pipeline=1)
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_SYNTHETIC, 0, knobs={"SY_FUSED": fused}, max_batch=1 << 17,
+                            log_bytes=64 * 4 * (1 << 19), pipeline=1)
     os_ = orc.Synthetic()
     outs = []
     for r in range(4):
