@@ -1304,8 +1304,9 @@ static hipError_t sy_launch_fused(nrg_ctx* c, const SyPartArgs& A, const SyDefer
         dyn_b = ((sizeof(SyBucketLds<SYF_PER>) + 15) & ~(size_t)15) + sy_bucket_dyn_bytes(B.ntiles);
     }
     hipStream_t st = c->stream;
-    // the first of each CU's two workgroups (0 .. 255, one per CU) partitions first
-    const u32 pfb = SY_FUSED_WG / 2;
+    // the first of each CU's two workgroups (0 .. 255, one per CU) partitions first (A/B, NRG_KNOB_EXP
+    // bit 12: every workgroup partitions first; bit 13: every workgroup replays its bucket first)
+    const u32 pfb = (c->exp & 0x1000) ? SY_FUSED_WG : (c->exp & 0x2000) ? 0u : SY_FUSED_WG / 2;
 #define SY_FUSED(CWV)                                                                                      \
     case CWV: {                                                                                            \
         const size_t dyn = std::max(sizeof(SyPartLds<CWV>), dyn_b);                                        \

@@ -28,17 +28,18 @@ def one(pattern):
 
 
 def pmc(path, counter):
-    acc = defaultdict(lambda: [0, 0.0])
+    """per kernel: (launches, MEDIAN value per launch) -- the median, so that the few partial
+    launches of a timed region (its first launch, the join's flush launches) do not pull the
+    per-round figure down"""
+    acc = defaultdict(list)
     if not path:
         return {}
     with open(path) as f:
         for row in csv.DictReader(f):
             if row.get("Counter_Name") != counter:
                 continue
-            a = acc[short(row["Kernel_Name"])]
-            a[0] += 1
-            a[1] += float(row["Counter_Value"])
-    return {k: (n, tot / n) for k, (n, tot) in acc.items()}
+            acc[short(row["Kernel_Name"])].append(float(row["Counter_Value"]))
+    return {k: (len(v), sorted(v)[len(v) // 2]) for k, v in acc.items()}
 
 
 def main():
@@ -90,8 +91,8 @@ def main():
     # finish of chunk e-1) or one synthetic round (sy_part with the previous sums + sy_bucket)
     if tk and tk.startswith("stack"):
         parts = ["st_round_kernel"]
-    elif tk and tk.startswith("synthetic"):
-        parts = ["sy_part_kernel", "sy_bucket_kernel"]
+    elif tk and tk.startswith("synthetic"):  # one launch per round (sy_round), or two
+        parts = ["sy_round_kernel"] if any("sy_round_kernel" in k for k in fetch) else ["sy_part_kernel", "sy_bucket_kernel"]
     else:  # a partition round adds its apply launch
         parts = ["hm_round_kernel"] + (["hm_papply_kernel"] if any("hm_papply" in k for k in fetch) else [])
 
