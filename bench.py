@@ -251,16 +251,21 @@ class Env:
         try:
             if self.world > 1:
                 dist.barrier()
-            if self.opening == "spin":
+            if self.opening in ("spin", "keep"):
                 # wait for the device with the host thread awake (a blocking sync parks it, and the
-                # first calls after the wake-up ran 20-80 us slow), then keep the core busy briefly
+                # first calls after the wake-up ran 20-80 us slow), then keep the core busy briefly.
+                # "keep" (A/B): the device stays busy too, on a ~100-us spin kernel, until just
+                # before the region opens
+                if self.opening == "keep":
+                    torch.cuda._sleep(200_000)
                 ev = torch.cuda.Event()
                 ev.record()
                 while not ev.query():
                     pass
-                t_end = time.perf_counter() + 1e-3
-                while time.perf_counter() < t_end:
-                    pass
+                if self.opening == "spin":
+                    t_end = time.perf_counter() + 1e-3
+                    while time.perf_counter() < t_end:
+                        pass
             torch.cuda.synchronize()
             t = time.perf_counter()
             marks = [t]
@@ -981,7 +986,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-prev-variant", action="store_true")
-    ap.add_argument("--opening", choices=["sync", "spin"], default="spin",
+    ap.add_argument("--opening", choices=["sync", "spin", "keep"], default="spin",
                     help="how the timed region's opening sync waits: polled with the host thread awake, then "
                          "torch.cuda.synchronize (default; profiles/r05_opening_ab.txt), or the plain sync alone")
     ap.add_argument("--no-kernel-timing", action="store_true", help="diagnostic: no HIP events in the timed region")
