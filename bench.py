@@ -540,7 +540,10 @@ def run_hashmap(args, env):
                              else "gloo rehearsal", Wg)
                          if world > 1 and not args.partitioned else "") +
                      ("; key-partitioned: rank p holds the keys with nrg_key_owner(k, %d) == p, Puts and Gets "
-                      "routed to their owners and answers back (RCCL send/recv)" % world if args.partitioned else "")),
+                      "routed to their owners and answers back (RCCL send/recv)%s" % (
+                          world, "; one rank owns every key: partition and route-back are the identity, the "
+                          "replay reads the caller's records and answers into its buffers" if world == 1 else "")
+                      if args.partitioned else "")),
         "baseline_config": "configs[1] (B1)" if (world == 1 and args.write_ratio == 10 and args.dist == "uniform")
         else ("configs[2] (B8 weak scaling)" if args.dist == "uniform" else "configs[3] (Z)"),
         "write_ratio_pct": args.write_ratio,

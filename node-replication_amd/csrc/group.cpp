@@ -123,9 +123,12 @@ struct Member {
     uint64_t cap_p[PT_DEPTH] = {}, cap_k[PT_DEPTH] = {};  // its owner-region capacities (n, n_gets)
     PtPlan plan[PT_DEPTH];
     uint32_t pt_epoch = 0;      // look-back descriptor tag of the last fused partition
-    hipStream_t pstream = nullptr;  // a one-rank group's partitions, beside the replay
+    hipStream_t pstream = nullptr;  // a one-rank group's partitions and route-backs, beside the replay
     hipEvent_t pin_ev = nullptr;    // the replica stream's work up to a post (inputs, older rounds)
+    hipEvent_t rd_ev = nullptr;     // a one-rank group: the replay launch that answered a round's reads
     uint64_t xwords[8] = {};    // this rank's host words of the exchange
+    uint64_t xw1[PT_DEPTH][8] = {};  // a one-rank group: the words of the round of that slot (its
+                                     // "exchange" needs no wait: its counts are its own n, n_gets)
     hipEvent_t pt_ev = nullptr;
     // Round headers and the length exchange (allocated at join, so a round cannot fail on them):
     //   hdr[b]  {n, fingerprint of seg_lens} sent with round b's segment; ghdr[b] every rank's
@@ -192,6 +195,7 @@ int member_init(Member& m, int nranks) {
     GCHK(hipEventCreateWithFlags(&m.pt_ev, hipEventDisableTiming));
     for (int q = 0; q < PT_DEPTH; q++) GCHK(hipEventCreateWithFlags(&m.cnt_ev[q], hipEventDisableTiming));
     GCHK(hipEventCreateWithFlags(&m.pin_ev, hipEventDisableTiming));
+    GCHK(hipEventCreateWithFlags(&m.rd_ev, hipEventDisableTiming));
     GCHK(hipStreamCreateWithFlags(&m.pstream, hipStreamNonBlocking));
     for (int b = 0; b < NBUF; b++) {
         GCHK(hipEventCreateWithFlags(&m.gathered[b], hipEventDisableTiming));
@@ -269,6 +273,7 @@ void member_free(Member& m, const Rccl* R) {
     if (m.pstream) (void)hipStreamSynchronize(m.pstream);
     if (m.pstream) (void)hipStreamDestroy(m.pstream);
     if (m.pin_ev) (void)hipEventDestroy(m.pin_ev);
+    if (m.rd_ev) (void)hipEventDestroy(m.rd_ev);
     if (m.in_ev) (void)hipEventDestroy(m.in_ev);
     if (m.cstream) (void)hipStreamDestroy(m.cstream);
     m = Member{};
@@ -667,6 +672,13 @@ int nrg_group_round_async(nrg_group* g, const nrg_round* rounds, const uint64_t*
 // Everything runs on the replica's stream. Every failure before a round's first send/recv is
 // agreed on by all ranks (the same exchanged words): the round is dropped everywhere and the call
 // that ran its stage A returns the error.
+// A one-rank group owns every key, so its partition is the identity and so is the route-back:
+// the owner's replay reads the caller's records and Get keys and answers straight into the
+// caller's buffers -- no data moves, as a cnr replica with one log appends and replays in place
+// (cnr/src/replica.rs:673-736). NRG_KNOB_EXP bit 16 (measurement) makes a one-rank group move
+// its data like a multi-rank one: partition copy on the side stream, route-back launch.
+static bool pt_ident(const nrg_group* g, const Member& m) { return g->nranks == 1 && !(m.ctx->exp & 0x10000); }
+
 static int pt_post(nrg_group* g, const nrg_round* rounds, uint64_t e) {
     const Rccl* R = g->R;
     const int G = g->nranks, nl = (int)g->m.size();
@@ -709,10 +721,18 @@ static int pt_post(nrg_group* g, const nrg_round* rounds, uint64_t e) {
         w[XW_RP_CAP] = G == 1 ? rp_own : std::min(rv[PR_RPUT].bytes / 16, rp_own);
         w[XW_RK_CAP] = G == 1 ? rk_own : std::min(rv[PR_RKEY].bytes / 8, rk_own);
         w[XW_ERR] = (uint64_t)(-err);
+        for (int q = 0; q < XW_N; q++) m.xw1[sl][q] = w[q];
         // A one-rank group partitions on a side stream, after everything queued on the replica's
         // stream so far (the inputs, the slot's previous round), beside the previous round's
         // replay queued next (with RCCL the partition stays in line: the count exchange must keep
         // its place among the communicator's operations)
+        if (pt_ident(g, m)) {  // nothing to partition (the counts are n, n_gets; the words are xw1)
+            m.xw1[sl][XW_RP_CAP] = m.xw1[sl][XW_RK_CAP] = ~0ull;  // nothing received: no buffer to grow
+            m.pr[sl] = x;
+            m.cap_p[sl] = err ? 0 : n;
+            m.cap_k[sl] = err ? 0 : k;
+            continue;
+        }
         hipStream_t ps = c->stream;
         if (G == 1) {
             ps = m.pstream;
@@ -747,6 +767,7 @@ static int pt_post(nrg_group* g, const nrg_round* rounds, uint64_t e) {
     for (int i = 0; i < nl; i++) {
         Member& m = g->m[i];
         RCHK(nrg::ctx_use_device(m.ctx));
+        if (pt_ident(g, m)) continue;
         if (G > 1)
             GCHK(hipMemcpyAsync(m.h_cnt[sl], m.pp[sl][PP_ALLCNT].p, (uint64_t)G * CW * 8, hipMemcpyDeviceToHost,
                                 m.ctx->stream));
@@ -763,12 +784,22 @@ static int pt_stage_a(nrg_group* g, uint64_t e) {
     const int sl = (int)(e % PT_DEPTH), par = (int)(e & 1);
     const uint64_t CW = 2 * (uint64_t)G + XW_N;
     g->pt_drop[sl] = true;  // until the round's payload has moved
+    // A one-rank group owns every key: its counts are its own n and n_gets and its words are its
+    // own, so the host does not wait for the partition (the replay waits for it on the device).
+    uint64_t H1[2 + XW_N];
     for (int i = 0; i < nl; i++) {
-        RCHK(nrg::ctx_use_device(g->m[i].ctx));
-        RCHK(wait_event(g, g->m[i].cnt_ev[sl], "partitioned count exchange"));
-        if (G == 1) GCHK(hipStreamWaitEvent(g->m[i].ctx->stream, g->m[i].cnt_ev[sl], 0));  // (side stream)
+        Member& m = g->m[i];
+        RCHK(nrg::ctx_use_device(m.ctx));
+        if (G == 1) {
+            if (!pt_ident(g, m)) GCHK(hipStreamWaitEvent(m.ctx->stream, m.cnt_ev[sl], 0));  // (side stream)
+            H1[0] = m.cap_p[sl];
+            H1[1] = m.cap_k[sl];
+            for (int q = 0; q < XW_N; q++) H1[2 + q] = m.xw1[sl][q];
+        } else {
+            RCHK(wait_event(g, m.cnt_ev[sl], "partitioned count exchange"));
+        }
     }
-    const uint64_t* H = g->m[0].h_cnt[sl];  // identical on every rank
+    const uint64_t* H = G == 1 ? H1 : g->m[0].h_cnt[sl];  // identical on every rank
     auto word = [&](int s, uint64_t k) { return H[(size_t)s * CW + 2 * G + k]; };
     for (int s = 0; s < G; s++)
         if (word(s, XW_ERR)) return -(int)word(s, XW_ERR);  // the same answer on every rank
@@ -840,8 +871,16 @@ static int pt_stage_a(nrg_group* g, uint64_t e) {
     }
     g->pt_drop[sl] = false;
     // where member i's replay reads its Puts / Get keys
-    auto rput_of = [&](int i) { return G == 1 ? g->m[i].pp[sl][PP_POUT].p : g->m[i].rv[par][PR_RPUT].p; };
-    auto rkey_of = [&](int i) { return G == 1 ? g->m[i].pp[sl][PP_KOUT].p : g->m[i].rv[par][PR_RKEY].p; };
+    auto rput_of = [&](int i) -> const void* {
+        return pt_ident(g, g->m[i]) ? (const void*)g->m[i].pr[sl].recs
+               : G == 1             ? g->m[i].pp[sl][PP_POUT].p
+                                    : g->m[i].rv[par][PR_RPUT].p;
+    };
+    auto rkey_of = [&](int i) -> const void* {
+        return pt_ident(g, g->m[i]) ? (const void*)g->m[i].pr[sl].get_keys
+               : G == 1             ? g->m[i].pp[sl][PP_KOUT].p
+                                    : g->m[i].rv[par][PR_RKEY].p;
+    };
     if (G > 1) {
         // Puts and Get keys to their owners (own part: a device copy)
         if (R->group_start() != ncclSuccess) return NRG_E_COMM;
@@ -891,8 +930,15 @@ static int pt_stage_a(nrg_group* g, uint64_t e) {
         const uint64_t ring_room = c->log_size > 2 * GC_FROM_HEAD ? c->log_size - GC_FROM_HEAD : GC_FROM_HEAD;
         const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(c->cfg.max_batch, ring_room));
         const nrg_put* rput = (const nrg_put*)rput_of(i);
-        uint64_t* rprev = any_prev ? (uint64_t*)m.rv[par][PR_RPREV].p : nullptr;
-        uint8_t* rprevf = any_prev ? (uint8_t*)m.rv[par][PR_RPREVF].p : nullptr;
+        const bool ident = pt_ident(g, m);
+        const nrg_round& x = m.pr[sl];
+        // (identity: the caller's own answer buffers, and previous values only if it asked)
+        uint64_t* rprev = ident ? (x.resp && x.some ? (uint64_t*)x.resp : nullptr)
+                                : any_prev ? (uint64_t*)m.rv[par][PR_RPREV].p : nullptr;
+        uint8_t* rprevf = ident ? (x.resp && x.some ? x.some : nullptr)
+                                : any_prev ? (uint8_t*)m.rv[par][PR_RPREVF].p : nullptr;
+        uint64_t* rval = ident ? x.get_vals : (uint64_t*)m.rv[par][PR_RVAL].p;
+        uint8_t* rfound = ident ? x.get_found : (uint8_t*)m.rv[par][PR_RFOUND].p;
         uint64_t off = 0;
         do {
             const uint64_t n = std::min(chunk, P.rp - off);
@@ -900,8 +946,7 @@ static int pt_stage_a(nrg_group* g, uint64_t e) {
             if (n || (last && P.rk))
                 RCHK(nrg_hashmap_round_async(c, rput + off, n, (uint32_t)m.rank + 1,
                                              last ? (const uint64_t*)rkey_of(i) : nullptr, last ? P.rk : 0,
-                                             last ? (uint64_t*)m.rv[par][PR_RVAL].p : nullptr,
-                                             last ? (uint8_t*)m.rv[par][PR_RFOUND].p : nullptr,
+                                             last ? rval : nullptr, last ? rfound : nullptr,
                                              rprev ? rprev + off : nullptr, rprevf ? rprevf + off : nullptr));
             off += n;
         } while (off < P.rp);
@@ -965,6 +1010,7 @@ static int pt_stage_b(nrg_group* g, uint64_t e) {
         const nrg_round& x = m.pr[sl];
         nrg_ctx* c = m.ctx;
         const int r = m.rank;
+        if (pt_ident(g, m)) continue;  // the replay answered into the caller's buffers
         RCHK(nrg::ctx_use_device(c));
         const bool mine = x.resp && x.some;
         const uint64_t cp = m.cap_p[sl], ck = m.cap_k[sl];
@@ -987,8 +1033,17 @@ static int pt_stage_b(nrg_group* g, uint64_t e) {
                                     hipMemcpyDeviceToDevice, s));
             }
         }
+        hipStream_t rs = c->stream;
+        if (G == 1 && (c->exp & 0x8000)) {  // NRG_KNOB_EXP bit 15
+            // (A/B) beside the next replay, on the side stream, after everything queued on the
+            // replica's stream so far: the launch that answered this round's reads (the replay of
+            // the round after, or a join) is the last of it
+            rs = m.pstream;
+            GCHK(hipEventRecord(m.rd_ev, c->stream));
+            GCHK(hipStreamWaitEvent(rs, m.rd_ev, 0));
+        }
         const hipError_t he = nrg::pt_route2(
-            c->stream, (const uint64_t*)aval, (const uint8_t*)afound, (const uint32_t*)m.pp[sl][PP_GPOS].p, x.n_gets,
+            rs, (const uint64_t*)aval, (const uint8_t*)afound, (const uint32_t*)m.pp[sl][PP_GPOS].p, x.n_gets,
             x.get_vals, x.get_found, (const uint64_t*)aprev, (const uint8_t*)aprevf,
             (const uint32_t*)m.pp[sl][PP_PPOS].p, mine ? x.n : 0, mine ? (uint64_t*)x.resp : nullptr, mine ? x.some : nullptr);
         if (he != hipSuccess) return hip_rc(he);
@@ -1016,6 +1071,11 @@ static int pt_flush(nrg_group* g) {
         if (g->broken) return g->broken;
         if (r && rc == NRG_OK) rc = r;
     }
+    if (g->nranks == 1)  // a one-rank group's route-backs ran on its side stream: ordered again
+        for (Member& m : g->m) {
+            RCHK(nrg::ctx_use_device(m.ctx));
+            RCHK(order(m, m.pstream, m.ctx->stream));
+        }
     return rc;
 }
 

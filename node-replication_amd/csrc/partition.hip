@@ -325,6 +325,32 @@ __global__ __launch_bounds__(PT_TPB) void pt_route2_kernel(PtRoute a, PtRoute b)
     }
 }
 
+// One owner: the stable partition is the identity (out = in, pos[i] = i, counts = n), a copy at
+// streaming rate instead of a look-back over 8192-record tiles (a one-rank group: 28 -> ~5 us).
+__global__ __launch_bounds__(PT_TPB) void pt_copy1_kernel(const u64* __restrict__ puts, u64 W, u64* __restrict__ pout,
+                                                          u32* __restrict__ ppos, const u64* __restrict__ keys, u64 R,
+                                                          u64* __restrict__ kout, u32* __restrict__ gpos, u64* counts,
+                                                          PtFWords xw) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        counts[0] = W;
+        counts[1] = R;
+#pragma unroll
+        for (u32 k = 0; k < PT_XW_MAX; k++)
+            if (k < xw.n) xw.dst[k] = xw.w[k];
+    }
+    const u64 stride = (u64)gridDim.x * PT_TPB;
+    for (u64 i = blockIdx.x * (u64)PT_TPB + threadIdx.x; i < W + R; i += stride) {
+        if (i < W) {
+            ((pt_u64x2*)pout)[i] = ((const pt_u64x2*)puts)[i];
+            ppos[i] = (u32)i;
+        } else {
+            const u64 j = i - W;
+            kout[j] = keys[j];
+            gpos[j] = (u32)j;
+        }
+    }
+}
+
 hipError_t pt_fused(hipStream_t s, const u64* puts, u64 W, u64 cap_p, u64* pout, u32* ppos, const u64* keys, u64 R,
                     u64 cap_k, u64* kout, u32* gpos, u64* desc, u32 parts, u32 epoch, u64* counts, const u64* xw,
                     u32 nxw) {
@@ -338,6 +364,12 @@ hipError_t pt_fused(hipStream_t s, const u64* puts, u64 W, u64 cap_p, u64* pout,
     for (u32 k = 0; k < nxw; k++) x.w[k] = xw[k];
     x.dst = counts + 2 * parts;
     x.n = nxw;
+    if (parts == 1) {
+        const u64 nb = (W + R + PT_TPB - 1) / PT_TPB;
+        pt_copy1_kernel<<<(unsigned)(nb < 2048 ? (nb ? nb : 1) : 2048), PT_TPB, 0, s>>>(puts, W, pout, ppos, keys, R, kout,
+                                                                                     gpos, counts, x);
+        return hipGetLastError();
+    }
     const u32 blocks = P.tiles + K.tiles;
     pt_fused_kernel<<<blocks ? blocks : 1u, PF_TPB, 0, s>>>(P, K, parts, (u64)(epoch & ((1u << 22) - 1)) << PD_EP, x);
     return hipGetLastError();

@@ -178,14 +178,19 @@ def test_partitioned_rounds_three_partitions_one_gpu(nrg, orc):
         r.close()
 
 
-def test_partitioned_group_round_one_rank(nrg, orc):
-    """nrg_group_partitioned_round through RCCL with one rank (send/recv to itself): the whole
-    routing path of the C ABI, answers and previous values against the NR replay."""
+@pytest.mark.parametrize("move", [0, 1])
+def test_partitioned_group_round_one_rank(nrg, orc, move):
+    """nrg_group_partitioned_round through RCCL with one rank: answers and previous values against
+    the NR replay. A one-rank group owns every key, so by default its partition and route-back are
+    the identity (the replay reads the caller's records and answers into the caller's buffers);
+    move = 1 (NRG_KNOB_EXP bit 16) moves the data as a multi-rank group does (partition copy on the
+    side stream, route-back launch)."""
     import torch
 
     from nrgpu.parallel import PartitionedGroup
 
-    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, log2_slots=17, max_batch=1 << 16, replica_id=1)
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, knobs={"EXP": 0x10000 * move}, log2_slots=17,
+                            max_batch=1 << 16, replica_id=1)
     dev.use_torch_stream()
     dev.hm_prefill_partition(20_000, 1, 0, 1)
     om = orc.HashMap()
@@ -211,6 +216,51 @@ def test_partitioned_group_round_one_rank(nrg, orc):
         ev, ef = om.get_batch(gk)
         np.testing.assert_array_equal(_u64(gv), ev)
         np.testing.assert_array_equal(gf.cpu().numpy(), ef.astype(np.uint8))
+    assert [int(x) for x in dev.hm_digest()] == [int(x) for x in om.digest()]
+    g.close()
+    dev.close()
+
+
+@pytest.mark.parametrize("move", [0, 1])
+def test_partitioned_group_one_rank_pipelined(nrg, orc, move):
+    """One rank, rounds pipelined three calls deep (round_async: call e partitions round e, replays
+    e-1, answers e-2), the caller's buffers distinct per round, then flush: every answer and
+    previous value against the NR replay, in both the identity and the data-moving form."""
+    import torch
+
+    from nrgpu.parallel import PartitionedGroup
+
+    dev = nrg.DeviceReplica(nrg._lib.NRG_DS_HASHMAP, 0, knobs={"EXP": 0x10000 * move}, log2_slots=17,
+                            max_batch=1 << 16, replica_id=1)
+    dev.use_torch_stream()
+    dev.hm_prefill_partition(20_000, 1, 0, 1)
+    om = orc.HashMap()
+    om.prefill_range(20_000, 1)
+    g = PartitionedGroup(dev, rank=0, world=1)
+    keep, exp = [], []
+    for rnd in range(6):
+        W, R = 20_000 + 500 * rnd, 40_000 - 1000 * rnd
+        k = orc.gen_uniform(W, 800 + rnd, 60_000)
+        v = orc.gen_raw(W, 810 + rnd)
+        gk = orc.gen_uniform(R, 820 + rnd, 60_000)
+        d_p, d_k = _cuda(_puts(k, v)), _cuda(gk)
+        gv = torch.full((R,), -1, dtype=torch.int64, device="cuda")
+        gf = torch.full((R,), 7, dtype=torch.uint8, device="cuda")
+        want = rnd % 2 == 0
+        pv = torch.full((W,), -1, dtype=torch.int64, device="cuda") if want else None
+        pf = torch.full((W,), 7, dtype=torch.uint8, device="cuda") if want else None
+        g.round_async(d_p, W, d_k, R, gv, gf, pv, pf)
+        keep.append((d_p, d_k, gv, gf, pv, pf))
+        p, f = om.replay(k, v)
+        exp.append((om.get_batch(gk), (p, f) if want else None))
+    g.flush()
+    torch.cuda.synchronize()
+    for rnd, ((_, _, gv, gf, pv, pf), ((ev, ef), pp)) in enumerate(zip(keep, exp)):
+        np.testing.assert_array_equal(_u64(gv), ev, err_msg=f"round {rnd}")
+        np.testing.assert_array_equal(gf.cpu().numpy(), ef.astype(np.uint8), err_msg=f"round {rnd}")
+        if pp is not None:
+            np.testing.assert_array_equal(_u64(pv), pp[0], err_msg=f"round {rnd} prev")
+            np.testing.assert_array_equal(pf.cpu().numpy(), pp[1].astype(np.uint8), err_msg=f"round {rnd} prev")
     assert [int(x) for x in dev.hm_digest()] == [int(x) for x in om.digest()]
     g.close()
     dev.close()
