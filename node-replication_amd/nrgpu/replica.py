@@ -754,8 +754,18 @@ class Replica:
         return self.execute_batch([op], tok)[0]
 
     def execute_batch(self, ops: Sequence, tok: ReplicaToken) -> list:
+        """Sync to ctail, then dispatch with this replica's replay excluded (the reference's
+        reader lock against the combiner, nr/src/replica.rs:483-497). The device answers reads
+        only with its copy of the log fully replayed (nrg_hashmap_get: NRG_E_NOT_SYNCED
+        otherwise), and other replicas' combiners may append to that copy after the sync: those
+        entries -- none of them this replica's own, whose combine appends and replays in one go --
+        are replayed first, under the log lock so that no further append lands before the read
+        (a read then sees a state at least as new as the ctail it synced to, as NR's does)."""
         self._sync_to(self.log.ctail)
-        return self.ds.read_batch(self.dev, list(ops))
+        with self._combiner:
+            with self.log.lock:
+                self.dev.log_exec()
+                return self.ds.read_batch(self.dev, list(ops))
 
     def sync(self, tok: Optional[ReplicaToken] = None):
         """Replica::sync (nr/src/replica.rs:473-479)"""
