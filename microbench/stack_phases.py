@@ -37,6 +37,7 @@ w0 = []
 R = 20
 fin = []
 q8 = []
+lb = []
 for r in range(R + 3):
     for i in range(BB):  # pipeline=1: a round's finish rides in the next launch
         dev.st_round_device(opsl[i], N, 1, resps[i & 1], somes[i & 1])
@@ -56,6 +57,13 @@ for r in range(R + 3):
         w0.append(((t9[:, 0] - t[:, 5]).mean() / 100.0, t9[:, 1].mean(), ((t[:, 6] - t[:, 8]).mean() / 100.0)))
     if r >= 3:
         acc += t - t[:, :1].min()
+        x = buf.reshape(tiles, 16).astype(np.float64)
+        o = x[:, 0].min()
+        pub, built, res, q1 = x[:, 15] - o, x[:, 12] - o, x[:, 13] - o, x[:, 14] - o
+        mpred = np.maximum.accumulate(np.concatenate([[0.0], pub[:-1]]))  # latest predecessor publish
+        lb.append(np.array([(pub - (x[:, 0] - o)).mean(), (built - pub).mean(), (res - built).mean(),
+                            (res - np.maximum(mpred, built)).mean(), pub.max(), np.argmax(pub),
+                            (q1 - built).mean(), (res - built).max()]))
 acc /= R
 start = acc[:, 0]
 print(f"N={N} tiles={tiles}: tile start spread {start.min() / 100:.2f}..{start.max() / 100:.2f} us")
@@ -81,3 +89,8 @@ print("  slowest loads: " + ", ".join("tile %d %.2f us (xcc %d se %d cu %d, %d o
 if q8:
     print("  of the unmatched-Pop phase, the intra-tile queries: mean %.2f us" % np.mean(q8))
     print("  wave 0's own queries %.2f us over a list of %.0f; pre-chunk pass %.2f us" % tuple(np.mean(w0, 0)))
+if lb:
+    v = np.mean(lb, 0) / np.array([100, 100, 100, 100, 100, 1, 100, 100])
+    print("  publish %.2f us after the tile's start; publish -> query structures built %.2f; wave 0's wait %.2f"
+          " (max %.2f), of it after the latest predecessor's publish (or the build) %.2f; latest publish at %.2f us"
+          " (tile ~%.0f); wave 1's queries %.2f" % (v[0], v[1], v[2], v[7], v[3], v[4], v[5], v[6]))

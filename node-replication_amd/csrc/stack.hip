@@ -420,6 +420,7 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
     xe = pew;
     const Fn tagg = {E, E - M};  // max(a, x + b) form for the look-back
     if (t == 0) __hip_atomic_store(&desc[tile], pack_agg(tagg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ST_MARK(15);  // published
     if (copy_later) {  // Log::append's copy of the wave's records
         if (ring_run) {
             uint4* w4 = (uint4*)(ring + rw0);
@@ -633,6 +634,7 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
         }
     };
 
+    ST_MARK(12);  // query structures built (wave 0 starts its look-back wait)
     if (wv == 0) {
         Fn acc = FN_ID;
         for (int g0 = 0; g0 < G; g0 += B) {
@@ -668,6 +670,7 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
                 if (g0 + q < G && r0 + g0 + q < np) acc = fn_then(acc, unpack_agg(v[q]));
         }
         acc = np ? wave_compose(acc) : Fn{0, 0};
+        ST_MARK(13);  // look-back resolved
         if (lane == 0) {
             s_D = fn_apply(acc, d0g);
             s_d0 = d0g;
@@ -677,6 +680,7 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
         // for the unclamped walk -- their own lists, then a share of wave 0's
         queries(wv, 0, 1);
         queries(0, wv - 1, ST_WAVES - 1);
+        if (dbg && t == 64) dbg[(u64)tile * 16 + 14] = wall_clock64();  // wave 1's queries done
     }
     __syncthreads();
     ST_MARK(4);
