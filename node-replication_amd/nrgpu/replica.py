@@ -678,6 +678,9 @@ class Replica:
         self._ctx: dict = {}
         self._resp: dict = {}
         self._reg = threading.Lock()
+        # a thread's pending ops are appended and taken under this lock (the reference's
+        # per-thread context rings, nr/src/context.rs:88-194, are lock-free SPSC queues)
+        self._ctx_lock = threading.Lock()
 
     # register (nr/src/replica.rs:279-298): tokens 1..=MAX_THREADS_PER_REPLICA
     def register(self) -> Optional[ReplicaToken]:
@@ -686,28 +689,31 @@ class Replica:
                 return None
             t = self._next
             self._next += 1
-            self._ctx[t] = []
-            self._resp[t] = []
+            with self._ctx_lock:
+                self._ctx[t] = []
+                self._resp[t] = []
             return ReplicaToken(t)
 
     def _enqueue(self, ops, tid):
-        q = self._ctx[tid]
-        if len(q) + len(ops) > MAX_PENDING_OPS and len(ops) <= MAX_PENDING_OPS:
-            return False
-        q.extend(ops)
-        return True
+        with self._ctx_lock:
+            q = self._ctx[tid]
+            if len(q) + len(ops) > MAX_PENDING_OPS and len(ops) <= MAX_PENDING_OPS:
+                return False
+            q.extend(ops)
+            return True
 
     def _combine(self):
         """Replica::combine (nr/src/replica.rs:544-595): collect every thread's pending ops,
         append them as one batch, replay the log, route this replica's responses back."""
         with self.log.lock:
             order, batch = [], []
-            for t in sorted(self._ctx):
-                q = self._ctx[t]
-                if q:
-                    order.append((t, len(q)))
-                    batch.extend(q)
-                    self._ctx[t] = []
+            with self._ctx_lock:
+                for t in sorted(self._ctx):
+                    q = self._ctx[t]
+                    if q:
+                        order.append((t, len(q)))
+                        batch.extend(q)
+                        self._ctx[t] = []
             if batch:
                 first = self.log.append(self.ds.encode(batch), self.idx)
                 resp, some = self.dev.log_exec(first, first + len(batch))
@@ -721,12 +727,16 @@ class Replica:
             st = self.dev.log_state()
             self.log.ctail = max(self.log.ctail, st["ltail"])
 
-    def _try_combine(self):
-        if self._combiner.acquire(blocking=False):
-            try:
-                self._combine()
-            finally:
-                self._combiner.release()
+    def _combine_until(self, done: Callable[[], bool]):
+        """Flat combining's wait (nr/src/replica.rs:508-541): until done(), become the combiner
+        and combine every thread's pending ops. The reference spins on a failed try-lock; a
+        Python thread spinning on the GIL only lets the combiner run every switch interval
+        (5 ms), so a thread blocks on the combiner lock instead and re-checks after it: a
+        combine that ran meanwhile may have carried its ops."""
+        while not done():
+            with self._combiner:
+                if not done():
+                    self._combine()
 
     def execute_mut(self, op, tok: ReplicaToken):
         """Replica::execute_mut (nr/src/replica.rs:345-356)"""
@@ -736,18 +746,15 @@ class Replica:
         """Host batcher: enqueue many of this thread's writes, combine once."""
         tid = tok.id()
         ops = list(ops)
-        while not self._enqueue(ops, tid):
-            self._try_combine()
+        self._combine_until(lambda: self._enqueue(ops, tid))
         want = len(ops)
-        while len(self._resp[tid]) < want:
-            self._try_combine()
+        self._combine_until(lambda: len(self._resp[tid]) >= want)
         out = self._resp[tid][:want]
         del self._resp[tid][:want]
         return out
 
     def _sync_to(self, ctail: int):
-        while self.dev.log_state()["ltail"] < ctail:
-            self._try_combine()
+        self._combine_until(lambda: self.dev.log_state()["ltail"] >= ctail)
 
     def execute(self, op, tok: ReplicaToken):
         """Replica::execute -> read_only (nr/src/replica.rs:404-410, :483-497)"""
