@@ -241,9 +241,10 @@ class Env:
 
     first_calls = []  # host us of the first step of every timed region of the process (diagnostic)
 
-    def timed(self, n, step, rep, host_s=None, finish=None):
+    def timed(self, n, step, rep, host_s=None, finish=None, evs=None):
         """Barrier + sync, K steps, the replica's deferred work launched, sync + barrier; max over
-        ranks of the wall time."""
+        ranks of the wall time. evs: {i: torch.cuda.Event} recorded on the stream right after
+        step i (the roofline window; the timed region proper passes none)."""
         torch, dist = self.torch, self.dist
         # Python's cyclic GC runs on allocation counts: held off inside the timed region (a
         # collection right before it made the first host call 50+ us: caches walked cold)
@@ -271,6 +272,8 @@ class Env:
             marks = [t]
             for i in range(n):
                 step(i)
+                if evs is not None and i in evs:
+                    evs[i].record()
                 if i < 3:
                     marks.append(time.perf_counter())
             # launches the last round's deferred apply + reads (and completes a pipelined group
@@ -330,23 +333,39 @@ ROOF_ROUNDS = 64  # rounds of the roofline region (at least --steps)
 
 def roofline_region(args, rep, run, names):
     """Kernel durations for the roofline, measured right after the timed region on the same
-    stream and workload: max(steps, ROOF_ROUNDS) more rounds with every timing_every-th launch
-    of the named kernels bracketed by HIP events stamped from their own dispatch. The timed
-    region itself carries no events (a bracketed launch costs wall time,
-    profiles/r02_s8_event_bracketing.txt), so `value` is the unperturbed rate.
-    Returns {name: (launches, total_ms)}."""
+    stream and workload (the timed region itself carries no events, so `value` is the
+    unperturbed rate), two ways:
+    * window (the line's avg_launch_us): a run of n = max(steps, ROOF_ROUNDS) rounds with one
+      HIP event on the stream after round 0's call and one after round n-1's; rounds 1..n-1 are
+      steady-state launches of the round's kernel(s), one round of work each, and nothing else
+      runs on the stream, so (stop - start) / (n - 1) is the per-round kernel time with no event
+      on any dispatch. Idle gaps between launches would count in it: it can only overstate.
+    * bracketed: another n rounds with every timing_every-th launch of the named kernels carrying
+      HIP events stamped from its own dispatch (hipExtLaunchKernelGGL). Those launches run
+      longer than unbracketed ones (stack: ~17 % over rocprof's duration,
+      profiles/r02_s8_event_bracketing.txt), so this is reported beside the window only.
+    Returns ({name: (launches, total_ms)}, (window rounds, window ms))."""
     if args.no_kernel_timing:
-        return {n: (0, 0.0) for n in names}
+        return {n: (0, 0.0) for n in names}, (0, 0.0)
+    torch = sys.modules["torch"]
+    nwin = max(args.steps, ROOF_ROUNDS)
+    evs = {0: torch.cuda.Event(enable_timing=True), nwin - 1: torch.cuda.Event(enable_timing=True)}
+    run(nwin, evs=evs)
+    win = (nwin - 1, evs[0].elapsed_time(evs[nwin - 1]))
     rep.kernel_timing(True, only=",".join(names), every=args.timing_every)
-    run(max(args.steps, ROOF_ROUNDS))
+    run(nwin)
     out = {n: rep.kernel_time(n) for n in names}
     rep.kernel_timing(False)
-    return out
+    return out, win
 
 
-def roofline(kernel, k_bytes, k_n, k_ms, args, traffic):
-    k_avg_s = (k_ms / 1e3 / k_n) if k_n else float("nan")
-    achieved = k_bytes / k_avg_s / 1e9 if k_n else None
+def roofline(kernel, k_bytes, k_n, k_ms, args, traffic, win=(0, 0.0)):
+    """k_n, k_ms: the bracketed launches (per round of work); win: the window (rounds, ms), which
+    gives avg_launch_us and `achieved` when measured."""
+    b_avg_s = (k_ms / 1e3 / k_n) if k_n else float("nan")
+    w_n, w_ms = win
+    k_avg_s = (w_ms / 1e3 / w_n) if w_n else b_avg_s
+    achieved = k_bytes / k_avg_s / 1e9 if (w_n or k_n) else None
     return {
         "bound": "hbm",
         "kernel": kernel,
@@ -357,12 +376,17 @@ def roofline(kernel, k_bytes, k_n, k_ms, args, traffic):
         "traffic": traffic.get("bytes_per_launch") if traffic else None,
         "traffic_source": traffic.get("source") if traffic else None,
         "bytes_per_launch": int(k_bytes),
-        "sampled_every": args.timing_every,
-        "region": "%d rounds after the timed region, every %d-th launch event-bracketed" % (
+        "region": ("rounds 1..%d of a %d-round run after the timed region, between two HIP events on the "
+                   "kernel's stream (no event on any dispatch); bracketed: another %d rounds, every %d-th "
+                   "launch with dispatch-stamped events" % (w_n, w_n + 1, w_n + 1, args.timing_every))
+        if w_n else "%d rounds after the timed region, every %d-th launch event-bracketed" % (
             max(args.steps, ROOF_ROUNDS), args.timing_every),
         "traffic_key": traffic_key(args),
-        "avg_launch_us": round(k_avg_s * 1e6, 3) if k_n else None,
-        "launches": k_n,
+        "avg_launch_us": round(k_avg_s * 1e6, 3) if (w_n or k_n) else None,
+        "launches": w_n if w_n else k_n,
+        "bracketed_avg_launch_us": round(b_avg_s * 1e6, 3) if k_n else None,
+        "bracketed_launches": k_n,
+        "sampled_every": args.timing_every,
     }
 
 
@@ -483,9 +507,9 @@ def run_hashmap(args, env):
             pgroup.flush()  # the last pipelined round
         rep.join()
 
-    def run(n, prev=False, host_s=None):
+    def run(n, prev=False, host_s=None, evs=None):
         mode["prev"], mode["n"] = prev, n
-        return env.timed(n, step, rep, host_s, finish=finish)
+        return env.timed(n, step, rep, host_s, finish=finish, evs=evs)
 
     mode["n"] = args.warmup
     WATCH.phase = "warmup rounds"
@@ -504,7 +528,7 @@ def run_hashmap(args, env):
     host_s = [0.0]
     WATCH.phase = "timed region"
     elapsed = run(args.steps, host_s=host_s)  # no events in the timed region
-    kt = roofline_region(args, rep, run, ["hm_round", "hm_papply"])
+    kt, win = roofline_region(args, rep, run, ["hm_round", "hm_papply"])
     (k_n, k_ms), (a_n, a_ms) = kt["hm_round"], kt["hm_papply"]
     if a_n and k_n:  # partition rounds: hm_round (partition + reads) + hm_papply (the table pass)
         k_ms = k_ms + a_ms * k_n / a_n
@@ -553,7 +577,7 @@ def run_hashmap(args, env):
     })
     res["roofline"] = roofline("hm_round+hm_papply" if a_n else "hm_round",
                                round_bytes, k_n, k_ms, args,
-                               measured_traffic(args))
+                               measured_traffic(args), win)
     res["round"] = {
         "algorithmic_bytes": int(round_bytes),
         "achieved_GBps": round(round_bytes / (elapsed / args.steps) / 1e9, 1),
@@ -733,13 +757,14 @@ def run_synthetic(args, env):
     for i in range(args.warmup):
         step(i)
     rep.sync()
-    def run(n):
+    def run(n, evs=None):
         mode["n"] = n
-        return env.timed(n, step, rep)
+        return env.timed(n, step, rep, evs=evs)
 
     WATCH.phase = "timed region"
     elapsed = run(args.steps)  # no events in the timed region
-    k_n, k_ms = roofline_region(args, rep, run, ["sy_replay"])["sy_replay"]
+    kt, win = roofline_region(args, rep, run, ["sy_replay"])
+    k_n, k_ms = kt["sy_replay"]
     rep.sync()
     value = world * N * args.steps / elapsed / 1e6
     if rank != 0:
@@ -757,7 +782,7 @@ def run_synthetic(args, env):
                             "ops_per_gpu_per_round": N,
                             "parallelism": "replicas%d" % world,
                         })
-    res["roofline"] = roofline("sy_replay", round_bytes, k_n, k_ms, args, measured_traffic(args))
+    res["roofline"] = roofline("sy_replay", round_bytes, k_n, k_ms, args, measured_traffic(args), win)
     res["round"] = {"algorithmic_bytes": int(round_bytes),
                     "touches_per_s": round(6 * Ng * args.steps / elapsed, 1)}
     if not args.no_cpu_baseline and world == 1:
@@ -840,13 +865,14 @@ def run_stack(args, env):
     for i in range(args.warmup):
         step(i)
     rep.sync()
-    def run(n):
+    def run(n, evs=None):
         mode["n"] = n
-        return env.timed(n, step, rep)
+        return env.timed(n, step, rep, evs=evs)
 
     WATCH.phase = "timed region"
     elapsed = run(args.steps)  # no events in the timed region
-    k_n, k_ms = roofline_region(args, rep, run, ["st_replay"])["st_replay"]
+    kt, win = roofline_region(args, rep, run, ["st_replay"])
+    k_n, k_ms = kt["st_replay"]
     rep.sync()
     value = world * N * args.steps / elapsed / 1e6
     if rank != 0:
@@ -863,7 +889,7 @@ def run_stack(args, env):
                             "ops_per_gpu_per_round": N,
                             "parallelism": "replicas%d" % world,
                         })
-    res["roofline"] = roofline("st_replay", round_bytes, k_n, k_ms, args, measured_traffic(args))
+    res["roofline"] = roofline("st_replay", round_bytes, k_n, k_ms, args, measured_traffic(args), win)
     res["round"] = {"algorithmic_bytes": int(round_bytes), "distinct_slots_written": int(S)}
     if not args.no_cpu_baseline and world == 1:
         res["cpu_baseline"] = stack_cpu_baseline(min(args.cpu_seconds, 10.0), N, args.stack_init)
