@@ -128,3 +128,22 @@ def test_stack_and_synth_cpu_baselines_go_through_nr(bench):
         json.dumps(out)
         assert out["kind"] == "port" and out["value"] > 0 and "restatement of nr" in out["sample"]
         assert out["one_thread_nr"]["cores"] == 1 and out["one_thread_sequential"]["value"] > 0
+
+
+def test_roofline_prefers_the_window(bench):
+    """The line's kernel time is the steady-state window ((stop - start) / rounds between two stream
+    events) when it was measured; the dispatch-bracketed average is reported beside it."""
+    import argparse
+
+    args = argparse.Namespace(timing_every=4, steps=400, workload="stack", ops_per_gpu=1_000_000, stack_init=50_000,
+                              write_ratio=10, key_space=10_000_000, prefill=1 << 23, log2_slots=26, dist="uniform",
+                              theta=0.99, scramble=False, gpus=1)
+    r = bench.roofline("st_replay", 12_000_000, 100, 100 * 0.0175, args, None, win=(399, 399 * 0.0147))
+    assert r["avg_launch_us"] == pytest.approx(14.7)
+    assert r["bracketed_avg_launch_us"] == pytest.approx(17.5)
+    assert r["achieved"] == pytest.approx(12e6 / 14.7e-6 / 1e9, rel=1e-3)
+    assert r["frac"] == pytest.approx(r["achieved"] / bench.HBM_PEAK_GBS, rel=1e-3)
+    assert r["launches"] == 399 and r["bracketed_launches"] == 100
+    # without a window (--no-kernel-timing has neither), the bracketed average stands in
+    r2 = bench.roofline("st_replay", 12_000_000, 100, 100 * 0.0175, args, None)
+    assert r2["avg_launch_us"] == pytest.approx(17.5)
