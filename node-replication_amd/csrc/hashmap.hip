@@ -29,7 +29,7 @@
 //   tile order = log order) in chunks, finds each key's last writer in an LDS hash, and that
 //   thread finds or claims the key's slot and stores its value: one table line read and written
 //   per distinct key. All Puts of a key share its home bucket, so one workgroup decides each key.
-//   1024-thread workgroups over <= 256 buckets for rounds of >= 64k Puts (256 over <= 1024
+//   512-thread workgroups over <= 512 buckets for rounds of >= 64k Puts (256 over <= 1024
 //   below), buckets dealt to XCDs in contiguous ranges, the next chunk's entries loaded while a
 //   chunk resolves. It runs at the memory-side request floor (profiles/r04_papply_phases.txt).
 //   With previous values every Put keeps its entry and one wave walks each chunk in log order:
@@ -1864,10 +1864,13 @@ hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool
         const u32 log2_slots = 64 - c->slot_shift;
         u32 nb_log = 0;
         while ((64ull << nb_log) < n && (1u << nb_log) < HM_BK_MAX) nb_log++;
-        // apply workgroup width (NRG_KNOB_PA_TPB; 0: 1024 threads over <= 256 buckets for rounds of
-        // >= PA_WIDE_MIN Puts without previous values, else 256 over <= 1024)
+        // apply workgroup width (NRG_KNOB_PA_TPB; 0: 512 threads over <= 512 buckets for rounds of
+        // >= PA_WIDE_MIN Puts without previous values, else 256 over <= 1024). Round 6, 512 vs 1024
+        // (profiles/r06/papply_width.txt): N = 8 per-GPU round 77.2 vs 78.9 us, N = 4 53.9-54.2 vs 54.9,
+        // configs[2] 251.1-251.6 vs 255.0, 100 % writes 71.4 vs 72.9, 50 % 54.0 vs 55.1, Zipf 10 % 30.4
+        // vs 30.8, Zipf 50 % 47.5 vs 47.9 (scrambled: equal)
         constexpr u64 PA_WIDE_MIN = 1ull << 16;
-        const u32 pa_t = want_prev ? 256u : c->pa_tpb ? c->pa_tpb : n >= PA_WIDE_MIN ? 1024u : 256u;
+        const u32 pa_t = want_prev ? 256u : c->pa_tpb ? c->pa_tpb : n >= PA_WIDE_MIN ? 512u : 256u;
         const u32 pa_nb_log = pa_t == 1024 ? PaGeo<false, 1024>::NB_LOG : pa_t == 512 ? PaGeo<false, 512>::NB_LOG
                                                                                       : PaGeo<false, 256>::NB_LOG;
         if (nb_log > pa_nb_log) nb_log = pa_nb_log;
