@@ -18,7 +18,7 @@ import nrgpu  # noqa: E402
 from nrgpu import _lib as L  # noqa: E402
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
-dev = nrgpu.DeviceReplica(L.NRG_DS_STACK, 0, knobs={"EXP": 2}, max_batch=N, stack_capacity=N * 4 + 100_000, pipeline=int(os.environ.get("PIPE", "1")),
+dev = nrgpu.DeviceReplica(L.NRG_DS_STACK, 0, knobs={"EXP": int(os.environ.get("EXP", "2"), 0)}, max_batch=N, stack_capacity=N * 4 + 100_000, pipeline=int(os.environ.get("PIPE", "1")),
                           log_bytes=64 * 4 * max(N, 8192))
 dev.use_torch_stream()
 dev.st_init(list(range(50_000)))

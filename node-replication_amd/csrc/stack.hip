@@ -157,12 +157,13 @@ __device__ __forceinline__ int st_find(const long long* s_tm, const long long* s
 // every 8-tile group (s_g8) and 64-tile group (s_gm). Returns this thread's minimum over the
 // tiles after `after` (pass ~0u for none).
 __device__ __forceinline__ long long st_stage(const long long* __restrict__ tmin, u32 tiles, long long* s_tm,
-                                              long long* s_g8, long long* s_gm, u32 after) {
+                                              long long* s_g8, long long* s_gm, u32 after, bool in_lds = false) {
     const int t = threadIdx.x, lane = t & 63;
     const u32 ngr = (tiles + 63) / 64;
     long long later = 1ll << 62;
     for (u32 k = t; k < ngr * 64; k += 256) {
-        const long long v = k < tiles ? tmin[k] : (1ll << 62);
+        // in_lds: s_tm[0, tiles) already holds the minima (st_copy_lds)
+        const long long v = k < tiles ? (in_lds ? s_tm[k] : tmin[k]) : (1ll << 62);
         if (k < tiles) s_tm[k] = v;
         if (k > after) later = v < later ? v : later;
         long long m = v;
@@ -175,6 +176,21 @@ __device__ __forceinline__ long long st_stage(const long long* __restrict__ tmin
         if (lane == 0) s_gm[k >> 6] = m;
     }
     return later;
+}
+
+// Copy the tile minima of a chunk (tiles x 8 B) into s_tm straight from global memory to LDS
+// (global_load_lds: no VGPR holds them and no wait is due until the caller's next vmcnt wait,
+// after which, with a barrier, the copy is visible to the workgroup). Called by one wave.
+__device__ __forceinline__ void st_copy_lds(const long long* tmin, u32 tiles, long long* s_tm) {
+    const u32 lane = threadIdx.x & 63, nd = 2 * tiles;
+    const u32* src = reinterpret_cast<const u32*>(tmin);
+    u32* dst = reinterpret_cast<u32*>(s_tm);
+    for (u32 j0 = 0; j0 < nd; j0 += 64) {
+        const u32 j = j0 + lane;
+        if (j < nd)
+            __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(src + j),
+                                             (void __attribute__((address_space(3)))*)(dst + j0), 4, 0, 0);
+    }
 }
 
 // A replay launch: the tile pass of chunk e (A) and, in the workgroups before it, the finish
@@ -485,29 +501,18 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
     ST_MARK(3);
 
     // ---- 3. look-back (wave 0): compose the aggregates of ALL earlier tiles (64 runs in
-    // parallel, 8 loads in flight per lane; the highest lane holds the oldest run). The loads of
-    // the first 8 per lane are issued now and land while the query structures are built: those
-    // need the tile's start depth only when the stack empties inside the tile, so they are
-    // built for the unclamped walk and rebuilt in that (rare) case. ----
+    // parallel, 8 loads in flight per lane; the highest lane holds the oldest run). The query
+    // structures are built first: they need the tile's start depth only when the stack empties
+    // inside the tile, so they are built for the unclamped walk and rebuilt in that (rare) case.
+    // Round 6: no global load is waited on between the aggregate's publication and the
+    // query-structure barrier (the look-back's first loads and the previous chunk's tile minima are
+    // issued after it): 3.9 -> 2.3 us from publication to query structures, 14.83-14.95 -> 14.22-14.26
+    // us per 1M-op round (profiles/r06/stack_lookback_after_build.txt). ----
     long long* sdepth = &ctl->depth0;             // depth after the chunk of each parity
-    // depth before this chunk: loaded by wave 0 alone and passed on through LDS, so no other
-    // wave waits on it (a vector load's wait would also wait for every store issued before it)
-    const long long d0g = wv == 0 ? sdepth[A.par ^ 1] : 0;
     const int np = (int)tile;
     const int G = (np + 63) / 64;
     const int r0 = (63 - lane) * G;
     constexpr int B = 8;
-    u64 v0[B];
-    if (wv == 0) {
-#pragma unroll
-        for (int q = 0; q < B; q++) {
-            const int idx = r0 + q;
-            v0[q] = (q < G && idx < np) ? __hip_atomic_load(&desc[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-        }
-    }
-    // the previous chunk's tile minima (read only by the pre-chunk pass, after the queries): staged
-    // here, after the aggregate is published, so their load is off the look-back's critical path
-    if (P.tiles) (void)st_stage(P.tl.tmin, P.tiles, s_ptm, s_pg8, s_pgm, ~0u);
 
     // Query structures for lane levels relative to the tile's lowest level: lane minimum amin_,
     // start dt_, and uq_ unmatched Pops that find an element. Outputs: s_min, the sparse table
@@ -636,6 +641,20 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
 
     ST_MARK(12);  // query structures built (wave 0 starts its look-back wait)
     if (wv == 0) {
+        // the previous chunk's tile minima (read only by the pre-chunk pass, after the queries):
+        // copied into LDS beside the look-back's loads, whose waits cover the copy; the group minima
+        // are staged from LDS after the look-back. (Loaded before the query structures, their
+        // latency held that barrier.)
+        if (P.tiles) st_copy_lds(P.tl.tmin, P.tiles, s_ptm);
+        // the look-back's first loads: issued only now, so no wait before the query-structure
+        // barrier covers them (agent-scope loads, served beyond the XCD's L2)
+        const long long d0g = sdepth[A.par ^ 1];
+        u64 v0[B];
+#pragma unroll
+        for (int q = 0; q < B; q++) {
+            const int idx = r0 + q;
+            v0[q] = (q < G && idx < np) ? __hip_atomic_load(&desc[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+        }
         Fn acc = FN_ID;
         for (int g0 = 0; g0 < G; g0 += B) {
             u64 v[B];
@@ -684,6 +703,7 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
     }
     __syncthreads();
     ST_MARK(4);
+    if (P.tiles) (void)st_stage(P.tl.tmin, P.tiles, s_ptm, s_pg8, s_pgm, ~0u, true);
     const long long D = s_D, d0 = s_d0;
     const long long T0 = D + M > 0 ? D + M : 0;              // the tile's lowest level
     const long long Dt = D + xe > xe - xm ? D + xe : xe - xm;  // the lane's start depth
