@@ -25,7 +25,8 @@ namespace nrg {
 
 #ifndef NRG_ST_OPS
 // ops per lane, measured at 1M-op rounds (bench.py --workload stack): 8 -> 17.4 us, 16 -> 18.8 us,
-// 32 -> 21.2 us (session 7, before the branch-free query walk: 21.5 / 20.6 / 22.7 us)
+// 32 -> 21.2 us (session 7, before the branch-free query walk: 21.5 / 20.6 / 22.7 us); round 6:
+// 4 (1024-op tiles, four per CU) 23.7 us against 8's 14.0 on one box (profiles/r06/stack_resp_policy.txt)
 #define NRG_ST_OPS 8
 #endif
 constexpr int SW_OPS = NRG_ST_OPS;          // ops per lane, replayed in order by that lane (<= 32)
@@ -220,6 +221,16 @@ typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void nt_store4(uint4* p, uint4 v) {
     const u32x4_t t = {v.x, v.y, v.z, v.w};
     __builtin_nontemporal_store(t, (u32x4_t*)p);
+}
+
+// A tile's Pop responses: the lane's wide store and the later single-op stores (the answers to
+// its unmatched Pops, from any wave of the tile, after a barrier) take the same cache policy, so
+// no ordering between a streamed and a plain store to one word is relied on. The plain form is a
+// relaxed atomic store: two plain-vs-streamed stores on either side of a branch are merged by the
+// compiler into one plain store, the hint dropped (profiles/r06/stack_resp_policy.txt).
+__device__ __forceinline__ void st_resp(u32* p, u32 v, u32 plain) {
+    if (plain) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    else __builtin_nontemporal_store(v, p);
 }
 
 __device__ __forceinline__ void wave_sync() {  // LDS written by other lanes of this wave
@@ -492,7 +503,7 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
             for (int q = 0; q < SW_OPS; q++) {
                 const u64 g = g0 + q;
                 if (base + q < n && g >= resp_lo && g < resp_hi) {
-                    resp[g - resp_lo] = rt[q];
+                    st_resp(&resp[g - resp_lo], rt[q], A.plain);
                     some[g - resp_lo] = (smask >> q) & 1;
                 }
             }
@@ -627,7 +638,7 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
                 if (v[i] >= 0) {
                     const u64 g = lo + tbase + pos;
                     if (resp && g >= resp_lo && g < resp_hi) {
-                        resp[g - resp_lo] = rv[i];
+                        st_resp(&resp[g - resp_lo], rv[i], A.plain);
                         some[g - resp_lo] = 1;
                     }
                 } else {  // its Push is in an earlier tile or before the chunk
@@ -722,7 +733,7 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
         for (u32 um = umask; um; um &= um - 1) {
             const u64 g = g0 + (u64)__builtin_ctz(um);
             if (resp && g >= resp_lo && g < resp_hi) {
-                resp[g - resp_lo] = 0;
+                st_resp(&resp[g - resp_lo], 0u, A.plain);
                 some[g - resp_lo] = 0;
             }
         }
