@@ -47,6 +47,12 @@ typedef u64 u64x2 __attribute__((ext_vector_type(2)));
 // after the last workgroup; streamed, they drain during the kernel. N = 8 per-GPU round 78.7 vs
 // 80.5 us, configs[2] 256.9 vs 263.4; stamp rounds keep plain stores (B1 34.5-34.7 plain vs
 // 34.7-35.0 streamed; profiles/r04_nt_stores.txt). NRG_KNOB_EXP bit 6 = plain everywhere (A/B).
+// Round 6: the compiler merges st_out's two branches into one plain store and drops the hint, so
+// only the 16-B log copy (st_rec) is streamed; the responses are plain stores. Streamed for real
+// (the plain branch as a relaxed wavefront-scope atomic store, which is not merged) they measured
+// the same on one box: B1 34.15-34.19 us per round by the window (stamp-round reads streamed) vs
+// 34.16-34.17, N = 8 per-GPU round 77.2-77.3 both, configs[2] 250.2 vs 250.7
+// (profiles/r06/nt_single_stores.txt).
 template <typename T>
 __device__ __forceinline__ void st_out(T* p, T v, bool plain) {
     if (plain) *p = v;

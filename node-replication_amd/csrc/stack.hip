@@ -226,10 +226,11 @@ __device__ __forceinline__ void nt_store4(uint4* p, uint4 v) {
 // A tile's Pop responses: the lane's wide store and the later single-op stores (the answers to
 // its unmatched Pops, from any wave of the tile, after a barrier) take the same cache policy, so
 // no ordering between a streamed and a plain store to one word is relied on. The plain form is a
-// relaxed atomic store: two plain-vs-streamed stores on either side of a branch are merged by the
-// compiler into one plain store, the hint dropped (profiles/r06/stack_resp_policy.txt).
+// relaxed wavefront-scope atomic store (the same plain store in the ISA): two plain-vs-streamed
+// stores on either side of a branch are merged by the compiler into one plain store, the hint
+// dropped (profiles/r06/stack_resp_policy.txt).
 __device__ __forceinline__ void st_resp(u32* p, u32 v, u32 plain) {
-    if (plain) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (plain) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     else __builtin_nontemporal_store(v, p);
 }
 

@@ -25,6 +25,12 @@ constexpr u32 SETBIT = 0x80000000u;
 // kernel-end L2 write-back, which pays on the stack and the hashmap's partition rounds, but not
 // here (56.6-56.9 vs 56.1-56.6 us per round plain; profiles/r04_nt_stores.txt): plain by default.
 typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
+// Round 6: the compiler merges st_out's two branches into one plain store and drops the hint, so
+// bits 7-9 compile to plain stores; only the 16-B log copy (st_op, bit 6) is streamed. Streamed
+// for real (the plain branch as a relaxed atomic store, not merged) every variant was slower on
+// one box, and the atomic form cost the plain default its merged wider stores: 44.9-45.8 us per
+// round before, 47.7-48.0 with the atomic plain form, 49.5-50.5 touch records or seen values
+// streamed, 47.5-47.6 responses streamed (profiles/r06/nt_single_stores.txt).
 template <typename T>
 __device__ __forceinline__ void st_out(T* p, T v, bool plain) {
     if (plain) *p = v;
