@@ -17,6 +17,7 @@ digests are compared across ranks.
                 replay of the global log, and the partitions' digests must add up to its digest.
 """
 import argparse
+import datetime
 import json
 import os
 import sys
@@ -93,6 +94,11 @@ def reads(rank, rnd, span):
     return oracle.gen_uniform(500 + 50 * rank, 1000 * rank + 10 * rnd + 3, span)
 
 
+def phase(msg):
+    """Progress on stderr, so a stalled rank shows where it stopped (tests/test_parallel.py)."""
+    print(f"[dist_worker {os.environ.get('RANK')}] {msg}", file=sys.stderr, flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--backend", choices=["cpu", "gpu"], default="cpu")
@@ -101,8 +107,10 @@ def main():
     ap.add_argument("--prefill", type=int, default=1000)
     ap.add_argument("--mode", choices=["replicated", "partitioned"], default="replicated")
     a = ap.parse_args()
-    dist.init_process_group("gloo")
+    phase("init_process_group")
+    dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=90))
     rank, world = dist.get_rank(), dist.get_world_size()
+    phase(f"rank {rank}/{world} joined")
     from nrgpu.parallel import ReplicatedHashMap
 
     if a.mode == "partitioned":
@@ -118,12 +126,14 @@ def main():
     else:
         dev_t = torch.device("cpu")
         rep = OracleReplica(a.prefill)
+    phase("replica ready")
     group = ReplicatedHashMap(rep, device=dev_t)
 
     model = oracle.HashMap()  # sequential replay of the global log, as one nr thread would see it
     model.prefill_range(a.prefill, 1)
     ok = True
     for rnd in range(a.rounds):
+        phase(f"round {rnd}")
         k, v = segment(rank, rnd, a.span)
         W = len(k)
         puts = torch.from_numpy(np.stack([k, v], 1).view(np.int64).copy()).to(dev_t)
@@ -177,6 +187,7 @@ def partitioned(a, rank, world):
     model.prefill_range(a.prefill, 1)
     ok = True
     for rnd in range(a.rounds):
+        phase(f"round {rnd}")
         k, v = segment(rank, rnd, a.span)
         W = len(k)
         puts = torch.from_numpy(np.stack([k, v], 1).view(np.int64).copy()).reshape(W, 2).to(dev_t)

@@ -31,6 +31,13 @@ def run_ranks(world, backend, timeout=180, extra=()):
         for p in procs:
             o, e = p.communicate(timeout=timeout)
             outs.append((p.returncode, o, e))
+    except subprocess.TimeoutExpired:
+        # name where each rank stalled (dist_worker prints its phases to stderr)
+        for p in procs:
+            p.kill()
+        tails = [p.communicate()[1][-1500:] for p in procs]
+        pytest.fail(f"ranks still running after {timeout} s; stderr tails:\n" +
+                    "\n".join(f"--- rank {r}:\n{t}" for r, t in enumerate(tails)))
     finally:
         for p in procs:
             if p.poll() is None:
