@@ -234,6 +234,22 @@ __device__ __forceinline__ void st_resp(u32* p, u32 v, u32 plain) {
     else __builtin_nontemporal_store(v, p);
 }
 
+// Round 6: the `some` bytes (the lane's 8-B store and the patches, NRG_ST_SOME_NT) and the finish's
+// stores (cross-tile answers and the commit, NRG_ST_FIN_NT) are streamed as well. Same box, two
+// pairs: 13.87-13.96 -> 13.71-13.78 us per 1M-op round (finish alone 13.73-13.84, some alone no
+// change; profiles/r06/stack_stream_some_finish.txt). Build with =0 for the plain A/B.
+#ifndef NRG_ST_SOME_NT
+#define NRG_ST_SOME_NT 1
+#endif
+#ifndef NRG_ST_FIN_NT
+#define NRG_ST_FIN_NT 1
+#endif
+template <bool NT, typename T>
+__device__ __forceinline__ void st_pol(T* p, T v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
 __device__ __forceinline__ void wave_sync() {  // LDS written by other lanes of this wave
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -497,7 +513,7 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
             } else {  // 8 ops per lane: one 8-B store
                 const uint2 b = uint2{((smask & 15u) * 0x204081u) & 0x01010101u,
                                       (((smask >> 4) & 15u) * 0x204081u) & 0x01010101u};
-                *(uint2*)sp = b;  // (streamed: +1.2 MB of partial-line writes per round, no faster)
+                st_pol<NRG_ST_SOME_NT>((u64*)sp, (u64)b.x | ((u64)b.y << 32));
             }
         } else if (resp) {
 #pragma unroll
@@ -505,7 +521,7 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
                 const u64 g = g0 + q;
                 if (base + q < n && g >= resp_lo && g < resp_hi) {
                     st_resp(&resp[g - resp_lo], rt[q], A.plain);
-                    some[g - resp_lo] = (smask >> q) & 1;
+                    st_pol<NRG_ST_SOME_NT>(&some[g - resp_lo], (uint8_t)((smask >> q) & 1));
                 }
             }
         }
@@ -640,7 +656,7 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
                     const u64 g = lo + tbase + pos;
                     if (resp && g >= resp_lo && g < resp_hi) {
                         st_resp(&resp[g - resp_lo], rv[i], A.plain);
-                        some[g - resp_lo] = 1;
+                        st_pol<NRG_ST_SOME_NT>(&some[g - resp_lo], (uint8_t)1);
                     }
                 } else {  // its Push is in an earlier tile or before the chunk
                     const u32 x = atomicAdd(&s_ucnt, 1u);
@@ -735,7 +751,7 @@ __device__ __forceinline__ void st_tile_role(const StPass& A, const StPass& P, u
             const u64 g = g0 + (u64)__builtin_ctz(um);
             if (resp && g >= resp_lo && g < resp_hi) {
                 st_resp(&resp[g - resp_lo], 0u, A.plain);
-                some[g - resp_lo] = 0;
+                st_pol<NRG_ST_SOME_NT>(&some[g - resp_lo], (uint8_t)0);
             }
         }
         if (t == 0) s_ucnt = 0;
@@ -841,11 +857,11 @@ __device__ __forceinline__ void st_finish_role(const StPass& P, u32 tile, DevCtl
         hi = hi < later ? hi : later;
         const u32* tab = tl.table + (u64)tile * ST_TILE;
         for (long long sl = tmin + t; sl < hi; sl += 256)
-            if ((u64)sl < cap) stack[sl] = tab[sl - tmin];
+            if ((u64)sl < cap) st_pol<NRG_ST_FIN_NT>(&stack[sl], tab[sl - tmin]);
     }
     if (pg != ~0ull) {
-        resp[pg - resp_lo] = pval;
-        some[pg - resp_lo] = 1;
+        st_pol<NRG_ST_FIN_NT>(&resp[pg - resp_lo], pval);
+        st_pol<NRG_ST_FIN_NT>(&some[pg - resp_lo], (uint8_t)1);
     }
     if (!one) {
         for (u32 j = t; j < cnt; j += 256) {
@@ -854,9 +870,9 @@ __device__ __forceinline__ void st_finish_role(const StPass& P, u32 tile, DevCtl
             if (g < resp_lo || g >= resp_hi) continue;
             const long long s = tmin + (v >> ST_PB);
             const int k = st_walk(s_tm, s_g8, s_gm, (int)tile - 1, s);
-            resp[g - resp_lo] = k >= 0 ? tl.table[(u64)k * ST_TILE + (u64)(s - s_tm[k])]
-                                       : (j == (u32)t ? uv0 : tl.uval[(u64)tile * ST_TILE + j]);
-            some[g - resp_lo] = 1;
+            st_pol<NRG_ST_FIN_NT>(&resp[g - resp_lo], k >= 0 ? tl.table[(u64)k * ST_TILE + (u64)(s - s_tm[k])]
+                                                        : (j == (u32)t ? uv0 : tl.uval[(u64)tile * ST_TILE + j]));
+            st_pol<NRG_ST_FIN_NT>(&some[g - resp_lo], (uint8_t)1);
         }
     }
 }
