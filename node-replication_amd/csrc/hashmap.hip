@@ -63,6 +63,27 @@ __device__ __forceinline__ void st_rec(nrg_put* p, const nrg_put& r, bool plain)
     else __builtin_nontemporal_store(u64x2{r.key, r.val}, (u64x2*)p);
 }
 
+// Round 6 (profiles/r06/b1_apply_nt.txt): the stamp-round apply's random value stores are streamed
+// (NRG_HM_APPLY_NT): they drain during the launch instead of in its end-of-kernel L2 write-back.
+// Same box, three pairs: 34.16-34.20 -> 33.93-34.02 us per B1 step (window 34.03-34.13 ->
+// 33.80-33.97); the driver's 20 steps 27,507-27,866 -> 27,823-27,875 Mops/s. Streaming the index
+// role's put_slot / win / over words (NRG_HM_TAG_NT) was slower (34.49-34.53 vs 34.25); the
+// partition apply's value stores: NRG_HM_PA_NT. Build with =0 / =1 for the A/B.
+#ifndef NRG_HM_APPLY_NT
+#define NRG_HM_APPLY_NT 1
+#endif
+#ifndef NRG_HM_TAG_NT
+#define NRG_HM_TAG_NT 0
+#endif
+#ifndef NRG_HM_PA_NT
+#define NRG_HM_PA_NT 0
+#endif
+template <bool NT, typename T>
+__device__ __forceinline__ void st_pol(T* p, T v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
 constexpr int TPB = 256;
 constexpr u32 SIDE_ID = 0x7FFFFFFFu;    // slot id standing for the side slot (slot ids are < 2^30)
 constexpr u32 FULL_SLOT = 0xFFFFFFFFu;  // no slot could be claimed (table full)
@@ -411,16 +432,16 @@ __device__ __forceinline__ void stamp_index_role(const StampJob& j, u32 blk, Slo
                 created++;
             }
             atomicMax(&s_side, (u32)(i + 1));
-            j.put_slot[i] = SIDE_SLOT;
+            st_pol<NRG_HM_TAG_NT>(&j.put_slot[i], SIDE_SLOT);
             continue;
         }
         const long long s = find_or_claim_marked(table, k, home[q], tmask, key0[q], e, &created);
         if (s < 0) {
             atomicOr(&ctl->err, ERR_TABLE_FULL);
-            j.put_slot[i] = FULL_SLOT;
+            st_pol<NRG_HM_TAG_NT>(&j.put_slot[i], FULL_SLOT);
             continue;
         }
-        j.put_slot[i] = (u32)s;
+        st_pol<NRG_HM_TAG_NT>(&j.put_slot[i], (u32)s);
         u32 h = (u32)(mix64((u64)s) & (HT - 1));
         for (;;) {
             const u32 old = atomicCAS(&s_slot[h], 0xFFFFFFFFu, (u32)s);
@@ -446,8 +467,8 @@ __device__ __forceinline__ void stamp_index_role(const StampJob& j, u32 blk, Slo
             const u64 mine = stamp_make(e, s_max[q]);
             const u64 old = atomicMax((unsigned long long*)&table[sl].st[par], (unsigned long long)mine);
             if (old < mine) {
-                j.win[s_max[q] - 1] = e;
-                if (stamp_epoch(old) == e && (u32)old) j.over[(u32)old - 1] = e;
+                st_pol<NRG_HM_TAG_NT>(&j.win[s_max[q] - 1], e);
+                if (stamp_epoch(old) == e && (u32)old) st_pol<NRG_HM_TAG_NT>(&j.over[(u32)old - 1], e);
             }
         }
     }
@@ -470,7 +491,7 @@ __device__ __forceinline__ void apply_role(const ApplyJob& j, u32 blk, Slot* tab
     } else if (s != FULL_SLOT) {
         // (a 16-B {key, val} store costs the same: a partial-line write is priced per line,
         // profiles/r03_apply_store_width.txt)
-        if (j.win[i] == j.epoch && j.over[i] != j.epoch) table[s].val = j.rec.at(i).val;
+        if (j.win[i] == j.epoch && j.over[i] != j.epoch) st_pol<NRG_HM_APPLY_NT>(&table[s].val, j.rec.at(i).val);
     }
 }
 
@@ -928,7 +949,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(PREV ? 3 : 4)
                 } else if (sl[r] < 0) {
                     atomicOr(&j.ctl->err, ERR_TABLE_FULL);
                 } else {
-                    j.table[sl[r]].val = x[r].y;
+                    st_pol<NRG_HM_PA_NT>(&j.table[sl[r]].val, x[r].y);
                     created += fr[r];
                 }
             }
