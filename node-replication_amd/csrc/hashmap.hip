@@ -67,17 +67,22 @@ __device__ __forceinline__ void st_rec(nrg_put* p, const nrg_put& r, bool plain)
 // (NRG_HM_APPLY_NT): they drain during the launch instead of in its end-of-kernel L2 write-back.
 // Same box, three pairs: 34.16-34.20 -> 33.93-34.02 us per B1 step (window 34.03-34.13 ->
 // 33.80-33.97); the driver's 20 steps 27,507-27,866 -> 27,823-27,875 Mops/s. Streaming the index
-// role's put_slot / win / over words (NRG_HM_TAG_NT) was slower (34.49-34.53 vs 34.25); the
-// partition apply's value stores: NRG_HM_PA_NT. Build with =0 / =1 for the A/B.
+// role's put_slot / win / over words (NRG_HM_TAG_NT) was slower (34.49-34.53 vs 34.25). Build
+// with =0 / =1 for the A/B.
 #ifndef NRG_HM_APPLY_NT
 #define NRG_HM_APPLY_NT 1
 #endif
 #ifndef NRG_HM_TAG_NT
 #define NRG_HM_TAG_NT 0
 #endif
+// The partition apply's value stores are streamed in rounds of at most PA_NT_MAX Puts: same box,
+// two pairs, N = 8 per-GPU round (800k Puts + 900k Gets) 77.24-77.35 -> 75.35-75.57 us, 50 % writes
+// 53.7-53.8 -> 53.1-53.2; configs[2]'s 4M Puts slower streamed (251.1-251.3 -> 257.3-258.3), so
+// they stay plain above it (profiles/r06/papply_nt.txt). NRG_HM_PA_NT=0 builds it plain throughout.
 #ifndef NRG_HM_PA_NT
-#define NRG_HM_PA_NT 0
+#define NRG_HM_PA_NT 1
 #endif
+constexpr u64 PA_NT_MAX = NRG_HM_PA_NT ? 2000000 : 0;
 template <bool NT, typename T>
 __device__ __forceinline__ void st_pol(T* p, T v) {
     if constexpr (NT) __builtin_nontemporal_store(v, p);
@@ -774,7 +779,8 @@ __device__ __forceinline__ void pa_resolve(Slot* table, u32 shift, u64 tmask, co
     }
 }
 
-template <bool PREV, int T>
+// NT: the table values are stored streamed (round 6; rounds of <= PA_NT_MAX Puts, see the launch)
+template <bool PREV, int T, bool NT = false>
 __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(PREV ? 3 : 4))) void hm_papply_kernel(PApplyJob j) {
     using G = PaGeo<PREV, T>;
     constexpr int PA_TPB = G::TPB, C = G::C, HT = G::HT, PER = G::PER;
@@ -949,7 +955,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(PREV ? 3 : 4)
                 } else if (sl[r] < 0) {
                     atomicOr(&j.ctl->err, ERR_TABLE_FULL);
                 } else {
-                    st_pol<NRG_HM_PA_NT>(&j.table[sl[r]].val, x[r].y);
+                    st_pol<NT>(&j.table[sl[r]].val, x[r].y);
                     created += fr[r];
                 }
             }
@@ -1945,6 +1951,8 @@ hipError_t hm_replay_chunk(nrg_ctx* c, const void* src_recs, u64 lo, u64 n, bool
         const unsigned dyn = ((ij.nblocks + 1) * 4 + ij.nblocks * 2 + 3) & ~3u;
         if (want_prev) NRG_LAUNCH(c, "hm_papply", (hm_papply_kernel<true, 256>), 1u << nb_log, 256, dyn, c->stream, aj);
         else if (pa_t == 1024) NRG_LAUNCH(c, "hm_papply", (hm_papply_kernel<false, 1024>), 1u << nb_log, 1024, dyn, c->stream, aj);
+        else if (pa_t == 512 && n <= PA_NT_MAX)
+            NRG_LAUNCH(c, "hm_papply", (hm_papply_kernel<false, 512, true>), 1u << nb_log, 512, dyn, c->stream, aj);
         else if (pa_t == 512) NRG_LAUNCH(c, "hm_papply", (hm_papply_kernel<false, 512>), 1u << nb_log, 512, dyn, c->stream, aj);
         else NRG_LAUNCH(c, "hm_papply", (hm_papply_kernel<false, 256>), 1u << nb_log, 256, dyn, c->stream, aj);
         if ((e = hipGetLastError()) != hipSuccess) return e;
