@@ -310,7 +310,7 @@ __device__ __forceinline__ void part_role(const IndexJob& j, u32 blk, u32 shift,
         u64x2 e;
         e.x = rec[q].key;
         e.y = rec[q].val;
-        ent[p] = e;
+        ent[p] = e;  // (streamed: 75.4-75.8 -> 93.5-93.7 us per N = 8 round, profiles/r06/papply_nt.txt)
         if (j.eidx) j.eidx[(u64)blk * TILE + p] = (u32)(base + (u64)(w * WT + q * 64 + lane));
     }
 }
