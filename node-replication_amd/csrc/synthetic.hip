@@ -45,6 +45,12 @@ __device__ __forceinline__ void st_op(nrg_synth_op* p, const nrg_synth_op& o, bo
     __builtin_nontemporal_store(a, (u64x2_t*)p);
     __builtin_nontemporal_store(b, (u64x2_t*)p + 1);
 }
+// Round 6: the sums' responses are streamed (compile-time, since st_out's hint is dropped): same box,
+// three pairs, 45.40-45.66 -> 44.35-44.61 us per 1M-op round (profiles/r06/synth_resp_nt.txt).
+// NRG_SY_RESP_NT=0 restores st_out (plain unless the A/B bit 9 asks, which compiles plain too).
+#ifndef NRG_SY_RESP_NT
+#define NRG_SY_RESP_NT 1
+#endif
 constexpr int MS_TPB = 256;
 constexpr int MS_ITEMS = 8;
 constexpr int MS_TILE = MS_TPB * MS_ITEMS;
@@ -1013,8 +1019,13 @@ __device__ __forceinline__ void sy_sum_role(const SySumArgs& S, u32 blk, u64* s_
         for (u32 i = tid; i < nops; i += SYC_TPB) {
             const u64 g = lo + op0 + i;
             if (g >= resp_lo && g < resp_hi) {
+#if NRG_SY_RESP_NT
+                __builtin_nontemporal_store(s_sum[i], &resp[g - resp_lo]);
+                if (some) __builtin_nontemporal_store((uint8_t)1, &some[g - resp_lo]);
+#else
                 st_out(&resp[g - resp_lo], s_sum[i], S.plain);
                 if (some) st_out(&some[g - resp_lo], (uint8_t)1, S.plain);
+#endif
             }
         }
     }
