@@ -539,6 +539,8 @@ __device__ __forceinline__ void read_role(const ReadJob& j, u32 blk, const Slot*
         w[r].y = 0;
         st[r] = 0;
         if (probe) {
+            // (round 6: with the streaming hint on these two loads, 34.04-34.13 -> 44.25-44.36 us per
+            // B1 round; profiles/r06/b1_apply_nt.txt)
             w[r] = *(const u64x2*)&table[s[r]];
             if (!j.quiet) st[r] = table[s[r]].st[par];
         }
