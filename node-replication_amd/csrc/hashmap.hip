@@ -1053,7 +1053,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(PREV ? 3 : 4)
                 const u32 h = hh[r];
                 const u32 sl = s_hs[h];
                 if (sl == SIDE_ID) j.ctl->sp.val = s_lv[h];
-                else if (sl != FULL_SLOT) j.table[sl].val = s_lv[h];
+                else if (sl != FULL_SLOT) j.table[sl].val = s_lv[h];  // (streamed, with the answers: slower, profiles/r06/papply_nt.txt)
                 if (h < HT) s_hk[h] = EMPTY_KEY;
                 s_hp[h] = 0;
                 s_h1[h] = NOFIRST;
